@@ -1,0 +1,256 @@
+/*
+ * ipxg.h -- C-ABI of the MI355X-native packet -> biflow engine.
+ *
+ * This is the drop-in boundary for ipfixprobe's per-packet hot path:
+ *
+ *   parse_packet()              /root/reference/src/plugins/input/parser/parser.cpp:673-805
+ *                               (declared parser.hpp:87-93)
+ *   NHTFlowCache::put_pkt()     /root/reference/src/plugins/storage/cache/src/cache.cpp:322-491
+ *   create_hash_key() + XXH64() cache.cpp:525-574, xxhash.h:2885-2901
+ *   FragmentationCache          cache/src/fragmentationCache/fragmentationCache.cpp:46-100
+ *   StoragePlugin virtuals      /root/reference/include/ipfixprobe/storagePlugin.hpp:54-72
+ *
+ * Plain C, plain pointers and sizes.  Every entry point returns 0 on success or a
+ * negative IPXG_E* code; no exception ever crosses this boundary (the reference throws
+ * PluginError, plugin.hpp:81-91 -- the C++ shim in ipfixprobe_amd/host maps codes back).
+ *
+ * Threading: one engine per input pipeline, called from one thread (the reference builds
+ * one NHTFlowCache per input thread, ipfixprobe.cpp:381-464).  An engine owns one HIP
+ * stream on one device.
+ */
+#ifndef IPXG_H
+#define IPXG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPXG_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------------------- */
+#define IPXG_OK 0
+#define IPXG_EINVAL (-1)   /* bad argument / option string                               */
+#define IPXG_ENOMEM (-2)   /* device or host allocation failed                           */
+#define IPXG_EDEVICE (-3)  /* HIP runtime error (message in ipxg_last_error)             */
+#define IPXG_EALIGN (-4)   /* a frame offset is not 16-byte aligned                      */
+#define IPXG_ETOOBIG (-5)  /* batch larger than IPXG_MAX_BATCH or arena > 4 GiB          */
+#define IPXG_EIO (-6)      /* file could not be read / unsupported capture format        */
+#define IPXG_ESTATE (-7)   /* call not valid in the engine's current state               */
+
+#define IPXG_MAX_BATCH (16u * 1024u * 1024u - 1u) /* per-batch counters are 24-bit     */
+
+/* Link types (pcap LINKTYPE / libpcap DLT numbers), reference pcap.cpp:178-200 and
+ * parser.cpp:704-726. */
+#define IPXG_DLT_EN10MB 1
+#define IPXG_DLT_RAW 12        /* libpcap DLT_RAW; LINKTYPE_RAW (101) is mapped to it    */
+#define IPXG_DLT_LINUX_SLL 113
+#define IPXG_DLT_LINUX_SLL2 276
+
+/* Flow end reasons, reference flowifc.hpp:236-240 */
+#define IPXG_FLOW_END_INACTIVE 0x01
+#define IPXG_FLOW_END_ACTIVE 0x02
+#define IPXG_FLOW_END_EOF 0x03
+#define IPXG_FLOW_END_FORCED 0x04
+#define IPXG_FLOW_END_NO_RES 0x05
+
+/* ---- input: one packet descriptor (16 B), frames live in a byte arena ---------------
+ * Replaces the (ts, data, len, caplen) argument tuple of parse_packet (parser.cpp:673-679).
+ * caplen/wirelen are uint16_t exactly as parse_packet's parameters (the pcap plugin passes
+ * pcap_pkthdr's 32-bit lengths into them, pcap.cpp:54-70, i.e. truncated mod 2^16).
+ * Timestamps are timeval split into unsigned 32-bit seconds and microseconds (the classic
+ * pcap record header's own width).  offset must be a multiple of 16. */
+typedef struct ipxg_pkt_desc {
+    uint32_t offset;  /* byte offset of the frame inside the batch arena               */
+    uint16_t caplen;  /* captured bytes present in the arena                            */
+    uint16_t wirelen; /* original length on the wire                                    */
+    uint32_t ts_sec;
+    uint32_t ts_usec;
+} ipxg_pkt_desc;
+
+#define IPXG_BATCH_DEVICE 0x1u /* arena and desc are device pointers (already in HBM)   */
+
+typedef struct ipxg_batch {
+    const uint8_t* arena;       /* frame bytes                                          */
+    uint64_t arena_len;         /* bytes valid in arena (<= 4 GiB)                      */
+    const ipxg_pkt_desc* desc;  /* n descriptors in arrival order                       */
+    uint32_t n;                 /* packets in this batch, <= IPXG_MAX_BATCH             */
+    uint32_t flags;             /* IPXG_BATCH_*                                          */
+} ipxg_batch;
+
+/* ---- output: one exported biflow record (128 B POD) ----------------------------------
+ * Mirrors ipxp::Flow (flowifc.hpp:245-268) minus the RecordExt chain, plus vlan_id (part
+ * of the flow key, cache.hpp:29-46) and end_reason.  IPv4 addresses occupy the first 4
+ * bytes of src_ip/dst_ip in network order (ipaddr_t.v4), the rest are zero. */
+typedef struct ipxg_flow_record {
+    uint64_t flow_hash;       /* XXH64 of the creating packet's forward key            */
+    uint32_t time_first_sec;
+    uint32_t time_first_usec;
+    uint32_t time_last_sec;
+    uint32_t time_last_usec;
+    uint64_t src_bytes;
+    uint64_t dst_bytes;
+    uint32_t src_packets;
+    uint32_t dst_packets;
+    uint8_t src_tcp_flags;
+    uint8_t dst_tcp_flags;
+    uint8_t ip_version;
+    uint8_t ip_proto;
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint8_t src_ip[16];
+    uint8_t dst_ip[16];
+    uint8_t src_mac[6];
+    uint8_t dst_mac[6];
+    uint16_t vlan_id;
+    uint8_t end_reason;       /* IPXG_FLOW_END_*                                        */
+    uint8_t reserved0;
+    uint8_t reserved[24];
+} ipxg_flow_record;
+
+/* ---- per-packet parse result (debug / parity entry point) ----------------------------
+ * The flow-relevant subset of ipxp::Packet (packet.hpp:46-147) after parse_packet. */
+typedef struct ipxg_parsed_pkt {
+    uint8_t valid;            /* parse_packet accepted the packet (pblock->cnt++)        */
+    uint8_t ip_version;
+    uint8_t ip_proto;
+    uint8_t tcp_flags;
+    uint16_t ethertype;
+    uint16_t ip_len;
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint16_t frag_off;
+    uint8_t more_fragments;
+    uint8_t ip_ttl;
+    uint32_t vlan_id;
+    uint32_t frag_id;
+    uint32_t mpls_top;
+    uint32_t tcp_mss;
+    uint64_t tcp_options;
+    uint8_t src_ip[16];
+    uint8_t dst_ip[16];
+    uint8_t src_mac[6];
+    uint8_t dst_mac[6];
+    uint8_t ip_tos;
+    uint8_t ip_flags;
+    uint16_t tcp_window;
+    uint32_t tcp_seq;
+    uint32_t tcp_ack;
+    uint64_t hash_fwd;        /* XXH64(key), 0 when the packet has no flow key          */
+    uint64_t hash_inv;        /* XXH64(inverse key)                                     */
+} ipxg_parsed_pkt;
+
+/* ---- engine ------------------------------------------------------------------------ */
+typedef struct ipxg_config {
+    uint32_t cache_exp;       /* s=  initial table capacity 2^s slots (4..30)          */
+    uint32_t line_exp;        /* l=  accepted for option compatibility                 */
+    uint32_t active_s;        /* a=  active timeout, seconds (default 300)             */
+    uint32_t inactive_s;      /* i=  inactive timeout, seconds (default 30)            */
+    uint32_t split_biflow;    /* S   1 = uniflows                                      */
+    uint32_t frag_enable;     /* fe= fragmentation cache on (default 1)                */
+    uint32_t frag_size;       /* fs= buckets (default 10007)                           */
+    uint32_t frag_timeout_s;  /* ft= seconds (default 3)                               */
+    int32_t device_id;        /* dev= HIP device ordinal                               */
+    uint32_t batch_pkts;      /* batch= max packets per submit (staging size)          */
+    uint32_t datalink;        /* IPXG_DLT_*                                            */
+    uint32_t reserved;
+} ipxg_config;
+
+typedef struct ipxg_stats {
+    /* parser counters, reference parser-stats.hpp:126-201 (the subset on the path) */
+    uint64_t seen_packets;
+    uint64_t parsed_packets;  /* pblock->cnt increments                                */
+    uint64_t unknown_packets;
+    uint64_t ipv4_packets;
+    uint64_t ipv6_packets;
+    uint64_t tcp_packets;
+    uint64_t udp_packets;
+    uint64_t mpls_packets;
+    uint64_t pppoe_packets;
+    uint64_t trill_packets;
+    uint64_t vlan_packets;
+    uint64_t ipv4_bytes;
+    uint64_t ipv6_bytes;
+    /* cache counters, reference cache.cpp:618-665 */
+    uint64_t end_inactive;
+    uint64_t end_active;
+    uint64_t end_eof;
+    uint64_t end_forced;
+    uint64_t end_no_res;
+    uint64_t flows_in_cache;
+    uint64_t total_exported;
+    uint64_t keyless_packets; /* valid packets without a flow key (create_hash_key false) */
+    uint64_t fragmented_packets;
+    uint64_t fragments_filled;
+    uint64_t complex_flows;   /* flow-batches resolved on the sequential device path    */
+    uint64_t table_capacity;
+    uint64_t table_rehashes;
+    uint64_t batches;
+} ipxg_stats;
+
+typedef struct ipxg_engine ipxg_engine;
+
+/* Fill *cfg with the reference defaults (cache.hpp:52-64, :91-102). */
+void ipxg_config_default(ipxg_config* cfg);
+/* Parse the reference cache option string ("s=20;a=300;i=30;S;fe=false;..."), plus
+ * dev= / batch= / dlt=, into *cfg (reference CacheOptParser, cache.hpp:81-221). */
+int ipxg_config_parse(const char* params, ipxg_config* cfg);
+
+int ipxg_create(const ipxg_config* cfg, ipxg_engine** out);
+int ipxg_destroy(ipxg_engine* eng);
+const char* ipxg_last_error(const ipxg_engine* eng);
+/* hipStream_t the engine launches on (for event timing by the caller). */
+void* ipxg_stream(ipxg_engine* eng);
+
+/* Parse + hash + biflow-cache update for one batch, in arrival order
+ * (= for each packet: parse_packet, then NHTFlowCache::put_pkt).  Host batches are
+ * staged to HBM with hipMemcpyAsync; device batches are read in place.  Returns after the
+ * batch has been applied (the stream is synchronised). */
+int ipxg_submit(ipxg_engine* eng, const ipxg_batch* batch);
+/* Export every flow idle for >= inactive seconds at now_sec (reference export_expired,
+ * cache.cpp:508-523, whole table at once). */
+int ipxg_expire(ipxg_engine* eng, int64_t now_sec);
+/* Export every remaining flow as FLOW_END_FORCED and empty the cache (cache.cpp:276-288). */
+int ipxg_finish(ipxg_engine* eng);
+/* Drop all state without exporting (engine reuse). */
+int ipxg_reset(ipxg_engine* eng);
+/* Number of exported records waiting in the device export buffer. */
+int ipxg_pending_exports(ipxg_engine* eng, size_t* n);
+/* Copy up to cap exported records to host memory out and remove them from the buffer. */
+int ipxg_poll_exports(ipxg_engine* eng, ipxg_flow_record* out, size_t cap, size_t* n);
+/* Device pointer to the export buffer and its current count (no copy; valid until the next
+ * engine call). */
+int ipxg_device_exports(ipxg_engine* eng, const ipxg_flow_record** dptr, size_t* n);
+/* Forget the pending exports without copying them (caller consumed them on device). */
+int ipxg_clear_exports(ipxg_engine* eng);
+int ipxg_get_stats(ipxg_engine* eng, ipxg_stats* out);
+
+/* ---- stateless device entry points (parity tests, tools) ---------------------------- */
+/* Run the device parser on a batch; out receives n records (host pointer). */
+int ipxg_parse_batch(ipxg_engine* eng, const ipxg_batch* batch, ipxg_parsed_pkt* out);
+/* XXH64(seed) of n keys of keylen bytes each, packed back to back, on the device. */
+int ipxg_xxh64_batch(ipxg_engine* eng, const uint8_t* keys, uint32_t keylen, uint32_t n,
+                     uint64_t seed, uint64_t* out);
+
+/* ---- host ingestion (pcap / pcapng files) -------------------------------------------
+ * Reads a whole capture into a host batch: frames at 16-byte aligned offsets, lengths
+ * truncated to 16 bits exactly as the reference passes them to parse_packet, nanosecond
+ * captures scaled to microseconds by integer division (libpcap's behaviour). */
+typedef struct ipxg_capture {
+    uint8_t* arena;
+    uint64_t arena_len;
+    ipxg_pkt_desc* desc;
+    uint32_t n;
+    uint32_t datalink;        /* IPXG_DLT_* of the capture                              */
+} ipxg_capture;
+
+int ipxg_capture_load(const char* path, ipxg_capture** out);
+void ipxg_capture_free(ipxg_capture* cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IPXG_H */

@@ -1,0 +1,996 @@
+/*
+ * ipxg_oracle.c -- CPU restatement of ipfixprobe's parse -> XXH64 -> NHTFlowCache path.
+ * TEST INFRASTRUCTURE ONLY (see ipxg_oracle.h).  Each function cites the reference
+ * file:line it restates; paths are relative to /root/reference.
+ */
+#include "ipxg_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ===================================================================================== */
+/* XXH64 -- src/plugins/storage/cache/src/xxhash.h:2725-2901 (xxHash 0.8.1)             */
+/* ===================================================================================== */
+#define XP1 0x9E3779B185EBCA87ULL /* xxhash.h:2725 */
+#define XP2 0xC2B2AE3D27D4EB4FULL
+#define XP3 0x165667B19E3779F9ULL
+#define XP4 0x85EBCA77C2B2AE63ULL
+#define XP5 0x27D4EB2F165667C5ULL
+
+static uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static uint64_t rd64le(const uint8_t* p)
+{
+    uint64_t v = 0;
+    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+    return v;
+}
+static uint32_t rd32le(const uint8_t* p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+/* XXH64_round xxhash.h:2754-2760 */
+static uint64_t xx_round(uint64_t acc, uint64_t in)
+{
+    acc += in * XP2;
+    acc = rotl64(acc, 31);
+    return acc * XP1;
+}
+/* XXH64_mergeRound :2762-2768 */
+static uint64_t xx_merge(uint64_t acc, uint64_t val)
+{
+    val = xx_round(0, val);
+    acc ^= val;
+    return acc * XP1 + XP4;
+}
+/* XXH64_avalanche :2771-2778 */
+static uint64_t xx_aval(uint64_t h)
+{
+    h ^= h >> 33;
+    h *= XP2;
+    h ^= h >> 29;
+    h *= XP3;
+    h ^= h >> 32;
+    return h;
+}
+
+/* XXH64_endian_align + XXH64_finalize, xxhash.h:2799-2873 */
+uint64_t oracle_xxh64(const void* data, size_t len, uint64_t seed)
+{
+    const uint8_t* p = (const uint8_t*)data;
+    uint64_t h;
+    if (len >= 32) {
+        const uint8_t* limit = p + len - 31;
+        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+        do {
+            v1 = xx_round(v1, rd64le(p));
+            v2 = xx_round(v2, rd64le(p + 8));
+            v3 = xx_round(v3, rd64le(p + 16));
+            v4 = xx_round(v4, rd64le(p + 24));
+            p += 32;
+        } while (p < limit);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xx_merge(h, v1);
+        h = xx_merge(h, v2);
+        h = xx_merge(h, v3);
+        h = xx_merge(h, v4);
+    } else {
+        h = seed + XP5;
+    }
+    h += (uint64_t)len;
+    size_t rem = len & 31;
+    while (rem >= 8) {
+        h ^= xx_round(0, rd64le(p));
+        p += 8;
+        h = rotl64(h, 27) * XP1 + XP4;
+        rem -= 8;
+    }
+    if (rem >= 4) {
+        h ^= (uint64_t)rd32le(p) * XP1;
+        p += 4;
+        h = rotl64(h, 23) * XP2 + XP3;
+        rem -= 4;
+    }
+    while (rem > 0) {
+        h ^= (uint64_t)(*p++) * XP5;
+        h = rotl64(h, 11) * XP1;
+        --rem;
+    }
+    return xx_aval(h);
+}
+
+/* ===================================================================================== */
+/* Parser -- src/plugins/input/parser/parser.cpp                                         */
+/* Offsets are absolute byte offsets into the frame; "data_len" values are uint16_t     */
+/* exactly where the reference passes uint16_t parameters (so they wrap identically).   */
+/* A `throw` of the reference is modelled by setting c->err and unwinding.              */
+/* ===================================================================================== */
+#define ETH_P_8021AD 0x88A8 /* headers.hpp:35 */
+#define ETH_P_8021Q 0x8100
+#define ETH_P_IP 0x0800
+#define ETH_P_IPV6 0x86DD
+#define ETH_P_MPLS_UC 0x8847
+#define ETH_P_MPLS_MC 0x8848
+#define ETH_P_PPP_SES 0x8864
+#define ETH_P_TRILL 0x22F3 /* parser.hpp:57 */
+#define GRE_CHECKSUM 0x8000 /* headers.hpp:60-62 */
+#define GRE_KEY 0x2000
+#define GRE_SEQNUM 0x1000
+#define IPV6_FRAGMENT_OFFSET 0xFFF8 /* headers.hpp:53-54 */
+#define IPV6_MORE_FRAGMENTS 0x1
+
+typedef struct {
+    uint16_t ethertype;
+    uint32_t vlan_id;
+    uint8_t src_mac[6];
+    uint8_t dst_mac[6];
+} eth_out;
+
+typedef struct {
+    const uint8_t* d;
+    uint32_t cap;
+    int beyond;
+    int err;
+    ipxg_parsed_pkt* p;
+    uint16_t ip_payload_len;
+    ipxg_stats* st;
+} pctx;
+
+static uint8_t B8(pctx* c, uint32_t o)
+{
+    if (o < c->cap) return c->d[o];
+    c->beyond = 1;
+    return 0;
+}
+static uint16_t BE16(pctx* c, uint32_t o) { return (uint16_t)((B8(c, o) << 8) | B8(c, o + 1)); }
+static uint32_t BE32(pctx* c, uint32_t o)
+{
+    return ((uint32_t)B8(c, o) << 24) | ((uint32_t)B8(c, o + 1) << 16) | ((uint32_t)B8(c, o + 2) << 8) |
+           B8(c, o + 3);
+}
+static void COPY(pctx* c, uint8_t* dst, uint32_t o, int n)
+{
+    for (int i = 0; i < n; ++i) dst[i] = B8(c, o + (uint32_t)i);
+}
+#define THROW(c)         \
+    do {                 \
+        (c)->err = 1;    \
+        return 0;        \
+    } while (0)
+#define CHK(c)               \
+    do {                     \
+        if ((c)->err) return 0; \
+    } while (0)
+
+/* parse_eth_hdr parser.cpp:68-155 */
+static uint16_t parse_eth_hdr(pctx* c, uint32_t base, uint16_t data_len, eth_out* e)
+{
+    if (14 > data_len) THROW(c);
+    uint16_t hdr_len = 14;
+    uint16_t ethertype = BE16(c, base + 12);
+    COPY(c, e->dst_mac, base, 6);
+    COPY(c, e->src_mac, base + 6, 6);
+    e->vlan_id = 0;
+    if (ethertype == ETH_P_8021AD || ethertype == ETH_P_8021Q) {
+        if (4 > (int)data_len - (int)hdr_len) THROW(c);
+        uint16_t vlan = BE16(c, base + hdr_len);
+        e->vlan_id = vlan & 0x0FFF;
+        hdr_len += 4;
+        ethertype = BE16(c, base + hdr_len - 2);
+    }
+    while (ethertype == ETH_P_8021Q) {
+        if (4 > (int)data_len - (int)hdr_len) THROW(c);
+        hdr_len += 4;
+        ethertype = BE16(c, base + hdr_len - 2);
+    }
+    e->ethertype = ethertype;
+    return hdr_len;
+}
+
+static void eth_to_pkt(const eth_out* e, ipxg_parsed_pkt* p)
+{
+    memcpy(p->dst_mac, e->dst_mac, 6);
+    memcpy(p->src_mac, e->src_mac, 6);
+    p->vlan_id = e->vlan_id;
+    p->ethertype = e->ethertype;
+}
+
+/* parse_sll parser.cpp:165-189 (struct sll_header: pkttype, hatype, halen, addr[8], protocol) */
+static uint16_t parse_sll(pctx* c, uint16_t data_len)
+{
+    if (16 > data_len) THROW(c);
+    if (BE16(c, 2) == 1) COPY(c, c->p->src_mac, 6, 6); /* ARPHRD_ETHER */
+    else memset(c->p->src_mac, 0, 6);
+    memset(c->p->dst_mac, 0, 6);
+    c->p->ethertype = BE16(c, 14);
+    return 16;
+}
+
+/* parse_sll2 parser.cpp:192-217 (struct sll2_header: protocol, mbz, if_index, hatype,
+ * pkttype, halen, addr[8]) */
+static uint16_t parse_sll2(pctx* c, uint16_t data_len)
+{
+    if (20 > data_len) THROW(c);
+    if (BE16(c, 8) == 1) COPY(c, c->p->src_mac, 12, 6);
+    else memset(c->p->src_mac, 0, 6);
+    memset(c->p->dst_mac, 0, 6);
+    c->p->ethertype = BE16(c, 0);
+    return 20;
+}
+
+/* parse_trill parser.cpp:228-249; trill_hdr little-endian bitfields headers.hpp:230-246 */
+static uint16_t parse_trill(pctx* c, uint32_t base, uint16_t data_len)
+{
+    if (6 > data_len) THROW(c);
+    uint8_t b0 = B8(c, base), b1 = B8(c, base + 1);
+    uint8_t op_len = (uint8_t)(((b0 & 0x7) << 2) | (b1 >> 6));
+    uint8_t op_len_bytes = (uint8_t)(op_len * 4);
+    return (uint16_t)(6 + op_len_bytes);
+}
+
+static uint16_t parse_ipv4_hdr(pctx* c, uint32_t base, uint16_t data_len);
+static uint16_t parse_ipv6_hdr(pctx* c, uint32_t base, uint16_t data_len);
+static uint16_t process_mpls(pctx* c, uint32_t base, uint16_t data_len);
+static uint16_t process_pppoe(pctx* c, uint32_t base, uint16_t data_len);
+
+/* parse_gre parser.cpp:256-302 */
+static uint16_t parse_gre(pctx* c, uint32_t base, uint16_t data_len)
+{
+    int gre_len = 4;
+    if (data_len < gre_len) THROW(c);
+    uint16_t flags = BE16(c, base);
+    uint16_t type = BE16(c, base + 2);
+    if (flags & GRE_CHECKSUM) gre_len += 4;
+    if (flags & GRE_KEY) gre_len += 4;
+    if (flags & GRE_SEQNUM) gre_len += 4;
+    if (data_len < gre_len) THROW(c);
+    base += (uint32_t)gre_len;
+    data_len = (uint16_t)(data_len - gre_len);
+    uint16_t r;
+    switch (type) {
+    case ETH_P_IP:
+        r = parse_ipv4_hdr(c, base, data_len);
+        CHK(c);
+        return (uint16_t)(r + gre_len);
+    case ETH_P_IPV6:
+        r = parse_ipv6_hdr(c, base, data_len);
+        CHK(c);
+        return (uint16_t)(r + gre_len);
+    case ETH_P_MPLS_UC:
+    case ETH_P_MPLS_MC:
+        r = process_mpls(c, base, data_len);
+        CHK(c);
+        return (uint16_t)(r + gre_len);
+    case ETH_P_PPP_SES:
+        r = process_pppoe(c, base, data_len);
+        CHK(c);
+        return (uint16_t)(r + gre_len);
+    default:
+        c->p->ip_proto = 47; /* IPPROTO_GRE */
+        return 0;
+    }
+}
+
+/* parse_ipv4_hdr parser.cpp:311-356 */
+static uint16_t parse_ipv4_hdr(pctx* c, uint32_t base, uint16_t data_len)
+{
+    if (20 > data_len) THROW(c);
+    const int ihl = (B8(c, base) & 0x0F) << 2;
+    uint8_t protocol = B8(c, base + 9);
+    if (protocol == 47) {
+        if (data_len < ihl) THROW(c);
+        uint16_t r = parse_gre(c, base + (uint32_t)ihl, (uint16_t)(data_len - ihl));
+        CHK(c);
+        return (uint16_t)(r + ihl);
+    }
+    ipxg_parsed_pkt* p = c->p;
+    p->ip_version = 4;
+    p->ip_proto = protocol;
+    p->ip_tos = B8(c, base + 1);
+    p->ip_len = BE16(c, base + 2);
+    c->ip_payload_len = (uint16_t)(p->ip_len - ihl);
+    p->ip_ttl = B8(c, base + 8);
+    uint16_t fo = BE16(c, base + 6);
+    p->ip_flags = (uint8_t)((fo & 0xE000) >> 13);
+    memset(p->src_ip, 0, 16);
+    memset(p->dst_ip, 0, 16);
+    COPY(c, p->src_ip, base + 12, 4);
+    COPY(c, p->dst_ip, base + 16, 4);
+    p->frag_id = BE16(c, base + 4);
+    p->frag_off = fo & 0x1FFF;
+    p->more_fragments = (fo & 0x2000) ? 1 : 0;
+    return (uint16_t)ihl;
+}
+
+/* skip_ipv6_ext_hdrs parser.cpp:365-414 */
+static uint16_t skip_ipv6_ext_hdrs(pctx* c, uint32_t base, uint16_t data_len)
+{
+    ipxg_parsed_pkt* p = c->p;
+    uint32_t ext = base;
+    uint8_t next_hdr = p->ip_proto;
+    uint32_t hdrs_len = 0;
+    for (;;) {
+        if (hdrs_len > data_len || 2u > (uint32_t)data_len - hdrs_len) THROW(c);
+        if (next_hdr == 0 || next_hdr == 60) { /* HOPOPTS, DSTOPTS */
+            hdrs_len += ((uint32_t)B8(c, ext + 1) << 3) + 8;
+        } else if (next_hdr == 43) { /* ROUTING */
+            hdrs_len += ((uint32_t)B8(c, base + hdrs_len + 1) << 3) + 8;
+        } else if (next_hdr == 51) { /* AH: (len << 2) - 2, parser.cpp:382 */
+            hdrs_len += (uint32_t)(((int)B8(c, ext + 1) << 2) - 2);
+        } else if (next_hdr == 44) { /* FRAGMENT */
+            uint32_t fr = base + hdrs_len;
+            p->frag_id = BE32(c, fr + 4);
+            uint16_t fo = BE16(c, fr + 2);
+            p->frag_off = fo & IPV6_FRAGMENT_OFFSET;
+            p->more_fragments = (fo & IPV6_MORE_FRAGMENTS) ? 1 : 0;
+            hdrs_len += 8;
+        } else if (next_hdr == 135) { /* MH */
+            hdrs_len += ((uint32_t)B8(c, ext + 1) << 3) + 8;
+            if (B8(c, ext) == 59) {
+                p->ip_proto = 59;
+                break;
+            }
+        } else {
+            break;
+        }
+        if (hdrs_len > 65535u) THROW(c);
+        next_hdr = B8(c, ext);
+        ext = base + hdrs_len;
+        p->ip_proto = next_hdr;
+    }
+    if (hdrs_len > 65535u) THROW(c);
+    c->ip_payload_len = (uint16_t)(c->ip_payload_len - hdrs_len);
+    return (uint16_t)hdrs_len;
+}
+
+/* parse_ipv6_hdr parser.cpp:423-460 */
+static uint16_t parse_ipv6_hdr(pctx* c, uint32_t base, uint16_t data_len)
+{
+    uint16_t hdr_len = 40;
+    if (40 > data_len) THROW(c);
+    ipxg_parsed_pkt* p = c->p;
+    p->ip_version = 6;
+    p->ip_tos = (uint8_t)((BE32(c, base) & 0x0ff00000) >> 20);
+    p->ip_proto = B8(c, base + 6);
+    p->ip_ttl = B8(c, base + 7);
+    p->ip_flags = 0;
+    c->ip_payload_len = BE16(c, base + 4);
+    p->ip_len = (uint16_t)(c->ip_payload_len + 40);
+    COPY(c, p->src_ip, base + 8, 16);
+    COPY(c, p->dst_ip, base + 24, 16);
+    if (p->ip_proto != 6 && p->ip_proto != 17) {
+        uint16_t r = skip_ipv6_ext_hdrs(c, base + hdr_len, (uint16_t)(data_len - hdr_len));
+        CHK(c);
+        hdr_len = (uint16_t)(hdr_len + r);
+    }
+    return hdr_len;
+}
+
+/* parse_tcp_hdr parser.cpp:469-543 */
+static uint16_t parse_tcp_hdr(pctx* c, uint32_t base, uint16_t data_len)
+{
+    if (20 > data_len) THROW(c);
+    ipxg_parsed_pkt* p = c->p;
+    p->src_port = BE16(c, base);
+    p->dst_port = BE16(c, base + 2);
+    p->tcp_seq = BE32(c, base + 4);
+    p->tcp_ack = BE32(c, base + 8);
+    p->tcp_flags = B8(c, base + 13);
+    p->tcp_window = BE16(c, base + 14);
+    int hdr_len = (B8(c, base + 12) >> 4) << 2;
+    int hdr_opt_len = hdr_len - 20;
+    int i = 0;
+    if (hdr_len > data_len) THROW(c);
+    while (i < hdr_opt_len) {
+        uint32_t opt = base + 20 + (uint32_t)i;
+        uint8_t kind = B8(c, opt);
+        if (i + 1 >= hdr_opt_len) {
+            if (kind <= 1) return (uint16_t)hdr_len;
+            THROW(c);
+        }
+        uint8_t opt_len = (uint8_t)(kind <= 1 ? 1 : B8(c, opt + 1));
+        /* shift count taken mod 64, as the x86-64 / gfx950 shifters do (parser.cpp:528) */
+        p->tcp_options |= 1ULL << (((kind & 0xF8) + (7 - (kind & 7))) & 63);
+        if (kind == 0) break;
+        if (kind == 2) p->tcp_mss = BE32(c, opt + 2);
+        if (opt_len == 0) THROW(c);
+        i += opt_len;
+    }
+    return (uint16_t)hdr_len;
+}
+
+/* parse_udp_hdr parser.cpp:552-573 */
+static uint16_t parse_udp_hdr(pctx* c, uint32_t base, uint16_t data_len)
+{
+    if (8 > data_len) THROW(c);
+    c->p->src_port = BE16(c, base);
+    c->p->dst_port = BE16(c, base + 2);
+    return 8;
+}
+
+/* process_mpls_stack parser.cpp:581-602 */
+static uint16_t process_mpls_stack(pctx* c, uint32_t base, uint16_t data_len)
+{
+    uint16_t length = 0;
+    uint32_t w;
+    do {
+        uint32_t m = base + length;
+        length = (uint16_t)(length + 4);
+        if (0 > (int)data_len - (int)length) THROW(c);
+        w = BE32(c, m);
+    } while (!(w & 0x100));
+    return length;
+}
+
+/* process_mpls parser.cpp:611-634 (EoMPLS keeps the reference's `length =` at :625) */
+static uint16_t process_mpls(pctx* c, uint32_t base, uint16_t data_len)
+{
+    c->p->mpls_top = BE32(c, base);
+    uint16_t length = process_mpls_stack(c, base, data_len);
+    CHK(c);
+    uint8_t next_hdr = (uint8_t)((B8(c, base + length) & 0xF0) >> 4);
+    uint16_t r;
+    if (next_hdr == 4) {
+        r = parse_ipv4_hdr(c, base + length, (uint16_t)(data_len - length));
+        CHK(c);
+        length = (uint16_t)(length + r);
+    } else if (next_hdr == 6) {
+        r = parse_ipv6_hdr(c, base + length, (uint16_t)(data_len - length));
+        CHK(c);
+        length = (uint16_t)(length + r);
+    } else if (next_hdr == 0) {
+        eth_out tmp;
+        memset(&tmp, 0, sizeof(tmp));
+        length = (uint16_t)(length + 4);
+        length = parse_eth_hdr(c, base + length, (uint16_t)(data_len - length), &tmp);
+        CHK(c);
+        if (tmp.ethertype == ETH_P_IP) {
+            r = parse_ipv4_hdr(c, base + length, (uint16_t)(data_len - length));
+            CHK(c);
+            length = (uint16_t)(length + r);
+        } else if (tmp.ethertype == ETH_P_IPV6) {
+            r = parse_ipv6_hdr(c, base + length, (uint16_t)(data_len - length));
+            CHK(c);
+            length = (uint16_t)(length + r);
+        }
+    }
+    return length;
+}
+
+/* process_pppoe parser.cpp:643-671 */
+static uint16_t process_pppoe(pctx* c, uint32_t base, uint16_t data_len)
+{
+    if (8 > data_len) THROW(c);
+    uint16_t next_hdr = BE16(c, base + 6);
+    uint16_t length = 8;
+    if (B8(c, base + 1) != 0) return length; /* code */
+    uint16_t r;
+    if (next_hdr == 0x0021) {
+        r = parse_ipv4_hdr(c, base + length, (uint16_t)(data_len - length));
+        CHK(c);
+        length = (uint16_t)(length + r);
+    } else if (next_hdr == 0x0057) {
+        r = parse_ipv6_hdr(c, base + length, (uint16_t)(data_len - length));
+        CHK(c);
+        length = (uint16_t)(length + r);
+    }
+    return length;
+}
+
+/* parse_packet parser.cpp:673-805 (parse_all = false, as every input plugin passes) */
+static int parse_packet(pctx* c, uint16_t caplen, uint32_t datalink)
+{
+    ipxg_parsed_pkt* p = c->p;
+    ipxg_stats* st = c->st;
+    uint16_t data_offset = 0;
+    eth_out e;
+    st->seen_packets++;
+    if (datalink == 0 || datalink == IPXG_DLT_EN10MB) {
+        data_offset = parse_eth_hdr(c, 0, caplen, &e);
+        if (c->err) return 0;
+        eth_to_pkt(&e, p);
+    } else if (datalink == IPXG_DLT_LINUX_SLL) {
+        data_offset = parse_sll(c, caplen);
+        if (c->err) return 0;
+    } else if (datalink == IPXG_DLT_LINUX_SLL2) {
+        data_offset = parse_sll2(c, caplen);
+        if (c->err) return 0;
+    } else if (datalink == IPXG_DLT_RAW) {
+        uint8_t v = B8(c, 0) & 0xF0;
+        if (v == 0x40) p->ethertype = ETH_P_IP;
+        else if (v == 0x60) p->ethertype = ETH_P_IPV6;
+    } else {
+        st->unknown_packets++;
+        return 0;
+    }
+    if (p->ethertype == ETH_P_TRILL) {
+        data_offset = (uint16_t)(data_offset + parse_trill(c, data_offset, (uint16_t)(caplen - data_offset)));
+        if (c->err) return 0;
+        st->trill_packets++;
+        uint16_t r = parse_eth_hdr(c, data_offset, (uint16_t)(caplen - data_offset), &e);
+        if (c->err) return 0;
+        eth_to_pkt(&e, p);
+        data_offset = (uint16_t)(data_offset + r);
+    }
+    uint16_t r;
+    if (p->ethertype == ETH_P_IP) {
+        r = parse_ipv4_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
+        if (c->err) return 0;
+        data_offset = (uint16_t)(data_offset + r);
+    } else if (p->ethertype == ETH_P_IPV6) {
+        r = parse_ipv6_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
+        if (c->err) return 0;
+        data_offset = (uint16_t)(data_offset + r);
+    } else if (p->ethertype == ETH_P_MPLS_UC || p->ethertype == ETH_P_MPLS_MC) {
+        r = process_mpls(c, data_offset, (uint16_t)(caplen - data_offset));
+        if (c->err) return 0;
+        data_offset = (uint16_t)(data_offset + r);
+        st->mpls_packets++;
+    } else if (p->ethertype == ETH_P_PPP_SES) {
+        r = process_pppoe(c, data_offset, (uint16_t)(caplen - data_offset));
+        if (c->err) return 0;
+        data_offset = (uint16_t)(data_offset + r);
+        st->pppoe_packets++;
+    } else {
+        st->unknown_packets++;
+        return 0;
+    }
+    if (p->frag_off == 0) {
+        if (p->ip_proto == 6) {
+            parse_tcp_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
+            if (c->err) return 0;
+            st->tcp_packets++;
+        } else if (p->ip_proto == 17) {
+            parse_udp_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
+            if (c->err) return 0;
+            st->udp_packets++;
+        }
+    }
+    if (p->vlan_id) st->vlan_packets++;
+    if (p->ethertype == ETH_P_IP) {
+        st->ipv4_packets++;
+        st->ipv4_bytes += caplen;
+    } else if (p->ethertype == ETH_P_IPV6) {
+        st->ipv6_packets++;
+        st->ipv6_bytes += caplen;
+    }
+    st->parsed_packets++;
+    return 1;
+}
+
+/* ---- flow key (cache.hpp:29-46, create_hash_key cache.cpp:525-574) ------------------ */
+/* Builds the packed key and its inverse; returns the key length (0 = no key). */
+static int build_keys(const ipxg_parsed_pkt* p, uint8_t* key, uint8_t* inv)
+{
+    uint16_t vlan = (uint16_t)p->vlan_id;
+    if (p->ip_version == 4) {
+        key[0] = p->src_port & 0xFF;
+        key[1] = p->src_port >> 8;
+        key[2] = p->dst_port & 0xFF;
+        key[3] = p->dst_port >> 8;
+        key[4] = p->ip_proto;
+        key[5] = 4;
+        memcpy(key + 6, p->src_ip, 4);
+        memcpy(key + 10, p->dst_ip, 4);
+        key[14] = vlan & 0xFF;
+        key[15] = vlan >> 8;
+        inv[0] = p->dst_port & 0xFF;
+        inv[1] = p->dst_port >> 8;
+        inv[2] = p->src_port & 0xFF;
+        inv[3] = p->src_port >> 8;
+        inv[4] = p->ip_proto;
+        inv[5] = 4;
+        memcpy(inv + 6, p->dst_ip, 4);
+        memcpy(inv + 10, p->src_ip, 4);
+        inv[14] = vlan & 0xFF;
+        inv[15] = vlan >> 8;
+        return 16;
+    }
+    if (p->ip_version == 6) {
+        key[0] = p->src_port & 0xFF;
+        key[1] = p->src_port >> 8;
+        key[2] = p->dst_port & 0xFF;
+        key[3] = p->dst_port >> 8;
+        key[4] = p->ip_proto;
+        key[5] = 6;
+        memcpy(key + 6, p->src_ip, 16);
+        memcpy(key + 22, p->dst_ip, 16);
+        key[38] = vlan & 0xFF;
+        key[39] = vlan >> 8;
+        inv[0] = p->dst_port & 0xFF;
+        inv[1] = p->dst_port >> 8;
+        inv[2] = p->src_port & 0xFF;
+        inv[3] = p->src_port >> 8;
+        inv[4] = p->ip_proto;
+        inv[5] = 6;
+        memcpy(inv + 6, p->dst_ip, 16);
+        memcpy(inv + 22, p->src_ip, 16);
+        inv[38] = vlan & 0xFF;
+        inv[39] = vlan >> 8;
+        return 40;
+    }
+    return 0;
+}
+
+int oracle_parse(const uint8_t* data, uint16_t caplen, uint16_t wirelen, uint32_t ts_sec,
+                 uint32_t ts_usec, uint32_t datalink, ipxg_parsed_pkt* out, int* beyond_caplen)
+{
+    (void)wirelen;
+    (void)ts_sec;
+    (void)ts_usec;
+    ipxg_stats st;
+    memset(&st, 0, sizeof(st));
+    memset(out, 0, sizeof(*out));
+    pctx c = {data, caplen, 0, 0, out, 0, &st};
+    int ok = parse_packet(&c, caplen, datalink);
+    out->valid = (uint8_t)ok;
+    if (ok) {
+        uint8_t k[40], ki[40];
+        int kl = build_keys(out, k, ki);
+        if (kl) {
+            out->hash_fwd = oracle_xxh64(k, (size_t)kl, 0);
+            out->hash_inv = oracle_xxh64(ki, (size_t)kl, 0);
+        }
+    }
+    if (beyond_caplen) *beyond_caplen = c.beyond;
+    return ok;
+}
+
+/* ===================================================================================== */
+/* Fragmentation cache -- fragmentationCache.cpp:46-100, fragmentationTable.cpp:37-61,  */
+/* fragmentationKeyData.hpp:49-136, ringBuffer.hpp:212-227 (RING_SIZE 4)                 */
+/* ===================================================================================== */
+typedef struct {
+    uint8_t key[40];
+    uint16_t sport, dport;
+    uint32_t sec, usec;
+} frag_entry;
+
+typedef struct {
+    frag_entry e[4]; /* e[0] oldest .. e[n-1] newest */
+    uint32_t n;
+} frag_ring;
+
+static void frag_key(const ipxg_parsed_pkt* p, uint8_t* k)
+{
+    memset(k, 0, 40);
+    k[0] = p->ip_version; /* uint16_t ip_version, little-endian */
+    k[1] = 0;
+    memcpy(k + 2, p->src_ip, 16);
+    memcpy(k + 18, p->dst_ip, 16);
+    k[34] = (uint8_t)p->frag_id;
+    k[35] = (uint8_t)(p->frag_id >> 8);
+    k[36] = (uint8_t)(p->frag_id >> 16);
+    k[37] = (uint8_t)(p->frag_id >> 24);
+    k[38] = (uint8_t)p->vlan_id;
+    k[39] = (uint8_t)(p->vlan_id >> 8);
+}
+
+/* ===================================================================================== */
+/* NHTFlowCache -- cache.cpp                                                              */
+/* ===================================================================================== */
+typedef struct {
+    uint64_t hash; /* m_hash, 0 = empty (cache.cpp:84-87) */
+    ipxg_flow_record f;
+} orec;
+
+struct oracle_cache {
+    uint32_t cache_size, line_size, line_mask, line_new_idx, timeout_idx;
+    uint32_t active, inactive;
+    int split, frag_enable;
+    uint32_t frag_size, frag_timeout;
+    orec* recs;
+    uint32_t* tab; /* m_flow_table: slot -> record */
+    frag_ring* frings;
+    ipxg_flow_record* ex;
+    size_t ex_head, ex_n, ex_cap;
+    ipxg_stats st;
+    uint64_t flows_in_cache;
+};
+
+oracle_cache* oracle_cache_new(uint32_t cache_exp, uint32_t line_exp, uint32_t active_s,
+                               uint32_t inactive_s, int split_biflow, int frag_enable,
+                               uint32_t frag_size, uint32_t frag_timeout_s)
+{
+    oracle_cache* c = (oracle_cache*)calloc(1, sizeof(*c));
+    if (!c) return NULL;
+    /* NHTFlowCache::init cache.cpp:191-198 */
+    c->cache_size = 1u << cache_exp;
+    c->line_size = 1u << line_exp;
+    c->line_mask = (c->cache_size - 1) & ~(c->line_size - 1);
+    c->line_new_idx = c->line_size / 2;
+    c->active = active_s;
+    c->inactive = inactive_s;
+    c->split = split_biflow;
+    c->frag_enable = frag_enable;
+    c->frag_size = frag_size ? frag_size : 10007;
+    c->frag_timeout = frag_timeout_s;
+    c->recs = (orec*)calloc(c->cache_size, sizeof(orec));
+    c->tab = (uint32_t*)malloc(sizeof(uint32_t) * c->cache_size);
+    c->frings = (frag_ring*)calloc(c->frag_size, sizeof(frag_ring));
+    c->ex_cap = 1024;
+    c->ex = (ipxg_flow_record*)malloc(sizeof(ipxg_flow_record) * c->ex_cap);
+    if (!c->recs || !c->tab || !c->frings || !c->ex) {
+        oracle_cache_free(c);
+        return NULL;
+    }
+    for (uint32_t i = 0; i < c->cache_size; ++i) c->tab[i] = i;
+    return c;
+}
+
+void oracle_cache_free(oracle_cache* c)
+{
+    if (!c) return;
+    free(c->recs);
+    free(c->tab);
+    free(c->frings);
+    free(c->ex);
+    free(c);
+}
+
+/* FlowRecord::erase cache.cpp:52-71 (MACs are left in place, as the reference does) */
+static void rec_erase(orec* r)
+{
+    r->hash = 0;
+    uint8_t sm[6], dm[6];
+    memcpy(sm, r->f.src_mac, 6);
+    memcpy(dm, r->f.dst_mac, 6);
+    uint8_t reason = r->f.end_reason;
+    memset(&r->f, 0, sizeof(r->f));
+    memcpy(r->f.src_mac, sm, 6);
+    memcpy(r->f.dst_mac, dm, 6);
+    r->f.end_reason = reason;
+}
+
+/* FlowRecord::create cache.cpp:94-132 */
+static void rec_create(orec* r, const ipxg_parsed_pkt* p, uint32_t sec, uint32_t usec, uint64_t hash)
+{
+    ipxg_flow_record* f = &r->f;
+    f->src_packets = 1;
+    r->hash = hash;
+    f->time_first_sec = f->time_last_sec = sec;
+    f->time_first_usec = f->time_last_usec = usec;
+    f->flow_hash = hash;
+    memcpy(f->src_mac, p->src_mac, 6);
+    memcpy(f->dst_mac, p->dst_mac, 6);
+    f->vlan_id = (uint16_t)p->vlan_id;
+    if (p->ip_version == 4) {
+        f->ip_version = 4;
+        f->ip_proto = p->ip_proto;
+        memcpy(f->src_ip, p->src_ip, 4);
+        memcpy(f->dst_ip, p->dst_ip, 4);
+        f->src_bytes = p->ip_len;
+    } else if (p->ip_version == 6) {
+        f->ip_version = 6;
+        f->ip_proto = p->ip_proto;
+        memcpy(f->src_ip, p->src_ip, 16);
+        memcpy(f->dst_ip, p->dst_ip, 16);
+        f->src_bytes = p->ip_len;
+    }
+    if (p->ip_proto == 6) {
+        f->src_port = p->src_port;
+        f->dst_port = p->dst_port;
+        f->src_tcp_flags = p->tcp_flags;
+    } else if (p->ip_proto == 17 || p->ip_proto == 1 || p->ip_proto == 58) {
+        f->src_port = p->src_port;
+        f->dst_port = p->dst_port;
+    }
+}
+
+/* FlowRecord::update cache.cpp:134-152 */
+static void rec_update(orec* r, const ipxg_parsed_pkt* p, uint32_t sec, uint32_t usec, int src)
+{
+    ipxg_flow_record* f = &r->f;
+    f->time_last_sec = sec;
+    f->time_last_usec = usec;
+    if (src) {
+        f->src_packets++;
+        f->src_bytes += p->ip_len;
+        if (p->ip_proto == 6) f->src_tcp_flags |= p->tcp_flags;
+    } else {
+        f->dst_packets++;
+        f->dst_bytes += p->ip_len;
+        if (p->ip_proto == 6) f->dst_tcp_flags |= p->tcp_flags;
+    }
+}
+
+/* export_flow cache.cpp:262-274: hand the record to the export queue, empty the slot */
+static void export_flow(oracle_cache* c, uint32_t index, uint8_t reason)
+{
+    orec* r = &c->recs[c->tab[index]];
+    r->f.end_reason = reason;
+    switch (reason) {
+    case IPXG_FLOW_END_INACTIVE: c->st.end_inactive++; break;
+    case IPXG_FLOW_END_ACTIVE: c->st.end_active++; break;
+    case IPXG_FLOW_END_EOF: c->st.end_eof++; break;
+    case IPXG_FLOW_END_FORCED: c->st.end_forced++; break;
+    case IPXG_FLOW_END_NO_RES: c->st.end_no_res++; break;
+    }
+    c->st.total_exported++;
+    c->flows_in_cache--;
+    if (c->ex_head + c->ex_n == c->ex_cap) {
+        if (c->ex_head > 0) {
+            memmove(c->ex, c->ex + c->ex_head, c->ex_n * sizeof(*c->ex));
+            c->ex_head = 0;
+        } else {
+            c->ex_cap *= 2;
+            c->ex = (ipxg_flow_record*)realloc(c->ex, c->ex_cap * sizeof(*c->ex));
+        }
+    }
+    c->ex[c->ex_head + c->ex_n++] = r->f;
+    rec_erase(r);
+}
+
+/* get_export_reason cache.cpp:498-506 */
+static uint8_t export_reason(const ipxg_flow_record* f)
+{
+    return ((f->src_tcp_flags | f->dst_tcp_flags) & (0x01 | 0x04)) ? IPXG_FLOW_END_EOF
+                                                                   : IPXG_FLOW_END_INACTIVE;
+}
+
+/* export_expired cache.cpp:508-523 */
+void oracle_cache_export_expired(oracle_cache* c, int64_t ts)
+{
+    for (uint32_t i = c->timeout_idx; i < c->timeout_idx + c->line_new_idx; ++i) {
+        orec* r = &c->recs[c->tab[i]];
+        if (r->hash != 0 && ts - (int64_t)r->f.time_last_sec >= (int64_t)c->inactive)
+            export_flow(c, i, export_reason(&r->f));
+    }
+    c->timeout_idx = (c->timeout_idx + c->line_new_idx) & (c->cache_size - 1);
+}
+
+/* put_pkt_recursive cache.cpp:330-491 (no process plugins: every hook returns 0) */
+static void put_pkt_recursive(oracle_cache* c, const ipxg_parsed_pkt* p, uint32_t sec, uint32_t usec)
+{
+    uint8_t key[40], inv[40];
+    int keylen = build_keys(p, key, inv);
+    if (!keylen) return;
+    uint64_t hashval = oracle_xxh64(key, (size_t)keylen, 0);
+    int found = 0, source_flow = 1;
+    uint32_t line_index = (uint32_t)(hashval & c->line_mask);
+    uint32_t next_line = line_index + c->line_size;
+    uint32_t fi;
+    for (fi = line_index; fi < next_line; ++fi)
+        if (c->recs[c->tab[fi]].hash == hashval) {
+            found = 1;
+            break;
+        }
+    if (!found && !c->split) {
+        uint64_t hinv = oracle_xxh64(inv, (size_t)keylen, 0);
+        uint32_t li = (uint32_t)(hinv & c->line_mask);
+        for (fi = li; fi < li + c->line_size; ++fi)
+            if (c->recs[c->tab[fi]].hash == hinv) {
+                found = 1;
+                source_flow = 0;
+                hashval = hinv;
+                line_index = li;
+                break;
+            }
+    }
+    if (found) { /* move to front, :375-391 */
+        uint32_t flow = c->tab[fi];
+        for (uint32_t j = fi; j > line_index; --j) c->tab[j] = c->tab[j - 1];
+        c->tab[line_index] = flow;
+        fi = line_index;
+    } else {
+        for (fi = line_index; fi < next_line; ++fi)
+            if (c->recs[c->tab[fi]].hash == 0) {
+                found = 1;
+                break;
+            }
+        if (!found) { /* line full: evict the last slot, insert at the middle, :400-419 */
+            fi = next_line - 1;
+            export_flow(c, fi, IPXG_FLOW_END_NO_RES);
+            uint32_t new_idx = line_index + c->line_new_idx;
+            uint32_t flow = c->tab[fi];
+            for (uint32_t j = fi; j > new_idx; --j) c->tab[j] = c->tab[j - 1];
+            fi = new_idx;
+            c->tab[new_idx] = flow;
+        }
+    }
+    orec* r = &c->recs[c->tab[fi]];
+    uint8_t flw_flags = source_flow ? r->f.src_tcp_flags : r->f.dst_tcp_flags;
+    if ((p->tcp_flags & 0x02) && (flw_flags & (0x01 | 0x04))) { /* :431-438 */
+        export_flow(c, fi, IPXG_FLOW_END_EOF);
+        put_pkt_recursive(c, p, sec, usec);
+        return;
+    }
+    if (r->hash == 0) {
+        c->flows_in_cache++;
+        rec_create(r, p, sec, usec, hashval);
+    } else {
+        if ((int64_t)sec - (int64_t)r->f.time_last_sec >= (int64_t)c->inactive) { /* :453 */
+            export_flow(c, fi, export_reason(&r->f));
+            put_pkt_recursive(c, p, sec, usec);
+            return;
+        }
+        if ((int64_t)sec - (int64_t)r->f.time_first_sec >= (int64_t)c->active) { /* :464 */
+            export_flow(c, fi, IPXG_FLOW_END_ACTIVE);
+            put_pkt_recursive(c, p, sec, usec);
+            return;
+        }
+        rec_update(r, p, sec, usec, source_flow);
+    }
+    oracle_cache_export_expired(c, (int64_t)sec); /* :489 */
+}
+
+/* FragmentationCache::process_packet fragmentationCache.cpp:46-100 */
+static void frag_process(oracle_cache* c, ipxg_parsed_pkt* p, uint32_t sec, uint32_t usec)
+{
+    if (!(p->frag_off || p->more_fragments)) return;
+    c->st.fragmented_packets++;
+    uint8_t k[40];
+    frag_key(p, k);
+    frag_ring* ring = &c->frings[oracle_xxh64(k, 40, 0) % c->frag_size];
+    if (!p->frag_off && p->more_fragments) { /* first fragment: insert (ring push_back) */
+        if (ring->n == 4) {
+            memmove(&ring->e[0], &ring->e[1], 3 * sizeof(frag_entry));
+            ring->n = 3;
+        }
+        frag_entry* e = &ring->e[ring->n++];
+        memcpy(e->key, k, 40);
+        e->sport = p->src_port;
+        e->dport = p->dst_port;
+        e->sec = sec;
+        e->usec = usec;
+        return;
+    }
+    for (int i = (int)ring->n - 1; i >= 0; --i) { /* find, newest first */
+        frag_entry* e = &ring->e[i];
+        if (memcmp(e->key, k, 40) != 0) continue;
+        /* timeout check: packet.ts > data.timestamp + timeout (timevalUtils.hpp) */
+        uint64_t lim_sec = (uint64_t)e->sec + c->frag_timeout;
+        uint64_t lim_usec = e->usec;
+        if (lim_usec >= 1000000) {
+            lim_sec++;
+            lim_usec -= 1000000;
+        }
+        int later = (sec == lim_sec) ? (usec > lim_usec) : (sec > lim_sec);
+        if (!later) {
+            p->src_port = e->sport;
+            p->dst_port = e->dport;
+            c->st.fragments_filled++;
+        }
+        return;
+    }
+}
+
+void oracle_cache_run(oracle_cache* c, const uint8_t* arena, const ipxg_pkt_desc* desc, size_t n,
+                      uint32_t datalink)
+{
+    for (size_t i = 0; i < n; ++i) {
+        const ipxg_pkt_desc* d = &desc[i];
+        ipxg_parsed_pkt p;
+        memset(&p, 0, sizeof(p));
+        pctx pc = {arena + d->offset, d->caplen, 0, 0, &p, 0, &c->st};
+        if (!parse_packet(&pc, d->caplen, datalink)) continue;
+        if (c->frag_enable) frag_process(c, &p, d->ts_sec, d->ts_usec);
+        if (p.ip_version != 4 && p.ip_version != 6) c->st.keyless_packets++;
+        put_pkt_recursive(c, &p, d->ts_sec, d->ts_usec);
+    }
+}
+
+/* finish cache.cpp:276-288 */
+void oracle_cache_finish(oracle_cache* c)
+{
+    for (uint32_t i = 0; i < c->cache_size; ++i)
+        if (c->recs[c->tab[i]].hash != 0) export_flow(c, i, IPXG_FLOW_END_FORCED);
+}
+
+size_t oracle_cache_pending(const oracle_cache* c) { return c->ex_n; }
+
+size_t oracle_cache_take(oracle_cache* c, ipxg_flow_record* out, size_t cap)
+{
+    size_t k = c->ex_n < cap ? c->ex_n : cap;
+    memcpy(out, c->ex + c->ex_head, k * sizeof(*out));
+    c->ex_head += k;
+    c->ex_n -= k;
+    if (c->ex_n == 0) c->ex_head = 0;
+    return k;
+}
+
+void oracle_cache_stats(const oracle_cache* c, ipxg_stats* out)
+{
+    *out = c->st;
+    out->flows_in_cache = c->flows_in_cache;
+    out->table_capacity = c->cache_size;
+}

@@ -1,0 +1,132 @@
+"""ctypes wrapper around oracle/liboracle.so -- the CPU checker (test infrastructure).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from pcaputil import FLOW_DTYPE, PARSED_DTYPE, STATS_FIELDS
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_ROOT, "oracle", "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        vp, u8p = ctypes.c_void_p, ctypes.c_void_p
+        L.oracle_xxh64.restype = ctypes.c_uint64
+        L.oracle_xxh64.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint64]
+        L.oracle_parse.restype = ctypes.c_int
+        L.oracle_parse.argtypes = [u8p, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_uint32, vp,
+                                   ctypes.POINTER(ctypes.c_int)]
+        L.oracle_cache_new.restype = vp
+        L.oracle_cache_new.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_int, ctypes.c_int,
+                                                               ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_cache_free.argtypes = [vp]
+        L.oracle_cache_run.argtypes = [vp, u8p, vp, ctypes.c_size_t, ctypes.c_uint32]
+        L.oracle_cache_export_expired.argtypes = [vp, ctypes.c_int64]
+        L.oracle_cache_finish.argtypes = [vp]
+        L.oracle_cache_pending.restype = ctypes.c_size_t
+        L.oracle_cache_pending.argtypes = [vp]
+        L.oracle_cache_take.restype = ctypes.c_size_t
+        L.oracle_cache_take.argtypes = [vp, vp, ctypes.c_size_t]
+        L.oracle_cache_stats.argtypes = [vp, vp]
+        _LIB = L
+    return _LIB
+
+
+def xxh64(data: bytes, seed=0):
+    buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    return lib().oracle_xxh64(buf, len(data), seed)
+
+
+def parse(frame: bytes, caplen=None, wirelen=None, datalink=1, sec=0, usec=0):
+    """Returns (parsed record as numpy void, beyond_caplen flag)."""
+    out = np.zeros(1, dtype=PARSED_DTYPE)
+    cl = len(frame) if caplen is None else caplen
+    wl = cl if wirelen is None else wirelen
+    buf = ctypes.create_string_buffer(bytes(frame), max(len(frame), 1))
+    beyond = ctypes.c_int(0)
+    lib().oracle_parse(buf, cl, wl, sec, usec, datalink, out.ctypes.data, ctypes.byref(beyond))
+    return out[0], bool(beyond.value)
+
+
+def parse_batch(arena, desc, datalink=1):
+    out = np.zeros(len(desc), dtype=PARSED_DTYPE)
+    beyond = np.zeros(len(desc), dtype=bool)
+    L = lib()
+    rec = np.zeros(1, dtype=PARSED_DTYPE)
+    b = ctypes.c_int(0)
+    base = arena.ctypes.data
+    for i, d in enumerate(desc):
+        L.oracle_parse(ctypes.c_void_p(base + int(d["offset"])), int(d["caplen"]),
+                       int(d["wirelen"]), int(d["ts_sec"]), int(d["ts_usec"]), datalink,
+                       rec.ctypes.data, ctypes.byref(b))
+        out[i] = rec[0]
+        beyond[i] = bool(b.value)
+    return out, beyond
+
+
+class OracleCache:
+    """NHTFlowCache restatement; defaults are the reference's (cache.hpp:52-64, :91-102)."""
+
+    def __init__(self, cache_exp=17, line_exp=4, active=300, inactive=30, split_biflow=False,
+                 frag_enable=True, frag_size=10007, frag_timeout=3):
+        self._c = lib().oracle_cache_new(cache_exp, line_exp, active, inactive,
+                                         int(split_biflow), int(frag_enable), frag_size,
+                                         frag_timeout)
+        if not self._c:
+            raise MemoryError("oracle_cache_new failed")
+
+    def run(self, arena, desc, datalink=1):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc)
+        lib().oracle_cache_run(self._c, arena.ctypes.data, desc.ctypes.data, len(desc), datalink)
+
+    def export_expired(self, ts):
+        lib().oracle_cache_export_expired(self._c, ts)
+
+    def finish(self):
+        lib().oracle_cache_finish(self._c)
+
+    def take(self):
+        n = lib().oracle_cache_pending(self._c)
+        out = np.zeros(n, dtype=FLOW_DTYPE)
+        if n:
+            lib().oracle_cache_take(self._c, out.ctypes.data, n)
+        return out
+
+    def stats(self):
+        arr = (ctypes.c_uint64 * len(STATS_FIELDS))()
+        lib().oracle_cache_stats(self._c, arr)
+        return dict(zip(STATS_FIELDS, list(arr)))
+
+    def close(self):
+        if self._c:
+            lib().oracle_cache_free(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_capture(arena, desc, datalink=1, finish=True, **kw):
+    c = OracleCache(**kw)
+    c.run(arena, desc, datalink)
+    if finish:
+        c.finish()
+    recs = c.take()
+    st = c.stats()
+    c.close()
+    return recs, st
