@@ -227,6 +227,23 @@ int ipxg_device_exports(ipxg_engine* eng, const ipxg_flow_record** dptr, size_t*
 int ipxg_clear_exports(ipxg_engine* eng);
 int ipxg_get_stats(ipxg_engine* eng, ipxg_stats* out);
 
+/* ---- stage timing (HIP events on the engine's stream) --------------------------------- */
+typedef struct ipxg_timing {
+    double ingest_ms;          /* k_ingest: parse + hash + table accumulate               */
+    double finalize_ms;        /* k_finalize                                               */
+    double slow_ms;            /* fragment / overflow / complex-flow paths                 */
+    double finish_ms;          /* k_finish + table clear                                   */
+    uint64_t ingest_launches;
+    uint64_t finalize_launches;
+    uint64_t slow_launches;
+    uint64_t finish_launches;
+    uint64_t ingest_packets;   /* packets covered by the timed ingest launches             */
+} ipxg_timing;
+
+/* Enable (1) / disable (0) event timing; enabling also zeroes the accumulators. */
+int ipxg_profile(ipxg_engine* eng, int enable);
+int ipxg_get_timing(ipxg_engine* eng, ipxg_timing* out);
+
 /* ---- stateless device entry points (parity tests, tools) ---------------------------- */
 /* Run the device parser on a batch; out receives n records (host pointer). */
 int ipxg_parse_batch(ipxg_engine* eng, const ipxg_batch* batch, ipxg_parsed_pkt* out);

@@ -1,0 +1,660 @@
+// ipxg_engine.cpp -- host side of the C-ABI (include/ipxg.h): device memory, the per-batch
+// kernel sequence, table growth, the export buffer, and statistics.
+//
+// Per ipxg_submit (one batch, arrival order):
+//   stage (H2D if host batch) -> k_ingest -> [sync: control block]
+//   -> fragments? sort + k_frag_walk + k_frag_accumulate
+//   -> deferred probes? grow table (k_rehash) + k_deferred, until none
+//   -> k_finalize -> [sync]
+//   -> complex flows? k_complex_rank -> gather -> sort -> k_complex_walk
+//   -> grow the table if its load passed 1/2.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/ipxg.h"
+#include "ipxg_kernels.hpp"
+
+using namespace ipxg;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct ipxg_engine {
+    ipxg_config cfg;
+    hipStream_t st = nullptr;
+    std::string err;
+    // flow table
+    uint32_t cap = 0;
+    HotSlot* hot = nullptr;
+    ipxg_flow_record* cold = nullptr;
+    uint32_t* slot_rank = nullptr;
+    uint32_t keys = 0, live = 0;
+    // export buffer: records [ex_head, ex_count) are pending
+    ipxg_flow_record* ex = nullptr;
+    uint32_t ex_cap = 0;
+    uint32_t* ex_count_d = nullptr;
+    uint32_t ex_count = 0, ex_head = 0;
+    // control / stats
+    BatchCtl* ctl_d = nullptr;
+    BatchCtl* ctl_h = nullptr;  // pinned
+    uint32_t* misc_d = nullptr;  // [0] rehash failures
+    unsigned long long* stats_d = nullptr;
+    // staging for host batches
+    DevBuf arena, desc;
+    // scratch
+    DevBuf defer_a, defer_b, frag_list, frag_sorted, frag_ports, sort_tmp;
+    DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
+    FragEntry* frag_ent = nullptr;
+    uint32_t* frag_cnt = nullptr;
+    // host-side counters
+    uint64_t complex_total = 0, rehashes = 0, batches = 0;
+    bool prev_valid = false;
+    uint32_t prev_sec = 0, prev_usec = 0;
+    // stage timing
+    bool prof = false;
+    hipEvent_t ev[8] = {};
+    ipxg_timing tm = {};
+};
+
+// event pairs: [0,1] ingest, [2,3] finalize, [4,5] slow paths, [6,7] finish
+static void ev_rec(ipxg_engine* e, int i) {
+    if (e->prof) (void)hipEventRecord(e->ev[i], e->st);
+}
+static double ev_ms(ipxg_engine* e, int a) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e->ev[a], e->ev[a + 1]) != hipSuccess) return 0.0;
+    return ms;
+}
+
+#define HIPCHK(e, call)                                                                  \
+    do {                                                                                 \
+        hipError_t _r = (call);                                                          \
+        if (_r != hipSuccess) {                                                          \
+            (e)->err = std::string(#call) + ": " + hipGetErrorString(_r);                \
+            return IPXG_EDEVICE;                                                         \
+        }                                                                                \
+    } while (0)
+
+static int set_err(ipxg_engine* e, int code, const std::string& msg) {
+    if (e) e->err = msg;
+    return code;
+}
+
+static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
+    if (b.bytes >= need && b.p) return IPXG_OK;
+    size_t nb = std::max<size_t>(need, b.bytes + b.bytes / 2);
+    if (nb < 256) nb = 256;
+    if (b.p) HIPCHK(e, hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.p, nb) != hipSuccess) return set_err(e, IPXG_ENOMEM, "hipMalloc failed");
+    b.bytes = nb;
+    return IPXG_OK;
+}
+
+static TableView table_view(ipxg_engine* e) { return TableView{e->hot, e->cold, e->slot_rank, e->cap - 1}; }
+
+static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_count_d, e->ex_cap}; }
+
+static FragView frag_view(ipxg_engine* e) {
+    return FragView{e->frag_ent, e->frag_cnt, (uint64_t*)e->frag_list.p, (uint64_t*)e->frag_sorted.p,
+                    (uint32_t*)e->frag_ports.p};
+}
+
+static Params params(ipxg_engine* e) {
+    Params p = {};
+    p.dlt = e->cfg.datalink;
+    p.active_s = e->cfg.active_s;
+    p.inactive_s = e->cfg.inactive_s;
+    p.bucket_w = std::max<uint32_t>(1, e->cfg.inactive_s / 2);
+    p.split_biflow = e->cfg.split_biflow;
+    p.frag_enable = e->cfg.frag_enable;
+    p.frag_size = e->cfg.frag_size ? e->cfg.frag_size : 10007;
+    p.frag_timeout_s = e->cfg.frag_timeout_s;
+    p.force_complex = e->cfg.inactive_s < 2 ? 1 : 0;
+    p.prev_valid = e->prev_valid;
+    p.prev_sec = e->prev_sec;
+    p.prev_usec = e->prev_usec;
+    return p;
+}
+
+static int alloc_table(ipxg_engine* e, uint32_t cap, HotSlot** hot, ipxg_flow_record** cold, uint32_t** rank) {
+    if (hipMalloc((void**)hot, sizeof(HotSlot) * (size_t)cap) != hipSuccess) return IPXG_ENOMEM;
+    if (hipMalloc((void**)cold, sizeof(ipxg_flow_record) * (size_t)cap) != hipSuccess) {
+        hipFree(*hot);
+        return IPXG_ENOMEM;
+    }
+    if (hipMalloc((void**)rank, sizeof(uint32_t) * (size_t)cap) != hipSuccess) {
+        hipFree(*hot);
+        hipFree(*cold);
+        return IPXG_ENOMEM;
+    }
+    HIPCHK(e, hipMemsetAsync(*hot, 0, sizeof(HotSlot) * (size_t)cap, e->st));
+    return IPXG_OK;
+}
+
+static int sync_ctl(ipxg_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, sizeof(BatchCtl), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(&e->ex_count, e->ex_count_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return IPXG_OK;
+}
+
+// Rebuild the table at new_cap, dropping dead slots (no live record, untouched).
+static int rehash(ipxg_engine* e, uint32_t new_cap) {
+    HotSlot* nh;
+    ipxg_flow_record* nc;
+    uint32_t* nr;
+    int rc = alloc_table(e, new_cap, &nh, &nc, &nr);
+    if (rc) return set_err(e, rc, "table allocation failed (capacity " + std::to_string(new_cap) + ")");
+    HIPCHK(e, hipMemsetAsync(e->misc_d, 0, sizeof(uint32_t), e->st));
+    TableView to{nh, nc, nr, new_cap - 1};
+    launch_rehash(e->st, table_view(e), e->cap, to, e->misc_d);
+    HIPCHK(e, hipGetLastError());
+    uint32_t fail = 0;
+    HIPCHK(e, hipMemcpyAsync(&fail, e->misc_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipFree(e->hot));
+    HIPCHK(e, hipFree(e->cold));
+    HIPCHK(e, hipFree(e->slot_rank));
+    e->hot = nh;
+    e->cold = nc;
+    e->slot_rank = nr;
+    e->cap = new_cap;
+    e->rehashes++;
+    if (fail) return set_err(e, IPXG_ENOMEM, "rehash could not place every flow");
+    return IPXG_OK;
+}
+
+static int ensure_export(ipxg_engine* e, size_t extra) {
+    size_t pending = e->ex_count - e->ex_head;
+    if (e->ex_count + extra <= e->ex_cap) return IPXG_OK;
+    size_t need = pending + extra;
+    if (need > 0xFFFFFFF0ull) return set_err(e, IPXG_ENOMEM, "export buffer would exceed 2^32 records");
+    if (need <= e->ex_cap && e->ex_head >= pending) {  // compact in place (no overlap)
+        if (pending)
+            HIPCHK(e, hipMemcpyAsync(e->ex, e->ex + e->ex_head, pending * sizeof(ipxg_flow_record),
+                                     hipMemcpyDeviceToDevice, e->st));
+    } else {
+        size_t ncap = std::max<size_t>(need, (size_t)e->ex_cap * 2);
+        ipxg_flow_record* nb;
+        if (hipMalloc((void**)&nb, ncap * sizeof(ipxg_flow_record)) != hipSuccess)
+            return set_err(e, IPXG_ENOMEM, "export buffer allocation failed");
+        if (pending)
+            HIPCHK(e, hipMemcpyAsync(nb, e->ex + e->ex_head, pending * sizeof(ipxg_flow_record),
+                                     hipMemcpyDeviceToDevice, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+        HIPCHK(e, hipFree(e->ex));
+        e->ex = nb;
+        e->ex_cap = (uint32_t)ncap;
+    }
+    e->ex_head = 0;
+    e->ex_count = (uint32_t)pending;
+    HIPCHK(e, hipMemcpyAsync(e->ex_count_d, &e->ex_count, sizeof(uint32_t), hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return IPXG_OK;
+}
+
+static uint32_t pow2_at_least(uint64_t v) {
+    uint32_t c = 16;
+    while (c < v && c < (1u << 30)) c <<= 1;
+    return c;
+}
+
+extern "C" {
+
+void ipxg_config_default(ipxg_config* cfg) {
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->cache_exp = 17;  // cache.hpp:54
+    cfg->line_exp = 4;    // cache.hpp:60
+    cfg->active_s = 300;  // cache.hpp:63-64
+    cfg->inactive_s = 30;
+    cfg->split_biflow = 0;
+    cfg->frag_enable = 1;  // cache.hpp:99-102
+    cfg->frag_size = 10007;
+    cfg->frag_timeout_s = 3;
+    cfg->device_id = 0;
+    cfg->batch_pkts = 1u << 20;
+    cfg->datalink = IPXG_DLT_EN10MB;
+}
+
+int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
+    if (!cfg || !out) return IPXG_EINVAL;
+    *out = nullptr;
+    if (cfg->cache_exp < 4 || cfg->cache_exp > 30) return IPXG_EINVAL;
+    if (cfg->frag_enable && cfg->frag_size == 0) return IPXG_EINVAL;
+    ipxg_engine* e = new ipxg_engine();
+    e->cfg = *cfg;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        delete e;
+        return IPXG_EDEVICE;
+    }
+    if (cfg->device_id < 0 || cfg->device_id >= ndev || hipSetDevice(cfg->device_id) != hipSuccess) {
+        delete e;
+        return IPXG_EINVAL;
+    }
+    int rc = IPXG_OK;
+    auto fail = [&](int code) {
+        ipxg_destroy(e);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) return fail(IPXG_EDEVICE);
+    // the reference sizes its table 2^s with 16-way lines; ours is open-addressed and grows,
+    // so start at 2^s but never below 2^16
+    uint32_t cap = 1u << std::max<uint32_t>(cfg->cache_exp, 16);
+    if ((rc = alloc_table(e, cap, &e->hot, &e->cold, &e->slot_rank))) return fail(rc);
+    e->cap = cap;
+    e->ex_cap = 1u << 16;
+    if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->ex_count_d, sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->ctl_d, sizeof(BatchCtl)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipHostMalloc((void**)&e->ctl_h, sizeof(BatchCtl), hipHostMallocDefault) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->misc_d, 16 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->stats_d, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long)) != hipSuccess)
+        return fail(IPXG_ENOMEM);
+    const uint32_t fs = cfg->frag_size ? cfg->frag_size : 10007;
+    if (hipMalloc((void**)&e->frag_ent, (size_t)fs * 4 * sizeof(FragEntry)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->frag_cnt, (size_t)fs * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+    if (hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+    if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
+        return fail(IPXG_EDEVICE);
+    if (hipStreamSynchronize(e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+    *out = e;
+    return IPXG_OK;
+}
+
+int ipxg_destroy(ipxg_engine* e) {
+    if (!e) return IPXG_OK;
+    if (e->st) hipStreamSynchronize(e->st);
+    hipFree(e->hot);
+    hipFree(e->cold);
+    hipFree(e->slot_rank);
+    hipFree(e->ex);
+    hipFree(e->ex_count_d);
+    hipFree(e->ctl_d);
+    if (e->ctl_h) hipHostFree(e->ctl_h);
+    hipFree(e->misc_d);
+    hipFree(e->stats_d);
+    hipFree(e->frag_ent);
+    hipFree(e->frag_cnt);
+    for (hipEvent_t ev : e->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->frag_list, &e->frag_sorted,
+                      &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank})
+        hipFree(b->p);
+    if (e->st) (void)hipStreamDestroy(e->st);
+    delete e;
+    return IPXG_OK;
+}
+
+const char* ipxg_last_error(const ipxg_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+void* ipxg_stream(ipxg_engine* e) { return e ? (void*)e->st : nullptr; }
+
+int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
+    if (!e || !batch) return IPXG_EINVAL;
+    const uint32_t n = batch->n;
+    if (n == 0) return IPXG_OK;
+    if (n > IPXG_MAX_BATCH) return set_err(e, IPXG_ETOOBIG, "batch larger than IPXG_MAX_BATCH");
+    if (batch->arena_len > (1ull << 32)) return set_err(e, IPXG_ETOOBIG, "arena larger than 4 GiB");
+    if (!batch->arena || !batch->desc) return set_err(e, IPXG_EINVAL, "null arena/desc");
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    BatchView bv;
+    bv.n = n;
+    if (batch->flags & IPXG_BATCH_DEVICE) {
+        bv.arena = batch->arena;
+        bv.desc = batch->desc;
+    } else {
+        if ((rc = ensure(e, e->arena, batch->arena_len + 64))) return rc;
+        if ((rc = ensure(e, e->desc, (size_t)n * sizeof(ipxg_pkt_desc)))) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->arena.p, batch->arena, batch->arena_len, hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, hipMemcpyAsync(e->desc.p, batch->desc, (size_t)n * sizeof(ipxg_pkt_desc),
+                                 hipMemcpyHostToDevice, e->st));
+        bv.arena = (const uint8_t*)e->arena.p;
+        bv.desc = (const ipxg_pkt_desc*)e->desc.p;
+    }
+    bv.base_sec = BASE_FROM_DESC0;  // kernels read desc[0] themselves (no host round trip)
+    // per-batch scratch sized for the worst case (every packet deferred / a fragment)
+    if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
+    if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
+    if (e->cfg.frag_enable) {
+        if ((rc = ensure(e, e->frag_list, (size_t)n * 8))) return rc;
+        if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
+    }
+    if ((rc = ensure_export(e, n))) return rc;
+    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+
+    Params p = params(e);
+    FragView fv = frag_view(e);
+    ev_rec(e, 0);
+    launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
+    ev_rec(e, 1);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = sync_ctl(e))) return rc;
+    const BatchCtl c1 = *e->ctl_h;
+    if (e->prof) {
+        e->tm.ingest_ms += ev_ms(e, 0);
+        e->tm.ingest_launches++;
+        e->tm.ingest_packets += n;
+    }
+    bool slow = false;
+
+    // fragmentation cache: order fragments by (bucket, arrival) and replay the rings
+    uint32_t ndef = c1.deferred;
+    if (c1.frag_count) {
+        if (!slow) ev_rec(e, 4);
+        slow = true;
+        const uint32_t nf = c1.frag_count;
+        if ((rc = ensure(e, e->frag_sorted, (size_t)nf * 8))) return rc;
+        size_t tb = 0;
+        HIPCHK(e, sort_keys_u64(nullptr, tb, nullptr, nullptr, nf, 64, e->st));
+        if ((rc = ensure(e, e->sort_tmp, tb))) return rc;
+        fv = frag_view(e);
+        tb = e->sort_tmp.bytes;
+        HIPCHK(e, sort_keys_u64(e->sort_tmp.p, tb, fv.list, fv.sorted, nf, 64, e->st));
+        launch_frag_walk(e->st, bv, p, fv, nf, e->stats_d);
+        HIPCHK(e, hipGetLastError());
+        launch_frag_accumulate(e->st, bv, p, table_view(e), fv, nf, e->ctl_d, (uint32_t*)e->defer_a.p);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        ndef = e->ctl_h->deferred;
+    }
+    // table overflow: grow and re-apply the deferred packets
+    while (ndef) {
+        if (!slow) ev_rec(e, 4);
+        slow = true;
+        if ((rc = rehash(e, e->cap * 2))) return rc;
+        HIPCHK(e, hipMemsetAsync(&e->ctl_d->deferred, 0, sizeof(uint32_t), e->st));
+        launch_deferred(e->st, bv, p, table_view(e), frag_view(e), (const uint32_t*)e->defer_a.p, ndef,
+                        e->ctl_d, (uint32_t*)e->defer_b.p);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        ndef = e->ctl_h->deferred;
+        std::swap(e->defer_a, e->defer_b);
+    }
+
+    if (slow) {
+        ev_rec(e, 5);
+        HIPCHK(e, hipStreamSynchronize(e->st));
+        if (e->prof) {
+            e->tm.slow_ms += ev_ms(e, 4);
+            e->tm.slow_launches++;
+        }
+    }
+    p.force_complex = p.force_complex || c1.nonmono;
+    ev_rec(e, 2);
+    launch_finalize(e->st, bv, p, table_view(e), frag_view(e), export_view(e), e->ctl_d, e->stats_d);
+    ev_rec(e, 3);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = sync_ctl(e))) return rc;
+    if (e->prof) {
+        e->tm.finalize_ms += ev_ms(e, 2);
+        e->tm.finalize_launches++;
+    }
+    const uint32_t ncx = e->ctl_h->complex_count;
+    if (ncx) {
+        ev_rec(e, 4);
+        e->complex_total += ncx;
+        if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 5 * 4))) return rc;
+        uint32_t* cr = (uint32_t*)e->cx_rank.p;
+        ComplexView cx = {nullptr, nullptr, cr, cr + ncx, cr + 2 * (size_t)ncx, cr + 3 * (size_t)ncx};
+        launch_complex_rank(e->st, table_view(e), cx, e->ctl_d, e->cap);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        const uint32_t npk = (uint32_t)(e->ctl_h->cx_alloc & 0xFFFFFFFFu);
+        if ((rc = ensure(e, e->cx_list, (size_t)npk * 8 + 8))) return rc;
+        if ((rc = ensure(e, e->cx_sorted, (size_t)npk * 8 + 8))) return rc;
+        cx.list = (uint64_t*)e->cx_list.p;
+        cx.sorted = (uint64_t*)e->cx_sorted.p;
+        launch_complex_gather(e->st, bv, p, table_view(e), frag_view(e), cx);
+        HIPCHK(e, hipGetLastError());
+        int bits = 24;
+        while ((1ull << (bits - 24)) < ncx) bits++;
+        size_t tb = 0;
+        HIPCHK(e, sort_keys_u64(nullptr, tb, nullptr, nullptr, npk, bits, e->st));
+        if ((rc = ensure(e, e->sort_tmp, tb))) return rc;
+        tb = e->sort_tmp.bytes;
+        HIPCHK(e, sort_keys_u64(e->sort_tmp.p, tb, cx.list, cx.sorted, npk, bits, e->st));
+        launch_complex_walk(e->st, bv, p, table_view(e), frag_view(e), cx, ncx, export_view(e), e->ctl_d,
+                            e->stats_d);
+        ev_rec(e, 5);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        if (e->prof) {
+            e->tm.slow_ms += ev_ms(e, 4);
+            e->tm.slow_launches++;
+        }
+    }
+    e->keys = e->ctl_h->keys;
+    e->live = e->ctl_h->live;
+    e->prev_valid = true;
+    e->prev_sec = e->ctl_h->last_sec;
+    e->prev_usec = e->ctl_h->last_usec;
+    e->batches++;
+    // keep the load factor <= 1/2 for the next batch (dead slots are dropped by the rebuild)
+    if ((uint64_t)e->keys * 2 > e->cap) {
+        uint32_t ncap = pow2_at_least((uint64_t)e->live * 4 + 1);
+        if (ncap < e->cap) ncap = e->cap;
+        if ((rc = rehash(e, ncap))) return rc;
+        e->keys = e->live;
+    }
+    return IPXG_OK;
+}
+
+int ipxg_expire(ipxg_engine* e, int64_t now_sec) {
+    if (!e) return IPXG_EINVAL;
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if ((rc = ensure_export(e, e->live))) return rc;
+    launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+    launch_count(e->st, table_view(e), e->cap, e->ctl_d);
+    if ((rc = sync_ctl(e))) return rc;
+    e->keys = e->ctl_h->keys;
+    e->live = e->ctl_h->live;
+    return IPXG_OK;
+}
+
+int ipxg_finish(ipxg_engine* e) {
+    if (!e) return IPXG_EINVAL;
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if ((rc = ensure_export(e, e->live))) return rc;
+    ev_rec(e, 6);
+    launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
+    ev_rec(e, 7);
+    HIPCHK(e, hipMemcpyAsync(&e->ex_count, e->ex_count_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    if (e->prof) {
+        e->tm.finish_ms += ev_ms(e, 6);
+        e->tm.finish_launches++;
+    }
+    e->keys = e->live = 0;
+    e->prev_valid = false;
+    return IPXG_OK;
+}
+
+int ipxg_reset(ipxg_engine* e) {
+    if (!e) return IPXG_EINVAL;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
+    const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
+    HIPCHK(e, hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st));
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    e->ex_count = e->ex_head = 0;
+    e->keys = e->live = 0;
+    e->prev_valid = false;
+    return IPXG_OK;
+}
+
+int ipxg_pending_exports(ipxg_engine* e, size_t* n) {
+    if (!e || !n) return IPXG_EINVAL;
+    *n = e->ex_count - e->ex_head;
+    return IPXG_OK;
+}
+
+int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t* n) {
+    if (!e || !n || (cap && !out)) return IPXG_EINVAL;
+    size_t k = std::min<size_t>(cap, e->ex_count - e->ex_head);
+    if (k) {
+        HIPCHK(e, hipSetDevice(e->cfg.device_id));
+        HIPCHK(e, hipMemcpyAsync(out, e->ex + e->ex_head, k * sizeof(ipxg_flow_record), hipMemcpyDeviceToHost,
+                                 e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    e->ex_head += (uint32_t)k;
+    if (e->ex_head == e->ex_count) {
+        e->ex_head = e->ex_count = 0;
+        HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    *n = k;
+    return IPXG_OK;
+}
+
+int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n) {
+    if (!e || !dptr || !n) return IPXG_EINVAL;
+    *dptr = e->ex + e->ex_head;
+    *n = e->ex_count - e->ex_head;
+    return IPXG_OK;
+}
+
+int ipxg_clear_exports(ipxg_engine* e) {
+    if (!e) return IPXG_EINVAL;
+    e->ex_head = e->ex_count = 0;
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return IPXG_OK;
+}
+
+int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
+    if (!e || !out) return IPXG_EINVAL;
+    unsigned long long h[STAT_SHARDS * ST_COUNT];
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    HIPCHK(e, hipMemcpyAsync(h, e->stats_d, sizeof(h), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    uint64_t s[ST_COUNT] = {};
+    for (int sh = 0; sh < STAT_SHARDS; ++sh)
+        for (int k = 0; k < ST_COUNT; ++k) s[k] += h[sh * ST_COUNT + k];
+    std::memset(out, 0, sizeof(*out));
+    out->seen_packets = s[ST_SEEN];
+    out->parsed_packets = s[ST_PARSED];
+    out->unknown_packets = s[ST_UNKNOWN];
+    out->ipv4_packets = s[ST_IPV4];
+    out->ipv6_packets = s[ST_IPV6];
+    out->tcp_packets = s[ST_TCP];
+    out->udp_packets = s[ST_UDP];
+    out->mpls_packets = s[ST_MPLS];
+    out->pppoe_packets = s[ST_PPPOE];
+    out->trill_packets = s[ST_TRILL];
+    out->vlan_packets = s[ST_VLAN];
+    out->ipv4_bytes = s[ST_IPV4_BYTES];
+    out->ipv6_bytes = s[ST_IPV6_BYTES];
+    out->end_inactive = s[ST_END_INACTIVE];
+    out->end_active = s[ST_END_ACTIVE];
+    out->end_eof = s[ST_END_EOF];
+    out->end_forced = s[ST_END_FORCED];
+    out->end_no_res = s[ST_END_NO_RES];
+    out->flows_in_cache = e->live;
+    out->total_exported = s[ST_END_INACTIVE] + s[ST_END_ACTIVE] + s[ST_END_EOF] + s[ST_END_FORCED] +
+                          s[ST_END_NO_RES];
+    out->keyless_packets = s[ST_KEYLESS];
+    out->fragmented_packets = s[ST_FRAGMENTED];
+    out->fragments_filled = s[ST_FRAG_FILLED];
+    out->complex_flows = e->complex_total;
+    out->table_capacity = e->cap;
+    out->table_rehashes = e->rehashes;
+    out->batches = e->batches;
+    return IPXG_OK;
+}
+
+int ipxg_profile(ipxg_engine* e, int enable) {
+    if (!e) return IPXG_EINVAL;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (enable && !e->ev[0])
+        for (hipEvent_t& ev : e->ev) HIPCHK(e, hipEventCreate(&ev));
+    e->prof = enable != 0;
+    if (enable) e->tm = ipxg_timing{};
+    return IPXG_OK;
+}
+
+int ipxg_get_timing(ipxg_engine* e, ipxg_timing* out) {
+    if (!e || !out) return IPXG_EINVAL;
+    *out = e->tm;
+    return IPXG_OK;
+}
+
+int ipxg_parse_batch(ipxg_engine* e, const ipxg_batch* batch, ipxg_parsed_pkt* out) {
+    if (!e || !batch || !out) return IPXG_EINVAL;
+    const uint32_t n = batch->n;
+    if (!n) return IPXG_OK;
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    BatchView bv;
+    bv.n = n;
+    bv.base_sec = 0;
+    if (batch->flags & IPXG_BATCH_DEVICE) {
+        bv.arena = batch->arena;
+        bv.desc = batch->desc;
+    } else {
+        if ((rc = ensure(e, e->arena, batch->arena_len + 64))) return rc;
+        if ((rc = ensure(e, e->desc, (size_t)n * sizeof(ipxg_pkt_desc)))) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->arena.p, batch->arena, batch->arena_len, hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, hipMemcpyAsync(e->desc.p, batch->desc, (size_t)n * sizeof(ipxg_pkt_desc), hipMemcpyHostToDevice,
+                                 e->st));
+        bv.arena = (const uint8_t*)e->arena.p;
+        bv.desc = (const ipxg_pkt_desc*)e->desc.p;
+    }
+    ipxg_parsed_pkt* d_out;
+    HIPCHK(e, hipMalloc((void**)&d_out, (size_t)n * sizeof(ipxg_parsed_pkt)));
+    launch_parse_batch(e->st, bv, e->cfg.datalink, d_out);
+    hipError_t le = hipGetLastError();
+    if (le == hipSuccess)
+        le = hipMemcpyAsync(out, d_out, (size_t)n * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st);
+    if (le == hipSuccess) le = hipStreamSynchronize(e->st);
+    (void)hipFree(d_out);
+    if (le != hipSuccess) return set_err(e, IPXG_EDEVICE, hipGetErrorString(le));
+    return IPXG_OK;
+}
+
+int ipxg_xxh64_batch(ipxg_engine* e, const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
+                     uint64_t* out) {
+    if (!e || (n && (!keys || !out))) return IPXG_EINVAL;
+    if (!n) return IPXG_OK;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    uint8_t* dk;
+    uint64_t* dh;
+    size_t kb = (size_t)keylen * n;
+    HIPCHK(e, hipMalloc((void**)&dk, kb ? kb : 1));
+    if (hipMalloc((void**)&dh, (size_t)n * 8) != hipSuccess) {
+        (void)hipFree(dk);
+        return set_err(e, IPXG_ENOMEM, "hipMalloc failed");
+    }
+    hipError_t le = kb ? hipMemcpyAsync(dk, keys, kb, hipMemcpyHostToDevice, e->st) : hipSuccess;
+    if (le == hipSuccess) {
+        launch_xxh64(e->st, dk, keylen, n, seed, dh);
+        le = hipGetLastError();
+    }
+    if (le == hipSuccess) le = hipMemcpyAsync(out, dh, (size_t)n * 8, hipMemcpyDeviceToHost, e->st);
+    if (le == hipSuccess) le = hipStreamSynchronize(e->st);
+    (void)hipFree(dk);
+    (void)hipFree(dh);
+    if (le != hipSuccess) return set_err(e, IPXG_EDEVICE, hipGetErrorString(le));
+    return IPXG_OK;
+}
+
+}  // extern "C"

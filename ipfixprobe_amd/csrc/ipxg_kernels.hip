@@ -1,0 +1,885 @@
+// ipxg_kernels.hip -- the engine's HIP kernels for gfx950.
+//
+// Per batch (ipxg_submit):
+//   k_ingest<INGEST>   one lane per packet: stage <=128 header bytes in LDS, parse
+//                      (parse_packet), build key + inverse key, 2x XXH64, probe the open-
+//                      addressed flow table by the canonical hash, and fold the packet into
+//                      the slot's per-batch accumulators with integer atomics.  Fragments
+//                      are diverted to the fragmentation-cache path.      (HBM-bound)
+//   k_frag_walk        fragments sorted by (bucket, index): one lane per bucket replays the
+//                      reference's 4-entry ring in arrival order (fragmentationCache.cpp).
+//   k_frag_accumulate  folds the port-resolved fragments into the table.
+//   k_finalize         one lane per slot: applies the reference's split rules at the batch
+//                      boundary and merges the batch accumulators into the flow record, or
+//                      marks the flow "complex" when a split could fall inside the batch.
+//   k_complex_*        complex flows only: gather their packets, sort by index, and replay
+//                      put_pkt_recursive sequentially per flow (cache.cpp:330-491).
+// Maintenance: k_expire (export_expired), k_finish (finish), k_rehash (table growth).
+#include "ipxg_device.hpp"
+#include "ipxg_kernels.hpp"
+
+namespace ipxg {
+
+// ---- helpers ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave-aggregated append: one atomic per wave instead of one per lane.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+    uint64_t m = __ballot(pred);
+    if (m == 0) return 0;
+    uint32_t lane = lane_id();
+    uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    return base + (uint32_t)__popcll(below);
+}
+
+template <class T>
+__device__ __forceinline__ T ld_relaxed(T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
+// zero-masked past caplen, plus one zero chunk so straddling reads see zeros.
+__device__ __forceinline__ void stage_frame(uint32_t* col, const uint8_t* arena, uint32_t off,
+                                            uint32_t cap) {
+    const uint32_t nbytes = cap < IPXG_WIN ? cap : IPXG_WIN;
+    const uint32_t nch = (nbytes + 15) >> 4;
+    const uint8_t* f = arena + off;
+    constexpr int NCH = IPXG_WIN / 16;
+    if ((off & 15) == 0) {
+        uint4 v[NCH];
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            v[ch] = make_uint4(0, 0, 0, 0);
+            if ((uint32_t)ch < nch) v[ch] = *reinterpret_cast<const uint4*>(f + 16 * ch);
+        }
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            if ((uint32_t)ch > nch) break;
+            uint32_t w[4] = {v[ch].x, v[ch].y, v[ch].z, v[ch].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                int b0 = 16 * ch + 4 * k;
+                int valid = (int)cap - b0;
+                uint32_t m = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+                col[(4 * ch + k) * IPXG_BLOCK] = w[k] & m;
+            }
+        }
+    } else {  // unaligned frame: byte loads (correct for any offset)
+        for (uint32_t dw = 0; dw < 4 * (nch + (nch < NCH ? 1 : 0)); ++dw) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t o = dw * 4 + k;
+                if (o < nbytes) w |= (uint32_t)f[o] << (8 * k);
+            }
+            col[dw * IPXG_BLOCK] = w;
+        }
+    }
+}
+
+// LDS window with caplen guard (bytes >= caplen read as 0).
+struct LdsFrame {
+    LdsWin w;
+    __device__ __forceinline__ uint32_t b(uint32_t o) const { return o < w.g.cap ? w.b(o) : 0u; }
+    __device__ __forceinline__ uint32_t le32(uint32_t o) const { return o < w.g.cap ? w.le32(o) : 0u; }
+};
+
+__device__ __forceinline__ void apply_frag_ports(const Params& p, const FragView& f, uint32_t idx,
+                                                 DevPkt& pk) {
+    if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
+        uint32_t pp = f.ports[idx];
+        pk.src_port = (uint16_t)(pp >> 16);
+        pk.dst_port = (uint16_t)(pp & 0xFFFF);
+    }
+}
+
+// canonical biflow hash and the packet's direction relative to it
+__device__ __forceinline__ void canon(const DevPkt& pk, const Params& p, uint64_t& lo, uint32_t& cdir,
+                                      uint64_t& hf) {
+    FlowKey kf, ki;
+    build_keys(pk, kf, ki);
+    hf = key_hash(kf);
+    if (p.split_biflow) {
+        lo = hf;
+        cdir = 0;
+        return;
+    }
+    uint64_t hi = key_hash(ki);
+    lo = hf < hi ? hf : hi;
+    cdir = hf > hi ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint32_t time_bucket(uint32_t sec, uint32_t base, uint32_t w) {
+    if (sec < base) return 63;
+    uint32_t b = (sec - base) / w;
+    return b > 62 ? 63 : b;
+}
+
+// Probe for (and if absent claim) the slot of canonical hash lo; nullptr after MAX_PROBE.
+__device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo) {
+    uint32_t s = (uint32_t)lo & t.mask;
+    for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
+        HotSlot* h = &t.hot[s];
+        uint64_t k = ld_relaxed(&h->key);
+        if (k == 0) {
+            unsigned long long old = atomicCAS((unsigned long long*)&h->key, 0ull, (unsigned long long)lo);
+            k = old == 0 ? lo : old;
+        }
+        if (k == lo) return h;
+        s = (s + 1) & t.mask;
+    }
+    return nullptr;
+}
+
+__device__ __forceinline__ int64_t probe_find(const TableView& t, uint64_t lo) {
+    uint32_t s = (uint32_t)lo & t.mask;
+    for (uint32_t probe = 0; probe <= t.mask; ++probe) {
+        uint64_t k = t.hot[s].key;
+        if (k == lo) return s;
+        if (k == 0) return -1;
+        s = (s + 1) & t.mask;
+    }
+    return -1;
+}
+
+// Fold one packet into its flow's per-batch accumulators (NHTFlowCache::put_pkt's update,
+// cache.cpp:134-152, as order-independent reductions keyed by packet index).
+__device__ __forceinline__ bool flow_accumulate(const TableView& t, const Params& p, const BatchView& b,
+                                                const DevPkt& pk, uint32_t idx, uint32_t sec) {
+    uint64_t lo, hf;
+    uint32_t cdir;
+    canon(pk, p, lo, cdir, hf);
+    HotSlot* h = probe_insert(t, lo);
+    if (!h) return false;
+    atomicAdd((unsigned long long*)&h->acc[cdir], (1ull << 40) | (uint64_t)pk.ip_len);
+    atomicMax(&h->last1, idx + 1);
+    const uint32_t fn = ~idx;
+    if (ld_relaxed(&h->first_n) < fn) atomicMax(&h->first_n, fn);
+    const uint64_t tb = 1ull << time_bucket(sec, b.base_sec, p.bucket_w);
+    if (!(ld_relaxed(&h->tbits) & tb)) atomicOr((unsigned long long*)&h->tbits, (unsigned long long)tb);
+    const uint32_t fl = pk.tcp_flags;
+    if (pk.ip_proto == 6 && fl) {
+        atomicOr(&h->tflags, fl << (8 * cdir));
+        if (fl & 0x02) atomicMax(&h->syn1[cdir], idx + 1);
+        if (fl & 0x05) atomicMax(&h->fin_n[cdir], ~idx);
+    }
+    return true;
+}
+
+__device__ __forceinline__ void flush_counts(const ParseCounts& c, uint32_t keyless, uint32_t frags,
+                                             uint32_t* sc) {
+    atomicAdd(&sc[ST_SEEN], c.seen);
+    atomicAdd(&sc[ST_PARSED], c.parsed);
+    atomicAdd(&sc[ST_UNKNOWN], c.unknown);
+    atomicAdd(&sc[ST_IPV4], c.ipv4);
+    atomicAdd(&sc[ST_IPV6], c.ipv6);
+    atomicAdd(&sc[ST_TCP], c.tcp);
+    atomicAdd(&sc[ST_UDP], c.udp);
+    atomicAdd(&sc[ST_MPLS], c.mpls);
+    atomicAdd(&sc[ST_PPPOE], c.pppoe);
+    atomicAdd(&sc[ST_TRILL], c.trill);
+    atomicAdd(&sc[ST_VLAN], c.vlan);
+    atomicAdd(&sc[ST_IPV4_BYTES], c.ipv4_bytes);
+    atomicAdd(&sc[ST_IPV6_BYTES], c.ipv6_bytes);
+    atomicAdd(&sc[ST_KEYLESS], keyless);
+    atomicAdd(&sc[ST_FRAGMENTED], frags);
+}
+
+__device__ __forceinline__ void flush_block_stats(uint32_t* sc, unsigned long long* stats) {
+    __syncthreads();
+    if (threadIdx.x < ST_COUNT && sc[threadIdx.x])
+        atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + threadIdx.x],
+                  (unsigned long long)sc[threadIdx.x]);
+}
+
+// ---- K1: ingest ------------------------------------------------------------------------
+enum IngestMode { MODE_INGEST = 0, MODE_GATHER = 1 };
+
+template <int MODE>
+__global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, TableView t, FragView f,
+                                                       BatchCtl* ctl, uint32_t* deferred_list,
+                                                       unsigned long long* stats, ComplexView cx) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    __shared__ uint32_t sc[ST_COUNT];
+    const uint32_t tid = threadIdx.x;
+    if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
+    if (tid < ST_COUNT) sc[tid] = 0;
+    __syncthreads();
+    ParseCounts c = {};
+    uint32_t keyless = 0, frags = 0;
+    uint32_t* col = &win[tid];
+    for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < b.n; base += gridDim.x * IPXG_BLOCK) {
+        const uint32_t i = base + tid;
+        const bool act = i < b.n;
+        ipxg_pkt_desc d = {0, 0, 0, 0, 0};
+        if (act) d = b.desc[i];
+        if (MODE == MODE_INGEST) {
+            const uint64_t ts = ((uint64_t)d.ts_sec << 32) | d.ts_usec;
+            uint64_t prev = (uint64_t)__shfl_up((unsigned long long)ts, 1);
+            bool has_prev = i > 0 || p.prev_valid;
+            if (lane_id() == 0) {
+                if (i > 0 && act) {
+                    ipxg_pkt_desc q = b.desc[i - 1];
+                    prev = ((uint64_t)q.ts_sec << 32) | q.ts_usec;
+                } else {
+                    prev = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
+                }
+            }
+            if (act && has_prev && ts < prev) ctl->nonmono = 1;
+            if (act && i == b.n - 1) {
+                ctl->last_sec = d.ts_sec;
+                ctl->last_usec = d.ts_usec;
+            }
+        }
+        if (!act) continue;
+        stage_frame(col, b.arena, d.offset, d.caplen);
+        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        DevPkt pk;
+        if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
+        if (pk.ip_version != 4 && pk.ip_version != 6) {
+            keyless++;
+            continue;
+        }
+        const bool is_frag = p.frag_enable && (pk.frag_off || pk.more_fragments);
+        if (MODE == MODE_INGEST) {
+            if (is_frag) {
+                frags++;
+                uint32_t bucket = (uint32_t)(frag_key_hash(pk) % (uint64_t)p.frag_size);
+                uint32_t pos = atomicAdd(&ctl->frag_count, 1u);
+                f.list[pos] = ((uint64_t)bucket << 24) | i;
+                continue;
+            }
+            if (!flow_accumulate(t, p, b, pk, i, d.ts_sec)) {
+                uint32_t pos = atomicAdd(&ctl->deferred, 1u);
+                deferred_list[pos] = i;
+            }
+        } else {  // MODE_GATHER: collect the packets of complex flows
+            if (is_frag) apply_frag_ports(p, f, i, pk);
+            uint64_t lo, hf;
+            uint32_t cdir;
+            canon(pk, p, lo, cdir, hf);
+            int64_t s = probe_find(t, lo);
+            if (s >= 0 && (t.hot[s].state & SLOT_COMPLEX)) {
+                uint32_t r = t.slot_rank[s];
+                uint32_t pos = atomicAdd(&cx.cursor[r], 1u);
+                cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
+            }
+        }
+    }
+    if (MODE == MODE_INGEST) {
+        flush_counts(c, keyless, frags, sc);
+        flush_block_stats(sc, stats);
+    }
+}
+
+static inline uint32_t grid_for(uint32_t n, uint32_t maxg) {
+    uint32_t g = (n + IPXG_BLOCK - 1) / IPXG_BLOCK;
+    if (g > maxg) g = maxg;
+    return g ? g : 1;
+}
+
+void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                   BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats) {
+    ComplexView cx = {};
+    hipLaunchKernelGGL(k_ingest<MODE_INGEST>, dim3(grid_for(b.n, 1024)), dim3(IPXG_BLOCK), 0, st, b, p,
+                       t, f, ctl, deferred_list, stats, cx);
+}
+
+void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t,
+                           FragView f, ComplexView cx) {
+    hipLaunchKernelGGL(k_ingest<MODE_GATHER>, dim3(grid_for(b.n, 1024)), dim3(IPXG_BLOCK), 0, st, b, p,
+                       t, f, nullptr, nullptr, nullptr, cx);
+}
+
+// ---- re-parse of one packet straight from HBM --------------------------------------------
+template <bool FULL>
+__device__ __forceinline__ bool reparse(const BatchView& b, const Params& p, const FragView& f,
+                                        uint32_t idx, DevPkt& pk, ipxg_pkt_desc& d) {
+    d = b.desc[idx];
+    GlobalSrc g{b.arena + d.offset, d.caplen};
+    ParseCounts dummy = {};
+    if (!parse_frame<FULL>(g, d.caplen, p.dlt, pk, dummy)) return false;
+    apply_frag_ports(p, f, idx, pk);
+    return true;
+}
+
+// ---- fragmentation cache -----------------------------------------------------------------
+__device__ __forceinline__ void frag_words(const DevPkt& pk, uint64_t w[5]) {
+    const uint32_t* s = pk.sip;
+    const uint32_t* d = pk.dip;
+    w[0] = (uint64_t)pk.ip_version | ((uint64_t)s[0] << 16) | ((uint64_t)(s[1] & 0xFFFF) << 48);
+    w[1] = (uint64_t)(s[1] >> 16) | ((uint64_t)s[2] << 16) | ((uint64_t)(s[3] & 0xFFFF) << 48);
+    w[2] = (uint64_t)(s[3] >> 16) | ((uint64_t)d[0] << 16) | ((uint64_t)(d[1] & 0xFFFF) << 48);
+    w[3] = (uint64_t)(d[1] >> 16) | ((uint64_t)d[2] << 16) | ((uint64_t)(d[3] & 0xFFFF) << 48);
+    w[4] = (uint64_t)(d[3] >> 16) | ((uint64_t)pk.frag_id << 16) | ((uint64_t)(pk.vlan_id & 0xFFFF) << 48);
+}
+
+// One lane per bucket segment of the (bucket, index)-sorted fragment list: replay the ring
+// (FragmentationTable::insert/find, RingBuffer push_back with overwrite) in arrival order.
+__global__ __launch_bounds__(256) void k_frag_walk(BatchView b, Params p, FragView f, uint32_t nfrag,
+                                                   unsigned long long* stats) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nfrag) return;
+    const uint32_t bucket = (uint32_t)(f.sorted[j] >> 24);
+    if (j > 0 && (uint32_t)(f.sorted[j - 1] >> 24) == bucket) return;
+    FragEntry* E = f.ent + (size_t)bucket * 4;
+    uint32_t cnt = f.cnt[bucket];
+    uint32_t filled = 0;
+    for (uint32_t k = j; k < nfrag && (uint32_t)(f.sorted[k] >> 24) == bucket; ++k) {
+        const uint32_t idx = (uint32_t)(f.sorted[k] & 0xFFFFFF);
+        ipxg_pkt_desc d = b.desc[idx];
+        GlobalSrc g{b.arena + d.offset, d.caplen};
+        ParseCounts dummy = {};
+        DevPkt pk;
+        parse_frame<false>(g, d.caplen, p.dlt, pk, dummy);
+        uint64_t w[5];
+        frag_words(pk, w);
+        uint32_t ports = ((uint32_t)pk.src_port << 16) | pk.dst_port;
+        if (!pk.frag_off && pk.more_fragments) {  // first fragment: insert
+            if (cnt == 4) {
+                for (int e = 0; e < 3; ++e) E[e] = E[e + 1];
+                cnt = 3;
+            }
+            FragEntry& e = E[cnt++];
+            for (int q = 0; q < 5; ++q) e.kw[q] = w[q];
+            e.sport = pk.src_port;
+            e.dport = pk.dst_port;
+            e.sec = d.ts_sec;
+            e.usec = d.ts_usec;
+        } else {
+            for (int e = (int)cnt - 1; e >= 0; --e) {
+                const FragEntry& x = E[e];
+                if (x.kw[0] != w[0] || x.kw[1] != w[1] || x.kw[2] != w[2] || x.kw[3] != w[3] || x.kw[4] != w[4])
+                    continue;
+                // packet.ts > data.timestamp + timeout (timevalUtils.hpp:27-47)
+                uint64_t ls = (uint64_t)x.sec + p.frag_timeout_s, lu = x.usec;
+                if (lu >= 1000000) {
+                    ls++;
+                    lu -= 1000000;
+                }
+                bool later = (d.ts_sec == ls) ? (d.ts_usec > lu) : (d.ts_sec > ls);
+                if (!later) {
+                    ports = ((uint32_t)x.sport << 16) | x.dport;
+                    filled++;
+                }
+                break;
+            }
+        }
+        f.ports[idx] = ports;
+    }
+    f.cnt[bucket] = cnt;
+    if (filled) atomicAdd(&stats[ST_FRAG_FILLED], (unsigned long long)filled);
+}
+
+void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,
+                      unsigned long long* stats) {
+    hipLaunchKernelGGL(k_frag_walk, dim3((nfrag + 255) / 256), dim3(256), 0, st, b, p, f, nfrag, stats);
+}
+
+__global__ __launch_bounds__(256) void k_frag_accumulate(BatchView b, Params p, TableView t, FragView f,
+                                                         uint32_t nfrag, BatchCtl* ctl,
+                                                         uint32_t* deferred_list) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nfrag) return;
+    if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.desc[0].ts_sec;
+    const uint32_t idx = (uint32_t)(f.list[j] & 0xFFFFFF);
+    DevPkt pk;
+    ipxg_pkt_desc d;
+    if (!reparse<false>(b, p, f, idx, pk, d)) return;
+    if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec)) {
+        uint32_t pos = atomicAdd(&ctl->deferred, 1u);
+        deferred_list[pos] = idx;
+    }
+}
+
+void launch_frag_accumulate(hipStream_t st, const BatchView& b, const Params& p, TableView t,
+                            FragView f, uint32_t nfrag, BatchCtl* ctl, uint32_t* deferred_list) {
+    hipLaunchKernelGGL(k_frag_accumulate, dim3((nfrag + 255) / 256), dim3(256), 0, st, b, p, t, f, nfrag,
+                       ctl, deferred_list);
+}
+
+// Re-apply packets whose probe failed before the table was grown.
+__global__ __launch_bounds__(256) void k_deferred(BatchView b, Params p, TableView t, FragView f,
+                                                  const uint32_t* in_list, uint32_t n_in, BatchCtl* ctl,
+                                                  uint32_t* out_list) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_in) return;
+    if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.desc[0].ts_sec;
+    const uint32_t idx = in_list[j];
+    DevPkt pk;
+    ipxg_pkt_desc d;
+    if (!reparse<false>(b, p, f, idx, pk, d)) return;
+    if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec)) {
+        uint32_t pos = atomicAdd(&ctl->deferred, 1u);
+        out_list[pos] = idx;
+    }
+}
+
+void launch_deferred(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                     const uint32_t* in_list, uint32_t n_in, BatchCtl* ctl, uint32_t* out_list) {
+    hipLaunchKernelGGL(k_deferred, dim3((n_in + 255) / 256), dim3(256), 0, st, b, p, t, f, in_list, n_in,
+                       ctl, out_list);
+}
+
+// ---- flow record construction (FlowRecord::create/update, cache.cpp:94-152) ---------------
+__device__ __forceinline__ void rec_create(ipxg_flow_record& r, const DevPkt& pk, const ipxg_pkt_desc& d,
+                                           uint64_t hf, uint32_t cdir) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) w[k] = 0;
+    r.flow_hash = hf;
+    r.time_first_sec = r.time_last_sec = d.ts_sec;
+    r.time_first_usec = r.time_last_usec = d.ts_usec;
+    r.ip_version = pk.ip_version;
+    r.ip_proto = pk.ip_proto;
+    for (int k = 0; k < 4; ++k) {
+        for (int q = 0; q < 4; ++q) {
+            r.src_ip[4 * k + q] = (uint8_t)(pk.sip[k] >> (8 * q));
+            r.dst_ip[4 * k + q] = (uint8_t)(pk.dip[k] >> (8 * q));
+        }
+    }
+    const uint32_t m[3] = {pk.mac_lo, pk.mac_mid, pk.mac_hi};
+    for (int q = 0; q < 6; ++q) {
+        r.dst_mac[q] = (uint8_t)(m[q >> 2] >> (8 * (q & 3)));
+        r.src_mac[q] = (uint8_t)(m[(q + 6) >> 2] >> (8 * ((q + 6) & 3)));
+    }
+    const uint8_t pr = pk.ip_proto;
+    if (pr == 6 || pr == 17 || pr == 1 || pr == 58) {
+        r.src_port = pk.src_port;
+        r.dst_port = pk.dst_port;
+    }
+    r.vlan_id = (uint16_t)pk.vlan_id;
+    r.reserved[0] = (uint8_t)cdir;  // creator's canonical direction (not exported)
+}
+
+__device__ __forceinline__ uint8_t export_reason(const ipxg_flow_record& r) {
+    return ((r.src_tcp_flags | r.dst_tcp_flags) & 0x05) ? IPXG_FLOW_END_EOF : IPXG_FLOW_END_INACTIVE;
+}
+
+__device__ __forceinline__ void store_export(ExportView ex, uint32_t pos, const ipxg_flow_record& r,
+                                             uint8_t reason) {
+    if (pos >= ex.cap) return;  // host guarantees capacity; never taken
+    ipxg_flow_record o = r;
+    o.end_reason = reason;
+    o.reserved0 = 0;
+    for (int k = 0; k < 24; ++k) o.reserved[k] = 0;
+    ex.buf[pos] = o;
+}
+
+__device__ __forceinline__ void reason_count(uint32_t* sc, uint8_t reason) {
+    atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
+}
+
+__device__ __forceinline__ void clear_slot(HotSlot* h, uint64_t key, uint32_t state) {
+    HotSlot z = {};
+    z.key = key;
+    z.state = state;
+    *h = z;
+}
+
+// ---- K3: finalize ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableView t, FragView f,
+                                                  ExportView ex, BatchCtl* ctl, unsigned long long* stats,
+                                                  uint32_t cap) {
+    __shared__ uint32_t sc[ST_COUNT];
+    __shared__ uint32_t cnt[4];  // keys, live, complex, exported
+    if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t keys = 0, live_n = 0, cx_n = 0, ex_n = 0;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        HotSlot h = t.hot[s];
+        bool do_export = false;
+        uint8_t reason = 0;
+        ipxg_flow_record er;
+        if (h.key != 0) {
+            keys++;
+            if (h.last1 == 0) {
+                if (h.state & SLOT_LIVE) live_n++;
+            } else {
+                const uint32_t first = ~h.first_n, last = h.last1 - 1;
+                const bool live = h.state & SLOT_LIVE;
+                ipxg_flow_record rec;
+                if (live) rec = t.cold[s];
+                DevPkt fp;
+                ipxg_pkt_desc df;
+                reparse<true>(b, p, f, first, fp, df);
+                const ipxg_pkt_desc dl = b.desc[last];
+                uint64_t lo, hf;
+                uint32_t cdf;
+                canon(fp, p, lo, cdf, hf);
+                const uint32_t I = p.inactive_s, A = p.active_s;
+                // the reference's checks at the batch's first packet (cache.cpp:431-472)
+                uint8_t bsplit = 0;
+                if (live) {
+                    const uint32_t creator = rec.reserved[0];
+                    const bool dsrc = p.split_biflow || cdf == creator;
+                    const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
+                    if ((fp.tcp_flags & 0x02) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
+                    else if ((int64_t)df.ts_sec - (int64_t)rec.time_last_sec >= (int64_t)I) bsplit = export_reason(rec);
+                    else if ((int64_t)df.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
+                }
+                const bool cont = live && !bsplit;
+                // could a split fall strictly inside the batch?
+                bool cx = p.force_complex != 0;
+                const uint64_t tb = h.tbits;
+                if (tb >> 63) cx = true;
+                else if (tb) {
+                    uint64_t x = tb >> __builtin_ctzll(tb);
+                    if (x & (x + 1)) cx = true;  // an empty bucket between two busy ones
+                }
+                const uint32_t tfirst = cont ? rec.time_first_sec : df.ts_sec;
+                if ((int64_t)dl.ts_sec - (int64_t)tfirst >= (int64_t)A) cx = true;
+                for (int dd = 0; dd < 2; ++dd) {
+                    if (!h.syn1[dd]) continue;
+                    const uint32_t sidx = h.syn1[dd] - 1;
+                    if (cont) {
+                        const uint8_t cf = (uint32_t)dd == rec.reserved[0] ? rec.src_tcp_flags : rec.dst_tcp_flags;
+                        if (cf & 0x05) cx = true;
+                    }
+                    if (h.fin_n[dd] && sidx > ~h.fin_n[dd]) cx = true;
+                }
+                if (cx) {
+                    t.hot[s].state = h.state | SLOT_COMPLEX;
+                    cx_n++;
+                } else {
+                    if (bsplit) {
+                        do_export = true;
+                        reason = bsplit;
+                        er = rec;
+                    }
+                    if (!cont) rec_create(rec, fp, df, hf, cdf);
+                    const uint32_t sd = rec.reserved[0];
+                    const uint64_t as = h.acc[sd], ad = h.acc[sd ^ 1];
+                    rec.src_packets += (uint32_t)(as >> 40);
+                    rec.src_bytes += as & ACC_BYTES_MASK;
+                    rec.dst_packets += (uint32_t)(ad >> 40);
+                    rec.dst_bytes += ad & ACC_BYTES_MASK;
+                    rec.src_tcp_flags |= (uint8_t)(h.tflags >> (8 * sd));
+                    rec.dst_tcp_flags |= (uint8_t)(h.tflags >> (8 * (sd ^ 1)));
+                    rec.time_last_sec = dl.ts_sec;
+                    rec.time_last_usec = dl.ts_usec;
+                    t.cold[s] = rec;
+                    clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+                    live_n++;
+                }
+            }
+        }
+        uint32_t pos = wave_append(ex.count, do_export);
+        if (do_export) {
+            store_export(ex, pos, er, reason);
+            reason_count(sc, reason);
+            ex_n++;
+        }
+    }
+    atomicAdd(&cnt[0], keys);
+    atomicAdd(&cnt[1], live_n);
+    atomicAdd(&cnt[2], cx_n);
+    atomicAdd(&cnt[3], ex_n);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (cnt[0]) atomicAdd(&ctl->keys, cnt[0]);
+        if (cnt[1]) atomicAdd(&ctl->live, cnt[1]);
+        if (cnt[2]) atomicAdd(&ctl->complex_count, cnt[2]);
+        if (cnt[3]) atomicAdd(&ctl->exported, cnt[3]);
+    }
+    flush_block_stats(sc, stats);
+}
+
+static inline uint32_t table_grid(uint32_t cap) {
+    uint32_t g = (cap + 255) / 256;
+    return g > 2048 ? 2048 : g;
+}
+
+void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                     ExportView ex, BatchCtl* ctl, unsigned long long* stats) {
+    const uint32_t cap = t.mask + 1;
+    hipLaunchKernelGGL(k_finalize, dim3(table_grid(cap)), dim3(256), 0, st, b, p, t, f, ex, ctl, stats, cap);
+}
+
+// ---- complex flows: sequential replay of put_pkt_recursive ------------------------------
+__global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView cx, BatchCtl* ctl,
+                                                      uint32_t cap) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        const HotSlot& h = t.hot[s];
+        if (h.key == 0 || !(h.state & SLOT_COMPLEX)) continue;
+        const uint32_t npk = (uint32_t)(h.acc[0] >> 40) + (uint32_t)(h.acc[1] >> 40);
+        unsigned long long old = atomicAdd((unsigned long long*)&ctl->cx_alloc, (1ull << 32) | npk);
+        const uint32_t r = (uint32_t)(old >> 32);
+        t.slot_rank[s] = r;
+        cx.slot_of[r] = s;
+        cx.seg[r] = (uint32_t)old;
+        cx.len[r] = npk;
+        cx.cursor[r] = 0;
+    }
+}
+
+void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap) {
+    hipLaunchKernelGGL(k_complex_rank, dim3(table_grid(cap)), dim3(256), 0, st, t, cx, ctl, cap);
+}
+
+__global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, TableView t, FragView f,
+                                                     ComplexView cx, uint32_t nranks, ExportView ex,
+                                                     BatchCtl* ctl, unsigned long long* stats) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nranks) return;
+    const uint32_t s = cx.slot_of[r];
+    const HotSlot h = t.hot[s];
+    bool live = h.state & SLOT_LIVE;
+    ipxg_flow_record rec;
+    if (live) rec = t.cold[s];
+    const uint32_t seg = cx.seg[r], len = cx.len[r];
+    const uint32_t I = p.inactive_s, A = p.active_s;
+    uint32_t n_ex = 0;
+    for (uint32_t k = 0; k < len; ++k) {
+        const uint32_t idx = (uint32_t)(cx.sorted[seg + k] & 0xFFFFFF);
+        DevPkt pk;
+        ipxg_pkt_desc d;
+        reparse<true>(b, p, f, idx, pk, d);
+        uint64_t lo, hf;
+        uint32_t cdir;
+        canon(pk, p, lo, cdir, hf);
+        bool dsrc = true;
+        if (live) {  // cache.cpp:428-472
+            dsrc = p.split_biflow || cdir == rec.reserved[0];
+            const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
+            uint8_t reason = 0;
+            if ((pk.tcp_flags & 0x02) && (flw & 0x05)) reason = IPXG_FLOW_END_EOF;
+            else if ((int64_t)d.ts_sec - (int64_t)rec.time_last_sec >= (int64_t)I) reason = export_reason(rec);
+            else if ((int64_t)d.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) reason = IPXG_FLOW_END_ACTIVE;
+            if (reason) {
+                uint32_t pos = atomicAdd(ex.count, 1u);
+                store_export(ex, pos, rec, reason);
+                atomicAdd(&stats[ST_END_INACTIVE + reason - 1], 1ull);
+                n_ex++;
+                live = false;
+            }
+        }
+        if (!live) {
+            rec_create(rec, pk, d, hf, cdir);
+            rec.src_packets = 1;
+            rec.src_bytes = pk.ip_len;
+            if (pk.ip_proto == 6) rec.src_tcp_flags = pk.tcp_flags;
+            live = true;
+        } else {
+            rec.time_last_sec = d.ts_sec;
+            rec.time_last_usec = d.ts_usec;
+            if (dsrc) {
+                rec.src_packets++;
+                rec.src_bytes += pk.ip_len;
+                if (pk.ip_proto == 6) rec.src_tcp_flags |= pk.tcp_flags;
+            } else {
+                rec.dst_packets++;
+                rec.dst_bytes += pk.ip_len;
+                if (pk.ip_proto == 6) rec.dst_tcp_flags |= pk.tcp_flags;
+            }
+        }
+    }
+    t.cold[s] = rec;
+    clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+    if (n_ex) atomicAdd(&ctl->exported, n_ex);
+}
+
+void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                         ComplexView cx, uint32_t nranks, ExportView ex, BatchCtl* ctl,
+                         unsigned long long* stats) {
+    hipLaunchKernelGGL(k_complex_walk, dim3((nranks + 63) / 64), dim3(64), 0, st, b, p, t, f, cx, nranks,
+                       ex, ctl, stats);
+}
+
+// ---- maintenance: export_expired / finish / rehash / count ------------------------------
+__global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t cap, int64_t now,
+                                                ExportView ex, unsigned long long* stats) {
+    __shared__ uint32_t sc[ST_COUNT];
+    if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        const HotSlot& h = t.hot[s];
+        bool do_export = false;
+        uint8_t reason = 0;
+        ipxg_flow_record rec;
+        if (h.key != 0 && (h.state & SLOT_LIVE)) {
+            rec = t.cold[s];
+            if (now - (int64_t)rec.time_last_sec >= (int64_t)p.inactive_s) {
+                do_export = true;
+                reason = export_reason(rec);
+                t.hot[s].state = h.state & ~SLOT_LIVE;
+            }
+        }
+        uint32_t pos = wave_append(ex.count, do_export);
+        if (do_export) {
+            store_export(ex, pos, rec, reason);
+            reason_count(sc, reason);
+        }
+    }
+    flush_block_stats(sc, stats);
+}
+
+void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
+                   ExportView ex, unsigned long long* stats) {
+    hipLaunchKernelGGL(k_expire, dim3(table_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats);
+}
+
+__global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
+                                                unsigned long long* stats) {
+    __shared__ uint32_t sc[ST_COUNT];
+    if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        const HotSlot& h = t.hot[s];
+        const bool do_export = h.key != 0 && (h.state & SLOT_LIVE);
+        uint32_t pos = wave_append(ex.count, do_export);
+        if (do_export) {
+            store_export(ex, pos, t.cold[s], IPXG_FLOW_END_FORCED);
+            reason_count(sc, IPXG_FLOW_END_FORCED);
+        }
+    }
+    flush_block_stats(sc, stats);
+}
+
+void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats) {
+    hipLaunchKernelGGL(k_finish, dim3(table_grid(cap)), dim3(256), 0, st, t, cap, ex, stats);
+}
+
+__global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_cap, TableView to,
+                                                uint32_t* fail) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < from_cap; s += gridDim.x * blockDim.x) {
+        const HotSlot h = from.hot[s];
+        if (h.key == 0) continue;
+        if (!(h.state & (SLOT_LIVE | SLOT_COMPLEX)) && h.last1 == 0) continue;  // dead slot
+        uint32_t ns = (uint32_t)h.key & to.mask;
+        bool ok = false;
+        for (uint32_t probe = 0; probe <= to.mask; ++probe) {
+            unsigned long long old = atomicCAS((unsigned long long*)&to.hot[ns].key, 0ull,
+                                               (unsigned long long)h.key);
+            if (old == 0) {
+                ok = true;
+                break;
+            }
+            ns = (ns + 1) & to.mask;
+        }
+        if (!ok) {
+            atomicAdd(fail, 1u);
+            continue;
+        }
+        HotSlot c = h;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&to.hot[ns]);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&c);
+        for (int k = 2; k < 16; ++k) dst[k] = src[k];  // key already claimed
+        to.cold[ns] = from.cold[s];
+    }
+}
+
+void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail) {
+    hipLaunchKernelGGL(k_rehash, dim3(table_grid(from_cap)), dim3(256), 0, st, from, from_cap, to, fail);
+}
+
+__global__ __launch_bounds__(256) void k_count(TableView t, uint32_t cap, BatchCtl* ctl) {
+    uint32_t keys = 0, live = 0;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        const HotSlot& h = t.hot[s];
+        if (h.key) {
+            keys++;
+            if (h.state & SLOT_LIVE) live++;
+        }
+    }
+    if (keys) atomicAdd(&ctl->keys, keys);
+    if (live) atomicAdd(&ctl->live, live);
+}
+
+void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl) {
+    hipLaunchKernelGGL(k_count, dim3(table_grid(cap)), dim3(256), 0, st, t, cap, ctl);
+}
+
+// ---- stateless entry points ------------------------------------------------------------------
+__global__ __launch_bounds__(IPXG_BLOCK) void k_parse_batch(BatchView b, uint32_t dlt, ipxg_parsed_pkt* out) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    const uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x;
+    if (i >= b.n) return;
+    const ipxg_pkt_desc d = b.desc[i];
+    uint32_t* col = &win[threadIdx.x];
+    stage_frame(col, b.arena, d.offset, d.caplen);
+    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    DevPkt pk;
+    ParseCounts c = {};
+    ipxg_parsed_pkt o;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+    for (int k = 0; k < (int)(sizeof(o) / 4); ++k) ow[k] = 0;
+    const bool ok = parse_frame<true>(S, d.caplen, dlt, pk, c);
+    o.valid = ok;
+    o.ip_version = pk.ip_version;
+    o.ip_proto = pk.ip_proto;
+    o.tcp_flags = pk.tcp_flags;
+    o.ethertype = pk.ethertype;
+    o.ip_len = pk.ip_len;
+    o.src_port = pk.src_port;
+    o.dst_port = pk.dst_port;
+    o.frag_off = pk.frag_off;
+    o.more_fragments = pk.more_fragments;
+    o.ip_ttl = pk.ip_ttl;
+    o.vlan_id = pk.vlan_id;
+    o.frag_id = pk.frag_id;
+    o.mpls_top = pk.mpls_top;
+    o.tcp_mss = pk.tcp_mss;
+    o.tcp_options = pk.tcp_options;
+    for (int k = 0; k < 4; ++k)
+        for (int q = 0; q < 4; ++q) {
+            o.src_ip[4 * k + q] = (uint8_t)(pk.sip[k] >> (8 * q));
+            o.dst_ip[4 * k + q] = (uint8_t)(pk.dip[k] >> (8 * q));
+        }
+    const uint32_t m[3] = {pk.mac_lo, pk.mac_mid, pk.mac_hi};
+    for (int q = 0; q < 6; ++q) {
+        o.dst_mac[q] = (uint8_t)(m[q >> 2] >> (8 * (q & 3)));
+        o.src_mac[q] = (uint8_t)(m[(q + 6) >> 2] >> (8 * ((q + 6) & 3)));
+    }
+    o.ip_tos = pk.ip_tos;
+    o.ip_flags = pk.ip_flags;
+    o.tcp_window = pk.tcp_window;
+    o.tcp_seq = pk.tcp_seq;
+    o.tcp_ack = pk.tcp_ack;
+    if (ok && (pk.ip_version == 4 || pk.ip_version == 6)) {
+        FlowKey kf, ki;
+        build_keys(pk, kf, ki);
+        o.hash_fwd = key_hash(kf);
+        o.hash_inv = key_hash(ki);
+    }
+    out[i] = o;
+}
+
+void launch_parse_batch(hipStream_t st, const BatchView& b, uint32_t dlt, ipxg_parsed_pkt* out) {
+    hipLaunchKernelGGL(k_parse_batch, dim3((b.n + IPXG_BLOCK - 1) / IPXG_BLOCK), dim3(IPXG_BLOCK), 0, st, b,
+                       dlt, out);
+}
+
+__global__ __launch_bounds__(256) void k_xxh64(const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
+                                               uint64_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* k = keys + (size_t)i * keylen;
+    if (seed == 0 && keylen == 16) {
+        uint64_t w0 = 0, w1 = 0;
+        for (int q = 7; q >= 0; --q) {
+            w0 = (w0 << 8) | k[q];
+            w1 = (w1 << 8) | k[8 + q];
+        }
+        out[i] = xxh64_16(w0, w1);
+    } else if (seed == 0 && keylen == 40) {
+        uint64_t w[5] = {0, 0, 0, 0, 0};
+        for (int j = 0; j < 5; ++j)
+            for (int q = 7; q >= 0; --q) w[j] = (w[j] << 8) | k[8 * j + q];
+        out[i] = xxh64_40(w[0], w[1], w[2], w[3], w[4]);
+    } else {
+        out[i] = xxh64_any(k, keylen, seed);
+    }
+}
+
+void launch_xxh64(hipStream_t st, const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
+                  uint64_t* out) {
+    hipLaunchKernelGGL(k_xxh64, dim3((n + 255) / 256), dim3(256), 0, st, keys, keylen, n, seed, out);
+}
+
+}  // namespace ipxg

@@ -1,0 +1,143 @@
+// ipxg_kernels.hpp -- device data layout shared by the kernels and the host engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ipxg.h"
+
+namespace ipxg {
+
+// One flow-table slot's hot half: the 64-byte line every packet of the flow touches.
+// All-zero == empty and "no packets this batch", so the table is cleared by a memset.
+// Per-batch accumulators are folded into the cold record by k_finalize and re-zeroed.
+struct alignas(64) HotSlot {
+    uint64_t key;      // 0  canonical flow hash: min(XXH64(key), XXH64(key_inv)); 0 = empty
+    uint32_t first_n;  // 8  ~(first packet index in this batch), max-reduced; 0 = none
+    uint32_t last1;    // 12 last packet index in this batch + 1, max-reduced; 0 = untouched
+    uint64_t tbits;    // 16 occupancy of (inactive/2)-second buckets since the batch start
+    uint64_t acc[2];   // 24 per canonical direction: packets << 40 | IP bytes
+    uint32_t tflags;   // 40 OR of TCP flags, canonical dir 0 in bits 0-7, dir 1 in bits 8-15
+    uint32_t fin_n[2]; // 44 ~(first FIN|RST packet index) per direction, max-reduced
+    uint32_t syn1[2];  // 52 last SYN packet index + 1 per direction, max-reduced
+    uint32_t state;    // 60 SLOT_LIVE | SLOT_COMPLEX
+};
+static_assert(sizeof(HotSlot) == 64, "hot slot must be one 64-byte line");
+
+constexpr uint32_t SLOT_LIVE = 1u, SLOT_COMPLEX = 2u;
+constexpr uint64_t ACC_BYTES_MASK = (1ull << 40) - 1;
+constexpr uint32_t MAX_PROBE = 64;
+
+// Per-batch control block, zeroed before every batch.
+struct BatchCtl {
+    uint32_t nonmono;        // a packet's timestamp went backwards
+    uint32_t frag_count;     // fragments routed to the fragmentation-cache path
+    uint32_t deferred;       // packets whose table probe exceeded MAX_PROBE
+    uint32_t complex_count;  // flows k_finalize handed to the sequential path
+    uint64_t cx_alloc;       // (rank << 32) | packets, complex-flow segment allocator
+    uint32_t keys;           // non-empty slots after k_finalize
+    uint32_t live;           // live records after k_finalize
+    uint32_t last_sec, last_usec;  // timestamp of the batch's last packet
+    uint32_t exported;       // records exported while applying this batch
+    uint32_t pad[5];
+};
+
+// Fragmentation-cache ring entry (fragmentationKeyData.hpp:49-112), 4 per bucket.
+struct FragEntry {
+    uint64_t kw[5];  // the 40-byte FragmentationKey as little-endian words
+    uint16_t sport, dport;
+    uint32_t sec, usec;
+    uint32_t pad[3];
+};
+static_assert(sizeof(FragEntry) == 64, "");
+
+// Device statistics, sharded to spread the per-block atomics.
+constexpr int STAT_SHARDS = 16;
+enum StatIdx {
+    ST_SEEN, ST_PARSED, ST_UNKNOWN, ST_IPV4, ST_IPV6, ST_TCP, ST_UDP, ST_MPLS, ST_PPPOE, ST_TRILL,
+    ST_VLAN, ST_IPV4_BYTES, ST_IPV6_BYTES, ST_KEYLESS, ST_FRAGMENTED, ST_FRAG_FILLED,
+    ST_END_INACTIVE, ST_END_ACTIVE, ST_END_EOF, ST_END_FORCED, ST_END_NO_RES, ST_COUNT
+};
+
+// Everything a kernel needs about the engine, passed by value.
+struct TableView {
+    HotSlot* hot;
+    ipxg_flow_record* cold;
+    uint32_t* slot_rank;
+    uint32_t mask;  // capacity - 1
+};
+
+struct ExportView {
+    ipxg_flow_record* buf;
+    uint32_t* count;
+    uint32_t cap;
+};
+
+struct Params {
+    uint32_t dlt;
+    uint32_t active_s, inactive_s;
+    uint32_t bucket_w;       // seconds per tbits bucket = inactive/2
+    uint32_t split_biflow;
+    uint32_t frag_enable;
+    uint32_t frag_size, frag_timeout_s;
+    uint32_t force_complex;  // route every touched flow to the sequential path
+    uint32_t prev_valid;     // prev_sec/prev_usec hold the previous batch's last timestamp
+    uint32_t prev_sec, prev_usec;
+};
+
+struct BatchView {
+    const uint8_t* arena;
+    const ipxg_pkt_desc* desc;
+    uint32_t n;
+    uint32_t base_sec;  // tbits bucket origin (first packet's seconds), or BASE_FROM_DESC0
+};
+constexpr uint32_t BASE_FROM_DESC0 = 0xFFFFFFFFu;
+
+struct FragView {
+    FragEntry* ent;      // frag_size * 4
+    uint32_t* cnt;       // frag_size
+    uint64_t* list;      // (bucket << 24) | packet index, frag_count entries
+    uint64_t* sorted;
+    uint32_t* ports;     // per packet index: resolved (sport << 16) | dport
+};
+
+struct ComplexView {
+    uint64_t* list;      // (rank << 24) | packet index
+    uint64_t* sorted;
+    uint32_t* cursor;    // per rank
+    uint32_t* slot_of;   // per rank
+    uint32_t* seg;       // per rank: segment start
+    uint32_t* len;       // per rank: packets
+};
+
+// ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
+void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                   BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
+void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,
+                      unsigned long long* stats);
+void launch_frag_accumulate(hipStream_t st, const BatchView& b, const Params& p, TableView t,
+                            FragView f, uint32_t nfrag, BatchCtl* ctl, uint32_t* deferred_list);
+void launch_deferred(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                     const uint32_t* in_list, uint32_t n_in, BatchCtl* ctl, uint32_t* out_list);
+void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                     ExportView ex, BatchCtl* ctl, unsigned long long* stats);
+void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap);
+void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t,
+                           FragView f, ComplexView cx);
+void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                         ComplexView cx, uint32_t nranks, ExportView ex, BatchCtl* ctl,
+                         unsigned long long* stats);
+void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
+                   ExportView ex, unsigned long long* stats);
+void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats);
+void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail);
+void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl);
+void launch_parse_batch(hipStream_t st, const BatchView& b, uint32_t dlt, ipxg_parsed_pkt* out);
+void launch_xxh64(hipStream_t st, const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
+                  uint64_t* out);
+
+// rocPRIM radix sort of 64-bit keys (slow paths only).  temp may be null to query size.
+hipError_t sort_keys_u64(void* temp, size_t& temp_bytes, const uint64_t* in, uint64_t* out,
+                         uint32_t n, int end_bit, hipStream_t st);
+
+}  // namespace ipxg

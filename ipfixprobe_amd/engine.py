@@ -1,0 +1,307 @@
+"""ctypes bindings of libipxg (include/ipxg.h) for the tests and bench.py.
+
+The product surface above the C-ABI is C++ (ipfixprobe_amd/host: the GpuFlowCache storage
+plugin and the ipxg_probe tool).  This module is plumbing: it loads the in-tree
+libipxg.so -- and fails loudly if it is missing or no GPU is present; there is no CPU
+fallback anywhere in the product path.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libipxg.so")
+
+DLT_EN10MB, DLT_RAW, DLT_LINUX_SLL, DLT_LINUX_SLL2 = 1, 12, 113, 276
+BATCH_DEVICE = 0x1
+MAX_BATCH = 16 * 1024 * 1024 - 1
+
+DESC_DTYPE = np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"),
+                       ("ts_sec", "<u4"), ("ts_usec", "<u4")])
+FLOW_DTYPE = np.dtype([
+    ("flow_hash", "<u8"),
+    ("time_first_sec", "<u4"), ("time_first_usec", "<u4"),
+    ("time_last_sec", "<u4"), ("time_last_usec", "<u4"),
+    ("src_bytes", "<u8"), ("dst_bytes", "<u8"),
+    ("src_packets", "<u4"), ("dst_packets", "<u4"),
+    ("src_tcp_flags", "u1"), ("dst_tcp_flags", "u1"), ("ip_version", "u1"), ("ip_proto", "u1"),
+    ("src_port", "<u2"), ("dst_port", "<u2"),
+    ("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,)),
+    ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)),
+    ("vlan_id", "<u2"), ("end_reason", "u1"), ("reserved0", "u1"), ("reserved", "u1", (24,)),
+])
+PARSED_DTYPE = np.dtype([
+    ("valid", "u1"), ("ip_version", "u1"), ("ip_proto", "u1"), ("tcp_flags", "u1"),
+    ("ethertype", "<u2"), ("ip_len", "<u2"), ("src_port", "<u2"), ("dst_port", "<u2"),
+    ("frag_off", "<u2"), ("more_fragments", "u1"), ("ip_ttl", "u1"),
+    ("vlan_id", "<u4"), ("frag_id", "<u4"), ("mpls_top", "<u4"), ("tcp_mss", "<u4"),
+    ("tcp_options", "<u8"),
+    ("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,)),
+    ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)),
+    ("ip_tos", "u1"), ("ip_flags", "u1"), ("tcp_window", "<u2"),
+    ("tcp_seq", "<u4"), ("tcp_ack", "<u4"),
+    ("hash_fwd", "<u8"), ("hash_inv", "<u8"),
+])
+STATS_FIELDS = [
+    "seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",
+    "tcp_packets", "udp_packets", "mpls_packets", "pppoe_packets", "trill_packets",
+    "vlan_packets", "ipv4_bytes", "ipv6_bytes", "end_inactive", "end_active", "end_eof",
+    "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
+    "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
+    "table_rehashes", "batches",
+]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "cache_exp", "line_exp", "active_s", "inactive_s", "split_biflow", "frag_enable",
+        "frag_size", "frag_timeout_s")] + [("device_id", ctypes.c_int32)] + \
+        [(n, ctypes.c_uint32) for n in ("batch_pkts", "datalink", "reserved")]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("arena_len", ctypes.c_uint64),
+                ("desc", ctypes.c_void_p), ("n", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ("ingest_ms", "finalize_ms", "slow_ms", "finish_ms")] + \
+        [(n, ctypes.c_uint64) for n in ("ingest_launches", "finalize_launches", "slow_launches",
+                                        "finish_launches", "ingest_packets")]
+
+
+class Capture(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("arena_len", ctypes.c_uint64),
+                ("desc", ctypes.c_void_p), ("n", ctypes.c_uint32), ("datalink", ctypes.c_uint32)]
+
+
+EXPORTED_SYMBOLS = [
+    "ipxg_config_default", "ipxg_config_parse", "ipxg_create", "ipxg_destroy",
+    "ipxg_last_error", "ipxg_stream", "ipxg_submit", "ipxg_expire", "ipxg_finish",
+    "ipxg_reset", "ipxg_pending_exports", "ipxg_poll_exports", "ipxg_device_exports",
+    "ipxg_clear_exports", "ipxg_get_stats", "ipxg_parse_batch", "ipxg_xxh64_batch",
+    "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
+]
+
+_LIB = None
+
+
+class IpxgError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the in-tree libipxg.so.  Raises if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise IpxgError("libipxg.so not built (%s): run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
+        L.ipxg_config_default.argtypes = [ctypes.POINTER(Config)]
+        L.ipxg_config_parse.argtypes = [ctypes.c_char_p, ctypes.POINTER(Config)]
+        L.ipxg_create.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(vp)]
+        L.ipxg_destroy.argtypes = [vp]
+        L.ipxg_last_error.argtypes = [vp]
+        L.ipxg_last_error.restype = ctypes.c_char_p
+        L.ipxg_stream.argtypes = [vp]
+        L.ipxg_stream.restype = vp
+        L.ipxg_submit.argtypes = [vp, ctypes.POINTER(Batch)]
+        L.ipxg_expire.argtypes = [vp, ctypes.c_int64]
+        L.ipxg_finish.argtypes = [vp]
+        L.ipxg_reset.argtypes = [vp]
+        L.ipxg_pending_exports.argtypes = [vp, ctypes.POINTER(sz)]
+        L.ipxg_poll_exports.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+        L.ipxg_device_exports.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.ipxg_clear_exports.argtypes = [vp]
+        L.ipxg_get_stats.argtypes = [vp, vp]
+        L.ipxg_parse_batch.argtypes = [vp, ctypes.POINTER(Batch), vp]
+        L.ipxg_xxh64_batch.argtypes = [vp, vp, u32, u32, ctypes.c_uint64, vp]
+        L.ipxg_capture_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(Capture))]
+        L.ipxg_capture_free.argtypes = [ctypes.POINTER(Capture)]
+        L.ipxg_profile.argtypes = [vp, ctypes.c_int]
+        L.ipxg_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
+        for name in EXPORTED_SYMBOLS:
+            if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default",
+                            "ipxg_capture_free"):
+                getattr(L, name).restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def make_config(params: str = "", **kw) -> Config:
+    """Reference defaults, then the cache option string, then keyword overrides."""
+    cfg = Config()
+    lib().ipxg_config_default(ctypes.byref(cfg))
+    if params:
+        rc = lib().ipxg_config_parse(params.encode(), ctypes.byref(cfg))
+        if rc:
+            raise IpxgError("invalid option string %r (rc %d)" % (params, rc))
+    for k, v in kw.items():
+        setattr(cfg, k, int(v))
+    return cfg
+
+
+def load_capture(path):
+    """pcap/pcapng -> (arena uint8 ndarray, desc DESC_DTYPE ndarray, datalink) via libipxg."""
+    p = ctypes.POINTER(Capture)()
+    rc = lib().ipxg_capture_load(os.fsencode(path), ctypes.byref(p))
+    if rc:
+        raise IpxgError("ipxg_capture_load(%s) failed: %d" % (path, rc))
+    c = p.contents
+    try:
+        arena = np.ctypeslib.as_array(ctypes.cast(c.arena, ctypes.POINTER(ctypes.c_uint8)),
+                                      shape=(c.arena_len,)).copy()
+        if c.n:
+            raw = np.ctypeslib.as_array(ctypes.cast(c.desc, ctypes.POINTER(ctypes.c_uint8)),
+                                        shape=(c.n * 16,)).copy()
+            desc = raw.view(DESC_DTYPE)
+        else:
+            desc = np.zeros(0, dtype=DESC_DTYPE)
+        return arena, desc, int(c.datalink)
+    finally:
+        lib().ipxg_capture_free(p)
+
+
+class Engine:
+    """One ipxg engine (one HIP stream on one device) -- the StoragePlugin-shaped lifecycle:
+    submit = put_pkt for a whole batch, expire = export_expired, finish = finish."""
+
+    def __init__(self, params: str = "", **kw):
+        self.cfg = make_config(params, **kw)
+        h = ctypes.c_void_p()
+        rc = lib().ipxg_create(ctypes.byref(self.cfg), ctypes.byref(h))
+        if rc:
+            raise IpxgError("ipxg_create failed (rc %d): no usable HIP device?" % rc)
+        self._h = h
+
+    def _check(self, rc, what):
+        if rc:
+            msg = lib().ipxg_last_error(self._h).decode(errors="replace")
+            raise IpxgError("%s failed (rc %d): %s" % (what, rc, msg))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stream(self):
+        return lib().ipxg_stream(self._h)
+
+    @staticmethod
+    def _batch(arena, desc, device=False):
+        b = Batch()
+        if device:  # torch tensors on cuda
+            b.arena = arena.data_ptr()
+            b.arena_len = arena.numel() * arena.element_size()
+            b.desc = desc.data_ptr()
+            b.n = desc.numel() * desc.element_size() // 16
+            b.flags = BATCH_DEVICE
+        else:
+            arena = np.ascontiguousarray(arena, dtype=np.uint8)
+            desc = np.ascontiguousarray(desc)
+            b.arena = arena.ctypes.data
+            b.arena_len = arena.nbytes
+            b.desc = desc.ctypes.data
+            b.n = len(desc)
+            b.flags = 0
+            b._keep = (arena, desc)
+        return b
+
+    def submit(self, arena, desc, device=False):
+        b = self._batch(arena, desc, device)
+        self._check(lib().ipxg_submit(self._h, ctypes.byref(b)), "ipxg_submit")
+
+    def submit_all(self, arena, desc, batch=None):
+        """Host capture in arrival order, cut into batches of at most `batch` packets."""
+        batch = batch or int(self.cfg.batch_pkts)
+        for s in range(0, len(desc), batch):
+            self.submit(arena, desc[s:s + batch])
+
+    def expire(self, now_sec):
+        self._check(lib().ipxg_expire(self._h, int(now_sec)), "ipxg_expire")
+
+    def finish(self):
+        self._check(lib().ipxg_finish(self._h), "ipxg_finish")
+
+    def reset(self):
+        self._check(lib().ipxg_reset(self._h), "ipxg_reset")
+
+    def pending(self):
+        n = ctypes.c_size_t()
+        self._check(lib().ipxg_pending_exports(self._h, ctypes.byref(n)), "ipxg_pending_exports")
+        return n.value
+
+    def poll(self):
+        n = self.pending()
+        out = np.zeros(n, dtype=FLOW_DTYPE)
+        got = ctypes.c_size_t()
+        self._check(lib().ipxg_poll_exports(self._h, out.ctypes.data if n else None, n,
+                                            ctypes.byref(got)), "ipxg_poll_exports")
+        return out[:got.value]
+
+    def device_exports(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._check(lib().ipxg_device_exports(self._h, ctypes.byref(p), ctypes.byref(n)),
+                    "ipxg_device_exports")
+        return p.value, n.value
+
+    def clear_exports(self):
+        self._check(lib().ipxg_clear_exports(self._h), "ipxg_clear_exports")
+
+    def stats(self):
+        arr = (ctypes.c_uint64 * len(STATS_FIELDS))()
+        self._check(lib().ipxg_get_stats(self._h, arr), "ipxg_get_stats")
+        return dict(zip(STATS_FIELDS, list(arr)))
+
+    def profile(self, enable=True):
+        self._check(lib().ipxg_profile(self._h, int(enable)), "ipxg_profile")
+
+    def timing(self):
+        t = Timing()
+        self._check(lib().ipxg_get_timing(self._h, ctypes.byref(t)), "ipxg_get_timing")
+        return {f: getattr(t, f) for f, _ in Timing._fields_}
+
+    def parse(self, arena, desc):
+        b = self._batch(arena, desc)
+        out = np.zeros(b.n, dtype=PARSED_DTYPE)
+        self._check(lib().ipxg_parse_batch(self._h, ctypes.byref(b), out.ctypes.data),
+                    "ipxg_parse_batch")
+        return out
+
+    def xxh64(self, keys: np.ndarray, keylen: int, seed: int = 0):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        n = keys.size // keylen if keylen else len(keys)
+        out = np.zeros(n, dtype=np.uint64)
+        self._check(lib().ipxg_xxh64_batch(self._h, keys.ctypes.data, keylen, n, seed,
+                                           out.ctypes.data), "ipxg_xxh64_batch")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ipxg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def run_capture(arena, desc, datalink=DLT_EN10MB, params="", batch=None, finish=True, **kw):
+    """Whole capture through the engine, returns (records, stats)."""
+    with Engine(params, datalink=datalink, **kw) as e:
+        e.submit_all(arena, desc, batch)
+        if finish:
+            e.finish()
+        recs = e.poll()
+        st = e.stats()
+    return recs, st

@@ -1,0 +1,127 @@
+// ipxg_probe -- minimal pipeline driver: pcap/pcapng file -> gpucache -> flow records.
+//
+//   ipxg_probe -i FILE [-s "s=20;a=300;i=30;..."] [-o csv|unirec] [-q BLOCK]
+//
+// The input side mirrors ipfixprobe's pcap plugin + input_storage_worker
+// (workers.cpp:40-140): packets are read in arrival order and handed to the storage plugin
+// one by one (put_pkt); at end of file the storage is finished (workers.cpp:136).  Output is
+// the basic biflow columns in the text form of the reference's functional tests (UniRec
+// logger, tests/functional/scripts/run_test.sh), one line per exported flow.
+#include <arpa/inet.h>
+#include <sys/time.h>
+#include <time.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "gpucache.hpp"
+
+namespace {
+
+struct CsvSink : ipxp::ExportSink {
+    FILE* f;
+    bool vlan;
+    size_t n = 0;
+    explicit CsvSink(FILE* out, bool with_vlan) : f(out), vlan(with_vlan) {}
+    static std::string ip(const uint8_t* a, int ver) {
+        char b[INET6_ADDRSTRLEN];
+        inet_ntop(ver == 4 ? AF_INET : AF_INET6, a, b, sizeof(b));
+        return b;
+    }
+    static std::string mac(const uint8_t* m) {
+        char b[32];
+        snprintf(b, sizeof(b), "%02x:%02x:%02x:%02x:%02x:%02x", m[0], m[1], m[2], m[3], m[4], m[5]);
+        return b;
+    }
+    static std::string tm(uint32_t s, uint32_t us) {
+        time_t t = s;
+        struct tm g;
+        gmtime_r(&t, &g);
+        char b[64];
+        strftime(b, sizeof(b), "%Y-%m-%dT%H:%M:%S", &g);
+        char o[80];
+        snprintf(o, sizeof(o), "%s.%06u", b, us);
+        return o;
+    }
+    void push(const ipxg_flow_record& r) override {
+        n++;
+        fprintf(f, "%s,%s,%llu,%llu,0,%s,%s,%s,%s,%u,%u,%u,%u,", ip(r.dst_ip, r.ip_version).c_str(),
+                ip(r.src_ip, r.ip_version).c_str(), (unsigned long long)r.src_bytes, (unsigned long long)r.dst_bytes,
+                tm(r.time_first_sec, r.time_first_usec).c_str(), tm(r.time_last_sec, r.time_last_usec).c_str(),
+                mac(r.dst_mac).c_str(), mac(r.src_mac).c_str(), r.src_packets, r.dst_packets, r.dst_port, r.src_port);
+        if (vlan) fprintf(f, "%u,", r.vlan_id);
+        fprintf(f, "0,%u,%u,%u\n", r.ip_proto, r.src_tcp_flags, r.dst_tcp_flags);
+    }
+};
+
+void usage() {
+    fprintf(stderr, "usage: ipxg_probe -i FILE [-s CACHE_OPTIONS] [-o csv|csv-vlan] [--stats]\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string in, opts, fmt = "csv";
+    bool stats = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        if (a == "-i" && i + 1 < argc) in = argv[++i];
+        else if (a == "-s" && i + 1 < argc) opts = argv[++i];
+        else if (a == "-o" && i + 1 < argc) fmt = argv[++i];
+        else if (a == "--stats") stats = true;
+        else {
+            usage();
+            return 2;
+        }
+    }
+    if (in.empty()) {
+        usage();
+        return 2;
+    }
+    ipxg_capture* cap = nullptr;
+    int rc = ipxg_capture_load(in.c_str(), &cap);
+    if (rc) {
+        fprintf(stderr, "ipxg_probe: cannot read %s (%d)\n", in.c_str(), rc);
+        return 1;
+    }
+    // the capture's link type, unless the option string names one
+    ipxg_config probe_cfg;
+    ipxg_config_default(&probe_cfg);
+    probe_cfg.datalink = 0;
+    if (ipxg_config_parse(opts.c_str(), &probe_cfg) != IPXG_OK) {
+        fprintf(stderr, "ipxg_probe: invalid option string\n");
+        return 2;
+    }
+    if (probe_cfg.datalink == 0) opts += (opts.empty() ? "" : ";") + std::string("dlt=") + std::to_string(cap->datalink);
+    CsvSink sink(stdout, fmt == "csv-vlan");
+    try {
+        ipxp::GpuFlowCache cache(opts, &sink);
+        for (uint32_t i = 0; i < cap->n; ++i) {
+            const ipxg_pkt_desc& d = cap->desc[i];
+            ipxp::RawPacket p;
+            p.ts.tv_sec = d.ts_sec;
+            p.ts.tv_usec = d.ts_usec;
+            p.packet = cap->arena + d.offset;
+            p.packet_len = d.caplen;
+            p.packet_len_wire = d.wirelen;
+            cache.put_pkt(p);
+        }
+        cache.finish();
+        if (stats) {
+            ipxg_stats s = cache.stats();
+            fprintf(stderr, "packets seen %llu parsed %llu flows exported %llu (forced %llu, inactive %llu, "
+                    "active %llu, eof %llu)\n",
+                    (unsigned long long)s.seen_packets, (unsigned long long)s.parsed_packets,
+                    (unsigned long long)s.total_exported, (unsigned long long)s.end_forced,
+                    (unsigned long long)s.end_inactive, (unsigned long long)s.end_active,
+                    (unsigned long long)s.end_eof);
+        }
+    } catch (const ipxp::PluginError& e) {
+        fprintf(stderr, "ipxg_probe: %s\n", e.what());
+        ipxg_capture_free(cap);
+        return 1;
+    }
+    ipxg_capture_free(cap);
+    return 0;
+}
