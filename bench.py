@@ -209,7 +209,7 @@ def main():
     flows = gen_flows(args.flows, rank, world, args.seed)
     frames, desc = build_batch(flows, args.packets, args.seed + rank, device)
     torch.cuda.synchronize()
-    eng = Engine("s=20", device_id=local)
+    eng = Engine("s=%d" % max(16, int(math.ceil(math.log2(4 * args.flows)))), device_id=local)
 
     def step():
         eng.submit(frames, desc, device=True)

@@ -23,6 +23,7 @@
 #define IPXG_WIN 128          // header bytes staged in LDS per packet (B_pkt)
 #define IPXG_WIN_DW (IPXG_WIN / 4)
 #define IPXG_MAX_L3_HOPS 64   // bound on the GRE/MPLS/PPPoE header chain (reference: recursion)
+#define IPXG_MAX_EXT_STEPS 4096  // bound on the IPv6 extension-header walk (reference: may not return)
 
 namespace ipxg {
 
@@ -269,8 +270,9 @@ __device__ __forceinline__ uint32_t parse_ipv6(const S& s, uint32_t base, uint32
         const uint32_t eb = base + 40;
         const uint32_t dl = (data_len - 40) & 0xFFFF;
         uint32_t ext = eb, next_hdr = proto, hdrs_len = 0;
-        for (;;) {
+        for (int step = 0;; ++step) {
             if (hdrs_len > dl || 2u > dl - hdrs_len) { err = true; return 0; }
+            if (step >= IPXG_MAX_EXT_STEPS) { err = true; return 0; }  // AH +2/-2 cycle, see oracle
             if (next_hdr == 0 || next_hdr == 60) {
                 hdrs_len += (rd8(s, ext + 1) << 3) + 8;
             } else if (next_hdr == 43) {
@@ -312,7 +314,7 @@ enum L3Kind : uint32_t { L3_IPV4, L3_IPV6, L3_GRE, L3_MPLS, L3_PPPOE, L3_DONE };
 // accumulated mod 2^16 here (EoMPLS *replaces* the running MPLS length, parser.cpp:625).
 template <bool FULL, class S>
 __device__ __forceinline__ uint32_t parse_l3(const S& s, uint32_t kind, uint32_t base, uint32_t dl,
-                                             DevPkt& p, bool& err) {
+                                             uint32_t caplen, DevPkt& p, bool& err) {
     uint32_t total = 0;
     for (int hop = 0; hop < IPXG_MAX_L3_HOPS; ++hop) {
         dl &= 0xFFFF;
@@ -360,6 +362,7 @@ __device__ __forceinline__ uint32_t parse_l3(const S& s, uint32_t kind, uint32_t
                 uint32_t m = base + length;
                 length = (length + 4) & 0xFFFF;
                 if (0 > (int)dl - (int)length) { err = true; return 0; }
+                if (m + 4 > caplen) { err = true; return 0; }  // see oracle process_mpls_stack
                 w = rd32(s, m);
             } while (!(w & 0x100));
             uint32_t nh = (rd8(s, base + length) & 0xF0) >> 4;
@@ -512,7 +515,7 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
         c.unknown++;
         return false;
     }
-    uint32_t r = parse_l3<FULL>(s, kind, off, (caplen - off) & 0xFFFF, p, err);
+    uint32_t r = parse_l3<FULL>(s, kind, off, (caplen - off) & 0xFFFF, caplen, p, err);
     if (err) return false;
     if (kind == L3_MPLS) c.mpls++;
     if (kind == L3_PPPOE) c.pppoe++;

@@ -536,8 +536,7 @@ int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n
 int ipxg_clear_exports(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     e->ex_head = e->ex_count = 0;
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));  // ordered on the stream
     return IPXG_OK;
 }
 

@@ -114,20 +114,31 @@ __device__ __forceinline__ void canon(const DevPkt& pk, const Params& p, uint64_
 }
 
 __device__ __forceinline__ uint32_t time_bucket(uint32_t sec, uint32_t base, uint32_t w) {
-    if (sec < base) return 63;
+    if (sec < base) return 31;
     uint32_t b = (sec - base) / w;
-    return b > 62 ? 63 : b;
+    return b > 30 ? 31 : b;
 }
 
 // Probe for (and if absent claim) the slot of canonical hash lo; nullptr after MAX_PROBE.
-__device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo) {
+// One 16-byte load per probe returns the key together with first_n and tbits, so the
+// caller can skip reductions that cannot change them.  A stale copy is harmless: a stale
+// empty key falls through to the CAS (which returns the true owner), and stale first_n/tbits
+// only cause a redundant atomic.
+__device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo, uint4& head) {
     uint32_t s = (uint32_t)lo & t.mask;
     for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
         HotSlot* h = &t.hot[s];
-        uint64_t k = ld_relaxed(&h->key);
+        head = *reinterpret_cast<const uint4*>(h);
+        uint64_t k = ((uint64_t)head.y << 32) | head.x;
         if (k == 0) {
             unsigned long long old = atomicCAS((unsigned long long*)&h->key, 0ull, (unsigned long long)lo);
-            k = old == 0 ? lo : old;
+            if (old == 0) {
+                head = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), 0, 0);
+                return h;
+            }
+            k = old;
+            head.z = 0;  // unknown: force the reductions
+            head.w = 0;
         }
         if (k == lo) return h;
         s = (s + 1) & t.mask;
@@ -153,14 +164,15 @@ __device__ __forceinline__ bool flow_accumulate(const TableView& t, const Params
     uint64_t lo, hf;
     uint32_t cdir;
     canon(pk, p, lo, cdir, hf);
-    HotSlot* h = probe_insert(t, lo);
+    uint4 head;
+    HotSlot* h = probe_insert(t, lo, head);
     if (!h) return false;
     atomicAdd((unsigned long long*)&h->acc[cdir], (1ull << 40) | (uint64_t)pk.ip_len);
     atomicMax(&h->last1, idx + 1);
     const uint32_t fn = ~idx;
-    if (ld_relaxed(&h->first_n) < fn) atomicMax(&h->first_n, fn);
-    const uint64_t tb = 1ull << time_bucket(sec, b.base_sec, p.bucket_w);
-    if (!(ld_relaxed(&h->tbits) & tb)) atomicOr((unsigned long long*)&h->tbits, (unsigned long long)tb);
+    if (head.z < fn) atomicMax(&h->first_n, fn);
+    const uint32_t tb = 1u << time_bucket(sec, b.base_sec, p.bucket_w);
+    if (!(head.w & tb)) atomicOr(&h->tbits, tb);
     const uint32_t fl = pk.tcp_flags;
     if (pk.ip_proto == 6 && fl) {
         atomicOr(&h->tflags, fl << (8 * cdir));
@@ -303,6 +315,20 @@ __device__ __forceinline__ bool reparse(const BatchView& b, const Params& p, con
     GlobalSrc g{b.arena + d.offset, d.caplen};
     ParseCounts dummy = {};
     if (!parse_frame<FULL>(g, d.caplen, p.dlt, pk, dummy)) return false;
+    apply_frag_ports(p, f, idx, pk);
+    return true;
+}
+
+// Same, but the header bytes are staged into this lane's LDS column with 16-byte loads
+// (blockDim.x must be IPXG_BLOCK).
+template <bool FULL>
+__device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p, const FragView& f,
+                                            uint32_t idx, uint32_t* col, DevPkt& pk, ipxg_pkt_desc& d) {
+    d = b.desc[idx];
+    stage_frame(col, b.arena, d.offset, d.caplen);
+    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    ParseCounts dummy = {};
+    if (!parse_frame<FULL>(S, d.caplen, p.dlt, pk, dummy)) return false;
     apply_frag_ports(p, f, idx, pk);
     return true;
 }
@@ -485,6 +511,7 @@ __device__ __forceinline__ void clear_slot(HotSlot* h, uint64_t key, uint32_t st
 __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableView t, FragView f,
                                                   ExportView ex, BatchCtl* ctl, unsigned long long* stats,
                                                   uint32_t cap) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     __shared__ uint32_t sc[ST_COUNT];
     __shared__ uint32_t cnt[4];  // keys, live, complex, exported
     if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
@@ -507,7 +534,7 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
                 if (live) rec = t.cold[s];
                 DevPkt fp;
                 ipxg_pkt_desc df;
-                reparse<true>(b, p, f, first, fp, df);
+                reparse_lds<true>(b, p, f, first, &win[threadIdx.x], fp, df);
                 const ipxg_pkt_desc dl = b.desc[last];
                 uint64_t lo, hf;
                 uint32_t cdf;
@@ -526,10 +553,10 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
                 const bool cont = live && !bsplit;
                 // could a split fall strictly inside the batch?
                 bool cx = p.force_complex != 0;
-                const uint64_t tb = h.tbits;
-                if (tb >> 63) cx = true;
+                const uint32_t tb = h.tbits;
+                if (tb >> 31) cx = true;
                 else if (tb) {
-                    uint64_t x = tb >> __builtin_ctzll(tb);
+                    uint32_t x = tb >> __builtin_ctz(tb);
                     if (x & (x + 1)) cx = true;  // an empty bucket between two busy ones
                 }
                 const uint32_t tfirst = cont ? rec.time_first_sec : df.ts_sec;

@@ -14,13 +14,15 @@ namespace ipxg {
 struct alignas(64) HotSlot {
     uint64_t key;      // 0  canonical flow hash: min(XXH64(key), XXH64(key_inv)); 0 = empty
     uint32_t first_n;  // 8  ~(first packet index in this batch), max-reduced; 0 = none
-    uint32_t last1;    // 12 last packet index in this batch + 1, max-reduced; 0 = untouched
-    uint64_t tbits;    // 16 occupancy of (inactive/2)-second buckets since the batch start
-    uint64_t acc[2];   // 24 per canonical direction: packets << 40 | IP bytes
-    uint32_t tflags;   // 40 OR of TCP flags, canonical dir 0 in bits 0-7, dir 1 in bits 8-15
-    uint32_t fin_n[2]; // 44 ~(first FIN|RST packet index) per direction, max-reduced
-    uint32_t syn1[2];  // 52 last SYN packet index + 1 per direction, max-reduced
-    uint32_t state;    // 60 SLOT_LIVE | SLOT_COMPLEX
+    uint32_t tbits;    // 12 occupancy of (inactive/2)-second buckets since the batch start,
+                       //    bit 31 = beyond bucket 30
+    uint64_t acc[2];   // 16 per canonical direction: packets << 40 | IP bytes
+    uint32_t last1;    // 32 last packet index in this batch + 1, max-reduced; 0 = untouched
+    uint32_t tflags;   // 36 OR of TCP flags, canonical dir 0 in bits 0-7, dir 1 in bits 8-15
+    uint32_t fin_n[2]; // 40 ~(first FIN|RST packet index) per direction, max-reduced
+    uint32_t syn1[2];  // 48 last SYN packet index + 1 per direction, max-reduced
+    uint32_t state;    // 56 SLOT_LIVE | SLOT_COMPLEX
+    uint32_t pad;      // 60
 };
 static_assert(sizeof(HotSlot) == 64, "hot slot must be one 64-byte line");
 

@@ -117,6 +117,7 @@ uint64_t oracle_xxh64(const void* data, size_t len, uint64_t seed)
 #define GRE_SEQNUM 0x1000
 #define IPV6_FRAGMENT_OFFSET 0xFFF8 /* headers.hpp:53-54 */
 #define IPV6_MORE_FRAGMENTS 0x1
+#define IPXG_MAX_EXT_STEPS 4096
 
 typedef struct {
     uint16_t ethertype;
@@ -308,8 +309,14 @@ static uint16_t skip_ipv6_ext_hdrs(pctx* c, uint32_t base, uint16_t data_len)
     uint32_t ext = base;
     uint8_t next_hdr = p->ip_proto;
     uint32_t hdrs_len = 0;
-    for (;;) {
+    for (int step = 0;; ++step) {
         if (hdrs_len > data_len || 2u > (uint32_t)data_len - hdrs_len) THROW(c);
+        /* AH with length 1 then 0 moves the walk +2/-2 forever (parser.cpp:382): the
+         * reference never returns.  Walks longer than IPXG_MAX_EXT_STEPS are malformed here. */
+        if (step >= IPXG_MAX_EXT_STEPS) {
+            c->beyond = 1;
+            THROW(c);
+        }
         if (next_hdr == 0 || next_hdr == 60) { /* HOPOPTS, DSTOPTS */
             hdrs_len += ((uint32_t)B8(c, ext + 1) << 3) + 8;
         } else if (next_hdr == 43) { /* ROUTING */
@@ -416,6 +423,13 @@ static uint16_t process_mpls_stack(pctx* c, uint32_t base, uint16_t data_len)
         uint32_t m = base + length;
         length = (uint16_t)(length + 4);
         if (0 > (int)data_len - (int)length) THROW(c);
+        /* A label word past caplen is only reachable through a wrapped data_len (the
+         * reference then reads out of bounds, and with zero fill would never see BoS):
+         * defined here as malformed. */
+        if (m + 4 > c->cap) {
+            c->beyond = 1;
+            THROW(c);
+        }
         w = BE32(c, m);
     } while (!(w & 0x100));
     return length;

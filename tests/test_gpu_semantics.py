@@ -1,0 +1,223 @@
+"""Device parity on synthetic inputs the fixtures do not reach: a parser fuzz corpus over
+every encapsulation, and multi-flow streams that trigger each split rule of
+put_pkt_recursive (cache.cpp:431-472), the fragmentation cache, table growth and expiry,
+cut into batches so that carried-in flow state crosses batch boundaries."""
+import numpy as np
+import pytest
+
+import flowcmp
+import oracle_py
+import pcaputil
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_kwargs(params):
+    kw = {"cache_exp": 20}
+    for tok in filter(None, params.split(";")):
+        k, _, v = tok.partition("=")
+        if k == "a":
+            kw["active"] = int(v)
+        elif k == "i":
+            kw["inactive"] = int(v)
+        elif k == "S":
+            kw["split_biflow"] = True
+        elif k == "fe":
+            kw["frag_enable"] = v == "true"
+        elif k == "ft":
+            kw["frag_timeout"] = int(v)
+        elif k == "fs":
+            kw["frag_size"] = int(v)
+    return kw
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from ipfixprobe_amd import Engine
+    cache = {}
+
+    def get(dl):
+        if dl not in cache:
+            cache[dl] = Engine(datalink=dl)
+        return cache[dl]
+    yield get
+    for e in cache.values():
+        e.close()
+
+
+def _cmp_parse(e, arena, desc, dl):
+    got = e.parse(arena, desc)
+    want, beyond = oracle_py.parse_batch(arena, desc, dl)
+    bad = []
+    for i in range(len(desc)):
+        if beyond[i]:
+            continue
+        fields = pcaputil.PARSED_DTYPE.names if want[i]["valid"] else ("valid",)
+        for f in fields:
+            if not np.array_equal(got[i][f], want[i][f]):
+                bad.append((i, f, got[i][f], want[i][f]))
+    return bad, want
+
+
+@pytest.mark.parametrize("seed", [3, 4, 5])
+def test_parse_fuzz_ethernet(engines, seed):
+    corpus = synth.fuzz_corpus(20000, seed=seed)
+    arena, desc = synth.to_batch(corpus)
+    bad, want = _cmp_parse(engines(1), arena, desc, 1)
+    assert not bad, bad[:10]
+    assert want["valid"].sum() > 10000  # the corpus really exercises valid chains
+
+
+@pytest.mark.parametrize("dl", [113, 276, 12])
+def test_parse_fuzz_linktypes(engines, dl):
+    rng = np.random.default_rng(dl)
+    frames = []
+    for _ in range(4000):
+        et, l3 = synth._l3(rng)
+        if dl == 113:
+            f = synth.sll(l3, et, hatype=int(rng.integers(0, 3)))
+        elif dl == 276:
+            f = synth.sll2(l3, et, hatype=int(rng.integers(0, 3)))
+        else:
+            f = l3 if et in (0x0800, 0x86DD) and rng.random() < 0.9 else bytes(rng.integers(0, 256, 40, dtype=np.uint8))
+        cl = len(f) if rng.random() < 0.9 else int(rng.integers(0, len(f) + 1))
+        frames.append((f[:cl], cl, len(f)))
+    arena, desc = synth.to_batch(frames)
+    bad, _ = _cmp_parse(engines(dl), arena, desc, dl)
+    assert not bad, bad[:10]
+
+
+def test_parse_unaligned_offsets(engines):
+    corpus = synth.fuzz_corpus(3000, seed=9)
+    arena, desc = synth.to_batch(corpus)
+    # shift every frame by 1..15 bytes: the byte-wise staging path
+    pk = []
+    big = np.zeros(len(arena) + 16 * len(desc) + 64, dtype=np.uint8)
+    off = 0
+    nd = desc.copy()
+    for i, d in enumerate(desc):
+        off += 1 + (i % 15)
+        big[off: off + d["caplen"]] = arena[d["offset"]: d["offset"] + d["caplen"]]
+        nd[i]["offset"] = off
+        off += int(d["caplen"])
+    bad, _ = _cmp_parse(engines(1), big[: off + 16], nd, 1)
+    assert not bad, bad[:10]
+    del pk
+
+
+STREAMS = [
+    dict(seed=7, n_flows=300, n_pkts=6000, params=""),
+    dict(seed=8, n_flows=30, n_pkts=6000, params="", long_gap_share=0.0005),  # active timeouts
+    dict(seed=9, n_flows=60, n_pkts=5000, params="a=20;i=5"),
+    dict(seed=10, n_flows=200, n_pkts=5000, params="S"),
+    dict(seed=11, n_flows=200, n_pkts=5000, params="fe=false"),
+    dict(seed=12, n_flows=100, n_pkts=4000, params="i=1"),  # every flow on the sequential path
+    dict(seed=13, n_flows=150, n_pkts=5000, params="ft=1;fs=7", v6_share=0.5, vlan_share=0.4),
+]
+
+
+def _stream(case):
+    kw = {k: v for k, v in case.items() if k != "params"}
+    return synth.flow_stream(**kw).batch()
+
+
+@pytest.mark.parametrize("batch", [None, 1, 37, 1000])
+@pytest.mark.parametrize("ci", range(len(STREAMS)))
+def test_stream_parity(ci, batch):
+    from ipfixprobe_amd import run_capture
+    case = STREAMS[ci]
+    arena, desc = _stream(case)
+    want, wst = oracle_py.run_capture(arena, desc, 1, **oracle_kwargs(case["params"]))
+    assert wst["end_no_res"] == 0
+    got, gst = run_capture(arena, desc, params=case["params"], batch=batch)
+    d = flowcmp.diff(got, want)
+    assert not d, d
+    assert gst["fragmented_packets"] == wst["fragmented_packets"]
+    assert gst["fragments_filled"] == wst["fragments_filled"]
+
+
+def test_stream_reasons_and_counts():
+    """Every record the oracle closes by a split rule (EOF / INACTIVE / ACTIVE) is closed
+    by the engine too; only records still open at the end differ in reason (FORCED vs the
+    sweep's INACTIVE)."""
+    from ipfixprobe_amd import run_capture
+    case = STREAMS[1]
+    arena, desc = _stream(case)
+    want, wst = oracle_py.run_capture(arena, desc, 1, **oracle_kwargs(case["params"]))
+    got, gst = run_capture(arena, desc, params=case["params"])
+    assert gst["end_active"] == wst["end_active"] > 0
+    assert gst["end_eof"] >= 1
+    assert len(got) == len(want)
+
+
+def test_expire_exports_everything_idle():
+    from ipfixprobe_amd import Engine
+    case = STREAMS[0]
+    arena, desc = _stream(case)
+    want, _ = oracle_py.run_capture(arena, desc, 1, **oracle_kwargs(case["params"]))
+    with Engine() as e:
+        e.submit_all(arena, desc, 500)
+        e.expire(int(desc["ts_sec"][-1]) + 31)
+        mid = e.poll()
+        assert e.stats()["flows_in_cache"] == 0
+        e.finish()
+        rest = e.poll()
+    assert len(rest) == 0
+    assert set(np.unique(mid["end_reason"])) <= {1, 3}
+    d = flowcmp.diff(mid, want)
+    assert not d, d
+
+
+def test_table_growth_and_deferral():
+    """Start at 2^16 slots and push 200k new flows in one batch: probes overflow, the table
+    is rebuilt mid-batch and the deferred packets re-applied."""
+    from ipfixprobe_amd import run_capture
+    rng = np.random.default_rng(5)
+    frames = []
+    for i in range(200_000):
+        f = synth.pad(synth.eth(synth.mac(1), synth.mac(2), 0x0800) +
+                      synth.ipv4(synth.ip4(0x0A000000 + i), synth.ip4(0xC0A80001), 17,
+                                 synth.udp(int(rng.integers(1024, 65536)), 53)))
+        frames.append((f, len(f), len(f)))
+    frames += frames[:50_000]  # second packets of the first 50k flows
+    arena, desc = synth.to_batch(frames)
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=22)
+    got, st = run_capture(arena, desc, params="s=16")
+    assert st["table_rehashes"] >= 1
+    d = flowcmp.diff(got, want)
+    assert not d, d
+
+
+def test_nonmonotonic_conserves_packets():
+    """Out-of-order timestamps are outside the parity contract (the reference's sweep then
+    depends on table positions); the engine must still account for every packet."""
+    from ipfixprobe_amd import run_capture
+    arena, desc = _stream(STREAMS[0])
+    d2 = desc.copy()
+    rng = np.random.default_rng(1)
+    j = rng.choice(len(d2), 300, replace=False)
+    d2["ts_sec"][j] -= rng.integers(0, 100, 300).astype(np.uint32)
+    got, st = run_capture(arena, d2)
+    keyed = st["parsed_packets"] - st["keyless_packets"]
+    assert int(got["src_packets"].sum() + got["dst_packets"].sum()) == keyed
+    assert st["complex_flows"] > 0
+
+
+def test_bench_size_parity():
+    """The bench workload itself (10M 64 B packets, 100k biflows) against the oracle."""
+    import torch
+
+    import bench
+    flows = bench.gen_flows(100_000, 0, 1, 1234)
+    frames, desc = bench.build_batch(flows, 10_000_000, 1234, torch.device("cuda", 0))
+    from ipfixprobe_amd import Engine
+    with Engine("s=19") as e:
+        e.submit(frames, desc, device=True)
+        e.finish()
+        got = e.poll()
+    dn = desc.cpu().numpy().view(pcaputil.DESC_DTYPE)
+    want, wst = oracle_py.run_capture(frames.cpu().numpy(), dn, 1, cache_exp=21)
+    assert len(want) == 100_000 and wst["end_no_res"] == 0
+    d = flowcmp.diff(got, want)
+    assert not d, d

@@ -1,0 +1,27 @@
+"""CPU: the oracle on the synthetic corpora (conservation laws; the corpora really reach
+the code paths the GPU tests compare)."""
+import numpy as np
+
+import oracle_py
+import synth
+
+
+def test_fuzz_corpus_reaches_every_encapsulation():
+    arena, desc = synth.to_batch(synth.fuzz_corpus(20000, seed=3))
+    p, beyond = oracle_py.parse_batch(arena, desc)
+    v = p[p["valid"] == 1]
+    et = set(v["ethertype"].tolist())
+    assert {0x0800, 0x86DD, 0x8847, 0x8848, 0x8864} <= et
+    assert (v["vlan_id"] != 0).sum() > 100
+    assert ((v["frag_off"] != 0) | (v["more_fragments"] != 0)).sum() > 100
+    assert (v["tcp_options"] != 0).sum() > 100
+    assert beyond.sum() < 500
+
+
+def test_stream_conserves_packets_and_splits():
+    arena, desc = synth.flow_stream(seed=8, n_flows=30, n_pkts=6000, long_gap_share=0.0005).batch()
+    recs, st = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    assert int(recs["src_packets"].sum() + recs["dst_packets"].sum()) == st["parsed_packets"] - st["keyless_packets"]
+    assert st["end_active"] > 0 and st["end_inactive"] > 0 and st["end_eof"] > 0
+    assert st["fragments_filled"] > 0 and st["end_no_res"] == 0
+    assert np.all(recs["time_last_sec"] >= recs["time_first_sec"])
