@@ -98,7 +98,8 @@ def test_parse_unaligned_offsets(engines):
     nd = desc.copy()
     for i, d in enumerate(desc):
         off += 1 + (i % 15)
-        big[off: off + d["caplen"]] = arena[d["offset"]: d["offset"] + d["caplen"]]
+        o, c = int(d["offset"]), int(d["caplen"])
+        big[off: off + c] = arena[o: o + c]
         nd[i]["offset"] = off
         off += int(d["caplen"])
     bad, _ = _cmp_parse(engines(1), big[: off + 16], nd, 1)
