@@ -95,6 +95,13 @@ def lib():
     """Load the in-tree libipxg.so.  Raises if it has not been built."""
     global _LIB
     if _LIB is None:
+        try:
+            # torch ships its own libamdhip64.so.7; loading it first makes libipxg bind to
+            # that same runtime (identical soname), so one process never holds two HIP
+            # runtimes when the tests/bench also use torch for device buffers.
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise IpxgError("libipxg.so not built (%s): run __graft_entry__.build()" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
