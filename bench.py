@@ -10,12 +10,15 @@ rank owns a disjoint range of the canonical flow hash (the NIC-RSS analogue, SUR
 so there is no collective in the data path; at N > 1 the per-GPU export buffers are gathered
 to rank 0 over RCCL inside the step (the path's only exchange).
 
-Prints one JSON line (rank 0).  roofline.achieved = algorithmic bytes of k_ingest per launch
-(64 B frame + 16 B descriptor per packet) / its average duration, timed with
-HIP events on the engine's stream.
+Prints one JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch of the
+dominant kernel k_bin (64 B frame + 16 B descriptor per packet) / its average
+duration, timed with HIP events on the engine's stream; roofline.stage gives the same bytes
+over the whole ingest (k_bin + k_reduce).  roofline.traffic is the HBM bytes per k_bin launch
+from the newest committed rocprofv3 PMC summary (profiles/*/pmc_summary.json, collected by
+tools/gpu_pmc.sh), or null when none covers k_bin.
 """
 import argparse
-import ctypes
+import glob
 import json
 import math
 import os
@@ -158,28 +161,69 @@ def gather_exports(eng, rank, world, device):
     return total
 
 
-def cpu_baseline(frames, desc, flows_per_shard):
-    """The oracle (CPU restatement of the reference path) on the same bytes, one core."""
+def cpu_baseline(frames, desc, flows_per_shard, threads=16, reps=3):
+    """The oracle (CPU restatement of the reference path) on the same packets, one pipeline
+    per core as the reference scales (one input thread + private NHTFlowCache per RSS queue,
+    ipfixprobe.cpp:381-464): packets are dealt to `threads` shards by a symmetric hash of the
+    IP pair (the NIC's symmetric RSS on IPs, dpdkDevice.cpp:230-262 -- not timed), each shard
+    runs parse_packet + put_pkt + finish in its own thread (ctypes drops the GIL)."""
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py
     arena = frames.cpu().numpy()
     d = desc.cpu().numpy().view(np.uint8).view(
         np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"),
                   ("ts_sec", "<u4"), ("ts_usec", "<u4")]))
-    s = min(30, int(math.ceil(math.log2(max(flows_per_shard, 2)))) + 4)  # BASELINE.md sizing
-    c = oracle_py.OracleCache(cache_exp=s)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    fr = arena.reshape(-1, 64)
+    ip = lambda c: fr[:, c:c + 4].view(">u4").reshape(-1).astype(np.uint64)  # noqa: E731
+    sym = (ip(26) ^ ip(30)) * np.uint64(0x9E3779B97F4A7C15)
+    shard = ((sym >> np.uint64(40)) % np.uint64(threads)).astype(np.int64)
+    parts = [np.ascontiguousarray(d[shard == k]) for k in range(threads)]
+    s_exp = min(30, int(math.ceil(math.log2(max(flows_per_shard // threads, 2)))) + 4)
+    caches = [oracle_py.OracleCache(cache_exp=s_exp) for _ in range(threads)]
+    counts = [0] * threads
+
+    def work(k):
+        for _ in range(reps):
+            caches[k].run(arena, parts[k], 1)
+            caches[k].finish()
+            counts[k] += len(caches[k].take())
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
     t0 = time.perf_counter()
-    c.run(arena, d, 1)
-    c.finish()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
     dt = time.perf_counter() - t0
-    n_rec = len(c.take())
-    st = c.stats()
-    c.close()
-    return {"value": round(len(d) / dt / 1e6, 3), "unit": "Mpkts/s", "cores": 1, "kind": "port",
-            "sample": "the full bench batch (%d packets, %d flows) through oracle/ipxg_oracle.c "
-                      "(parse_packet + NHTFlowCache::put_pkt + finish restated in C, s=%d, "
-                      "gcc -O2), one host core, %.1f s; %d records, NO_RES evictions %d"
-                      % (len(d), flows_per_shard, s, dt, n_rec, st["end_no_res"])}
+    no_res = sum(c.stats()["end_no_res"] for c in caches)
+    for c in caches:
+        c.close()
+    pkts = len(d) * reps
+    return {"value": round(pkts / dt / 1e6, 3), "unit": "Mpkts/s", "cores": threads, "kind": "port",
+            "sample": "the bench batch (%d packets, %d flows) x%d passes through oracle/ipxg_oracle.c "
+                      "(parse_packet + NHTFlowCache::put_pkt + finish restated in C, gcc -O2), "
+                      "%d threads each owning a symmetric-IP-hash shard with its own cache (s=%d), "
+                      "%.2f s wall; %d records, NO_RES evictions %d"
+                      % (len(d), flows_per_shard, reps, threads, s_exp, dt, sum(counts), no_res)}
+
+
+def pmc_traffic(kernel="k_bin"):
+    """HBM bytes per launch of `kernel` from the newest profiles/*/pmc_summary.json:
+    FETCH_SIZE (KiB; doubled -- gfx950 tallies wide streaming reads at half, MI355X_MICROARCH.md
+    'HBM') + WRITE_SIZE (KiB), both per launch."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json"))):
+        try:
+            with open(p) as f:
+                js = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for name, v in js.items():
+            if kernel in name and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                best = (p, (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0)
+    return best
 
 
 def main():
@@ -192,6 +236,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the records against the oracle")
+    ap.add_argument("--ingest", default="binned", choices=["binned", "atomic"])
+    ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
     import torch
@@ -209,7 +255,8 @@ def main():
     flows = gen_flows(args.flows, rank, world, args.seed)
     frames, desc = build_batch(flows, args.packets, args.seed + rank, device)
     torch.cuda.synchronize()
-    eng = Engine("s=%d" % max(16, int(math.ceil(math.log2(4 * args.flows)))), device_id=local)
+    eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(4 * args.flows)))), args.ingest),
+                 device_id=local)
 
     def step():
         eng.submit(frames, desc, device=True)
@@ -253,12 +300,17 @@ def main():
         dt = float(t.item())
     total_pkts = args.packets * args.steps * world
     value = total_pkts / dt / 1e6
-    ingest_s = tm["ingest_ms"] / max(tm["ingest_launches"], 1) / 1e3
-    achieved = ALG_BYTES_PER_PKT * args.packets / ingest_s / 1e9 if ingest_s > 0 else 0.0
+    per_launch = lambda k: tm[k + "_ms"] / max(tm[k + "_launches"], 1)  # noqa: E731
+    bin_ms, red_ms = per_launch("ingest"), per_launch("reduce")
+    alg = ALG_BYTES_PER_PKT * args.packets
+    achieved = alg / (bin_ms / 1e3) / 1e9 if bin_ms > 0 else 0.0
+    stage = alg / ((bin_ms + red_ms) / 1e3) / 1e9 if bin_ms > 0 else 0.0
+    kname = "k_bin" if args.ingest == "binned" else "k_ingest"
+    pmc = pmc_traffic(kname)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(frames, desc, args.flows)
+            cpu = cpu_baseline(frames, desc, args.flows, threads=args.cpu_threads)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpkts/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
@@ -268,16 +320,22 @@ def main():
                                    "biflows per GPU; step = parse + XXH64 + biflow-cache update + "
                                    "finish (all flows exported)" % (args.packets, args.flows),
                        "packets_per_gpu": args.packets, "flows_per_gpu": args.flows,
+                       "ingest": args.ingest,
                        "parallelism": "flow-hash-range shards x%d, RCCL gather of export buffers"
                                       % world if world > 1 else "single GPU"},
-            "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None,
-                         "algorithmic_bytes_per_launch": ALG_BYTES_PER_PKT * args.packets,
-                         "avg_launch_ms": round(ingest_s * 1e3, 4)},
+                         "traffic": round(pmc[1]) if pmc else None,
+                         "traffic_source": os.path.relpath(pmc[0], ROOT) if pmc else None,
+                         "algorithmic_bytes_per_launch": alg,
+                         "avg_launch_ms": round(bin_ms, 4),
+                         "stage": {"kernels": "k_bin+k_reduce", "achieved": round(stage, 1),
+                                   "frac": round(stage / HBM_PEAK_GBS, 4),
+                                   "avg_ms": round(bin_ms + red_ms, 4)}},
             "stage_ms_per_step": {k: round(tm[k + "_ms"] / max(args.steps, 1), 4)
-                                  for k in ("ingest", "finalize", "slow", "finish")},
+                                  for k in ("ingest", "reduce", "finalize", "slow", "finish")},
             "flows_exported_per_step": int(st["end_forced"] // max(st["batches"], 1)),
+            "spilled_packets": int(st["spilled_packets"]),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

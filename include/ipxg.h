@@ -155,8 +155,13 @@ typedef struct ipxg_config {
     int32_t device_id;        /* dev= HIP device ordinal                               */
     uint32_t batch_pkts;      /* batch= max packets per submit (staging size)          */
     uint32_t datalink;        /* IPXG_DLT_*                                            */
-    uint32_t reserved;
+    uint32_t flags;           /* IPXG_CFG_*                                            */
 } ipxg_config;
+
+/* ipxg_config.flags */
+#define IPXG_CFG_ATOMIC_INGEST 0x1u /* ingest=atomic: fold every packet into the table with
+                                       device atomics (one kernel) instead of the binned
+                                       two-phase ingest; kept for A/B measurement          */
 
 typedef struct ipxg_stats {
     /* parser counters, reference parser-stats.hpp:126-201 (the subset on the path) */
@@ -188,6 +193,8 @@ typedef struct ipxg_stats {
     uint64_t table_capacity;
     uint64_t table_rehashes;
     uint64_t batches;
+    uint64_t spilled_packets; /* packets that fell back from the binned ingest to direct
+                                 device atomics (partition region or LDS table full)    */
 } ipxg_stats;
 
 typedef struct ipxg_engine ipxg_engine;
@@ -229,11 +236,13 @@ int ipxg_get_stats(ipxg_engine* eng, ipxg_stats* out);
 
 /* ---- stage timing (HIP events on the engine's stream) --------------------------------- */
 typedef struct ipxg_timing {
-    double ingest_ms;          /* k_ingest: parse + hash + table accumulate               */
-    double finalize_ms;        /* k_finalize                                               */
+    double ingest_ms;          /* k_bin: parse + hash + partition (atomic mode: k_ingest)  */
+    double reduce_ms;          /* k_reduce: per-flow aggregation + table merge (+finalise) */
+    double finalize_ms;        /* k_finalize table scan (only when k_reduce could not)     */
     double slow_ms;            /* fragment / overflow / complex-flow paths                 */
     double finish_ms;          /* k_finish + table clear                                   */
     uint64_t ingest_launches;
+    uint64_t reduce_launches;
     uint64_t finalize_launches;
     uint64_t slow_launches;
     uint64_t finish_launches;

@@ -4,7 +4,8 @@
 // "active", "inactive", "split", "frag-enable", "frag-size", "frag-timeout"
 // (CacheOptParser, cache.hpp:81-221; OptionsParser::parse, options.cpp:62-160: ';'-separated
 // tokens, "name=value" or "name" followed by its value as the next token), plus the GPU keys
-// "dev"/"device", "batch" and "dlt" (EN10MB | RAW | LINUX_SLL | LINUX_SLL2 or a number).
+// "dev"/"device", "batch", "dlt" (EN10MB | RAW | LINUX_SLL | LINUX_SLL2 or a number) and
+// "ingest" (binned | atomic).
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -89,6 +90,11 @@ extern "C" int ipxg_config_parse(const char* params, ipxg_config* cfg) {
         } else if (name == "batch") {
             if (!arg(a) || !to_u32(a, v) || v == 0 || v > IPXG_MAX_BATCH) return IPXG_EINVAL;
             cfg->batch_pkts = v;
+        } else if (name == "ingest") {
+            if (!arg(a)) return IPXG_EINVAL;
+            if (a == "atomic") cfg->flags |= IPXG_CFG_ATOMIC_INGEST;
+            else if (a == "binned") cfg->flags &= ~IPXG_CFG_ATOMIC_INGEST;
+            else return IPXG_EINVAL;
         } else if (name == "dlt") {
             if (!arg(a)) return IPXG_EINVAL;
             if (a == "EN10MB") cfg->datalink = IPXG_DLT_EN10MB;

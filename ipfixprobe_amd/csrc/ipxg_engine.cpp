@@ -2,12 +2,14 @@
 // kernel sequence, table growth, the export buffer, and statistics.
 //
 // Per ipxg_submit (one batch, arrival order):
-//   stage (H2D if host batch) -> k_ingest -> [sync: control block]
+//   stage (H2D if host batch) -> k_bin -> k_reduce (merges + finalises the flows)
+//   -> [sync: control block]
 //   -> fragments? sort + k_frag_walk + k_frag_accumulate
 //   -> deferred probes? grow table (k_rehash) + k_deferred, until none
-//   -> k_finalize -> [sync]
+//   -> anything k_reduce could not finalise (ctl->pending)? k_finalize scan -> [sync]
 //   -> complex flows? k_complex_rank -> gather -> sort -> k_complex_walk
 //   -> grow the table if its load passed 1/2.
+// In the common case (no fragments, no overflow) that is two kernels and one host sync.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,8 +41,9 @@ struct ipxg_engine {
     // export buffer: records [ex_head, ex_count) are pending
     ipxg_flow_record* ex = nullptr;
     uint32_t ex_cap = 0;
-    uint32_t* ex_count_d = nullptr;
+    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag
     uint32_t ex_count = 0, ex_head = 0;
+    uint32_t ex_host[2] = {0, 0};
     // control / stats
     BatchCtl* ctl_d = nullptr;
     BatchCtl* ctl_h = nullptr;  // pinned
@@ -51,19 +54,21 @@ struct ipxg_engine {
     // scratch
     DevBuf defer_a, defer_b, frag_list, frag_sorted, frag_ports, sort_tmp;
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
+    DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
+    uint32_t last_touched = 0;           // flow aggregates of the previous batch
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
     // host-side counters
-    uint64_t complex_total = 0, rehashes = 0, batches = 0;
+    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0;
     bool prev_valid = false;
     uint32_t prev_sec = 0, prev_usec = 0;
     // stage timing
     bool prof = false;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[10] = {};
     ipxg_timing tm = {};
 };
 
-// event pairs: [0,1] ingest, [2,3] finalize, [4,5] slow paths, [6,7] finish
+// events: [0,1] ingest (k_bin), [1,2] k_reduce, [3,4] slow paths, [5,6] k_finalize, [7,8] finish
 static void ev_rec(ipxg_engine* e, int i) {
     if (e->prof) (void)hipEventRecord(e->ev[i], e->st);
 }
@@ -103,6 +108,33 @@ static TableView table_view(ipxg_engine* e) { return TableView{e->hot, e->cold, 
 
 static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_count_d, e->ex_cap}; }
 
+// Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
+// (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
+// than the batch's packets.  Regions hold 1.5x the mean share (+256) per k_reduce workgroup
+// and twice that per partition, for skew; what does not fit spills to atomics.
+static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
+    uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
+    if (est == 0 || est > n) est = n;
+    uint32_t bits = 0;
+    while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
+    const uint32_t P = 1u << bits;
+    const uint64_t avg = ((uint64_t)n + P - 1) / P;
+    const uint64_t want = avg + avg / 2 + 256;
+    const uint32_t chunk = (uint32_t)std::min<uint64_t>(want, RED_MAX_CHUNK);
+    const uint32_t groups = (uint32_t)std::max<uint64_t>(2, (2 * want + chunk - 1) / chunk);
+    int rc;
+    if ((rc = ensure(e, e->bin_rec, (size_t)P * groups * chunk * sizeof(uint4)))) return rc;
+    if ((rc = ensure(e, e->bin_count, (size_t)P * sizeof(uint32_t)))) return rc;
+    HIPCHK(e, hipMemsetAsync(e->bin_count.p, 0, (size_t)P * sizeof(uint32_t), e->st));
+    bv.rec = (uint4*)e->bin_rec.p;
+    bv.count = (uint32_t*)e->bin_count.p;
+    bv.cap = groups * chunk;
+    bv.chunk = chunk;
+    bv.part_bits = bits;
+    bv.groups = groups;
+    return IPXG_OK;
+}
+
 static FragView frag_view(ipxg_engine* e) {
     return FragView{e->frag_ent, e->frag_cnt, (uint64_t*)e->frag_list.p, (uint64_t*)e->frag_sorted.p,
                     (uint32_t*)e->frag_ports.p};
@@ -140,11 +172,23 @@ static int alloc_table(ipxg_engine* e, uint32_t cap, HotSlot** hot, ipxg_flow_re
     return IPXG_OK;
 }
 
-static int sync_ctl(ipxg_engine* e) {
-    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, sizeof(BatchCtl), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(&e->ex_count, e->ex_count_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
+static int read_ex_count(ipxg_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->ex_host, e->ex_count_d, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
     return IPXG_OK;
+}
+
+static int check_ex(ipxg_engine* e) {
+    e->ex_count = e->ex_host[0];
+    if (e->ex_host[1]) return set_err(e, IPXG_EDEVICE, "export buffer overflow (engine bug: capacity under-sized)");
+    return IPXG_OK;
+}
+
+static int sync_ctl(ipxg_engine* e) {
+    int rc;
+    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, sizeof(BatchCtl), hipMemcpyDeviceToHost, e->st));
+    if ((rc = read_ex_count(e))) return rc;
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return check_ex(e);
 }
 
 // Rebuild the table at new_cap, dropping dead slots (no live record, untouched).
@@ -254,7 +298,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->cap = cap;
     e->ex_cap = 1u << 16;
     if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
-    if (hipMalloc((void**)&e->ex_count_d, sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->ex_count_d, 2 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->ctl_d, sizeof(BatchCtl)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipHostMalloc((void**)&e->ctl_h, sizeof(BatchCtl), hipHostMallocDefault) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->misc_d, 16 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
@@ -264,7 +308,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (hipMalloc((void**)&e->frag_ent, (size_t)fs * 4 * sizeof(FragEntry)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->frag_cnt, (size_t)fs * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
-    if (hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+    if (hipMemsetAsync(e->ex_count_d, 0, 2 * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
         return fail(IPXG_EDEVICE);
     if (hipStreamSynchronize(e->st) != hipSuccess) return fail(IPXG_EDEVICE);
@@ -289,7 +333,8 @@ int ipxg_destroy(ipxg_engine* e) {
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->frag_list, &e->frag_sorted,
-                      &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank})
+                      &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
+                      &e->bin_count})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -336,9 +381,20 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 
     Params p = params(e);
     FragView fv = frag_view(e);
+    const bool binned = !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST);
+    BinView bins = {};
+    if (binned && (rc = setup_bins(e, n, bins))) return rc;
     ev_rec(e, 0);
-    launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
-    ev_rec(e, 1);
+    if (binned) {
+        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
+        ev_rec(e, 1);
+        launch_reduce(e->st, bv, p, table_view(e), fv, bins, export_view(e), e->ctl_d, (uint32_t*)e->defer_a.p,
+                      e->stats_d);
+        ev_rec(e, 2);
+    } else {
+        launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
+        ev_rec(e, 1);
+    }
     HIPCHK(e, hipGetLastError());
     if ((rc = sync_ctl(e))) return rc;
     const BatchCtl c1 = *e->ctl_h;
@@ -346,13 +402,17 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
+        if (binned) {
+            e->tm.reduce_ms += ev_ms(e, 1);
+            e->tm.reduce_launches++;
+        }
     }
     bool slow = false;
 
     // fragmentation cache: order fragments by (bucket, arrival) and replay the rings
     uint32_t ndef = c1.deferred;
     if (c1.frag_count) {
-        if (!slow) ev_rec(e, 4);
+        if (!slow) ev_rec(e, 3);
         slow = true;
         const uint32_t nf = c1.frag_count;
         if ((rc = ensure(e, e->frag_sorted, (size_t)nf * 8))) return rc;
@@ -371,7 +431,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     }
     // table overflow: grow and re-apply the deferred packets
     while (ndef) {
-        if (!slow) ev_rec(e, 4);
+        if (!slow) ev_rec(e, 3);
         slow = true;
         if ((rc = rehash(e, e->cap * 2))) return rc;
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->deferred, 0, sizeof(uint32_t), e->st));
@@ -382,28 +442,32 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         ndef = e->ctl_h->deferred;
         std::swap(e->defer_a, e->defer_b);
     }
-
     if (slow) {
-        ev_rec(e, 5);
+        ev_rec(e, 4);
         HIPCHK(e, hipStreamSynchronize(e->st));
         if (e->prof) {
-            e->tm.slow_ms += ev_ms(e, 4);
+            e->tm.slow_ms += ev_ms(e, 3);
             e->tm.slow_launches++;
         }
     }
-    p.force_complex = p.force_complex || c1.nonmono;
-    ev_rec(e, 2);
-    launch_finalize(e->st, bv, p, table_view(e), frag_view(e), export_view(e), e->ctl_d, e->stats_d);
-    ev_rec(e, 3);
-    HIPCHK(e, hipGetLastError());
-    if ((rc = sync_ctl(e))) return rc;
-    if (e->prof) {
-        e->tm.finalize_ms += ev_ms(e, 2);
-        e->tm.finalize_launches++;
+    // slots k_reduce could not finalise (fragments, deferrals, spills, multi-workgroup
+    // partitions; every slot in the atomic ingest mode): the full-table scan
+    const bool scan = !binned || c1.pending || c1.frag_count || c1.deferred;
+    if (scan) {
+        p.force_complex = p.force_complex || c1.nonmono;
+        ev_rec(e, 5);
+        launch_finalize(e->st, bv, p, table_view(e), frag_view(e), export_view(e), e->ctl_d, e->stats_d);
+        ev_rec(e, 6);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        if (e->prof) {
+            e->tm.finalize_ms += ev_ms(e, 5);
+            e->tm.finalize_launches++;
+        }
     }
     const uint32_t ncx = e->ctl_h->complex_count;
     if (ncx) {
-        ev_rec(e, 4);
+        ev_rec(e, 3);
         e->complex_total += ncx;
         if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 5 * 4))) return rc;
         uint32_t* cr = (uint32_t*)e->cx_rank.p;
@@ -411,6 +475,8 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         launch_complex_rank(e->st, table_view(e), cx, e->ctl_d, e->cap);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
+        if ((uint32_t)(e->ctl_h->cx_alloc >> 32) != ncx)
+            return set_err(e, IPXG_EDEVICE, "complex-flow count mismatch (engine bug)");
         const uint32_t npk = (uint32_t)(e->ctl_h->cx_alloc & 0xFFFFFFFFu);
         if ((rc = ensure(e, e->cx_list, (size_t)npk * 8 + 8))) return rc;
         if ((rc = ensure(e, e->cx_sorted, (size_t)npk * 8 + 8))) return rc;
@@ -427,19 +493,28 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         HIPCHK(e, sort_keys_u64(e->sort_tmp.p, tb, cx.list, cx.sorted, npk, bits, e->st));
         launch_complex_walk(e->st, bv, p, table_view(e), frag_view(e), cx, ncx, export_view(e), e->ctl_d,
                             e->stats_d);
-        ev_rec(e, 5);
+        ev_rec(e, 4);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         if (e->prof) {
-            e->tm.slow_ms += ev_ms(e, 4);
+            e->tm.slow_ms += ev_ms(e, 3);
             e->tm.slow_launches++;
         }
     }
-    e->keys = e->ctl_h->keys;
-    e->live = e->ctl_h->live;
+    const BatchCtl& c2 = *e->ctl_h;
+    if (scan) {  // the scan counted every slot
+        e->keys = c2.keys;
+        e->live = c2.live;
+    } else {
+        e->keys += c2.new_keys;
+        e->live += c2.new_live;
+    }
+    e->live += c2.cx_new_live;
+    e->last_touched = c2.touched;
+    e->spilled += c2.spilled;
     e->prev_valid = true;
-    e->prev_sec = e->ctl_h->last_sec;
-    e->prev_usec = e->ctl_h->last_usec;
+    e->prev_sec = c2.last_sec;
+    e->prev_usec = c2.last_usec;
     e->batches++;
     // keep the load factor <= 1/2 for the next batch (dead slots are dropped by the rebuild)
     if ((uint64_t)e->keys * 2 > e->cap) {
@@ -455,7 +530,7 @@ int ipxg_expire(ipxg_engine* e, int64_t now_sec) {
     if (!e) return IPXG_EINVAL;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
-    if ((rc = ensure_export(e, e->live))) return rc;
+    if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
     launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
@@ -470,16 +545,17 @@ int ipxg_finish(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
-    if ((rc = ensure_export(e, e->live))) return rc;
-    ev_rec(e, 6);
+    if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
+    ev_rec(e, 7);
     launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
-    ev_rec(e, 7);
-    HIPCHK(e, hipMemcpyAsync(&e->ex_count, e->ex_count_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+    ev_rec(e, 8);
+    if ((rc = read_ex_count(e))) return rc;
     HIPCHK(e, hipStreamSynchronize(e->st));
+    if ((rc = check_ex(e))) return rc;
     if (e->prof) {
-        e->tm.finish_ms += ev_ms(e, 6);
+        e->tm.finish_ms += ev_ms(e, 7);
         e->tm.finish_launches++;
     }
     e->keys = e->live = 0;
@@ -493,10 +569,11 @@ int ipxg_reset(ipxg_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
     const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
     HIPCHK(e, hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st));
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 2 * sizeof(uint32_t), e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->ex_count = e->ex_head = 0;
     e->keys = e->live = 0;
+    e->last_touched = 0;
     e->prev_valid = false;
     return IPXG_OK;
 }
@@ -578,6 +655,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->table_capacity = e->cap;
     out->table_rehashes = e->rehashes;
     out->batches = e->batches;
+    out->spilled_packets = e->spilled;
     return IPXG_OK;
 }
 

@@ -1,0 +1,316 @@
+// ipxg_ingest.hip -- the per-batch ingest of the packet -> biflow engine, in two phases with
+// no per-packet device-scope atomics (those execute at the memory side on CDNA4, ~20 G/s
+// chip-wide for lane-scattered addresses: MI355X_MICROARCH.md "Global float atomics").
+//
+//   k_bin     BIN_K packets per lane per tile: stage <= 128 header bytes in the lane's LDS
+//             column, parse (parse_packet, parser.cpp:673-805), build key + inverse key and
+//             2x XXH64 (create_hash_key + XXH64, cache.cpp:525-574, xxhash.h:2885-2901),
+//             then append a 16-byte record {canonical hash, packet index, contribution} to
+//             the region of its partition (bits 32.. of the canonical hash).  A tile ranks
+//             its records per partition with LDS atomics and reserves room with one
+//             coalesced device atomic per 64 partitions, so a partition's records of one
+//             tile land in one run.                                     (HBM-bound)
+//   k_reduce  one 1024-thread workgroup per partition chunk: aggregates the chunk's records
+//             per flow in an LDS hash table (LDS atomics), then merges each flow into its
+//             slot of the device table once -- a plain read-modify-write when the workgroup
+//             holds all of the partition's records, atomics otherwise -- and, when nothing
+//             else of the batch can touch the flow any more, applies the reference's split
+//             rules right there (finalize_slot), so the table is not scanned per batch.
+//
+// Records that do not fit (partition region full, LDS table full) fall back to direct
+// atomic accumulation (merge_packet_atomic); the engine then runs the k_finalize scan for
+// the batch (ctl->pending).  Both paths are order-independent reductions keyed by packet
+// index, so the result does not depend on which lane or workgroup runs first.
+#include "ipxg_table.hpp"
+
+namespace ipxg {
+
+constexpr int BIN_K = 8;                          // packets per lane per tile
+constexpr uint32_t BIN_TILE = BIN_K * IPXG_BLOCK;  // 2048 packets
+constexpr uint32_t NO_REC = 0xFFFFFFFFu;
+constexpr uint32_t RED_U = 4;                     // records in flight per thread
+constexpr uint32_t RED_MAX_PROBE = 256;
+constexpr uint32_t RED_FAILED = 0x80000000u;      // FlowAgg::tflags bit: table probe failed
+
+__device__ __forceinline__ void defer_packet(BatchCtl* ctl, uint32_t* list, uint32_t idx, bool from_bin) {
+    const uint32_t pos = atomicAdd(&ctl->deferred, 1u);
+    list[pos] = idx;
+    if (from_bin) atomicAdd(&ctl->a_deferred, 1u);
+}
+
+// ---- phase A ------------------------------------------------------------------------------
+// 128 VGPRs (4 waves/SIMD = the LDS limit of 4 workgroups per CU)
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* deferred_list,
+           unsigned long long* stats) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];    // 32 KiB: one header column per lane
+    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];    // 8 KiB: per-partition rank / base
+    const uint32_t tid = threadIdx.x;
+    if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
+    const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
+    ParseCounts c = {};
+    uint32_t keyless = 0, frags = 0, spilled = 0;
+    uint32_t* col = &win[tid];
+    for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
+        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
+        __syncthreads();
+        // the tile's records stay in registers (indexed by compile-time q only)
+        uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K];
+#pragma unroll
+        for (int q = 0; q < BIN_K; ++q) {
+            r0[q] = r1[q] = r2[q] = 0;
+            rk[q] = NO_REC;
+        }
+#pragma unroll 1
+        for (int j = 0; j < BIN_K; ++j) {
+            const uint32_t i = tile + (uint32_t)j * IPXG_BLOCK + tid;
+            const bool act = i < b.n;
+            ipxg_pkt_desc d = {0, 0, 0, 0, 0};
+            if (act) d = b.desc[i];
+            // a timestamp going backwards sends every flow of the batch to the sequential path
+            const uint64_t ts = ((uint64_t)d.ts_sec << 32) | d.ts_usec;
+            uint64_t prev = (uint64_t)__shfl_up((unsigned long long)ts, 1);
+            if (lane_id() == 0) {
+                if (i > 0 && act) {
+                    const ipxg_pkt_desc q = b.desc[i - 1];
+                    prev = ((uint64_t)q.ts_sec << 32) | q.ts_usec;
+                } else {
+                    prev = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
+                }
+            }
+            const bool has_prev = i > 0 || p.prev_valid;
+            if (act && has_prev && ts < prev) ctl->nonmono = 1;
+            if (act && i == b.n - 1) {
+                ctl->last_sec = d.ts_sec;
+                ctl->last_usec = d.ts_usec;
+            }
+            if (!act) continue;
+            stage_frame(col, b.arena, d.offset, d.caplen);
+            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+            DevPkt pk;
+            if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
+            if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
+                keyless++;
+                continue;
+            }
+            if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {  // fragmentation cache path
+                frags++;
+                const uint32_t bucket = (uint32_t)(frag_key_hash(pk) % (uint64_t)p.frag_size);
+                const uint32_t pos = atomicAdd(&ctl->frag_count, 1u);
+                f.list[pos] = ((uint64_t)bucket << 24) | i;
+                continue;
+            }
+            uint64_t lo, hf;
+            uint32_t cdir;
+            canon(pk, p, lo, cdir, hf);
+            const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
+            const uint32_t part = (uint32_t)(lo >> 32) & pmask;
+            const uint32_t rank = atomicAdd(&hist[part], 1u);
+#pragma unroll
+            for (int q = 0; q < BIN_K; ++q) {
+                if (q == j) {
+                    r0[q] = (uint32_t)lo;
+                    r1[q] = (uint32_t)(lo >> 32);
+                    r2[q] = m;
+                    rk[q] = rank;
+                }
+            }
+        }
+        __syncthreads();
+        // one reservation per non-empty partition: lanes = consecutive counters (256 B rows)
+        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) {
+            const uint32_t cnt = hist[q];
+            if (cnt) hist[q] = atomicAdd(&bv.count[q], cnt);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < BIN_K; ++q) {
+            if (rk[q] == NO_REC) continue;
+            const uint32_t part = r1[q] & pmask;
+            const uint32_t pos = hist[part] + rk[q];
+            const uint32_t idx = tile + (uint32_t)q * IPXG_BLOCK + tid;
+            if (pos < bv.cap) {
+                bv.rec[(size_t)part * bv.cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
+            } else {  // partition region full: accumulate straight into the table
+                spilled++;
+                const uint64_t lo = ((uint64_t)r1[q] << 32) | r0[q];
+                if (!merge_packet_atomic(t, lo, idx, r2[q], &ctl->new_keys))
+                    defer_packet(ctl, deferred_list, idx, true);
+            }
+        }
+        __syncthreads();  // hist is reset by the next tile
+    }
+    // block statistics, hist reused as the counter block
+    if (tid < ST_COUNT) hist[tid] = 0;
+    __syncthreads();
+    flush_counts(c, keyless, frags, hist);
+    flush_block_stats(hist, stats);
+    if (spilled) {
+        atomicAdd(&ctl->spilled, spilled);
+        ctl->pending = 1;
+    }
+}
+
+void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
+                BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats) {
+    uint32_t tiles = (b.n + BIN_TILE - 1) / BIN_TILE;
+    if (tiles > 2048) tiles = 2048;
+    hipLaunchKernelGGL(k_bin, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
+                       deferred_list, stats);
+}
+
+// ---- phase B ------------------------------------------------------------------------------
+// LDS flow table of k_reduce: linear probing on the low bits of the canonical hash
+__device__ __forceinline__ int lds_slot(FlowAgg* ht, uint64_t lo, bool insert) {
+    uint32_t e = (uint32_t)lo & (RED_ENTRIES - 1);
+    for (uint32_t probe = 0; probe < RED_MAX_PROBE; ++probe) {
+        unsigned long long k = ht[e].key;
+        if (k == 0) {
+            if (!insert) return -1;
+            k = atomicCAS(&ht[e].key, 0ull, (unsigned long long)lo);
+            if (k == 0) return (int)e;
+        }
+        if (k == lo) return (int)e;
+        e = (e + 1) & (RED_ENTRIES - 1);
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void lds_fold(FlowAgg& a, uint32_t idx, uint32_t m) {
+    const uint32_t cdir = misc_dir(m);
+    atomicAdd(&a.acc[cdir], (1ull << 40) | (unsigned long long)misc_len(m));
+    atomicMax(&a.last1, idx + 1);
+    atomicMax(&a.first_n, ~idx);
+    atomicOr(&a.tbits, 1u << misc_tb(m));
+    const uint32_t fl = misc_flags(m);
+    if (misc_tcp(m) && fl) {
+        atomicOr(&a.tflags, fl << (8 * cdir));
+        if (fl & 0x02) atomicMax(&a.syn1[cdir], idx + 1);
+        if (fl & 0x05) atomicMax(&a.fin_n[cdir], ~idx);
+    }
+}
+
+enum RedCount { C_KEYS, C_LIVE, C_CX, C_EX, C_TOUCH, C_SPILL, C_FAIL, C_N };
+
+__global__ __launch_bounds__(RED_THREADS) void k_reduce(BatchView b, Params p, TableView t, FragView f,
+                                                        BinView bv, ExportView ex, BatchCtl* ctl,
+                                                        uint32_t* deferred_list, unsigned long long* stats) {
+    __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
+    __shared__ uint32_t cnt[C_N];
+    __shared__ uint32_t sc[ST_COUNT];
+    const uint32_t part = blockIdx.x / bv.groups, g = blockIdx.x - part * bv.groups;
+    const uint32_t total = min(bv.count[part], bv.cap);
+    const uint32_t beg = g * bv.chunk;
+    if (beg >= total) return;  // uniform over the workgroup
+    const uint32_t end = min(total, beg + bv.chunk);
+    const bool multi = total > bv.chunk;  // other workgroups hold records of these flows too
+    const uint32_t tid = threadIdx.x;
+    {
+        uint4* z = reinterpret_cast<uint4*>(ht);
+        for (uint32_t q = tid; q < sizeof(ht) / 16; q += RED_THREADS) z[q] = make_uint4(0, 0, 0, 0);
+    }
+    if (tid < C_N) cnt[tid] = 0;
+    if (tid < ST_COUNT) sc[tid] = 0;
+    __syncthreads();
+    const uint4* recs = bv.rec + (size_t)part * bv.cap;
+    for (uint32_t k0 = beg; k0 < end; k0 += RED_THREADS * RED_U) {
+        uint4 r[RED_U];
+#pragma unroll
+        for (uint32_t u = 0; u < RED_U; ++u) {
+            const uint32_t k = k0 + u * RED_THREADS + tid;
+            r[u] = k < end ? recs[k] : make_uint4(0, 0, NO_REC, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < RED_U; ++u) {
+            if (r[u].z == NO_REC) continue;
+            const uint64_t lo = ((uint64_t)r[u].y << 32) | r[u].x;
+            const int e = lds_slot(ht, lo, true);
+            if (e >= 0) {
+                lds_fold(ht[e], r[u].z, r[u].w);
+            } else {  // LDS table full: straight into the device table
+                atomicAdd(&cnt[C_SPILL], 1u);
+                if (!merge_packet_atomic(t, lo, r[u].z, r[u].w, &ctl->new_keys))
+                    defer_packet(ctl, deferred_list, r[u].z, false);
+            }
+        }
+    }
+    __syncthreads();
+    // Nothing else of this batch can touch these flows when the workgroup holds all of the
+    // partition's records and no packet went to the fragment or deferred paths.
+    const bool fuse = !multi && ctl->frag_count == 0 && ctl->a_deferred == 0;
+    const bool force_cx = p.force_complex || ctl->nonmono;
+    uint32_t n_keys = 0, n_live = 0, n_cx = 0, n_ex = 0, n_touch = 0;
+    bool failed = false;
+    for (uint32_t e = tid; e < RED_ENTRIES; e += RED_THREADS) {  // same trip count in every lane
+        const FlowAgg a = ht[e];
+        bool do_export = false;
+        uint8_t reason = 0;
+        ipxg_flow_record er;
+        if (a.key) {
+            n_touch++;
+            uint4 head;
+            bool claimed;
+            HotSlot* hp = probe_insert(t, a.key, head, claimed);
+            if (claimed) n_keys++;
+            if (!hp) {
+                ht[e].tflags = a.tflags | RED_FAILED;
+                failed = true;
+            } else if (multi) {
+                agg_merge_atomic(hp, a);
+            } else {
+                HotSlot h = *hp;  // this workgroup is the slot's only writer in this kernel
+                h.key = a.key;
+                agg_fold(h, a);
+                if (fuse) {
+                    const FinResult fr = finalize_slot<false>(b, p, t, f, (uint32_t)(hp - t.hot), h, force_cx,
+                                                              nullptr, er);
+                    if (fr.status == FIN_COMPLEX) n_cx++;
+                    else if (fr.created) n_live++;
+                    do_export = fr.do_export;
+                    reason = fr.reason;
+                } else {
+                    *hp = h;
+                }
+            }
+        }
+        const uint32_t pos = wave_append(ex.count, do_export);
+        if (do_export) {
+            store_export(ex, pos, er, reason);
+            atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
+            n_ex++;
+        }
+    }
+    if (failed) atomicOr(&cnt[C_FAIL], 1u);
+    if (n_keys) atomicAdd(&cnt[C_KEYS], n_keys);
+    if (n_live) atomicAdd(&cnt[C_LIVE], n_live);
+    if (n_cx) atomicAdd(&cnt[C_CX], n_cx);
+    if (n_ex) atomicAdd(&cnt[C_EX], n_ex);
+    if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
+    __syncthreads();
+    if (cnt[C_FAIL]) {  // defer the packets of the flows that found no slot
+        for (uint32_t k = beg + tid; k < end; k += RED_THREADS) {
+            const uint4 r = recs[k];
+            const int e = lds_slot(ht, ((uint64_t)r.y << 32) | r.x, false);
+            if (e >= 0 && (ht[e].tflags & RED_FAILED)) defer_packet(ctl, deferred_list, r.z, false);
+        }
+    }
+    flush_block_stats(sc, stats);
+    if (tid == 0) {
+        if (cnt[C_KEYS]) atomicAdd(&ctl->new_keys, cnt[C_KEYS]);
+        if (cnt[C_LIVE]) atomicAdd(&ctl->new_live, cnt[C_LIVE]);
+        if (cnt[C_CX]) atomicAdd(&ctl->complex_count, cnt[C_CX]);
+        if (cnt[C_EX]) atomicAdd(&ctl->exported, cnt[C_EX]);
+        if (cnt[C_TOUCH]) atomicAdd(&ctl->touched, cnt[C_TOUCH]);
+        if (cnt[C_SPILL]) atomicAdd(&ctl->spilled, cnt[C_SPILL]);
+        if (!fuse || cnt[C_SPILL] || cnt[C_FAIL]) ctl->pending = 1;
+    }
+}
+
+void launch_reduce(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
+                   ExportView ex, BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats) {
+    const uint32_t grid = (1u << bv.part_bits) * bv.groups;
+    hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(RED_THREADS), 0, st, b, p, t, f, bv, ex, ctl, deferred_list,
+                       stats);
+}
+
+}  // namespace ipxg

@@ -1,211 +1,31 @@
-// ipxg_kernels.hip -- the engine's HIP kernels for gfx950.
+// ipxg_kernels.hip -- the engine's table and slow-path kernels for gfx950 (the per-batch
+// ingest, k_bin + k_reduce, is in ipxg_ingest.hip).
 //
-// Per batch (ipxg_submit):
-//   k_ingest<INGEST>   one lane per packet: stage <=128 header bytes in LDS, parse
-//                      (parse_packet), build key + inverse key, 2x XXH64, probe the open-
-//                      addressed flow table by the canonical hash, and fold the packet into
-//                      the slot's per-batch accumulators with integer atomics.  Fragments
-//                      are diverted to the fragmentation-cache path.      (HBM-bound)
+//   k_ingest<INGEST>   the atomic ingest mode (cfg flag IPXG_CFG_ATOMIC_INGEST, kept for A/B
+//                      measurement): one lane per packet folds straight into the table with
+//                      device atomics.  k_ingest<GATHER> collects the packets of complex flows.
 //   k_frag_walk        fragments sorted by (bucket, index): one lane per bucket replays the
 //                      reference's 4-entry ring in arrival order (fragmentationCache.cpp).
 //   k_frag_accumulate  folds the port-resolved fragments into the table.
-//   k_finalize         one lane per slot: applies the reference's split rules at the batch
-//                      boundary and merges the batch accumulators into the flow record, or
-//                      marks the flow "complex" when a split could fall inside the batch.
+//   k_deferred         re-applies packets whose probe failed, after the table has grown.
+//   k_finalize         full-table scan applying finalize_slot to every slot still holding
+//                      batch accumulators (when k_reduce could not finalise them itself).
 //   k_complex_*        complex flows only: gather their packets, sort by index, and replay
 //                      put_pkt_recursive sequentially per flow (cache.cpp:330-491).
 // Maintenance: k_expire (export_expired), k_finish (finish), k_rehash (table growth).
-#include "ipxg_device.hpp"
-#include "ipxg_kernels.hpp"
+#include "ipxg_table.hpp"
 
 namespace ipxg {
 
-// ---- helpers ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-
-// Wave-aggregated append: one atomic per wave instead of one per lane.
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
-    uint64_t m = __ballot(pred);
-    if (m == 0) return 0;
-    uint32_t lane = lane_id();
-    uint32_t leader = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
-    return base + (uint32_t)__popcll(below);
-}
-
-template <class T>
-__device__ __forceinline__ T ld_relaxed(T* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
-// zero-masked past caplen, plus one zero chunk so straddling reads see zeros.
-__device__ __forceinline__ void stage_frame(uint32_t* col, const uint8_t* arena, uint32_t off,
-                                            uint32_t cap) {
-    const uint32_t nbytes = cap < IPXG_WIN ? cap : IPXG_WIN;
-    const uint32_t nch = (nbytes + 15) >> 4;
-    const uint8_t* f = arena + off;
-    constexpr int NCH = IPXG_WIN / 16;
-    if ((off & 15) == 0) {
-        uint4 v[NCH];
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-            v[ch] = make_uint4(0, 0, 0, 0);
-            if ((uint32_t)ch < nch) v[ch] = *reinterpret_cast<const uint4*>(f + 16 * ch);
-        }
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-            if ((uint32_t)ch > nch) break;
-            uint32_t w[4] = {v[ch].x, v[ch].y, v[ch].z, v[ch].w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                int b0 = 16 * ch + 4 * k;
-                int valid = (int)cap - b0;
-                uint32_t m = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
-                col[(4 * ch + k) * IPXG_BLOCK] = w[k] & m;
-            }
-        }
-    } else {  // unaligned frame: byte loads (correct for any offset)
-        for (uint32_t dw = 0; dw < 4 * (nch + (nch < NCH ? 1 : 0)); ++dw) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint32_t o = dw * 4 + k;
-                if (o < nbytes) w |= (uint32_t)f[o] << (8 * k);
-            }
-            col[dw * IPXG_BLOCK] = w;
-        }
-    }
-}
-
-// LDS window with caplen guard (bytes >= caplen read as 0).
-struct LdsFrame {
-    LdsWin w;
-    __device__ __forceinline__ uint32_t b(uint32_t o) const { return o < w.g.cap ? w.b(o) : 0u; }
-    __device__ __forceinline__ uint32_t le32(uint32_t o) const { return o < w.g.cap ? w.le32(o) : 0u; }
-};
-
-__device__ __forceinline__ void apply_frag_ports(const Params& p, const FragView& f, uint32_t idx,
-                                                 DevPkt& pk) {
-    if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
-        uint32_t pp = f.ports[idx];
-        pk.src_port = (uint16_t)(pp >> 16);
-        pk.dst_port = (uint16_t)(pp & 0xFFFF);
-    }
-}
-
-// canonical biflow hash and the packet's direction relative to it
-__device__ __forceinline__ void canon(const DevPkt& pk, const Params& p, uint64_t& lo, uint32_t& cdir,
-                                      uint64_t& hf) {
-    FlowKey kf, ki;
-    build_keys(pk, kf, ki);
-    hf = key_hash(kf);
-    if (p.split_biflow) {
-        lo = hf;
-        cdir = 0;
-        return;
-    }
-    uint64_t hi = key_hash(ki);
-    lo = hf < hi ? hf : hi;
-    cdir = hf > hi ? 1u : 0u;
-}
-
-__device__ __forceinline__ uint32_t time_bucket(uint32_t sec, uint32_t base, uint32_t w) {
-    if (sec < base) return 31;
-    uint32_t b = (sec - base) / w;
-    return b > 30 ? 31 : b;
-}
-
-// Probe for (and if absent claim) the slot of canonical hash lo; nullptr after MAX_PROBE.
-// One 16-byte load per probe returns the key together with first_n and tbits, so the
-// caller can skip reductions that cannot change them.  A stale copy is harmless: a stale
-// empty key falls through to the CAS (which returns the true owner), and stale first_n/tbits
-// only cause a redundant atomic.
-__device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo, uint4& head) {
-    uint32_t s = (uint32_t)lo & t.mask;
-    for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
-        HotSlot* h = &t.hot[s];
-        head = *reinterpret_cast<const uint4*>(h);
-        uint64_t k = ((uint64_t)head.y << 32) | head.x;
-        if (k == 0) {
-            unsigned long long old = atomicCAS((unsigned long long*)&h->key, 0ull, (unsigned long long)lo);
-            if (old == 0) {
-                head = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), 0, 0);
-                return h;
-            }
-            k = old;
-            head.z = 0;  // unknown: force the reductions
-            head.w = 0;
-        }
-        if (k == lo) return h;
-        s = (s + 1) & t.mask;
-    }
-    return nullptr;
-}
-
-__device__ __forceinline__ int64_t probe_find(const TableView& t, uint64_t lo) {
-    uint32_t s = (uint32_t)lo & t.mask;
-    for (uint32_t probe = 0; probe <= t.mask; ++probe) {
-        uint64_t k = t.hot[s].key;
-        if (k == lo) return s;
-        if (k == 0) return -1;
-        s = (s + 1) & t.mask;
-    }
-    return -1;
-}
-
-// Fold one packet into its flow's per-batch accumulators (NHTFlowCache::put_pkt's update,
-// cache.cpp:134-152, as order-independent reductions keyed by packet index).
+// Fold one parsed packet into its flow's batch accumulators with device atomics (the
+// slow paths: fragments, deferred packets, and the atomic ingest mode).
 __device__ __forceinline__ bool flow_accumulate(const TableView& t, const Params& p, const BatchView& b,
-                                                const DevPkt& pk, uint32_t idx, uint32_t sec) {
+                                                const DevPkt& pk, uint32_t idx, uint32_t sec, uint32_t* new_keys) {
     uint64_t lo, hf;
     uint32_t cdir;
     canon(pk, p, lo, cdir, hf);
-    uint4 head;
-    HotSlot* h = probe_insert(t, lo, head);
-    if (!h) return false;
-    atomicAdd((unsigned long long*)&h->acc[cdir], (1ull << 40) | (uint64_t)pk.ip_len);
-    atomicMax(&h->last1, idx + 1);
-    const uint32_t fn = ~idx;
-    if (head.z < fn) atomicMax(&h->first_n, fn);
-    const uint32_t tb = 1u << time_bucket(sec, b.base_sec, p.bucket_w);
-    if (!(head.w & tb)) atomicOr(&h->tbits, tb);
-    const uint32_t fl = pk.tcp_flags;
-    if (pk.ip_proto == 6 && fl) {
-        atomicOr(&h->tflags, fl << (8 * cdir));
-        if (fl & 0x02) atomicMax(&h->syn1[cdir], idx + 1);
-        if (fl & 0x05) atomicMax(&h->fin_n[cdir], ~idx);
-    }
-    return true;
-}
-
-__device__ __forceinline__ void flush_counts(const ParseCounts& c, uint32_t keyless, uint32_t frags,
-                                             uint32_t* sc) {
-    atomicAdd(&sc[ST_SEEN], c.seen);
-    atomicAdd(&sc[ST_PARSED], c.parsed);
-    atomicAdd(&sc[ST_UNKNOWN], c.unknown);
-    atomicAdd(&sc[ST_IPV4], c.ipv4);
-    atomicAdd(&sc[ST_IPV6], c.ipv6);
-    atomicAdd(&sc[ST_TCP], c.tcp);
-    atomicAdd(&sc[ST_UDP], c.udp);
-    atomicAdd(&sc[ST_MPLS], c.mpls);
-    atomicAdd(&sc[ST_PPPOE], c.pppoe);
-    atomicAdd(&sc[ST_TRILL], c.trill);
-    atomicAdd(&sc[ST_VLAN], c.vlan);
-    atomicAdd(&sc[ST_IPV4_BYTES], c.ipv4_bytes);
-    atomicAdd(&sc[ST_IPV6_BYTES], c.ipv6_bytes);
-    atomicAdd(&sc[ST_KEYLESS], keyless);
-    atomicAdd(&sc[ST_FRAGMENTED], frags);
-}
-
-__device__ __forceinline__ void flush_block_stats(uint32_t* sc, unsigned long long* stats) {
-    __syncthreads();
-    if (threadIdx.x < ST_COUNT && sc[threadIdx.x])
-        atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + threadIdx.x],
-                  (unsigned long long)sc[threadIdx.x]);
+    return merge_packet_atomic(t, lo, idx, pack_misc(pk, cdir, time_bucket(sec, b.base_sec, p.bucket_w)),
+                               new_keys);
 }
 
 // ---- K1: ingest ------------------------------------------------------------------------
@@ -265,7 +85,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, Ta
                 f.list[pos] = ((uint64_t)bucket << 24) | i;
                 continue;
             }
-            if (!flow_accumulate(t, p, b, pk, i, d.ts_sec)) {
+            if (!flow_accumulate(t, p, b, pk, i, d.ts_sec, &ctl->new_keys)) {
                 uint32_t pos = atomicAdd(&ctl->deferred, 1u);
                 deferred_list[pos] = i;
             }
@@ -305,32 +125,6 @@ void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, 
                            FragView f, ComplexView cx) {
     hipLaunchKernelGGL(k_ingest<MODE_GATHER>, dim3(grid_for(b.n, 1024)), dim3(IPXG_BLOCK), 0, st, b, p,
                        t, f, nullptr, nullptr, nullptr, cx);
-}
-
-// ---- re-parse of one packet straight from HBM --------------------------------------------
-template <bool FULL>
-__device__ __forceinline__ bool reparse(const BatchView& b, const Params& p, const FragView& f,
-                                        uint32_t idx, DevPkt& pk, ipxg_pkt_desc& d) {
-    d = b.desc[idx];
-    GlobalSrc g{b.arena + d.offset, d.caplen};
-    ParseCounts dummy = {};
-    if (!parse_frame<FULL>(g, d.caplen, p.dlt, pk, dummy)) return false;
-    apply_frag_ports(p, f, idx, pk);
-    return true;
-}
-
-// Same, but the header bytes are staged into this lane's LDS column with 16-byte loads
-// (blockDim.x must be IPXG_BLOCK).
-template <bool FULL>
-__device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p, const FragView& f,
-                                            uint32_t idx, uint32_t* col, DevPkt& pk, ipxg_pkt_desc& d) {
-    d = b.desc[idx];
-    stage_frame(col, b.arena, d.offset, d.caplen);
-    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-    ParseCounts dummy = {};
-    if (!parse_frame<FULL>(S, d.caplen, p.dlt, pk, dummy)) return false;
-    apply_frag_ports(p, f, idx, pk);
-    return true;
 }
 
 // ---- fragmentation cache -----------------------------------------------------------------
@@ -416,7 +210,7 @@ __global__ __launch_bounds__(256) void k_frag_accumulate(BatchView b, Params p, 
     DevPkt pk;
     ipxg_pkt_desc d;
     if (!reparse<false>(b, p, f, idx, pk, d)) return;
-    if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec)) {
+    if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec, &ctl->new_keys)) {
         uint32_t pos = atomicAdd(&ctl->deferred, 1u);
         deferred_list[pos] = idx;
     }
@@ -439,7 +233,7 @@ __global__ __launch_bounds__(256) void k_deferred(BatchView b, Params p, TableVi
     DevPkt pk;
     ipxg_pkt_desc d;
     if (!reparse<false>(b, p, f, idx, pk, d)) return;
-    if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec)) {
+    if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec, &ctl->new_keys)) {
         uint32_t pos = atomicAdd(&ctl->deferred, 1u);
         out_list[pos] = idx;
     }
@@ -451,63 +245,11 @@ void launch_deferred(hipStream_t st, const BatchView& b, const Params& p, TableV
                        ctl, out_list);
 }
 
-// ---- flow record construction (FlowRecord::create/update, cache.cpp:94-152) ---------------
-__device__ __forceinline__ void rec_create(ipxg_flow_record& r, const DevPkt& pk, const ipxg_pkt_desc& d,
-                                           uint64_t hf, uint32_t cdir) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(&r);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) w[k] = 0;
-    r.flow_hash = hf;
-    r.time_first_sec = r.time_last_sec = d.ts_sec;
-    r.time_first_usec = r.time_last_usec = d.ts_usec;
-    r.ip_version = pk.ip_version;
-    r.ip_proto = pk.ip_proto;
-    for (int k = 0; k < 4; ++k) {
-        for (int q = 0; q < 4; ++q) {
-            r.src_ip[4 * k + q] = (uint8_t)(pk.sip[k] >> (8 * q));
-            r.dst_ip[4 * k + q] = (uint8_t)(pk.dip[k] >> (8 * q));
-        }
-    }
-    const uint32_t m[3] = {pk.mac_lo, pk.mac_mid, pk.mac_hi};
-    for (int q = 0; q < 6; ++q) {
-        r.dst_mac[q] = (uint8_t)(m[q >> 2] >> (8 * (q & 3)));
-        r.src_mac[q] = (uint8_t)(m[(q + 6) >> 2] >> (8 * ((q + 6) & 3)));
-    }
-    const uint8_t pr = pk.ip_proto;
-    if (pr == 6 || pr == 17 || pr == 1 || pr == 58) {
-        r.src_port = pk.src_port;
-        r.dst_port = pk.dst_port;
-    }
-    r.vlan_id = (uint16_t)pk.vlan_id;
-    r.reserved[0] = (uint8_t)cdir;  // creator's canonical direction (not exported)
-}
-
-__device__ __forceinline__ uint8_t export_reason(const ipxg_flow_record& r) {
-    return ((r.src_tcp_flags | r.dst_tcp_flags) & 0x05) ? IPXG_FLOW_END_EOF : IPXG_FLOW_END_INACTIVE;
-}
-
-__device__ __forceinline__ void store_export(ExportView ex, uint32_t pos, const ipxg_flow_record& r,
-                                             uint8_t reason) {
-    if (pos >= ex.cap) return;  // host guarantees capacity; never taken
-    ipxg_flow_record o = r;
-    o.end_reason = reason;
-    o.reserved0 = 0;
-    for (int k = 0; k < 24; ++k) o.reserved[k] = 0;
-    ex.buf[pos] = o;
-}
-
 __device__ __forceinline__ void reason_count(uint32_t* sc, uint8_t reason) {
     atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
 }
 
-__device__ __forceinline__ void clear_slot(HotSlot* h, uint64_t key, uint32_t state) {
-    HotSlot z = {};
-    z.key = key;
-    z.state = state;
-    *h = z;
-}
-
-// ---- K3: finalize ------------------------------------------------------------------------
+// ---- K3: finalize (full-table scan; the fast path finalises inside k_reduce) -------------
 __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableView t, FragView f,
                                                   ExportView ex, BatchCtl* ctl, unsigned long long* stats,
                                                   uint32_t cap) {
@@ -519,80 +261,25 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
     __syncthreads();
     uint32_t keys = 0, live_n = 0, cx_n = 0, ex_n = 0;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        HotSlot h = t.hot[s];
+        const HotSlot h = t.hot[s];
         bool do_export = false;
         uint8_t reason = 0;
         ipxg_flow_record er;
         if (h.key != 0) {
             keys++;
-            if (h.last1 == 0) {
-                if (h.state & SLOT_LIVE) live_n++;
+            const bool was_live = h.state & SLOT_LIVE;
+            if (h.last1 == 0 || (h.state & SLOT_COMPLEX)) {  // untouched, or already decided
+                if (was_live) live_n++;
             } else {
-                const uint32_t first = ~h.first_n, last = h.last1 - 1;
-                const bool live = h.state & SLOT_LIVE;
-                ipxg_flow_record rec;
-                if (live) rec = t.cold[s];
-                DevPkt fp;
-                ipxg_pkt_desc df;
-                reparse_lds<true>(b, p, f, first, &win[threadIdx.x], fp, df);
-                const ipxg_pkt_desc dl = b.desc[last];
-                uint64_t lo, hf;
-                uint32_t cdf;
-                canon(fp, p, lo, cdf, hf);
-                const uint32_t I = p.inactive_s, A = p.active_s;
-                // the reference's checks at the batch's first packet (cache.cpp:431-472)
-                uint8_t bsplit = 0;
-                if (live) {
-                    const uint32_t creator = rec.reserved[0];
-                    const bool dsrc = p.split_biflow || cdf == creator;
-                    const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
-                    if ((fp.tcp_flags & 0x02) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
-                    else if ((int64_t)df.ts_sec - (int64_t)rec.time_last_sec >= (int64_t)I) bsplit = export_reason(rec);
-                    else if ((int64_t)df.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
-                }
-                const bool cont = live && !bsplit;
-                // could a split fall strictly inside the batch?
-                bool cx = p.force_complex != 0;
-                const uint32_t tb = h.tbits;
-                if (tb >> 31) cx = true;
-                else if (tb) {
-                    uint32_t x = tb >> __builtin_ctz(tb);
-                    if (x & (x + 1)) cx = true;  // an empty bucket between two busy ones
-                }
-                const uint32_t tfirst = cont ? rec.time_first_sec : df.ts_sec;
-                if ((int64_t)dl.ts_sec - (int64_t)tfirst >= (int64_t)A) cx = true;
-                for (int dd = 0; dd < 2; ++dd) {
-                    if (!h.syn1[dd]) continue;
-                    const uint32_t sidx = h.syn1[dd] - 1;
-                    if (cont) {
-                        const uint8_t cf = (uint32_t)dd == rec.reserved[0] ? rec.src_tcp_flags : rec.dst_tcp_flags;
-                        if (cf & 0x05) cx = true;
-                    }
-                    if (h.fin_n[dd] && sidx > ~h.fin_n[dd]) cx = true;
-                }
-                if (cx) {
-                    t.hot[s].state = h.state | SLOT_COMPLEX;
+                const FinResult fr = finalize_slot<true>(b, p, t, f, s, h, p.force_complex != 0,
+                                                         &win[threadIdx.x], er);
+                if (fr.status == FIN_COMPLEX) {
                     cx_n++;
+                    if (was_live) live_n++;
                 } else {
-                    if (bsplit) {
-                        do_export = true;
-                        reason = bsplit;
-                        er = rec;
-                    }
-                    if (!cont) rec_create(rec, fp, df, hf, cdf);
-                    const uint32_t sd = rec.reserved[0];
-                    const uint64_t as = h.acc[sd], ad = h.acc[sd ^ 1];
-                    rec.src_packets += (uint32_t)(as >> 40);
-                    rec.src_bytes += as & ACC_BYTES_MASK;
-                    rec.dst_packets += (uint32_t)(ad >> 40);
-                    rec.dst_bytes += ad & ACC_BYTES_MASK;
-                    rec.src_tcp_flags |= (uint8_t)(h.tflags >> (8 * sd));
-                    rec.dst_tcp_flags |= (uint8_t)(h.tflags >> (8 * (sd ^ 1)));
-                    rec.time_last_sec = dl.ts_sec;
-                    rec.time_last_usec = dl.ts_usec;
-                    t.cold[s] = rec;
-                    clear_slot(&t.hot[s], h.key, SLOT_LIVE);
                     live_n++;
+                    do_export = fr.do_export;
+                    reason = fr.reason;
                 }
             }
         }
@@ -657,6 +344,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
     const uint32_t s = cx.slot_of[r];
     const HotSlot h = t.hot[s];
     bool live = h.state & SLOT_LIVE;
+    if (!live) atomicAdd(&ctl->cx_new_live, 1u);  // the slot ends the walk live
     ipxg_flow_record rec;
     if (live) rec = t.cold[s];
     const uint32_t seg = cx.seg[r], len = cx.len[r];
@@ -719,57 +407,89 @@ void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, Ta
 }
 
 // ---- maintenance: export_expired / finish / rehash / count ------------------------------
+constexpr uint32_t SCAN_PER_THREAD = 8;  // slots per thread in the export scans
+
+static inline uint32_t scan_grid(uint32_t cap) {
+    const uint32_t per = 256 * SCAN_PER_THREAD;
+    return (cap + per - 1) / per;
+}
+
+// Export every live record idle for >= inactive seconds at `now` (export_expired,
+// cache.cpp:508-523, over the whole table).  Slots [blk*2048, +2048), 8 per thread; one
+// export-buffer reservation per block (a single counter saturates at ~88 returning
+// atomics/us: MI355X_MICROARCH.md "dequeue").
 __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t cap, int64_t now,
                                                 ExportView ex, unsigned long long* stats) {
+    __shared__ uint32_t scratch[8];
     __shared__ uint32_t sc[ST_COUNT];
+    __shared__ uint32_t bbase;
     if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
+    uint32_t mask = 0, c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
+        const uint32_t s = base + j * 256 + threadIdx.x;
+        if (s >= cap) continue;
+        const uint64_t key = t.hot[s].key;
+        const uint32_t state = t.hot[s].state;
+        if (key != 0 && (state & SLOT_LIVE) &&
+            now - (int64_t)t.cold[s].time_last_sec >= (int64_t)p.inactive_s) {
+            t.hot[s].state = state & ~SLOT_LIVE;
+            mask |= 1u << j;
+            c++;
+        }
+    }
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
+    if (threadIdx.x == 0) bbase = total ? atomicAdd(ex.count, total) : 0;
     __syncthreads();
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const HotSlot& h = t.hot[s];
-        bool do_export = false;
-        uint8_t reason = 0;
-        ipxg_flow_record rec;
-        if (h.key != 0 && (h.state & SLOT_LIVE)) {
-            rec = t.cold[s];
-            if (now - (int64_t)rec.time_last_sec >= (int64_t)p.inactive_s) {
-                do_export = true;
-                reason = export_reason(rec);
-                t.hot[s].state = h.state & ~SLOT_LIVE;
-            }
-        }
-        uint32_t pos = wave_append(ex.count, do_export);
-        if (do_export) {
-            store_export(ex, pos, rec, reason);
-            reason_count(sc, reason);
-        }
+    uint32_t pos = bbase + off;
+#pragma unroll
+    for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
+        if (!(mask >> j & 1)) continue;
+        const ipxg_flow_record rec = t.cold[base + j * 256 + threadIdx.x];
+        const uint8_t reason = export_reason(rec);
+        store_export(ex, pos++, rec, reason);
+        reason_count(sc, reason);
     }
     flush_block_stats(sc, stats);
 }
 
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
                    ExportView ex, unsigned long long* stats) {
-    hipLaunchKernelGGL(k_expire, dim3(table_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats);
+    hipLaunchKernelGGL(k_expire, dim3(scan_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats);
 }
 
+// Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288).
 __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
                                                 unsigned long long* stats) {
-    __shared__ uint32_t sc[ST_COUNT];
-    if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const HotSlot& h = t.hot[s];
-        const bool do_export = h.key != 0 && (h.state & SLOT_LIVE);
-        uint32_t pos = wave_append(ex.count, do_export);
-        if (do_export) {
-            store_export(ex, pos, t.cold[s], IPXG_FLOW_END_FORCED);
-            reason_count(sc, IPXG_FLOW_END_FORCED);
+    __shared__ uint32_t scratch[8];
+    __shared__ uint32_t bbase;
+    const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
+    uint32_t mask = 0, c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
+        const uint32_t s = base + j * 256 + threadIdx.x;
+        if (s >= cap) continue;
+        if (t.hot[s].key != 0 && (t.hot[s].state & SLOT_LIVE)) {
+            mask |= 1u << j;
+            c++;
         }
     }
-    flush_block_stats(sc, stats);
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
+    if (threadIdx.x == 0) bbase = total ? atomicAdd(ex.count, total) : 0;
+    __syncthreads();
+    uint32_t pos = bbase + off;
+#pragma unroll
+    for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j)
+        if (mask >> j & 1) store_export(ex, pos++, t.cold[base + j * 256 + threadIdx.x], IPXG_FLOW_END_FORCED);
+    if (threadIdx.x == 0 && total)
+        atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + ST_END_FORCED], (unsigned long long)total);
 }
 
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats) {
-    hipLaunchKernelGGL(k_finish, dim3(table_grid(cap)), dim3(256), 0, st, t, cap, ex, stats);
+    hipLaunchKernelGGL(k_finish, dim3(scan_grid(cap)), dim3(256), 0, st, t, cap, ex, stats);
 }
 
 __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_cap, TableView to,

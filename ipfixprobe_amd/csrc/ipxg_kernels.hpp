@@ -34,14 +34,20 @@ constexpr uint32_t MAX_PROBE = 64;
 struct BatchCtl {
     uint32_t nonmono;        // a packet's timestamp went backwards
     uint32_t frag_count;     // fragments routed to the fragmentation-cache path
-    uint32_t deferred;       // packets whose table probe exceeded MAX_PROBE
-    uint32_t complex_count;  // flows k_finalize handed to the sequential path
+    uint32_t deferred;       // packets whose table probe exceeded MAX_PROBE (list length)
+    uint32_t a_deferred;     //   of which deferred by k_bin (read by k_reduce)
     uint64_t cx_alloc;       // (rank << 32) | packets, complex-flow segment allocator
-    uint32_t keys;           // non-empty slots after k_finalize
-    uint32_t live;           // live records after k_finalize
+    uint32_t complex_count;  // flows handed to the sequential path
+    uint32_t pending;        // touched slots left for the k_finalize scan
+    uint32_t keys;           // non-empty slots (k_finalize / k_count scans)
+    uint32_t live;           // live records (k_finalize / k_count scans)
+    uint32_t new_keys;       // slots claimed during this batch
+    uint32_t new_live;       // records created on a non-live slot by k_reduce
+    uint32_t cx_new_live;    // ... by k_complex_walk
     uint32_t last_sec, last_usec;  // timestamp of the batch's last packet
     uint32_t exported;       // records exported while applying this batch
-    uint32_t pad[5];
+    uint32_t touched;        // flow aggregates built by k_reduce (partition sizing)
+    uint32_t spilled;        // packets that fell back to direct atomic accumulation
 };
 
 // Fragmentation-cache ring entry (fragmentationKeyData.hpp:49-112), 4 per bucket.
@@ -71,7 +77,7 @@ struct TableView {
 
 struct ExportView {
     ipxg_flow_record* buf;
-    uint32_t* count;
+    uint32_t* count;  // [0] records appended, [1] overflow flag (never set when sized right)
     uint32_t cap;
 };
 
@@ -103,6 +109,22 @@ struct FragView {
     uint32_t* ports;     // per packet index: resolved (sport << 16) | dport
 };
 
+// Phase-A output of the ingest (k_bin -> k_reduce): one record region per partition of the
+// canonical flow hash (bits 32.. of lo).  Record = {lo, hi, packet index, pack_misc()}.
+struct BinView {
+    uint4* rec;          // parts * cap records
+    uint32_t* count;     // per partition, zeroed per batch (may exceed cap: overflow spilled)
+    uint32_t cap;        // record slots per partition = groups * chunk
+    uint32_t chunk;      // records per k_reduce workgroup
+    uint32_t part_bits;  // parts = 1 << part_bits
+    uint32_t groups;     // k_reduce workgroups per partition
+};
+constexpr uint32_t BIN_MAX_PART_BITS = 11;  // <= 2048 partitions (k_bin's LDS histogram)
+constexpr uint32_t RED_THREADS = 1024;      // k_reduce workgroup
+constexpr uint32_t RED_ENTRIES = 2048;      // k_reduce LDS flow table (56 B entries)
+constexpr uint32_t RED_TARGET_FLOWS = 600;  // flows per partition the host sizes for
+constexpr uint32_t RED_MAX_CHUNK = 65536;   // records per k_reduce workgroup at most
+
 struct ComplexView {
     uint64_t* list;      // (rank << 24) | packet index
     uint64_t* sorted;
@@ -113,6 +135,10 @@ struct ComplexView {
 };
 
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
+void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
+                BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
+void launch_reduce(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
+                   ExportView ex, BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
 void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,

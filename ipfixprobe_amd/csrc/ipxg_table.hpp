@@ -1,0 +1,465 @@
+// ipxg_table.hpp -- device helpers shared by the ingest kernels (ipxg_ingest.hip) and the
+// table kernels (ipxg_kernels.hip): wave/block counting, flow-table probing, the per-packet
+// and per-aggregate merges into a slot's batch accumulators, flow-record construction
+// (FlowRecord::create, cache.cpp:94-133) and the per-slot batch finalisation (the
+// reference's split rules of put_pkt_recursive, cache.cpp:428-486, applied at the batch
+// boundary from the recorded packet indices).
+#pragma once
+
+#include "ipxg_device.hpp"
+#include "ipxg_kernels.hpp"
+
+namespace ipxg {
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave-aggregated append: one atomic per wave instead of one per lane.  Every lane of the
+// wave must call it (convergent).
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+    uint64_t m = __ballot(pred);
+    if (m == 0) return 0;
+    uint32_t lane = lane_id();
+    uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    return base + (uint32_t)__popcll(below);
+}
+
+// Exclusive prefix sum of v over a block of NT threads (NT a multiple of 64, <= 1024);
+// *total receives the block sum.  `scratch` holds NT/64 + 1 words of LDS.  Contains
+// __syncthreads(): every thread of the block must call it.
+template <int NT>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
+    constexpr int NW = NT / 64;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) scratch[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (int k = 0; k < NW; ++k) {
+            uint32_t t = scratch[k];
+            scratch[k] = s;
+            s += t;
+        }
+        scratch[NW] = s;
+    }
+    __syncthreads();
+    const uint32_t r = scratch[w] + x - v;
+    *total = scratch[NW];
+    __syncthreads();
+    return r;
+}
+
+// ---- block statistics ---------------------------------------------------------------------
+__device__ __forceinline__ void flush_counts(const ParseCounts& c, uint32_t keyless, uint32_t frags,
+                                             uint32_t* sc) {
+    atomicAdd(&sc[ST_SEEN], c.seen);
+    atomicAdd(&sc[ST_PARSED], c.parsed);
+    atomicAdd(&sc[ST_UNKNOWN], c.unknown);
+    atomicAdd(&sc[ST_IPV4], c.ipv4);
+    atomicAdd(&sc[ST_IPV6], c.ipv6);
+    atomicAdd(&sc[ST_TCP], c.tcp);
+    atomicAdd(&sc[ST_UDP], c.udp);
+    atomicAdd(&sc[ST_MPLS], c.mpls);
+    atomicAdd(&sc[ST_PPPOE], c.pppoe);
+    atomicAdd(&sc[ST_TRILL], c.trill);
+    atomicAdd(&sc[ST_VLAN], c.vlan);
+    atomicAdd(&sc[ST_IPV4_BYTES], c.ipv4_bytes);
+    atomicAdd(&sc[ST_IPV6_BYTES], c.ipv6_bytes);
+    atomicAdd(&sc[ST_KEYLESS], keyless);
+    atomicAdd(&sc[ST_FRAGMENTED], frags);
+}
+
+// sc: ST_COUNT block-local counters in LDS; one device atomic per non-zero counter.
+__device__ __forceinline__ void flush_block_stats(uint32_t* sc, unsigned long long* stats) {
+    __syncthreads();
+    if (threadIdx.x < ST_COUNT && sc[threadIdx.x])
+        atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + threadIdx.x],
+                  (unsigned long long)sc[threadIdx.x]);
+}
+
+// ---- canonical biflow hash --------------------------------------------------------------
+// lo = min(XXH64(key), XXH64(key_inv)) identifies the biflow (the reference's identity is
+// the 64-bit hash too, cache.cpp:84-92, looked up forward then inverse, :341-373); cdir is
+// the packet's direction relative to lo; hf the forward hash (the record's flow_hash).
+__device__ __forceinline__ void canon(const DevPkt& pk, const Params& p, uint64_t& lo, uint32_t& cdir,
+                                      uint64_t& hf) {
+    FlowKey kf, ki;
+    build_keys(pk, kf, ki);
+    hf = key_hash(kf);
+    if (p.split_biflow) {
+        lo = hf;
+        cdir = 0;
+        return;
+    }
+    uint64_t hi = key_hash(ki);
+    lo = hf < hi ? hf : hi;
+    cdir = hf > hi ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint32_t time_bucket(uint32_t sec, uint32_t base, uint32_t w) {
+    if (sec < base) return 31;
+    uint32_t b = (sec - base) / w;
+    return b > 30 ? 31 : b;
+}
+
+// Per-packet contribution packed into one word (also the bin record's 4th word):
+// ip_len | tcp_flags << 16 | cdir << 24 | tcp << 25 | time bucket << 26.
+__device__ __forceinline__ uint32_t pack_misc(const DevPkt& pk, uint32_t cdir, uint32_t tb) {
+    return (uint32_t)pk.ip_len | ((uint32_t)pk.tcp_flags << 16) | (cdir << 24) |
+           ((pk.ip_proto == 6 ? 1u : 0u) << 25) | (tb << 26);
+}
+__device__ __forceinline__ uint32_t misc_len(uint32_t m) { return m & 0xFFFF; }
+__device__ __forceinline__ uint32_t misc_flags(uint32_t m) { return (m >> 16) & 0xFF; }
+__device__ __forceinline__ uint32_t misc_dir(uint32_t m) { return (m >> 24) & 1; }
+__device__ __forceinline__ bool misc_tcp(uint32_t m) { return (m >> 25) & 1; }
+__device__ __forceinline__ uint32_t misc_tb(uint32_t m) { return (m >> 26) & 31; }
+
+// ---- flow-table probing (open addressing, linear probing, capacity 2^k) ------------------
+// Probe for (and if absent claim) the slot of canonical hash lo; nullptr after MAX_PROBE.
+// One 16-byte load per probe returns the key together with first_n and tbits, so the
+// caller can skip reductions that cannot change them.  A stale copy is harmless: a stale
+// empty key falls through to the CAS (which returns the true owner), and stale first_n/tbits
+// only cause a redundant atomic.  *claimed is set when this call took an empty slot.
+__device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo, uint4& head, bool& claimed) {
+    uint32_t s = (uint32_t)lo & t.mask;
+    claimed = false;
+    for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
+        HotSlot* h = &t.hot[s];
+        head = *reinterpret_cast<const uint4*>(h);
+        uint64_t k = ((uint64_t)head.y << 32) | head.x;
+        if (k == 0) {
+            unsigned long long old = atomicCAS((unsigned long long*)&h->key, 0ull, (unsigned long long)lo);
+            if (old == 0) {
+                head = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), 0, 0);
+                claimed = true;
+                return h;
+            }
+            k = old;
+            head.z = 0;  // unknown: force the reductions
+            head.w = 0;
+        }
+        if (k == lo) return h;
+        s = (s + 1) & t.mask;
+    }
+    return nullptr;
+}
+
+__device__ __forceinline__ int64_t probe_find(const TableView& t, uint64_t lo) {
+    uint32_t s = (uint32_t)lo & t.mask;
+    for (uint32_t probe = 0; probe <= t.mask; ++probe) {
+        uint64_t k = t.hot[s].key;
+        if (k == lo) return s;
+        if (k == 0) return -1;
+        s = (s + 1) & t.mask;
+    }
+    return -1;
+}
+
+// Fold one packet (canonical hash lo, packet index idx, packed contribution m) into its
+// slot's batch accumulators with device atomics (NHTFlowCache::put_pkt's update,
+// cache.cpp:134-152, as order-independent reductions keyed by packet index).  Returns false
+// when the probe failed (the caller defers the packet until the table has grown).
+__device__ __forceinline__ bool merge_packet_atomic(const TableView& t, uint64_t lo, uint32_t idx, uint32_t m,
+                                                    uint32_t* new_keys) {
+    uint4 head;
+    bool claimed;
+    HotSlot* h = probe_insert(t, lo, head, claimed);
+    if (!h) return false;
+    if (claimed) atomicAdd(new_keys, 1u);
+    const uint32_t cdir = misc_dir(m);
+    atomicAdd((unsigned long long*)&h->acc[cdir], (1ull << 40) | (uint64_t)misc_len(m));
+    atomicMax(&h->last1, idx + 1);
+    const uint32_t fn = ~idx;
+    if (head.z < fn) atomicMax(&h->first_n, fn);
+    const uint32_t tb = 1u << misc_tb(m);
+    if (!(head.w & tb)) atomicOr(&h->tbits, tb);
+    const uint32_t fl = misc_flags(m);
+    if (misc_tcp(m) && fl) {
+        atomicOr(&h->tflags, fl << (8 * cdir));
+        if (fl & 0x02) atomicMax(&h->syn1[cdir], idx + 1);
+        if (fl & 0x05) atomicMax(&h->fin_n[cdir], ~idx);
+    }
+    return true;
+}
+
+// The accumulator half of a HotSlot, as a per-workgroup aggregate (k_reduce's LDS table).
+struct FlowAgg {
+    unsigned long long key;
+    unsigned long long acc[2];
+    uint32_t first_n, last1, tbits, tflags;
+    uint32_t fin_n[2], syn1[2];
+};
+static_assert(sizeof(FlowAgg) == 56, "");
+
+// plain merge of an aggregate into a slot image (commutative: sums, maxima, ORs)
+__device__ __forceinline__ void agg_fold(HotSlot& h, const FlowAgg& a) {
+    h.acc[0] += a.acc[0];
+    h.acc[1] += a.acc[1];
+    h.first_n = max(h.first_n, a.first_n);
+    h.last1 = max(h.last1, a.last1);
+    h.tbits |= a.tbits;
+    h.tflags |= a.tflags;
+    h.fin_n[0] = max(h.fin_n[0], a.fin_n[0]);
+    h.fin_n[1] = max(h.fin_n[1], a.fin_n[1]);
+    h.syn1[0] = max(h.syn1[0], a.syn1[0]);
+    h.syn1[1] = max(h.syn1[1], a.syn1[1]);
+}
+
+// atomic merge of an aggregate into a slot (when other workgroups may touch it too)
+__device__ __forceinline__ void agg_merge_atomic(HotSlot* h, const FlowAgg& a) {
+    if (a.acc[0]) atomicAdd((unsigned long long*)&h->acc[0], a.acc[0]);
+    if (a.acc[1]) atomicAdd((unsigned long long*)&h->acc[1], a.acc[1]);
+    atomicMax(&h->first_n, a.first_n);
+    atomicMax(&h->last1, a.last1);
+    if (a.tbits) atomicOr(&h->tbits, a.tbits);
+    if (a.tflags) atomicOr(&h->tflags, a.tflags);
+    for (int d = 0; d < 2; ++d) {
+        if (a.fin_n[d]) atomicMax(&h->fin_n[d], a.fin_n[d]);
+        if (a.syn1[d]) atomicMax(&h->syn1[d], a.syn1[d]);
+    }
+}
+
+// ---- flow record construction (FlowRecord::create/update, cache.cpp:94-152) ---------------
+__device__ __forceinline__ void rec_create(ipxg_flow_record& r, const DevPkt& pk, const ipxg_pkt_desc& d,
+                                           uint64_t hf, uint32_t cdir) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) w[k] = 0;
+    r.flow_hash = hf;
+    r.time_first_sec = r.time_last_sec = d.ts_sec;
+    r.time_first_usec = r.time_last_usec = d.ts_usec;
+    r.ip_version = pk.ip_version;
+    r.ip_proto = pk.ip_proto;
+    for (int k = 0; k < 4; ++k) {
+        for (int q = 0; q < 4; ++q) {
+            r.src_ip[4 * k + q] = (uint8_t)(pk.sip[k] >> (8 * q));
+            r.dst_ip[4 * k + q] = (uint8_t)(pk.dip[k] >> (8 * q));
+        }
+    }
+    const uint32_t m[3] = {pk.mac_lo, pk.mac_mid, pk.mac_hi};
+    for (int q = 0; q < 6; ++q) {
+        r.dst_mac[q] = (uint8_t)(m[q >> 2] >> (8 * (q & 3)));
+        r.src_mac[q] = (uint8_t)(m[(q + 6) >> 2] >> (8 * ((q + 6) & 3)));
+    }
+    const uint8_t pr = pk.ip_proto;
+    if (pr == 6 || pr == 17 || pr == 1 || pr == 58) {
+        r.src_port = pk.src_port;
+        r.dst_port = pk.dst_port;
+    }
+    r.vlan_id = (uint16_t)pk.vlan_id;
+    r.reserved[0] = (uint8_t)cdir;  // creator's canonical direction (not exported)
+}
+
+__device__ __forceinline__ uint8_t export_reason(const ipxg_flow_record& r) {
+    return ((r.src_tcp_flags | r.dst_tcp_flags) & 0x05) ? IPXG_FLOW_END_EOF : IPXG_FLOW_END_INACTIVE;
+}
+
+// ex.count[1] is raised if the host under-sized the buffer (reported as an error)
+__device__ __forceinline__ void store_export(ExportView ex, uint32_t pos, const ipxg_flow_record& r,
+                                             uint8_t reason) {
+    if (pos >= ex.cap) {
+        atomicOr(ex.count + 1, 1u);
+        return;
+    }
+    ipxg_flow_record o = r;
+    o.end_reason = reason;
+    o.reserved0 = 0;
+    for (int k = 0; k < 24; ++k) o.reserved[k] = 0;
+    ex.buf[pos] = o;
+}
+
+__device__ __forceinline__ void clear_slot(HotSlot* h, uint64_t key, uint32_t state) {
+    HotSlot z = {};
+    z.key = key;
+    z.state = state;
+    *h = z;
+}
+
+__device__ __forceinline__ void apply_frag_ports(const Params& p, const FragView& f, uint32_t idx,
+                                                 DevPkt& pk) {
+    if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
+        uint32_t pp = f.ports[idx];
+        pk.src_port = (uint16_t)(pp >> 16);
+        pk.dst_port = (uint16_t)(pp & 0xFFFF);
+    }
+}
+
+// ---- header staging into LDS ------------------------------------------------------------
+// Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
+// zero-masked past caplen, plus one zero chunk so straddling reads see zeros.
+__device__ __forceinline__ void stage_frame(uint32_t* col, const uint8_t* arena, uint32_t off,
+                                            uint32_t cap) {
+    const uint32_t nbytes = cap < IPXG_WIN ? cap : IPXG_WIN;
+    const uint32_t nch = (nbytes + 15) >> 4;
+    const uint8_t* f = arena + off;
+    constexpr int NCH = IPXG_WIN / 16;
+    if ((off & 15) == 0) {
+        uint4 v[NCH];
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            v[ch] = make_uint4(0, 0, 0, 0);
+            if ((uint32_t)ch < nch) v[ch] = *reinterpret_cast<const uint4*>(f + 16 * ch);
+        }
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            if ((uint32_t)ch > nch) break;
+            uint32_t w[4] = {v[ch].x, v[ch].y, v[ch].z, v[ch].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                int b0 = 16 * ch + 4 * k;
+                int valid = (int)cap - b0;
+                uint32_t m = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+                col[(4 * ch + k) * IPXG_BLOCK] = w[k] & m;
+            }
+        }
+    } else {  // unaligned frame: byte loads (correct for any offset)
+        for (uint32_t dw = 0; dw < 4 * (nch + (nch < NCH ? 1 : 0)); ++dw) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t o = dw * 4 + k;
+                if (o < nbytes) w |= (uint32_t)f[o] << (8 * k);
+            }
+            col[dw * IPXG_BLOCK] = w;
+        }
+    }
+}
+
+// LDS window with caplen guard (bytes >= caplen read as 0).
+struct LdsFrame {
+    LdsWin w;
+    __device__ __forceinline__ uint32_t b(uint32_t o) const { return o < w.g.cap ? w.b(o) : 0u; }
+    __device__ __forceinline__ uint32_t le32(uint32_t o) const { return o < w.g.cap ? w.le32(o) : 0u; }
+};
+
+// ---- re-parse of one packet -------------------------------------------------------------
+// straight from HBM (byte loads)
+template <bool FULL>
+__device__ __forceinline__ bool reparse(const BatchView& b, const Params& p, const FragView& f,
+                                        uint32_t idx, DevPkt& pk, ipxg_pkt_desc& d) {
+    d = b.desc[idx];
+    GlobalSrc g{b.arena + d.offset, d.caplen};
+    ParseCounts dummy = {};
+    if (!parse_frame<FULL>(g, d.caplen, p.dlt, pk, dummy)) return false;
+    apply_frag_ports(p, f, idx, pk);
+    return true;
+}
+
+// header bytes staged into this lane's LDS column with 16-byte loads (the column stride is
+// IPXG_BLOCK dwords)
+template <bool FULL>
+__device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p, const FragView& f,
+                                            uint32_t idx, uint32_t* col, DevPkt& pk, ipxg_pkt_desc& d) {
+    d = b.desc[idx];
+    stage_frame(col, b.arena, d.offset, d.caplen);
+    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    ParseCounts dummy = {};
+    if (!parse_frame<FULL>(S, d.caplen, p.dlt, pk, dummy)) return false;
+    apply_frag_ports(p, f, idx, pk);
+    return true;
+}
+
+// ---- per-slot batch finalisation ----------------------------------------------------------
+enum FinStatus : uint32_t { FIN_DONE = 1, FIN_COMPLEX = 2 };
+struct FinResult {
+    uint32_t status;   // FIN_DONE / FIN_COMPLEX
+    bool created;      // the slot held no live record before (a record was created)
+    bool do_export;    // the open record was closed at the batch boundary
+    uint8_t reason;
+};
+
+// h = the slot's complete batch image (key, accumulators, state) with h.last1 != 0.
+// Re-parses the batch's first packet of the flow (the creator fields and the boundary
+// checks need it), applies the reference's SYN-after-FIN/RST, inactive and active checks
+// at the batch's first packet (cache.cpp:431-472), and decides whether a split could fall
+// strictly inside the batch (a SYN after a FIN/RST in the same direction, a gap >= inactive
+// -- detected conservatively as an empty inactive/2 bucket between busy ones --, or the
+// active limit inside the batch).  If so the slot is marked complex (k_complex_walk replays
+// the flow's packets sequentially); otherwise the accumulators are folded into the record
+// and the slot cleared.  Writes the slot (and its cold record) back.
+// LDSW: stage the creator's headers in the lane's LDS column `col` (else byte loads).
+template <bool LDSW>
+__device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
+                                                   const FragView& f, uint32_t s, const HotSlot& h,
+                                                   bool force_cx, uint32_t* col, ipxg_flow_record& er) {
+    FinResult res = {FIN_DONE, false, false, 0};
+    const uint32_t first = ~h.first_n, last = h.last1 - 1;
+    const bool live = h.state & SLOT_LIVE;
+    ipxg_flow_record rec;
+    if (live) rec = t.cold[s];
+    DevPkt fp;
+    ipxg_pkt_desc df;
+    if (LDSW) reparse_lds<true>(b, p, f, first, col, fp, df);
+    else reparse<true>(b, p, f, first, fp, df);
+    const ipxg_pkt_desc dl = b.desc[last];
+    uint64_t lo, hf;
+    uint32_t cdf;
+    canon(fp, p, lo, cdf, hf);
+    const uint32_t I = p.inactive_s, A = p.active_s;
+    uint8_t bsplit = 0;
+    if (live) {
+        const uint32_t creator = rec.reserved[0];
+        const bool dsrc = p.split_biflow || cdf == creator;
+        const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
+        if ((fp.tcp_flags & 0x02) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
+        else if ((int64_t)df.ts_sec - (int64_t)rec.time_last_sec >= (int64_t)I) bsplit = export_reason(rec);
+        else if ((int64_t)df.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
+    }
+    const bool cont = live && !bsplit;
+    bool cx = force_cx;
+    const uint32_t tb = h.tbits;
+    if (tb >> 31) cx = true;
+    else if (tb) {
+        uint32_t x = tb >> __builtin_ctz(tb);
+        if (x & (x + 1)) cx = true;  // an empty bucket between two busy ones
+    }
+    const uint32_t tfirst = cont ? rec.time_first_sec : df.ts_sec;
+    if ((int64_t)dl.ts_sec - (int64_t)tfirst >= (int64_t)A) cx = true;
+    for (int dd = 0; dd < 2; ++dd) {
+        if (!h.syn1[dd]) continue;
+        const uint32_t sidx = h.syn1[dd] - 1;
+        if (cont) {
+            const uint8_t cf = (uint32_t)dd == rec.reserved[0] ? rec.src_tcp_flags : rec.dst_tcp_flags;
+            if (cf & 0x05) cx = true;
+        }
+        if (h.fin_n[dd] && sidx > ~h.fin_n[dd]) cx = true;
+    }
+    if (cx) {
+        HotSlot c = h;
+        c.state = h.state | SLOT_COMPLEX;
+        t.hot[s] = c;
+        res.status = FIN_COMPLEX;
+        return res;
+    }
+    if (bsplit) {
+        res.do_export = true;
+        res.reason = bsplit;
+        er = rec;
+    }
+    if (!cont) rec_create(rec, fp, df, hf, cdf);
+    const uint32_t sd = rec.reserved[0];
+    const uint64_t as = h.acc[sd], ad = h.acc[sd ^ 1];
+    rec.src_packets += (uint32_t)(as >> 40);
+    rec.src_bytes += as & ACC_BYTES_MASK;
+    rec.dst_packets += (uint32_t)(ad >> 40);
+    rec.dst_bytes += ad & ACC_BYTES_MASK;
+    rec.src_tcp_flags |= (uint8_t)(h.tflags >> (8 * sd));
+    rec.dst_tcp_flags |= (uint8_t)(h.tflags >> (8 * (sd ^ 1)));
+    rec.time_last_sec = dl.ts_sec;
+    rec.time_last_usec = dl.ts_usec;
+    t.cold[s] = rec;
+    clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+    res.created = !live;
+    return res;
+}
+
+}  // namespace ipxg

@@ -49,7 +49,7 @@ STATS_FIELDS = [
     "vlan_packets", "ipv4_bytes", "ipv6_bytes", "end_inactive", "end_active", "end_eof",
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
-    "table_rehashes", "batches",
+    "table_rehashes", "batches", "spilled_packets",
 ]
 
 
@@ -57,7 +57,7 @@ class Config(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in (
         "cache_exp", "line_exp", "active_s", "inactive_s", "split_biflow", "frag_enable",
         "frag_size", "frag_timeout_s")] + [("device_id", ctypes.c_int32)] + \
-        [(n, ctypes.c_uint32) for n in ("batch_pkts", "datalink", "reserved")]
+        [(n, ctypes.c_uint32) for n in ("batch_pkts", "datalink", "flags")]
 
 
 class Batch(ctypes.Structure):
@@ -66,9 +66,10 @@ class Batch(ctypes.Structure):
 
 
 class Timing(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_double) for n in ("ingest_ms", "finalize_ms", "slow_ms", "finish_ms")] + \
-        [(n, ctypes.c_uint64) for n in ("ingest_launches", "finalize_launches", "slow_launches",
-                                        "finish_launches", "ingest_packets")]
+    _fields_ = [(n, ctypes.c_double) for n in ("ingest_ms", "reduce_ms", "finalize_ms", "slow_ms",
+                                               "finish_ms")] + \
+        [(n, ctypes.c_uint64) for n in ("ingest_launches", "reduce_launches", "finalize_launches",
+                                        "slow_launches", "finish_launches", "ingest_packets")]
 
 
 class Capture(ctypes.Structure):

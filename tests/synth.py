@@ -291,3 +291,38 @@ def flow_stream(seed=7, n_flows=300, n_pkts=6000, v6_share=0.2, vlan_share=0.1, 
             gap = int(rng.integers(1, 20_000))
         st.add(eth(mac(3 if rev else 4), mac(4 if rev else 3), et, vlan) + l3, gap_us=gap)
     return st
+
+
+# ---- vectorised 64 B UDP frames (large synthetic batches) ------------------------------------
+def udp_frames(sip, dip, sport, dport, t0=1_600_000_000, dt_us=1, smac=None, dmac=None):
+    """numpy arrays of per-packet IPv4 addresses / UDP ports -> (arena, desc) of 64 B
+    Ethernet/IPv4/UDP frames (tot_len 50), one frame per 64 B slot, timestamps t0 + i*dt_us."""
+    import pcaputil
+    n = len(sip)
+    fr = np.zeros((n, 64), dtype=np.uint8)
+
+    def put(col, val, nbytes):
+        val = np.asarray(val, dtype=np.uint64)
+        for q in range(nbytes):
+            fr[:, col + q] = (val >> np.uint64(8 * (nbytes - 1 - q))) & np.uint64(0xFF)
+
+    put(0, 0x020000000001 if dmac is None else dmac, 6)
+    put(6, 0x020000000002 if smac is None else smac, 6)
+    fr[:, 12] = 0x08
+    fr[:, 14] = 0x45
+    fr[:, 17] = 50
+    fr[:, 22] = 64
+    fr[:, 23] = 17
+    put(26, sip, 4)
+    put(30, dip, 4)
+    put(34, sport, 2)
+    put(36, dport, 2)
+    fr[:, 39] = 30
+    desc = np.zeros(n, dtype=pcaputil.DESC_DTYPE)
+    t = np.uint64(t0) * np.uint64(1_000_000) + np.arange(n, dtype=np.uint64) * np.uint64(dt_us)
+    desc["offset"] = np.arange(n, dtype=np.uint64) * np.uint64(64)
+    desc["caplen"] = 64
+    desc["wirelen"] = 64
+    desc["ts_sec"] = t // np.uint64(1_000_000)
+    desc["ts_usec"] = t % np.uint64(1_000_000)
+    return fr.reshape(-1), desc

@@ -222,3 +222,88 @@ def test_bench_size_parity():
     assert len(want) == 100_000 and wst["end_no_res"] == 0
     d = flowcmp.diff(got, want)
     assert not d, d
+
+
+# ---- the binned ingest's fast and fallback paths (ipxg_ingest.hip) -------------------------
+NOFRAG = [
+    dict(seed=14, n_flows=300, n_pkts=6000, params="", frag=False),
+    dict(seed=15, n_flows=60, n_pkts=5000, params="a=20;i=5", frag=False),
+    dict(seed=16, n_flows=200, n_pkts=5000, params="S", frag=False, v6_share=0.5),
+]
+
+
+@pytest.mark.parametrize("batch", [None, 1, 37, 1000])
+@pytest.mark.parametrize("ci", range(len(NOFRAG)))
+def test_stream_parity_no_fragments(ci, batch):
+    """Without fragments k_reduce finalises the flows itself (no table scan)."""
+    from ipfixprobe_amd import run_capture
+    case = NOFRAG[ci]
+    arena, desc = _stream(case)
+    want, wst = oracle_py.run_capture(arena, desc, 1, **oracle_kwargs(case["params"]))
+    got, _ = run_capture(arena, desc, params=case["params"], batch=batch)
+    d = flowcmp.diff(got, want)
+    assert not d, d
+
+
+def test_fused_finalize_skips_table_scan():
+    from ipfixprobe_amd import Engine
+    arena, desc = _stream(NOFRAG[0])
+    want, _ = oracle_py.run_capture(arena, desc, 1, **oracle_kwargs(""))
+    with Engine() as e:
+        e.profile(True)
+        e.submit(arena, desc)
+        tm = e.timing()
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert tm["reduce_launches"] == 1 and tm["finalize_launches"] == 0, tm
+    assert st["spilled_packets"] == 0
+    d = flowcmp.diff(got, want)
+    assert not d, d
+
+
+def _udp_batch(rng, flow_of_pkt, n_flows, reverse_share=0.5):
+    sip = (10 << 24) + np.arange(n_flows, dtype=np.int64)
+    dip = np.full(n_flows, (192 << 24) | (168 << 16) | 1, dtype=np.int64)
+    sp = 1024 + (np.arange(n_flows, dtype=np.int64) * 7919) % 60000
+    dp = 1 + (np.arange(n_flows, dtype=np.int64) % 1000)
+    rev = rng.random(len(flow_of_pkt)) < reverse_share
+    f = flow_of_pkt
+    return synth.udp_frames(np.where(rev, dip[f], sip[f]), np.where(rev, sip[f], dip[f]),
+                            np.where(rev, dp[f], sp[f]), np.where(rev, sp[f], dp[f]))
+
+
+def test_elephant_flow_spills_and_multi_chunk():
+    """Half of 200k packets in one biflow: its partition overflows its region (spill to
+    device atomics) and spans several k_reduce workgroups (atomic merge, table scan)."""
+    from ipfixprobe_amd import run_capture
+    rng = np.random.default_rng(21)
+    n, F = 200_000, 5000
+    fop = np.where(rng.random(n) < 0.5, 0, rng.integers(1, F, n))
+    arena, desc = _udp_batch(rng, fop, F)
+    want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    got, st = run_capture(arena, desc, params="s=16")
+    assert st["spilled_packets"] > 0
+    d = flowcmp.diff(got, want)
+    assert not d, d
+
+
+def test_partition_estimate_too_small_overflows_lds():
+    """A first batch of 10 flows makes the engine size the next batch's partitions for 10
+    flows; the next batch brings 300k new flows: k_reduce's LDS tables overflow (spill),
+    the table overflows (deferral, growth), and every record must still match."""
+    from ipfixprobe_amd import Engine
+    rng = np.random.default_rng(22)
+    F = 300_010
+    fop = np.concatenate([np.arange(1000) % 10, 10 + rng.permutation(300_000)])
+    arena, desc = _udp_batch(rng, fop, F)
+    want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=22)
+    with Engine() as e:
+        e.submit(arena, desc[:1000])
+        e.submit(arena, desc[1000:])
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert st["spilled_packets"] > 0 and st["table_rehashes"] >= 1
+    d = flowcmp.diff(got, want)
+    assert not d, d
