@@ -39,6 +39,51 @@ __device__ __forceinline__ void defer_packet(BatchCtl* ctl, uint32_t* list, uint
 }
 
 // ---- phase A ------------------------------------------------------------------------------
+// The common frame shape -- Ethernet (no VLAN tag), IPv4 with IHL 5, UDP or TCP without
+// options -- read straight from its first 48 bytes in registers: exactly the fields, checks
+// and counters parse_frame produces for such a frame (parse_eth_hdr parser.cpp:68-155,
+// parse_ipv4_hdr :311-356, parse_tcp_hdr :469-543 with doff <= 5, parse_udp_hdr :552-573),
+// without staging it in LDS.  Returns false for any other shape (or a TCP header cut by
+// caplen): the caller then takes the general parser.  c0..c2 = bytes 0..47, caplen >= 48.
+__device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, const uint4& c2, uint32_t caplen,
+                                           DevPkt& p, ParseCounts& c) {
+    if ((c0.w & 0xFFFF) != 0x0008) return false;          // ethertype 0x0800 at bytes 12-13
+    if (((c0.w >> 16) & 0xFF) != 0x45) return false;      // version 4, IHL 5
+    const uint32_t proto = c1.y >> 24;                     // byte 23
+    if (proto == 47) return false;                         // GRE: the general parser recurses
+    const uint32_t fo = bswap16(c1.y);                     // bytes 20-21
+    const uint32_t frag_off = fo & 0x1FFF;
+    uint32_t ports = 0, flags = 0;
+    if (frag_off == 0 && proto == 6) {
+        if (caplen < 54) return false;                     // 20 > data_len: the general path drops it
+        if (((c2.w >> 20) & 0xF) > 5) return false;        // TCP options: the general option walk
+        flags = c2.w >> 24;                                // byte 47
+    }
+    if (frag_off == 0 && (proto == 6 || proto == 17)) ports = (c2.x >> 16) | (c2.y << 16);  // bytes 34-37
+    p.ip_version = 4;
+    p.ip_proto = (uint8_t)proto;
+    p.tcp_flags = (uint8_t)flags;
+    p.ethertype = 0x0800;
+    p.ip_len = bswap16(c1.x);                              // bytes 16-17
+    p.frag_id = bswap16(c1.x >> 16);                       // bytes 18-19
+    p.frag_off = (uint16_t)frag_off;
+    p.more_fragments = (fo & 0x2000) ? 1 : 0;
+    p.src_port = bswap16(ports);
+    p.dst_port = bswap16(ports >> 16);
+    p.vlan_id = 0;
+    p.sip[0] = (c1.z >> 16) | (c1.w << 16);                // bytes 26-29, memory order
+    p.dip[0] = (c1.w >> 16) | (c2.x << 16);                // bytes 30-33
+    p.sip[1] = p.sip[2] = p.sip[3] = 0;
+    p.dip[1] = p.dip[2] = p.dip[3] = 0;
+    c.seen++;
+    c.parsed++;
+    c.ipv4++;
+    c.ipv4_bytes += caplen;
+    if (frag_off == 0 && proto == 6) c.tcp++;
+    if (frag_off == 0 && proto == 17) c.udp++;
+    return true;
+}
+
 // 128 VGPRs (4 waves/SIMD = the LDS limit of 4 workgroups per CU)
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* deferred_list,
@@ -51,6 +96,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     ParseCounts c = {};
     uint32_t keyless = 0, frags = 0, spilled = 0;
     uint32_t* col = &win[tid];
+    const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
     for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
         for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
         __syncthreads();
@@ -85,10 +131,17 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                 ctl->last_usec = d.ts_usec;
             }
             if (!act) continue;
-            stage_frame(col, b.arena, d.offset, d.caplen);
-            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
             DevPkt pk;
-            if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
+            bool fast = false;
+            if (fast_ok && (d.offset & 15) == 0 && d.caplen >= 48) {
+                const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
+                fast = parse_fast(fr[0], fr[1], fr[2], d.caplen, pk, c);
+            }
+            if (!fast) {
+                stage_frame(col, b.arena, d.offset, d.caplen);
+                LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+                if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
+            }
             if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
                 keyless++;
                 continue;

@@ -307,3 +307,20 @@ def test_partition_estimate_too_small_overflows_lds():
     assert st["spilled_packets"] > 0 and st["table_rehashes"] >= 1
     d = flowcmp.diff(got, want)
     assert not d, d
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_flows_fuzz_corpus(seed):
+    """The parser fuzz corpus through the whole ingest (k_bin's register fast path for plain
+    Eth/IPv4/UDP|TCP frames and its general LDS path for everything else) against the
+    oracle's flow records and parser counters."""
+    from ipfixprobe_amd import run_capture
+    corpus = synth.fuzz_corpus(20000, seed=seed)
+    arena, desc = synth.to_batch(corpus)
+    want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    got, gst = run_capture(arena, desc)
+    d = flowcmp.diff(got, want)
+    assert not d, d
+    for k in ("seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",
+              "tcp_packets", "udp_packets", "vlan_packets", "keyless_packets"):
+        assert gst[k] == wst[k], k
