@@ -13,7 +13,7 @@ to rank 0 over RCCL inside the step (the path's only exchange).
 Prints one JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch of the
 dominant kernel k_bin (64 B frame + 16 B descriptor per packet) / its average
 duration, timed with HIP events on the engine's stream; roofline.stage gives the same bytes
-over the whole ingest (k_bin + k_reduce).  roofline.traffic is the HBM bytes per k_bin launch
+over the whole ingest (k_bin + k_bin_slow + k_reduce + k_fin_list).  roofline.traffic is the HBM bytes per k_bin launch
 from the newest committed rocprofv3 PMC summary (profiles/*/pmc_summary.json, collected by
 tools/gpu_pmc.sh), or null when none covers k_bin.
 """
@@ -301,7 +301,8 @@ def main():
     total_pkts = args.packets * args.steps * world
     value = total_pkts / dt / 1e6
     per_launch = lambda k: tm[k + "_ms"] / max(tm[k + "_launches"], 1)  # noqa: E731
-    bin_ms, red_ms = per_launch("ingest"), per_launch("reduce")
+    bin_ms = per_launch("ingest")
+    red_ms = (tm["ingest_slow_ms"] + tm["reduce_ms"] + tm["fin_ms"]) / max(tm["reduce_launches"], 1)
     alg = ALG_BYTES_PER_PKT * args.packets
     achieved = alg / (bin_ms / 1e3) / 1e9 if bin_ms > 0 else 0.0
     stage = alg / ((bin_ms + red_ms) / 1e3) / 1e9 if bin_ms > 0 else 0.0
@@ -329,11 +330,13 @@ def main():
                          "traffic_source": os.path.relpath(pmc[0], ROOT) if pmc else None,
                          "algorithmic_bytes_per_launch": alg,
                          "avg_launch_ms": round(bin_ms, 4),
-                         "stage": {"kernels": "k_bin+k_reduce", "achieved": round(stage, 1),
+                         "stage": {"kernels": "k_bin+k_bin_slow+k_reduce+k_fin_list",
+                                   "achieved": round(stage, 1),
                                    "frac": round(stage / HBM_PEAK_GBS, 4),
                                    "avg_ms": round(bin_ms + red_ms, 4)}},
             "stage_ms_per_step": {k: round(tm[k + "_ms"] / max(args.steps, 1), 4)
-                                  for k in ("ingest", "reduce", "finalize", "slow", "finish")},
+                                  for k in ("ingest", "ingest_slow", "reduce", "fin", "finalize", "slow",
+                                            "finish")},
             "flows_exported_per_step": int(st["end_forced"] // max(st["batches"], 1)),
             "spilled_packets": int(st["spilled_packets"]),
             "cpu_baseline": cpu,

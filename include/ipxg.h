@@ -237,7 +237,9 @@ int ipxg_get_stats(ipxg_engine* eng, ipxg_stats* out);
 /* ---- stage timing (HIP events on the engine's stream) --------------------------------- */
 typedef struct ipxg_timing {
     double ingest_ms;          /* k_bin: parse + hash + partition (atomic mode: k_ingest)  */
-    double reduce_ms;          /* k_reduce: per-flow aggregation + table merge (+finalise) */
+    double ingest_slow_ms;     /* k_bin_slow: frames for the general parser                */
+    double reduce_ms;          /* k_reduce: per-flow aggregation + table merge             */
+    double fin_ms;             /* k_fin_list: split rules on the flows k_reduce completed  */
     double finalize_ms;        /* k_finalize table scan (only when k_reduce could not)     */
     double slow_ms;            /* fragment / overflow / complex-flow paths                 */
     double finish_ms;          /* k_finish + table clear                                   */

@@ -2,14 +2,15 @@
 // kernel sequence, table growth, the export buffer, and statistics.
 //
 // Per ipxg_submit (one batch, arrival order):
-//   stage (H2D if host batch) -> k_bin -> k_reduce (merges + finalises the flows)
+//   stage (H2D if host batch) -> k_bin (register parser) -> k_bin_slow (general parser, the
+//   frames k_bin left) -> k_reduce (per-flow merge) -> k_fin_list (split rules)
 //   -> [sync: control block]
 //   -> fragments? sort + k_frag_walk + k_frag_accumulate
 //   -> deferred probes? grow table (k_rehash) + k_deferred, until none
 //   -> anything k_reduce could not finalise (ctl->pending)? k_finalize scan -> [sync]
 //   -> complex flows? k_complex_rank -> gather -> sort -> k_complex_walk
 //   -> grow the table if its load passed 1/2.
-// In the common case (no fragments, no overflow) that is two kernels and one host sync.
+// In the common case (no fragments, no overflow) that is four kernels and one host sync.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -55,6 +56,7 @@ struct ipxg_engine {
     DevBuf defer_a, defer_b, frag_list, frag_sorted, frag_ports, sort_tmp;
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
+    DevBuf slow_list, fin_list;          // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
@@ -64,11 +66,12 @@ struct ipxg_engine {
     uint32_t prev_sec = 0, prev_usec = 0;
     // stage timing
     bool prof = false;
-    hipEvent_t ev[10] = {};
+    hipEvent_t ev[11] = {};
     ipxg_timing tm = {};
 };
 
-// events: [0,1] ingest (k_bin), [1,2] k_reduce, [3,4] slow paths, [5,6] k_finalize, [7,8] finish
+// events: 0 | k_bin | 1 | k_bin_slow | 2 | k_reduce | 3 | k_fin_list | 4;
+//         [5,6] slow paths, [7,8] k_finalize, [9,10] finish
 static void ev_rec(ipxg_engine* e, int i) {
     if (e->prof) (void)hipEventRecord(e->ev[i], e->st);
 }
@@ -334,7 +337,7 @@ int ipxg_destroy(ipxg_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->frag_list, &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
-                      &e->bin_count})
+                      &e->bin_count, &e->slow_list, &e->fin_list})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -383,14 +386,24 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     FragView fv = frag_view(e);
     const bool binned = !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST);
     BinView bins = {};
-    if (binned && (rc = setup_bins(e, n, bins))) return rc;
+    if (binned) {
+        if ((rc = setup_bins(e, n, bins))) return rc;
+        if ((rc = ensure(e, e->slow_list, (size_t)n * 4))) return rc;
+        if ((rc = ensure(e, e->fin_list, (size_t)n * 4))) return rc;
+    }
     ev_rec(e, 0);
     if (binned) {
-        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
+        uint32_t* dl = (uint32_t*)e->defer_a.p;
+        uint32_t* sl = (uint32_t*)e->slow_list.p;
+        uint32_t* fl = (uint32_t*)e->fin_list.p;
+        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, e->stats_d);
         ev_rec(e, 1);
-        launch_reduce(e->st, bv, p, table_view(e), fv, bins, export_view(e), e->ctl_d, (uint32_t*)e->defer_a.p,
-                      e->stats_d);
+        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, e->stats_d);
         ev_rec(e, 2);
+        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl);
+        ev_rec(e, 3);
+        launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n);
+        ev_rec(e, 4);
     } else {
         launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
         ev_rec(e, 1);
@@ -403,7 +416,9 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
         if (binned) {
-            e->tm.reduce_ms += ev_ms(e, 1);
+            e->tm.ingest_slow_ms += ev_ms(e, 1);
+            e->tm.reduce_ms += ev_ms(e, 2);
+            e->tm.fin_ms += ev_ms(e, 3);
             e->tm.reduce_launches++;
         }
     }
@@ -412,7 +427,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     // fragmentation cache: order fragments by (bucket, arrival) and replay the rings
     uint32_t ndef = c1.deferred;
     if (c1.frag_count) {
-        if (!slow) ev_rec(e, 3);
+        if (!slow) ev_rec(e, 5);
         slow = true;
         const uint32_t nf = c1.frag_count;
         if ((rc = ensure(e, e->frag_sorted, (size_t)nf * 8))) return rc;
@@ -431,7 +446,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     }
     // table overflow: grow and re-apply the deferred packets
     while (ndef) {
-        if (!slow) ev_rec(e, 3);
+        if (!slow) ev_rec(e, 5);
         slow = true;
         if ((rc = rehash(e, e->cap * 2))) return rc;
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->deferred, 0, sizeof(uint32_t), e->st));
@@ -443,10 +458,10 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         std::swap(e->defer_a, e->defer_b);
     }
     if (slow) {
-        ev_rec(e, 4);
+        ev_rec(e, 6);
         HIPCHK(e, hipStreamSynchronize(e->st));
         if (e->prof) {
-            e->tm.slow_ms += ev_ms(e, 3);
+            e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
         }
     }
@@ -455,19 +470,19 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     const bool scan = !binned || c1.pending || c1.frag_count || c1.deferred;
     if (scan) {
         p.force_complex = p.force_complex || c1.nonmono;
-        ev_rec(e, 5);
+        ev_rec(e, 7);
         launch_finalize(e->st, bv, p, table_view(e), frag_view(e), export_view(e), e->ctl_d, e->stats_d);
-        ev_rec(e, 6);
+        ev_rec(e, 8);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         if (e->prof) {
-            e->tm.finalize_ms += ev_ms(e, 5);
+            e->tm.finalize_ms += ev_ms(e, 7);
             e->tm.finalize_launches++;
         }
     }
     const uint32_t ncx = e->ctl_h->complex_count;
     if (ncx) {
-        ev_rec(e, 3);
+        ev_rec(e, 5);
         e->complex_total += ncx;
         if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 5 * 4))) return rc;
         uint32_t* cr = (uint32_t*)e->cx_rank.p;
@@ -493,11 +508,11 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         HIPCHK(e, sort_keys_u64(e->sort_tmp.p, tb, cx.list, cx.sorted, npk, bits, e->st));
         launch_complex_walk(e->st, bv, p, table_view(e), frag_view(e), cx, ncx, export_view(e), e->ctl_d,
                             e->stats_d);
-        ev_rec(e, 4);
+        ev_rec(e, 6);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         if (e->prof) {
-            e->tm.slow_ms += ev_ms(e, 3);
+            e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
         }
     }
@@ -546,16 +561,16 @@ int ipxg_finish(ipxg_engine* e) {
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
-    ev_rec(e, 7);
+    ev_rec(e, 9);
     launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
-    ev_rec(e, 8);
+    ev_rec(e, 10);
     if ((rc = read_ex_count(e))) return rc;
     HIPCHK(e, hipStreamSynchronize(e->st));
     if ((rc = check_ex(e))) return rc;
     if (e->prof) {
-        e->tm.finish_ms += ev_ms(e, 7);
+        e->tm.finish_ms += ev_ms(e, 9);
         e->tm.finish_launches++;
     }
     e->keys = e->live = 0;

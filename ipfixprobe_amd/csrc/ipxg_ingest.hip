@@ -10,12 +10,15 @@
 //             its records per partition with LDS atomics and reserves room with one
 //             coalesced device atomic per 64 partitions, so a partition's records of one
 //             tile land in one run.                                     (HBM-bound)
+//   k_bin_slow  the frames k_bin's register parser does not take, through the general
+//             LDS-staged parser (parse_frame), emitted the same way.
 //   k_reduce  one 1024-thread workgroup per partition chunk: aggregates the chunk's records
 //             per flow in an LDS hash table (LDS atomics), then merges each flow into its
 //             slot of the device table once -- a plain read-modify-write when the workgroup
 //             holds all of the partition's records, atomics otherwise -- and, when nothing
-//             else of the batch can touch the flow any more, applies the reference's split
-//             rules right there (finalize_slot), so the table is not scanned per batch.
+//             else of the batch can touch the flow any more, lists the slot for k_fin_list.
+//   k_fin_list  applies the reference's split rules to the listed slots (finalize_slot), so
+//             the table is not scanned per batch.
 //
 // Records that do not fit (partition region full, LDS table full) fall back to direct
 // atomic accumulation (merge_packet_atomic); the engine then runs the k_finalize scan for
@@ -84,37 +87,131 @@ __device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, con
     return true;
 }
 
-// 128 VGPRs (4 waves/SIMD = the LDS limit of 4 workgroups per CU)
+__device__ __forceinline__ ipxg_pkt_desc load_desc(const BatchView& b, uint32_t i) {
+    ipxg_pkt_desc d = {0, 0, 0, 0, 0};
+    if (i < b.n) d = b.desc[i];
+    return d;
+}
+
+struct Head48 {  // bytes 0..47 of a frame
+    uint4 c0, c1, c2;
+};
+
+__device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.offset & 15) == 0 && d.caplen >= 48; }
+
+__device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_desc& d, bool ok) {
+    Head48 h;
+    h.c0 = h.c1 = h.c2 = make_uint4(0, 0, 0, 0);
+    if (ok) {
+        const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
+        h.c0 = fr[0];
+        h.c1 = fr[1];
+        h.c2 = fr[2];
+    }
+    return h;
+}
+
+// After every lane ranked its records of the tile in hist[part]: reserve room per partition
+// (one device atomic per non-empty partition, lanes on consecutive counters = 256-byte rows)
+// and write each record into its region; a full region spills to direct accumulation.
+// LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
+// tile + q * 256 + lane (k_bin).
+template <bool LISTED>
+__device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t P, uint32_t pmask, const BinView& bv,
+                                          const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
+                                          const uint32_t (&r0)[BIN_K], const uint32_t (&r1)[BIN_K],
+                                          const uint32_t (&r2)[BIN_K], const uint32_t (&rk)[BIN_K],
+                                          const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& spilled) {
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) {
+        const uint32_t cnt = hist[q];
+        if (cnt) hist[q] = atomicAdd(&bv.count[q], cnt);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BIN_K; ++q) {
+        if (rk[q] == NO_REC) continue;
+        const uint32_t part = r1[q] & pmask;
+        const uint32_t pos = hist[part] + rk[q];
+        const uint32_t idx = LISTED ? ix[q] : tile + (uint32_t)q * IPXG_BLOCK + threadIdx.x;
+        if (pos < bv.cap) {
+            bv.rec[(size_t)part * bv.cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
+        } else {  // partition region full: accumulate straight into the table
+            spilled++;
+            const uint64_t lo = ((uint64_t)r1[q] << 32) | r0[q];
+            if (!merge_packet_atomic(t, lo, idx, r2[q], &ctl->new_keys)) defer_packet(ctl, deferred_list, idx, true);
+        }
+    }
+    __syncthreads();  // hist is reset by the next tile
+}
+
+// rank one keyed, unfragmented packet in its partition and keep its record in slot j
+template <bool LISTED>
+__device__ __forceinline__ void tile_rank(uint32_t* hist, uint32_t pmask, const Params& p, const BatchView& b,
+                                          const DevPkt& pk, const ipxg_pkt_desc& d, uint32_t i, int j,
+                                          uint32_t (&r0)[BIN_K], uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K],
+                                          uint32_t (&rk)[BIN_K], uint32_t (&ix)[BIN_K]) {
+    uint64_t lo, hf;
+    uint32_t cdir;
+    canon(pk, p, lo, cdir, hf);
+    const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
+    const uint32_t rank = atomicAdd(&hist[(uint32_t)(lo >> 32) & pmask], 1u);
+#pragma unroll
+    for (int q = 0; q < BIN_K; ++q) {  // registers indexed by compile-time q only
+        if (q == j) {
+            r0[q] = (uint32_t)lo;
+            r1[q] = (uint32_t)(lo >> 32);
+            r2[q] = m;
+            rk[q] = rank;
+            if (LISTED) ix[q] = i;
+        }
+    }
+}
+
+__device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& p, const FragView& f, BatchCtl* ctl,
+                                                uint32_t i) {
+    const uint32_t bucket = (uint32_t)(frag_key_hash(pk) % (uint64_t)p.frag_size);
+    const uint32_t pos = atomicAdd(&ctl->frag_count, 1u);
+    f.list[pos] = ((uint64_t)bucket << 24) | i;
+}
+
+// Every packet of the batch, in tiles of BIN_K x 256: the descriptor two packets ahead and
+// the 48-byte head one packet ahead are in flight while a packet is parsed (the loop is
+// latency-bound otherwise).  Frames the register parser does not take go to the slow list
+// for k_bin_slow.  No LDS header staging here: LDS holds only the partition histogram, so
+// occupancy is set by registers.
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
-void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* deferred_list,
-           unsigned long long* stats) {
-    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];    // 32 KiB: one header column per lane
-    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];    // 8 KiB: per-partition rank / base
+void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
+           uint32_t* deferred_list, unsigned long long* stats) {
+    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / base
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
-    ParseCounts c = {};
-    uint32_t keyless = 0, frags = 0, spilled = 0;
-    uint32_t* col = &win[tid];
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    ParseCounts c = {};
+    uint32_t frags = 0, spilled = 0;
     for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
         for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
         __syncthreads();
-        // the tile's records stay in registers (indexed by compile-time q only)
-        uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K];
+        uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
 #pragma unroll
         for (int q = 0; q < BIN_K; ++q) {
-            r0[q] = r1[q] = r2[q] = 0;
+            r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
+        const uint32_t i0 = tile + tid;
+        ipxg_pkt_desc dc = load_desc(b, i0);
+        Head48 hc = load_head(b, dc, fast_ok && i0 < b.n && fast_shape(dc));
+        ipxg_pkt_desc dn = load_desc(b, i0 + IPXG_BLOCK);
 #pragma unroll 1
         for (int j = 0; j < BIN_K; ++j) {
             const uint32_t i = tile + (uint32_t)j * IPXG_BLOCK + tid;
+            const uint32_t in = i + IPXG_BLOCK;
+            const Head48 hn = load_head(b, dn, j + 1 < BIN_K && fast_ok && in < b.n && fast_shape(dn));
+            const ipxg_pkt_desc dnn = load_desc(b, j + 2 < BIN_K ? in + IPXG_BLOCK : 0xFFFFFFFFu);
             const bool act = i < b.n;
-            ipxg_pkt_desc d = {0, 0, 0, 0, 0};
-            if (act) d = b.desc[i];
             // a timestamp going backwards sends every flow of the batch to the sequential path
-            const uint64_t ts = ((uint64_t)d.ts_sec << 32) | d.ts_usec;
+            const uint64_t ts = ((uint64_t)dc.ts_sec << 32) | dc.ts_usec;
             uint64_t prev = (uint64_t)__shfl_up((unsigned long long)ts, 1);
             if (lane_id() == 0) {
                 if (i > 0 && act) {
@@ -127,73 +224,92 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const bool has_prev = i > 0 || p.prev_valid;
             if (act && has_prev && ts < prev) ctl->nonmono = 1;
             if (act && i == b.n - 1) {
-                ctl->last_sec = d.ts_sec;
-                ctl->last_usec = d.ts_usec;
+                ctl->last_sec = dc.ts_sec;
+                ctl->last_usec = dc.ts_usec;
             }
-            if (!act) continue;
             DevPkt pk;
-            bool fast = false;
-            if (fast_ok && (d.offset & 15) == 0 && d.caplen >= 48) {
-                const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
-                fast = parse_fast(fr[0], fr[1], fr[2], d.caplen, pk, c);
+            bool have = false, slow = false;
+            if (act) {
+                if (fast_ok && fast_shape(dc) && parse_fast(hc.c0, hc.c1, hc.c2, dc.caplen, pk, c)) have = true;
+                else slow = true;
             }
-            if (!fast) {
-                stage_frame(col, b.arena, d.offset, d.caplen);
-                LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-                if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
+            const uint32_t spos = wave_append(&ctl->slow_count, slow);
+            if (slow) slow_list[spos] = i;
+            if (have) {
+                if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {  // fragmentation cache path
+                    frags++;
+                    divert_fragment(pk, p, f, ctl, i);
+                } else {
+                    tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
+                }
             }
+            dc = dn;
+            hc = hn;
+            dn = dnn;
+        }
+        tile_emit<false>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
+    }
+    // block statistics, hist reused as the counter block
+    if (tid < ST_COUNT) hist[tid] = 0;
+    __syncthreads();
+    flush_counts(c, 0, frags, hist);
+    flush_block_stats(hist, stats);
+    if (spilled) {
+        atomicAdd(&ctl->spilled, spilled);
+        ctl->pending = 1;
+    }
+}
+
+// The frames k_bin left for the general parser (VLAN/QinQ, MPLS, PPPoE, GRE, TRILL, IPv6
+// and its extension headers, IPv4 options, TCP options, SLL/SLL2/raw link types, truncated
+// or unaligned frames): staged in the lane's LDS column, parsed by parse_frame, ranked and
+// emitted exactly like k_bin's records.  The list length is read on the device.
+// 128 VGPRs (4 waves/SIMD = the LDS limit of 4 workgroups per CU)
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
+                const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];  // 32 KiB: one header column per lane
+    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB
+    const uint32_t ns = ctl->slow_count;  // final: k_bin has completed
+    if (blockIdx.x * BIN_TILE >= ns) return;
+    const uint32_t tid = threadIdx.x;
+    if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
+    const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
+    ParseCounts c = {};
+    uint32_t keyless = 0, frags = 0, spilled = 0;
+    uint32_t* col = &win[tid];
+    for (uint32_t tile = blockIdx.x * BIN_TILE; tile < ns; tile += gridDim.x * BIN_TILE) {
+        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
+        __syncthreads();
+        uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
+#pragma unroll
+        for (int q = 0; q < BIN_K; ++q) {
+            r0[q] = r1[q] = r2[q] = ix[q] = 0;
+            rk[q] = NO_REC;
+        }
+#pragma unroll 1
+        for (int j = 0; j < BIN_K; ++j) {
+            const uint32_t k = tile + (uint32_t)j * IPXG_BLOCK + tid;
+            if (k >= ns) continue;
+            const uint32_t i = slow_list[k];
+            const ipxg_pkt_desc d = b.desc[i];
+            stage_frame(col, b.arena, d.offset, d.caplen);
+            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+            DevPkt pk;
+            if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
             if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
                 keyless++;
                 continue;
             }
-            if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {  // fragmentation cache path
+            if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
                 frags++;
-                const uint32_t bucket = (uint32_t)(frag_key_hash(pk) % (uint64_t)p.frag_size);
-                const uint32_t pos = atomicAdd(&ctl->frag_count, 1u);
-                f.list[pos] = ((uint64_t)bucket << 24) | i;
+                divert_fragment(pk, p, f, ctl, i);
                 continue;
             }
-            uint64_t lo, hf;
-            uint32_t cdir;
-            canon(pk, p, lo, cdir, hf);
-            const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
-            const uint32_t part = (uint32_t)(lo >> 32) & pmask;
-            const uint32_t rank = atomicAdd(&hist[part], 1u);
-#pragma unroll
-            for (int q = 0; q < BIN_K; ++q) {
-                if (q == j) {
-                    r0[q] = (uint32_t)lo;
-                    r1[q] = (uint32_t)(lo >> 32);
-                    r2[q] = m;
-                    rk[q] = rank;
-                }
-            }
+            tile_rank<true>(hist, pmask, p, b, pk, d, i, j, r0, r1, r2, rk, ix);
         }
-        __syncthreads();
-        // one reservation per non-empty partition: lanes = consecutive counters (256 B rows)
-        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) {
-            const uint32_t cnt = hist[q];
-            if (cnt) hist[q] = atomicAdd(&bv.count[q], cnt);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < BIN_K; ++q) {
-            if (rk[q] == NO_REC) continue;
-            const uint32_t part = r1[q] & pmask;
-            const uint32_t pos = hist[part] + rk[q];
-            const uint32_t idx = tile + (uint32_t)q * IPXG_BLOCK + tid;
-            if (pos < bv.cap) {
-                bv.rec[(size_t)part * bv.cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
-            } else {  // partition region full: accumulate straight into the table
-                spilled++;
-                const uint64_t lo = ((uint64_t)r1[q] << 32) | r0[q];
-                if (!merge_packet_atomic(t, lo, idx, r2[q], &ctl->new_keys))
-                    defer_packet(ctl, deferred_list, idx, true);
-            }
-        }
-        __syncthreads();  // hist is reset by the next tile
+        tile_emit<true>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
     }
-    // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
     flush_counts(c, keyless, frags, hist);
@@ -205,11 +321,19 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 }
 
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats) {
+                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
     uint32_t tiles = (b.n + BIN_TILE - 1) / BIN_TILE;
     if (tiles > 2048) tiles = 2048;
-    hipLaunchKernelGGL(k_bin, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
+    hipLaunchKernelGGL(k_bin, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
                        deferred_list, stats);
+}
+
+void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
+                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
+    uint32_t tiles = (b.n + BIN_TILE - 1) / BIN_TILE;  // upper bound: the list is not longer than the batch
+    if (tiles > 1024) tiles = 1024;
+    hipLaunchKernelGGL(k_bin_slow, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
+                       slow_list, deferred_list, stats);
 }
 
 // ---- phase B ------------------------------------------------------------------------------
@@ -243,14 +367,12 @@ __device__ __forceinline__ void lds_fold(FlowAgg& a, uint32_t idx, uint32_t m) {
     }
 }
 
-enum RedCount { C_KEYS, C_LIVE, C_CX, C_EX, C_TOUCH, C_SPILL, C_FAIL, C_N };
+enum RedCount { C_KEYS, C_TOUCH, C_SPILL, C_FAIL, C_N };
 
-__global__ __launch_bounds__(RED_THREADS) void k_reduce(BatchView b, Params p, TableView t, FragView f,
-                                                        BinView bv, ExportView ex, BatchCtl* ctl,
-                                                        uint32_t* deferred_list, unsigned long long* stats) {
+__global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
+                                                        uint32_t* deferred_list) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
     __shared__ uint32_t cnt[C_N];
-    __shared__ uint32_t sc[ST_COUNT];
     const uint32_t part = blockIdx.x / bv.groups, g = blockIdx.x - part * bv.groups;
     const uint32_t total = min(bv.count[part], bv.cap);
     const uint32_t beg = g * bv.chunk;
@@ -263,7 +385,6 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(BatchView b, Params p, T
         for (uint32_t q = tid; q < sizeof(ht) / 16; q += RED_THREADS) z[q] = make_uint4(0, 0, 0, 0);
     }
     if (tid < C_N) cnt[tid] = 0;
-    if (tid < ST_COUNT) sc[tid] = 0;
     __syncthreads();
     const uint4* recs = bv.rec + (size_t)part * bv.cap;
     for (uint32_t k0 = beg; k0 < end; k0 += RED_THREADS * RED_U) {
@@ -289,16 +410,15 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(BatchView b, Params p, T
     }
     __syncthreads();
     // Nothing else of this batch can touch these flows when the workgroup holds all of the
-    // partition's records and no packet went to the fragment or deferred paths.
+    // partition's records and no packet went to the fragment or deferred paths: then the
+    // merged slot is complete and goes on the finalise list (k_fin_list).
     const bool fuse = !multi && ctl->frag_count == 0 && ctl->a_deferred == 0;
-    const bool force_cx = p.force_complex || ctl->nonmono;
-    uint32_t n_keys = 0, n_live = 0, n_cx = 0, n_ex = 0, n_touch = 0;
+    uint32_t n_keys = 0, n_touch = 0;
     bool failed = false;
     for (uint32_t e = tid; e < RED_ENTRIES; e += RED_THREADS) {  // same trip count in every lane
         const FlowAgg a = ht[e];
-        bool do_export = false;
-        uint8_t reason = 0;
-        ipxg_flow_record er;
+        uint32_t slot = 0;
+        bool listed = false;
         if (a.key) {
             n_touch++;
             uint4 head;
@@ -314,30 +434,16 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(BatchView b, Params p, T
                 HotSlot h = *hp;  // this workgroup is the slot's only writer in this kernel
                 h.key = a.key;
                 agg_fold(h, a);
-                if (fuse) {
-                    const FinResult fr = finalize_slot<false>(b, p, t, f, (uint32_t)(hp - t.hot), h, force_cx,
-                                                              nullptr, er);
-                    if (fr.status == FIN_COMPLEX) n_cx++;
-                    else if (fr.created) n_live++;
-                    do_export = fr.do_export;
-                    reason = fr.reason;
-                } else {
-                    *hp = h;
-                }
+                *hp = h;
+                slot = (uint32_t)(hp - t.hot);
+                listed = fuse;
             }
         }
-        const uint32_t pos = wave_append(ex.count, do_export);
-        if (do_export) {
-            store_export(ex, pos, er, reason);
-            atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
-            n_ex++;
-        }
+        const uint32_t pos = wave_append(&ctl->fin_count, listed);
+        if (listed) fin_list[pos] = slot;
     }
     if (failed) atomicOr(&cnt[C_FAIL], 1u);
     if (n_keys) atomicAdd(&cnt[C_KEYS], n_keys);
-    if (n_live) atomicAdd(&cnt[C_LIVE], n_live);
-    if (n_cx) atomicAdd(&cnt[C_CX], n_cx);
-    if (n_ex) atomicAdd(&cnt[C_EX], n_ex);
     if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
     __syncthreads();
     if (cnt[C_FAIL]) {  // defer the packets of the flows that found no slot
@@ -347,22 +453,73 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(BatchView b, Params p, T
             if (e >= 0 && (ht[e].tflags & RED_FAILED)) defer_packet(ctl, deferred_list, r.z, false);
         }
     }
-    flush_block_stats(sc, stats);
     if (tid == 0) {
         if (cnt[C_KEYS]) atomicAdd(&ctl->new_keys, cnt[C_KEYS]);
-        if (cnt[C_LIVE]) atomicAdd(&ctl->new_live, cnt[C_LIVE]);
-        if (cnt[C_CX]) atomicAdd(&ctl->complex_count, cnt[C_CX]);
-        if (cnt[C_EX]) atomicAdd(&ctl->exported, cnt[C_EX]);
         if (cnt[C_TOUCH]) atomicAdd(&ctl->touched, cnt[C_TOUCH]);
         if (cnt[C_SPILL]) atomicAdd(&ctl->spilled, cnt[C_SPILL]);
         if (!fuse || cnt[C_SPILL] || cnt[C_FAIL]) ctl->pending = 1;
     }
 }
 
-void launch_reduce(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                   ExportView ex, BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats) {
+void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
+                   uint32_t* deferred_list) {
     const uint32_t grid = (1u << bv.part_bits) * bv.groups;
-    hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(RED_THREADS), 0, st, b, p, t, f, bv, ex, ctl, deferred_list,
+    hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list, deferred_list);
+}
+
+// ---- finalisation of the flows k_reduce completed -----------------------------------------
+// One lane per listed slot: finalize_slot with the creator's headers staged in the lane's
+// LDS column (256-thread blocks keep the register budget of the general parser).
+__global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
+                                                         ExportView ex, BatchCtl* ctl, const uint32_t* fin_list,
+                                                         unsigned long long* stats) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    __shared__ uint32_t sc[ST_COUNT];
+    __shared__ uint32_t cnt[3];  // new live, complex, exported
+    const uint32_t nf = ctl->fin_count;  // final: k_reduce has completed
+    if (blockIdx.x * IPXG_BLOCK >= nf) return;
+    const uint32_t tid = threadIdx.x;
+    if (tid < ST_COUNT) sc[tid] = 0;
+    if (tid < 3) cnt[tid] = 0;
+    __syncthreads();
+    const bool force_cx = p.force_complex || ctl->nonmono;
+    uint32_t n_live = 0, n_cx = 0, n_ex = 0;
+    for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {
+        const uint32_t k = base + tid;
+        bool do_export = false;
+        uint8_t reason = 0;
+        ipxg_flow_record er;
+        if (k < nf) {
+            const uint32_t s = fin_list[k];
+            const FinResult fr = finalize_slot<true>(b, p, t, f, s, t.hot[s], force_cx, &win[tid], er);
+            if (fr.status == FIN_COMPLEX) n_cx++;
+            else if (fr.created) n_live++;
+            do_export = fr.do_export;
+            reason = fr.reason;
+        }
+        const uint32_t pos = wave_append(ex.count, do_export);
+        if (do_export) {
+            store_export(ex, pos, er, reason);
+            atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
+            n_ex++;
+        }
+    }
+    if (n_live) atomicAdd(&cnt[0], n_live);
+    if (n_cx) atomicAdd(&cnt[1], n_cx);
+    if (n_ex) atomicAdd(&cnt[2], n_ex);
+    flush_block_stats(sc, stats);
+    if (tid == 0) {
+        if (cnt[0]) atomicAdd(&ctl->new_live, cnt[0]);
+        if (cnt[1]) atomicAdd(&ctl->complex_count, cnt[1]);
+        if (cnt[2]) atomicAdd(&ctl->exported, cnt[2]);
+    }
+}
+
+void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
+                     BatchCtl* ctl, const uint32_t* fin_list, unsigned long long* stats, uint32_t max_n) {
+    uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
+    if (grid > 1024) grid = 1024;
+    hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, ex, ctl, fin_list,
                        stats);
 }
 

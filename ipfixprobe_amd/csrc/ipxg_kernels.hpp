@@ -48,6 +48,8 @@ struct BatchCtl {
     uint32_t exported;       // records exported while applying this batch
     uint32_t touched;        // flow aggregates built by k_reduce (partition sizing)
     uint32_t spilled;        // packets that fell back to direct atomic accumulation
+    uint32_t slow_count;     // packets k_bin left for k_bin_slow
+    uint32_t fin_count;      // slots k_reduce listed for k_fin_list
 };
 
 // Fragmentation-cache ring entry (fragmentationKeyData.hpp:49-112), 4 per bucket.
@@ -136,9 +138,13 @@ struct ComplexView {
 
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
-void launch_reduce(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                   ExportView ex, BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
+                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats);
+void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
+                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats);
+void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
+                   uint32_t* deferred_list);
+void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
+                     BatchCtl* ctl, const uint32_t* fin_list, unsigned long long* stats, uint32_t max_n);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
 void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,

@@ -66,8 +66,8 @@ class Batch(ctypes.Structure):
 
 
 class Timing(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_double) for n in ("ingest_ms", "reduce_ms", "finalize_ms", "slow_ms",
-                                               "finish_ms")] + \
+    _fields_ = [(n, ctypes.c_double) for n in ("ingest_ms", "ingest_slow_ms", "reduce_ms", "fin_ms",
+                                               "finalize_ms", "slow_ms", "finish_ms")] + \
         [(n, ctypes.c_uint64) for n in ("ingest_launches", "reduce_launches", "finalize_launches",
                                         "slow_launches", "finish_launches", "ingest_packets")]
 
