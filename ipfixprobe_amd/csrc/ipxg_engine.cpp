@@ -113,8 +113,9 @@ static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_c
 
 // Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
 // (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
-// than the batch's packets.  Regions hold 1.5x the mean share (+256) per k_reduce workgroup
-// and twice that per partition, for skew; what does not fit spills to atomics.
+// than the batch's packets.  Regions hold 1.5x the mean share (+256, + k_bin's padding of
+// each tile's run to 4 records) per k_reduce workgroup and twice that per partition, for
+// skew; what does not fit spills to atomics.
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
     if (est == 0 || est > n) est = n;
@@ -122,7 +123,8 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
     const uint32_t P = 1u << bits;
     const uint64_t avg = ((uint64_t)n + P - 1) / P;
-    const uint64_t want = avg + avg / 2 + 256;
+    const uint64_t tiles = ((uint64_t)n + 2047) / 2048;  // k_bin tiles: each pads its runs to 4 records
+    const uint64_t want = (avg + avg / 2 + 256 + 3 * std::min<uint64_t>(tiles, avg + avg / 2) + 3) & ~3ull;
     const uint32_t chunk = (uint32_t)std::min<uint64_t>(want, RED_MAX_CHUNK);
     const uint32_t groups = (uint32_t)std::max<uint64_t>(2, (2 * want + chunk - 1) / chunk);
     int rc;

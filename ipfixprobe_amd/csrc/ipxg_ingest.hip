@@ -114,6 +114,10 @@ __device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_d
 // After every lane ranked its records of the tile in hist[part]: reserve room per partition
 // (one device atomic per non-empty partition, lanes on consecutive counters = 256-byte rows)
 // and write each record into its region; a full region spills to direct accumulation.
+// Reservations are rounded up to 4 records (64 bytes) and the tail filled with null records
+// (k_reduce skips them), so every 64-byte segment of a region is written by one workgroup:
+// unaligned runs shared by workgroups on different XCDs were written back as partial lines
+// by each XCD's L2 (2.4x the record bytes in WRITE_SIZE).
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
 template <bool LISTED>
@@ -125,7 +129,12 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t P, uint32_t p
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) {
         const uint32_t cnt = hist[q];
-        if (cnt) hist[q] = atomicAdd(&bv.count[q], cnt);
+        if (!cnt) continue;
+        const uint32_t padded = (cnt + 3) & ~3u;
+        const uint32_t base = atomicAdd(&bv.count[q], padded);
+        hist[q] = base;
+        for (uint32_t k = base + cnt; k < base + padded && k < bv.cap; ++k)
+            bv.rec[(size_t)q * bv.cap + k] = make_uint4(0, 0, NO_REC, 0);
     }
     __syncthreads();
 #pragma unroll
@@ -184,6 +193,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / base
+    __shared__ uint32_t slowbuf[BIN_TILE];              // 8 KiB: the tile's packets for k_bin_slow
+    __shared__ uint32_t nslow, slow_base;
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
@@ -192,6 +203,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     uint32_t frags = 0, spilled = 0;
     for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
         for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
+        if (tid == 0) nslow = 0;
         __syncthreads();
         uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
 #pragma unroll
@@ -233,8 +245,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                 if (fast_ok && fast_shape(dc) && parse_fast(hc.c0, hc.c1, hc.c2, dc.caplen, pk, c)) have = true;
                 else slow = true;
             }
-            const uint32_t spos = wave_append(&ctl->slow_count, slow);
-            if (slow) slow_list[spos] = i;
+            if (slow) slowbuf[atomicAdd(&nslow, 1u)] = i;
             if (have) {
                 if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {  // fragmentation cache path
                     frags++;
@@ -248,6 +259,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             dn = dnn;
         }
         tile_emit<false>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
+        // the tile's slow packets: one list reservation per tile
+        const uint32_t ns = nslow;
+        if (tid == 0 && ns) slow_base = atomicAdd(&ctl->slow_count, ns);
+        __syncthreads();
+        for (uint32_t k = tid; k < ns; k += IPXG_BLOCK) slow_list[slow_base + k] = slowbuf[k];
     }
     // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
@@ -373,6 +389,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                                                         uint32_t* deferred_list) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
     __shared__ uint32_t cnt[C_N];
+    __shared__ uint32_t scan_s[RED_THREADS / 64 + 1];
+    __shared__ uint32_t fin_base;
     const uint32_t part = blockIdx.x / bv.groups, g = blockIdx.x - part * bv.groups;
     const uint32_t total = min(bv.count[part], bv.cap);
     const uint32_t beg = g * bv.chunk;
@@ -413,12 +431,14 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     // partition's records and no packet went to the fragment or deferred paths: then the
     // merged slot is complete and goes on the finalise list (k_fin_list).
     const bool fuse = !multi && ctl->frag_count == 0 && ctl->a_deferred == 0;
-    uint32_t n_keys = 0, n_touch = 0;
+    uint32_t n_keys = 0, n_touch = 0, n_list = 0;
+    uint32_t listed[RED_ENTRIES / RED_THREADS];
     bool failed = false;
-    for (uint32_t e = tid; e < RED_ENTRIES; e += RED_THREADS) {  // same trip count in every lane
+#pragma unroll
+    for (uint32_t q = 0; q < RED_ENTRIES / RED_THREADS; ++q) {
+        const uint32_t e = tid + q * RED_THREADS;
         const FlowAgg a = ht[e];
-        uint32_t slot = 0;
-        bool listed = false;
+        listed[q] = NO_REC;
         if (a.key) {
             n_touch++;
             uint4 head;
@@ -435,13 +455,23 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                 h.key = a.key;
                 agg_fold(h, a);
                 *hp = h;
-                slot = (uint32_t)(hp - t.hot);
-                listed = fuse;
+                if (fuse) {
+                    listed[q] = (uint32_t)(hp - t.hot);
+                    n_list++;
+                }
             }
         }
-        const uint32_t pos = wave_append(&ctl->fin_count, listed);
-        if (listed) fin_list[pos] = slot;
     }
+    // one reservation on the finalise list per workgroup (a single counter saturates at ~88
+    // returning atomics per us: MI355X_MICROARCH.md "dequeue")
+    uint32_t listed_n;
+    uint32_t pos = block_exclusive_scan<RED_THREADS>(n_list, scan_s, &listed_n);
+    if (tid == 0) fin_base = listed_n ? atomicAdd(&ctl->fin_count, listed_n) : 0;
+    __syncthreads();
+    pos += fin_base;
+#pragma unroll
+    for (uint32_t q = 0; q < RED_ENTRIES / RED_THREADS; ++q)
+        if (listed[q] != NO_REC) fin_list[pos++] = listed[q];
     if (failed) atomicOr(&cnt[C_FAIL], 1u);
     if (n_keys) atomicAdd(&cnt[C_KEYS], n_keys);
     if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
