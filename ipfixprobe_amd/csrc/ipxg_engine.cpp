@@ -123,7 +123,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
     const uint32_t P = 1u << bits;
     const uint64_t avg = ((uint64_t)n + P - 1) / P;
-    const uint64_t tiles = ((uint64_t)n + 2047) / 2048;  // k_bin tiles: each pads its runs to 4 records
+    const uint64_t tiles = ((uint64_t)n + 1023) / 1024;  // k_bin tiles (>= 1024 packets): each pads its runs
     const uint64_t want = (avg + avg / 2 + 256 + 3 * std::min<uint64_t>(tiles, avg + avg / 2) + 3) & ~3ull;
     const uint32_t chunk = (uint32_t)std::min<uint64_t>(want, RED_MAX_CHUNK);
     const uint32_t groups = (uint32_t)std::max<uint64_t>(2, (2 * want + chunk - 1) / chunk);

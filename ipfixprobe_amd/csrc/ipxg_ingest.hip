@@ -28,10 +28,22 @@
 
 namespace ipxg {
 
-constexpr int BIN_K = 8;                          // packets per lane per tile
+#ifndef IPXG_BIN_K
+#define IPXG_BIN_K 8
+#endif
+#ifndef IPXG_BIN_WAVES
+#define IPXG_BIN_WAVES 4
+#endif
+#ifndef IPXG_BIN_GRID
+#define IPXG_BIN_GRID 2048
+#endif
+#ifndef IPXG_RED_U
+#define IPXG_RED_U 16
+#endif
+constexpr int BIN_K = IPXG_BIN_K;                 // packets per lane per tile
 constexpr uint32_t BIN_TILE = BIN_K * IPXG_BLOCK;  // 2048 packets
 constexpr uint32_t NO_REC = 0xFFFFFFFFu;
-constexpr uint32_t RED_U = 4;                     // records in flight per thread
+constexpr uint32_t RED_U = IPXG_RED_U;            // records in flight per thread
 constexpr uint32_t RED_MAX_PROBE = 256;
 constexpr uint32_t RED_FAILED = 0x80000000u;      // FlowAgg::tflags bit: table probe failed
 
@@ -189,7 +201,7 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 // latency-bound otherwise).  Frames the register parser does not take go to the slow list
 // for k_bin_slow.  No LDS header staging here: LDS holds only the partition histogram, so
 // occupancy is set by registers.
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / base
@@ -339,7 +351,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
     uint32_t tiles = (b.n + BIN_TILE - 1) / BIN_TILE;
-    if (tiles > 2048) tiles = 2048;
+    if (tiles > IPXG_BIN_GRID) tiles = IPXG_BIN_GRID;
     hipLaunchKernelGGL(k_bin, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
                        deferred_list, stats);
 }

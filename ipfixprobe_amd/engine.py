@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libipxg.so")
+# IPXG_LIB: an alternative build of the same library (tuning experiments, tools/variants.sh)
+LIB_PATH = os.environ.get("IPXG_LIB") or os.path.join(_HERE, "libipxg.so")
 
 DLT_EN10MB, DLT_RAW, DLT_LINUX_SLL, DLT_LINUX_SLL2 = 1, 12, 113, 276
 BATCH_DEVICE = 0x1
