@@ -58,16 +58,18 @@ __device__ __forceinline__ void defer_packet(BatchCtl* ctl, uint32_t* list, uint
 // options -- read straight from its first 48 bytes in registers: exactly the fields, checks
 // and counters parse_frame produces for such a frame (parse_eth_hdr parser.cpp:68-155,
 // parse_ipv4_hdr :311-356, parse_tcp_hdr :469-543 with doff <= 5, parse_udp_hdr :552-573),
-// without staging it in LDS.  Returns false for any other shape (or a TCP header cut by
-// caplen): the caller then takes the general parser.  c0..c2 = bytes 0..47, caplen >= 48.
+// without staging it in LDS.  Returns false for any other shape, a TCP header cut by caplen,
+// or a fragment when the fragmentation cache is on: the caller then takes the general
+// path.  c0..c2 = bytes 0..47, caplen >= 48.
 __device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, const uint4& c2, uint32_t caplen,
-                                           DevPkt& p, ParseCounts& c) {
+                                           bool frag_enable, DevPkt& p, ParseCounts& c) {
     if ((c0.w & 0xFFFF) != 0x0008) return false;          // ethertype 0x0800 at bytes 12-13
     if (((c0.w >> 16) & 0xFF) != 0x45) return false;      // version 4, IHL 5
     const uint32_t proto = c1.y >> 24;                     // byte 23
     if (proto == 47) return false;                         // GRE: the general parser recurses
     const uint32_t fo = bswap16(c1.y);                     // bytes 20-21
     const uint32_t frag_off = fo & 0x1FFF;
+    if (frag_enable && (fo & 0x3FFF)) return false;        // a fragment: the fragmentation-cache path
     uint32_t ports = 0, flags = 0;
     if (frag_off == 0 && proto == 6) {
         if (caplen < 54) return false;                     // 20 > data_len: the general path drops it
@@ -99,11 +101,11 @@ __device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, con
     return true;
 }
 
-__device__ __forceinline__ ipxg_pkt_desc load_desc(const BatchView& b, uint32_t i) {
-    ipxg_pkt_desc d = {0, 0, 0, 0, 0};
-    if (i < b.n) d = b.desc[i];
-    return d;
-}
+// A readable 48-byte frame of zeros: the loads below are issued unconditionally (a lane with
+// nothing to load reads this), so the number of loads in flight is the same on every path
+// and the compiler's s_waitcnt can wait for exactly the one it needs (a conditional load
+// made it wait for all of them, vmcnt(0), defeating the prefetch).
+__device__ uint4 g_zero_head[3];
 
 struct Head48 {  // bytes 0..47 of a frame
     uint4 c0, c1, c2;
@@ -112,14 +114,11 @@ struct Head48 {  // bytes 0..47 of a frame
 __device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.offset & 15) == 0 && d.caplen >= 48; }
 
 __device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_desc& d, bool ok) {
+    const uint4* fr = ok ? reinterpret_cast<const uint4*>(b.arena + d.offset) : g_zero_head;
     Head48 h;
-    h.c0 = h.c1 = h.c2 = make_uint4(0, 0, 0, 0);
-    if (ok) {
-        const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
-        h.c0 = fr[0];
-        h.c1 = fr[1];
-        h.c2 = fr[2];
-    }
+    h.c0 = fr[0];
+    h.c1 = fr[1];
+    h.c2 = fr[2];
     return h;
 }
 
@@ -196,23 +195,39 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
     f.list[pos] = ((uint64_t)bucket << 24) | i;
 }
 
-// Every packet of the batch, in tiles of BIN_K x 256: the descriptor two packets ahead and
-// the 48-byte head one packet ahead are in flight while a packet is parsed (the loop is
-// latency-bound otherwise).  Frames the register parser does not take go to the slow list
-// for k_bin_slow.  No LDS header staging here: LDS holds only the partition histogram, so
-// occupancy is set by registers.
+// Every packet of the batch, in tiles of BIN_K x 256.  Software-pipelined: the descriptors of
+// the packet two steps ahead (and of its predecessor, for the timestamp order check) and the
+// 48-byte head of the next packet are in flight while a packet is parsed; the loop issues no
+// other global memory operation.  Frames the register parser does not take go to the slow
+// list for k_bin_slow.  No LDS header staging here: LDS holds only the partition histogram
+// and the tile's slow list, so occupancy is set by registers.
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / base
-    __shared__ uint32_t slowbuf[BIN_TILE];              // 8 KiB: the tile's packets for k_bin_slow
+    __shared__ uint32_t slowbuf[BIN_TILE];              // the tile's packets for k_bin_slow
     __shared__ uint32_t nslow, slow_base;
     const uint32_t tid = threadIdx.x;
-    if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
+    if (b.n == 0) return;
+    const uint32_t last = b.n - 1;
+    const uint32_t base_sec = b.base_sec == BASE_FROM_DESC0 ? b.desc[0].ts_sec : b.base_sec;
+    b.base_sec = base_sec;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    const uint64_t ts_before = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
-    uint32_t frags = 0, spilled = 0;
+    uint32_t spilled = 0;
+    bool nonmono = false;
+    // ts of the packet before i (packet 0 compares with itself; its predecessor, the previous
+    // batch's last packet, is checked once below) -- an unconditional load
+    auto prev_ts = [&](uint32_t i) -> uint64_t {
+        const uint2 w = *reinterpret_cast<const uint2*>(&b.desc[i - (i != 0)].ts_sec);
+        return ((uint64_t)w.x << 32) | w.y;
+    };
+    if (blockIdx.x == 0 && tid == 0 && p.prev_valid) {
+        const ipxg_pkt_desc d0 = b.desc[0];
+        if ((((uint64_t)d0.ts_sec << 32) | d0.ts_usec) < ts_before) nonmono = true;
+    }
     for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
         for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
         if (tid == 0) nslow = 0;
@@ -223,52 +238,40 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
-        const uint32_t i0 = tile + tid;
-        ipxg_pkt_desc dc = load_desc(b, i0);
-        Head48 hc = load_head(b, dc, fast_ok && i0 < b.n && fast_shape(dc));
-        ipxg_pkt_desc dn = load_desc(b, i0 + IPXG_BLOCK);
+        // pipeline prologue: descriptors of steps 0 and 1, head of step 0
+        uint32_t i = tile + tid;
+        ipxg_pkt_desc dc = b.desc[min(i, last)];
+        uint64_t pc = prev_ts(min(i, last));
+        ipxg_pkt_desc dn = b.desc[min(i + IPXG_BLOCK, last)];
+        uint64_t pn = prev_ts(min(i + IPXG_BLOCK, last));
+        Head48 hc = load_head(b, dc, fast_ok && i < b.n && fast_shape(dc));
 #pragma unroll 1
-        for (int j = 0; j < BIN_K; ++j) {
-            const uint32_t i = tile + (uint32_t)j * IPXG_BLOCK + tid;
-            const uint32_t in = i + IPXG_BLOCK;
-            const Head48 hn = load_head(b, dn, j + 1 < BIN_K && fast_ok && in < b.n && fast_shape(dn));
-            const ipxg_pkt_desc dnn = load_desc(b, j + 2 < BIN_K ? in + IPXG_BLOCK : 0xFFFFFFFFu);
+        for (int j = 0; j < BIN_K; ++j, i += IPXG_BLOCK) {
+            // issue: descriptors two steps ahead, then the next head (its descriptor, dn, was
+            // issued a step ago: waiting for it does not wait for the current head)
+            const uint32_t i2 = min(i + 2 * IPXG_BLOCK, last);
+            const ipxg_pkt_desc dnn = b.desc[i2];
+            const uint64_t pnn = prev_ts(i2);
+            const Head48 hn = load_head(b, dn, fast_ok && i + IPXG_BLOCK < b.n && fast_shape(dn));
+            // this step's packet: dc, pc and hc were loaded at least one step ago
             const bool act = i < b.n;
-            // a timestamp going backwards sends every flow of the batch to the sequential path
             const uint64_t ts = ((uint64_t)dc.ts_sec << 32) | dc.ts_usec;
-            uint64_t prev = (uint64_t)__shfl_up((unsigned long long)ts, 1);
-            if (lane_id() == 0) {
-                if (i > 0 && act) {
-                    const ipxg_pkt_desc q = b.desc[i - 1];
-                    prev = ((uint64_t)q.ts_sec << 32) | q.ts_usec;
-                } else {
-                    prev = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
-                }
-            }
-            const bool has_prev = i > 0 || p.prev_valid;
-            if (act && has_prev && ts < prev) ctl->nonmono = 1;
-            if (act && i == b.n - 1) {
-                ctl->last_sec = dc.ts_sec;
-                ctl->last_usec = dc.ts_usec;
-            }
+            if (act && ts < pc) nonmono = true;
             DevPkt pk;
             bool have = false, slow = false;
             if (act) {
-                if (fast_ok && fast_shape(dc) && parse_fast(hc.c0, hc.c1, hc.c2, dc.caplen, pk, c)) have = true;
-                else slow = true;
+                if (fast_ok && fast_shape(dc) && parse_fast(hc.c0, hc.c1, hc.c2, dc.caplen, p.frag_enable, pk, c))
+                    have = true;
+                else
+                    slow = true;
             }
             if (slow) slowbuf[atomicAdd(&nslow, 1u)] = i;
-            if (have) {
-                if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {  // fragmentation cache path
-                    frags++;
-                    divert_fragment(pk, p, f, ctl, i);
-                } else {
-                    tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
-                }
-            }
+            if (have) tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
             dc = dn;
-            hc = hn;
+            pc = pn;
             dn = dnn;
+            pn = pnn;
+            hc = hn;
         }
         tile_emit<false>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
         // the tile's slow packets: one list reservation per tile
@@ -277,10 +280,16 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         __syncthreads();
         for (uint32_t k = tid; k < ns; k += IPXG_BLOCK) slow_list[slow_base + k] = slowbuf[k];
     }
+    if (tid == 0 && blockIdx.x == (last / BIN_TILE) % gridDim.x) {
+        const ipxg_pkt_desc d = b.desc[last];  // the batch's last timestamp (next batch's order check)
+        ctl->last_sec = d.ts_sec;
+        ctl->last_usec = d.ts_usec;
+    }
+    if (nonmono) ctl->nonmono = 1;
     // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
-    flush_counts(c, 0, frags, hist);
+    flush_counts(c, 0, 0, hist);
     flush_block_stats(hist, stats);
     if (spilled) {
         atomicAdd(&ctl->spilled, spilled);
