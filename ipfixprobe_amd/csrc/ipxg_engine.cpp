@@ -676,6 +676,12 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     return IPXG_OK;
 }
 
+int ipxg_probe_counters(ipxg_engine* e, uint64_t* out) {
+    if (!e || !out) return IPXG_EINVAL;
+    for (int k = 0; k < 8; ++k) out[k] = e->ctl_h->probe[k];
+    return IPXG_OK;
+}
+
 int ipxg_profile(ipxg_engine* e, int enable) {
     if (!e) return IPXG_EINVAL;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));

@@ -38,7 +38,16 @@ namespace ipxg {
 #define IPXG_BIN_GRID 2048
 #endif
 #ifndef IPXG_RED_U
-#define IPXG_RED_U 16
+#define IPXG_RED_U 4
+#endif
+// IPXG_PROBE builds accumulate per-phase shader clocks of k_bin into ctl->probe (read with
+// ipxg_probe_counters): [0] tile start, [1] packet loop, [2] emit, [3] slow-list flush.
+#ifdef IPXG_PROBE
+#define PROBE_T(v) const uint64_t v = __builtin_readcyclecounter()
+#define PROBE_ADD(k, a, b) probe_acc[k] += (b) - (a)
+#else
+#define PROBE_T(v)
+#define PROBE_ADD(k, a, b)
 #endif
 constexpr int BIN_K = IPXG_BIN_K;                 // packets per lane per tile
 constexpr uint32_t BIN_TILE = BIN_K * IPXG_BLOCK;  // 2048 packets
@@ -228,10 +237,16 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         const ipxg_pkt_desc d0 = b.desc[0];
         if ((((uint64_t)d0.ts_sec << 32) | d0.ts_usec) < ts_before) nonmono = true;
     }
+#ifdef IPXG_PROBE
+    uint64_t probe_acc[4] = {0, 0, 0, 0};
+#endif
     for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
+        PROBE_T(t0);
         for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
         if (tid == 0) nslow = 0;
         __syncthreads();
+        PROBE_T(t1);
+        PROBE_ADD(0, t0, t1);
         uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
 #pragma unroll
         for (int q = 0; q < BIN_K; ++q) {
@@ -273,13 +288,23 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             pn = pnn;
             hc = hn;
         }
+        PROBE_T(t2);
+        PROBE_ADD(1, t1, t2);
         tile_emit<false>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
+        PROBE_T(t3);
+        PROBE_ADD(2, t2, t3);
         // the tile's slow packets: one list reservation per tile
         const uint32_t ns = nslow;
         if (tid == 0 && ns) slow_base = atomicAdd(&ctl->slow_count, ns);
         __syncthreads();
         for (uint32_t k = tid; k < ns; k += IPXG_BLOCK) slow_list[slow_base + k] = slowbuf[k];
+        PROBE_T(t4);
+        PROBE_ADD(3, t3, t4);
     }
+#ifdef IPXG_PROBE
+    if (lane_id() == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long*)&ctl->probe[k], (unsigned long long)probe_acc[k]);
+#endif
     if (tid == 0 && blockIdx.x == (last / BIN_TILE) % gridDim.x) {
         const ipxg_pkt_desc d = b.desc[last];  // the batch's last timestamp (next batch's order check)
         ctl->last_sec = d.ts_sec;

@@ -50,6 +50,7 @@ struct BatchCtl {
     uint32_t spilled;        // packets that fell back to direct atomic accumulation
     uint32_t slow_count;     // packets k_bin left for k_bin_slow
     uint32_t fin_count;      // slots k_reduce listed for k_fin_list
+    uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
 // Fragmentation-cache ring entry (fragmentationKeyData.hpp:49-112), 4 per bucket.

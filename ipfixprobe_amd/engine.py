@@ -84,6 +84,7 @@ EXPORTED_SYMBOLS = [
     "ipxg_reset", "ipxg_pending_exports", "ipxg_poll_exports", "ipxg_device_exports",
     "ipxg_clear_exports", "ipxg_get_stats", "ipxg_parse_batch", "ipxg_xxh64_batch",
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
+    "ipxg_probe_counters",
 ]
 
 _LIB = None
@@ -131,6 +132,7 @@ def lib():
         L.ipxg_capture_free.argtypes = [ctypes.POINTER(Capture)]
         L.ipxg_profile.argtypes = [vp, ctypes.c_int]
         L.ipxg_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
+        L.ipxg_probe_counters.argtypes = [vp, vp]
         for name in EXPORTED_SYMBOLS:
             if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default",
                             "ipxg_capture_free"):
@@ -271,6 +273,11 @@ class Engine:
         t = Timing()
         self._check(lib().ipxg_get_timing(self._h, ctypes.byref(t)), "ipxg_get_timing")
         return {f: getattr(t, f) for f, _ in Timing._fields_}
+
+    def probe_counters(self):
+        out = np.zeros(8, dtype=np.uint64)
+        self._check(lib().ipxg_probe_counters(self._h, out.ctypes.data), "ipxg_probe_counters")
+        return out
 
     def parse(self, arena, desc):
         b = self._batch(arena, desc)

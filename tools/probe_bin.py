@@ -1,0 +1,35 @@
+"""Per-phase shader clocks of k_bin on the bench batch (library built with -DIPXG_PROBE:
+IPXG_LIB=ipfixprobe_amd/variants/probe.so python3 tools/probe_bin.py)."""
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import bench
+    from ipfixprobe_amd import Engine
+    dev = torch.device("cuda", 0)
+    flows = bench.gen_flows(100_000, 0, 1, 1234)
+    frames, desc = bench.build_batch(flows, 10_000_000, 1234, dev)
+    eng = Engine("s=%d" % int(math.ceil(math.log2(4 * 100_000))))
+    eng.profile(True)
+    for _ in range(3):
+        eng.submit(frames, desc, device=True)
+        eng.finish()
+        eng.clear_exports()
+    pc = eng.probe_counters()
+    tm = eng.timing()
+    waves = 2048 * 4
+    names = ["tile start", "packet loop", "emit", "slow flush"]
+    tot = sum(int(x) for x in pc[:4])
+    for k, nme in enumerate(names):
+        print("%-12s %12.0f cycles/wave  %5.1f %%" % (nme, int(pc[k]) / waves, 100.0 * int(pc[k]) / max(tot, 1)))
+    print("k_bin avg %.4f ms" % (tm["ingest_ms"] / tm["ingest_launches"]))
+
+
+if __name__ == "__main__":
+    main()
