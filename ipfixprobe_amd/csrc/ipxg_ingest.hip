@@ -151,7 +151,11 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t P, uint32_t p
         const uint32_t cnt = hist[q];
         if (!cnt) continue;
         const uint32_t padded = (cnt + 3) & ~3u;
+#ifdef IPXG_EXP_NORESERVE  // timing experiment only: results are wrong
+        const uint32_t base = ((blockIdx.x * 8 + (tile / BIN_TILE) % 8) * 16) % (bv.cap - 64);
+#else
         const uint32_t base = atomicAdd(&bv.count[q], padded);
+#endif
         hist[q] = base;
         for (uint32_t k = base + cnt; k < base + padded && k < bv.cap; ++k)
             bv.rec[(size_t)q * bv.cap + k] = make_uint4(0, 0, NO_REC, 0);
@@ -182,7 +186,13 @@ __device__ __forceinline__ void tile_rank(uint32_t* hist, uint32_t pmask, const 
                                           uint32_t (&rk)[BIN_K], uint32_t (&ix)[BIN_K]) {
     uint64_t lo, hf;
     uint32_t cdir;
+#ifdef IPXG_EXP_NOHASH  // timing experiment only: results are wrong
+    lo = ((uint64_t)pk.sip[0] << 32) ^ pk.dip[0] ^ ((uint64_t)pk.src_port << 16) ^ pk.dst_port;
+    cdir = 0;
+    hf = lo;
+#else
     canon(pk, p, lo, cdir, hf);
+#endif
     const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
     const uint32_t rank = atomicAdd(&hist[(uint32_t)(lo >> 32) & pmask], 1u);
 #pragma unroll
