@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -113,53 +114,32 @@ static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_c
 
 // Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
 // (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
-// than the batch's packets.  Regions hold 1.5x the mean share (+256, + k_bin's padding of
-// each tile's run to 4 records) per k_reduce workgroup and twice that per partition, for
-// skew; what does not fit spills to atomics.
+// than the batch's packets.  k_bin runs bin_grid persistent workgroups over the 2048-packet
+// tiles; each owns one segment per partition, sized for 1.5x its mean share of records plus
+// 4 standard deviations (binomial) and a margin; what does not fit spills to atomics.
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
     if (est == 0 || est > n) est = n;
     uint32_t bits = 0;
     while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
     const uint32_t P = 1u << bits;
-    const uint64_t avg = ((uint64_t)n + P - 1) / P;
-    const uint64_t tiles = ((uint64_t)n + 1023) / 1024;  // k_bin tiles (>= 1024 packets): each pads its runs
-    const uint64_t want = (avg + avg / 2 + 256 + 3 * std::min<uint64_t>(tiles, avg + avg / 2) + 3) & ~3ull;
-    const uint32_t chunk = (uint32_t)std::min<uint64_t>(want, RED_MAX_CHUNK);
-    const uint32_t groups = (uint32_t)std::max<uint64_t>(2, (2 * want + chunk - 1) / chunk);
+    const uint64_t tiles = ((uint64_t)n + 2047) / 2048;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, 1024);
+    const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * 2048, n);
+    const double mean = (double)per_block / P;
+    const uint64_t seg = ((uint64_t)(mean * 1.5 + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
+    const uint32_t cols = 2 * grid;
     int rc;
-    if ((rc = ensure(e, e->bin_rec, (size_t)P * groups * chunk * sizeof(uint4)))) return rc;
-    if ((rc = ensure(e, e->bin_count, (size_t)P * sizeof(uint32_t)))) return rc;
-    HIPCHK(e, hipMemsetAsync(e->bin_count.p, 0, (size_t)P * sizeof(uint32_t), e->st));
+    if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
+    if ((rc = ensure(e, e->bin_count, (size_t)P * cols * sizeof(uint32_t)))) return rc;
+    HIPCHK(e, hipMemsetAsync(e->bin_count.p, 0, (size_t)P * cols * sizeof(uint32_t), e->st));
     bv.rec = (uint4*)e->bin_rec.p;
     bv.count = (uint32_t*)e->bin_count.p;
-    bv.cap = groups * chunk;
-    bv.chunk = chunk;
+    bv.seg_cap = (uint32_t)seg;
+    bv.cols = cols;
+    bv.bin_grid = grid;
     bv.part_bits = bits;
-    bv.groups = groups;
     return IPXG_OK;
-}
-
-static FragView frag_view(ipxg_engine* e) {
-    return FragView{e->frag_ent, e->frag_cnt, (uint64_t*)e->frag_list.p, (uint64_t*)e->frag_sorted.p,
-                    (uint32_t*)e->frag_ports.p};
-}
-
-static Params params(ipxg_engine* e) {
-    Params p = {};
-    p.dlt = e->cfg.datalink;
-    p.active_s = e->cfg.active_s;
-    p.inactive_s = e->cfg.inactive_s;
-    p.bucket_w = std::max<uint32_t>(1, e->cfg.inactive_s / 2);
-    p.split_biflow = e->cfg.split_biflow;
-    p.frag_enable = e->cfg.frag_enable;
-    p.frag_size = e->cfg.frag_size ? e->cfg.frag_size : 10007;
-    p.frag_timeout_s = e->cfg.frag_timeout_s;
-    p.force_complex = e->cfg.inactive_s < 2 ? 1 : 0;
-    p.prev_valid = e->prev_valid;
-    p.prev_sec = e->prev_sec;
-    p.prev_usec = e->prev_usec;
-    return p;
 }
 
 static int alloc_table(ipxg_engine* e, uint32_t cap, HotSlot** hot, ipxg_flow_record** cold, uint32_t** rank) {

@@ -34,9 +34,6 @@ namespace ipxg {
 #ifndef IPXG_BIN_WAVES
 #define IPXG_BIN_WAVES 4
 #endif
-#ifndef IPXG_BIN_GRID
-#define IPXG_BIN_GRID 2048
-#endif
 #ifndef IPXG_RED_U
 #define IPXG_RED_U 4
 #endif
@@ -131,34 +128,27 @@ __device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_d
     return h;
 }
 
-// After every lane ranked its records of the tile in hist[part]: reserve room per partition
-// (one device atomic per non-empty partition, lanes on consecutive counters = 256-byte rows)
-// and write each record into its region; a full region spills to direct accumulation.
-// Reservations are rounded up to 4 records (64 bytes) and the tail filled with null records
-// (k_reduce skips them), so every 64-byte segment of a region is written by one workgroup:
-// unaligned runs shared by workgroups on different XCDs were written back as partial lines
-// by each XCD's L2 (2.4x the record bytes in WRITE_SIZE).
+// After every lane ranked its records of the tile in hist[part]: each partition's records
+// of the tile follow the ones of the block's earlier tiles in the block's own segment of
+// that partition (fill[part] = records so far), so no workgroup shares a write position
+// with another and no device atomic is needed (a shared counter per partition, hit once
+// per tile by every workgroup, saturated at the memory-side atomic rate: ~35 % of k_bin).
+// A full segment spills to direct accumulation.
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
 template <bool LISTED>
-__device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t P, uint32_t pmask, const BinView& bv,
-                                          const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
-                                          const uint32_t (&r0)[BIN_K], const uint32_t (&r1)[BIN_K],
-                                          const uint32_t (&r2)[BIN_K], const uint32_t (&rk)[BIN_K],
-                                          const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& spilled) {
+__device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint32_t P, uint32_t pmask,
+                                          const BinView& bv, uint32_t col, const TableView& t, BatchCtl* ctl,
+                                          uint32_t* deferred_list, const uint32_t (&r0)[BIN_K],
+                                          const uint32_t (&r1)[BIN_K], const uint32_t (&r2)[BIN_K],
+                                          const uint32_t (&rk)[BIN_K], const uint32_t (&ix)[BIN_K], uint32_t tile,
+                                          uint32_t& spilled) {
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) {
         const uint32_t cnt = hist[q];
-        if (!cnt) continue;
-        const uint32_t padded = (cnt + 3) & ~3u;
-#ifdef IPXG_EXP_NORESERVE  // timing experiment only: results are wrong
-        const uint32_t base = ((blockIdx.x * 8 + (tile / BIN_TILE) % 8) * 16) % (bv.cap - 64);
-#else
-        const uint32_t base = atomicAdd(&bv.count[q], padded);
-#endif
+        const uint32_t base = fill[q];
+        fill[q] = base + cnt;
         hist[q] = base;
-        for (uint32_t k = base + cnt; k < base + padded && k < bv.cap; ++k)
-            bv.rec[(size_t)q * bv.cap + k] = make_uint4(0, 0, NO_REC, 0);
     }
     __syncthreads();
 #pragma unroll
@@ -167,15 +157,20 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t P, uint32_t p
         const uint32_t part = r1[q] & pmask;
         const uint32_t pos = hist[part] + rk[q];
         const uint32_t idx = LISTED ? ix[q] : tile + (uint32_t)q * IPXG_BLOCK + threadIdx.x;
-        if (pos < bv.cap) {
-            bv.rec[(size_t)part * bv.cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
-        } else {  // partition region full: accumulate straight into the table
+        if (pos < bv.seg_cap) {
+            bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
+        } else {  // segment full: accumulate straight into the table
             spilled++;
             const uint64_t lo = ((uint64_t)r1[q] << 32) | r0[q];
             if (!merge_packet_atomic(t, lo, idx, r2[q], &ctl->new_keys)) defer_packet(ctl, deferred_list, idx, true);
         }
     }
     __syncthreads();  // hist is reset by the next tile
+}
+
+// the block's record counts per partition (its column of bv.count)
+__device__ __forceinline__ void seg_counts(const uint32_t* fill, uint32_t P, const BinView& bv, uint32_t col) {
+    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + col] = min(fill[q], bv.seg_cap);
 }
 
 // rank one keyed, unfragmented packet in its partition and keep its record in slot j
@@ -224,9 +219,11 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / base
+    __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: records in the block's segments
     __shared__ uint32_t slowbuf[BIN_TILE];              // the tile's packets for k_bin_slow
     __shared__ uint32_t nslow, slow_base;
     const uint32_t tid = threadIdx.x;
+    for (uint32_t q = tid; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     if (b.n == 0) return;
     const uint32_t last = b.n - 1;
     const uint32_t base_sec = b.base_sec == BASE_FROM_DESC0 ? b.desc[0].ts_sec : b.base_sec;
@@ -300,7 +297,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
-        tile_emit<false>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
+        tile_emit<false>(hist, fill, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile,
+                         spilled);
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         // the tile's slow packets: one list reservation per tile
@@ -321,6 +319,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         ctl->last_usec = d.ts_usec;
     }
     if (nonmono) ctl->nonmono = 1;
+    seg_counts(fill, P, bv, blockIdx.x);
     // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
@@ -342,8 +341,11 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
                 const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];  // 32 KiB: one header column per lane
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB
+    __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB
     const uint32_t ns = ctl->slow_count;  // final: k_bin has completed
-    if (blockIdx.x * BIN_TILE >= ns) return;
+    if (blockIdx.x * BIN_TILE >= ns) return;  // its column stays zero (memset per batch)
+    for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
+    const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
@@ -380,8 +382,9 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             }
             tile_rank<true>(hist, pmask, p, b, pk, d, i, j, r0, r1, r2, rk, ix);
         }
-        tile_emit<true>(hist, P, pmask, bv, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
+        tile_emit<true>(hist, fill, P, pmask, bv, bcol, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
     }
+    seg_counts(fill, P, bv, bcol);
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
     flush_counts(c, keyless, frags, hist);
@@ -394,18 +397,14 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
 
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
-    uint32_t tiles = (b.n + BIN_TILE - 1) / BIN_TILE;
-    if (tiles > IPXG_BIN_GRID) tiles = IPXG_BIN_GRID;
-    hipLaunchKernelGGL(k_bin, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
+    hipLaunchKernelGGL(k_bin, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
                        deferred_list, stats);
 }
 
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                      BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
-    uint32_t tiles = (b.n + BIN_TILE - 1) / BIN_TILE;  // upper bound: the list is not longer than the batch
-    if (tiles > 1024) tiles = 1024;
-    hipLaunchKernelGGL(k_bin_slow, dim3(tiles ? tiles : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
-                       slow_list, deferred_list, stats);
+    hipLaunchKernelGGL(k_bin_slow, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
+                       deferred_list, stats);
 }
 
 // ---- phase B ------------------------------------------------------------------------------
@@ -440,33 +439,65 @@ __device__ __forceinline__ void lds_fold(FlowAgg& a, uint32_t idx, uint32_t m) {
 }
 
 enum RedCount { C_KEYS, C_TOUCH, C_SPILL, C_FAIL, C_N };
+constexpr uint32_t RED_MAX_COLS = 2 * BIN_MAX_GRID;
 
+// record k (0 <= k < total) of the partition: in the segment s with pre[s] <= k < pre[s+1]
+__device__ __forceinline__ uint4 seg_record(const uint4* segs, const uint32_t* pre, uint32_t cols,
+                                            uint32_t seg_cap, uint32_t k) {
+    uint32_t lo = 0, hi = cols;  // pre[lo] <= k < pre[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= k) lo = mid;
+        else hi = mid;
+    }
+    return segs[(size_t)lo * seg_cap + (k - pre[lo])];
+}
+
+// One workgroup per partition: the partition's records sit in one segment per k_bin /
+// k_bin_slow workgroup (bv.count gives their lengths); a prefix sum over the segment lengths
+// in LDS maps the partition's record k to its segment.
 __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
                                                         uint32_t* deferred_list) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
+    __shared__ uint32_t pre[RED_MAX_COLS + 1];
     __shared__ uint32_t cnt[C_N];
     __shared__ uint32_t scan_s[RED_THREADS / 64 + 1];
     __shared__ uint32_t fin_base;
-    const uint32_t part = blockIdx.x / bv.groups, g = blockIdx.x - part * bv.groups;
-    const uint32_t total = min(bv.count[part], bv.cap);
-    const uint32_t beg = g * bv.chunk;
-    if (beg >= total) return;  // uniform over the workgroup
-    const uint32_t end = min(total, beg + bv.chunk);
-    const bool multi = total > bv.chunk;  // other workgroups hold records of these flows too
+    const uint32_t part = blockIdx.x;
     const uint32_t tid = threadIdx.x;
+    const uint32_t cols = bv.cols;
+    const uint32_t* cnts = bv.count + (size_t)part * cols;
+    // segment lengths -> exclusive prefix (cols <= RED_MAX_COLS = 4 per thread)
+    uint32_t v[RED_MAX_COLS / RED_THREADS], my = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
+        const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
+        v[q] = c < cols ? cnts[c] : 0;
+        my += v[q];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<RED_THREADS>(my, scan_s, &total);
+    if (total == 0) return;  // uniform over the workgroup
+#pragma unroll
+    for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
+        const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
+        if (c < cols) pre[c] = run;
+        run += v[q];
+    }
+    if (tid == 0) pre[cols] = total;
     {
         uint4* z = reinterpret_cast<uint4*>(ht);
         for (uint32_t q = tid; q < sizeof(ht) / 16; q += RED_THREADS) z[q] = make_uint4(0, 0, 0, 0);
     }
     if (tid < C_N) cnt[tid] = 0;
     __syncthreads();
-    const uint4* recs = bv.rec + (size_t)part * bv.cap;
-    for (uint32_t k0 = beg; k0 < end; k0 += RED_THREADS * RED_U) {
+    const uint4* segs = bv.rec + (size_t)part * cols * bv.seg_cap;
+    for (uint32_t k0 = 0; k0 < total; k0 += RED_THREADS * RED_U) {
         uint4 r[RED_U];
 #pragma unroll
         for (uint32_t u = 0; u < RED_U; ++u) {
             const uint32_t k = k0 + u * RED_THREADS + tid;
-            r[u] = k < end ? recs[k] : make_uint4(0, 0, NO_REC, 0);
+            r[u] = k < total ? seg_record(segs, pre, cols, bv.seg_cap, k) : make_uint4(0, 0, NO_REC, 0);
         }
 #pragma unroll
         for (uint32_t u = 0; u < RED_U; ++u) {
@@ -483,10 +514,10 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         }
     }
     __syncthreads();
-    // Nothing else of this batch can touch these flows when the workgroup holds all of the
-    // partition's records and no packet went to the fragment or deferred paths: then the
+    // Nothing else of this batch can touch these flows when no packet went to the fragment or
+    // deferred paths (spilled packets were accumulated by k_bin, before this kernel): then the
     // merged slot is complete and goes on the finalise list (k_fin_list).
-    const bool fuse = !multi && ctl->frag_count == 0 && ctl->a_deferred == 0;
+    const bool fuse = ctl->frag_count == 0 && ctl->a_deferred == 0;
     uint32_t n_keys = 0, n_touch = 0, n_list = 0;
     uint32_t listed[RED_ENTRIES / RED_THREADS];
     bool failed = false;
@@ -504,8 +535,6 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
             if (!hp) {
                 ht[e].tflags = a.tflags | RED_FAILED;
                 failed = true;
-            } else if (multi) {
-                agg_merge_atomic(hp, a);
             } else {
                 HotSlot h = *hp;  // this workgroup is the slot's only writer in this kernel
                 h.key = a.key;
@@ -533,8 +562,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
     __syncthreads();
     if (cnt[C_FAIL]) {  // defer the packets of the flows that found no slot
-        for (uint32_t k = beg + tid; k < end; k += RED_THREADS) {
-            const uint4 r = recs[k];
+        for (uint32_t k = tid; k < total; k += RED_THREADS) {
+            const uint4 r = seg_record(segs, pre, cols, bv.seg_cap, k);
             const int e = lds_slot(ht, ((uint64_t)r.y << 32) | r.x, false);
             if (e >= 0 && (ht[e].tflags & RED_FAILED)) defer_packet(ctl, deferred_list, r.z, false);
         }
@@ -549,8 +578,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
                    uint32_t* deferred_list) {
-    const uint32_t grid = (1u << bv.part_bits) * bv.groups;
-    hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list, deferred_list);
+    hipLaunchKernelGGL(k_reduce, dim3(1u << bv.part_bits), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list,
+                       deferred_list);
 }
 
 // ---- finalisation of the flows k_reduce completed -----------------------------------------

@@ -112,21 +112,24 @@ struct FragView {
     uint32_t* ports;     // per packet index: resolved (sport << 16) | dport
 };
 
-// Phase-A output of the ingest (k_bin -> k_reduce): one record region per partition of the
-// canonical flow hash (bits 32.. of lo).  Record = {lo, hi, packet index, pack_misc()}.
+// Phase-A output of the ingest (k_bin / k_bin_slow -> k_reduce): per partition of the
+// canonical flow hash (bits 32.. of lo), one segment per k_bin and per k_bin_slow workgroup
+// ("column"), so every workgroup appends to its own segments without device atomics.
+// Record = {lo, hi, packet index, pack_misc()}.  Segment (part, col) starts at record
+// (part * cols + col) * seg_cap; count[part * cols + col] = its length.
 struct BinView {
-    uint4* rec;          // parts * cap records
-    uint32_t* count;     // per partition, zeroed per batch (may exceed cap: overflow spilled)
-    uint32_t cap;        // record slots per partition = groups * chunk
-    uint32_t chunk;      // records per k_reduce workgroup
+    uint4* rec;          // parts * cols * seg_cap records
+    uint32_t* count;     // parts * cols segment lengths (zeroed per batch)
+    uint32_t seg_cap;    // records per segment (a full segment spills to device atomics)
+    uint32_t cols;       // 2 * bin_grid: k_bin's columns, then k_bin_slow's
+    uint32_t bin_grid;   // workgroups of k_bin (and of k_bin_slow)
     uint32_t part_bits;  // parts = 1 << part_bits
-    uint32_t groups;     // k_reduce workgroups per partition
 };
-constexpr uint32_t BIN_MAX_PART_BITS = 11;  // <= 2048 partitions (k_bin's LDS histogram)
+constexpr uint32_t BIN_MAX_PART_BITS = 11;  // <= 2048 partitions (LDS histograms of k_bin)
+constexpr uint32_t BIN_MAX_GRID = 2048;     // k_bin workgroups (persistent over the tiles)
 constexpr uint32_t RED_THREADS = 1024;      // k_reduce workgroup
 constexpr uint32_t RED_ENTRIES = 2048;      // k_reduce LDS flow table (56 B entries)
 constexpr uint32_t RED_TARGET_FLOWS = 600;  // flows per partition the host sizes for
-constexpr uint32_t RED_MAX_CHUNK = 65536;   // records per k_reduce workgroup at most
 
 struct ComplexView {
     uint64_t* list;      // (rank << 24) | packet index
