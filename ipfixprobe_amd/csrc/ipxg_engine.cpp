@@ -142,6 +142,28 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     return IPXG_OK;
 }
 
+static FragView frag_view(ipxg_engine* e) {
+    return FragView{e->frag_ent, e->frag_cnt, (uint64_t*)e->frag_list.p, (uint64_t*)e->frag_sorted.p,
+                    (uint32_t*)e->frag_ports.p};
+}
+
+static Params params(ipxg_engine* e) {
+    Params p = {};
+    p.dlt = e->cfg.datalink;
+    p.active_s = e->cfg.active_s;
+    p.inactive_s = e->cfg.inactive_s;
+    p.bucket_w = std::max<uint32_t>(1, e->cfg.inactive_s / 2);
+    p.split_biflow = e->cfg.split_biflow;
+    p.frag_enable = e->cfg.frag_enable;
+    p.frag_size = e->cfg.frag_size ? e->cfg.frag_size : 10007;
+    p.frag_timeout_s = e->cfg.frag_timeout_s;
+    p.force_complex = e->cfg.inactive_s < 2 ? 1 : 0;
+    p.prev_valid = e->prev_valid;
+    p.prev_sec = e->prev_sec;
+    p.prev_usec = e->prev_usec;
+    return p;
+}
+
 static int alloc_table(ipxg_engine* e, uint32_t cap, HotSlot** hot, ipxg_flow_record** cold, uint32_t** rank) {
     if (hipMalloc((void**)hot, sizeof(HotSlot) * (size_t)cap) != hipSuccess) return IPXG_ENOMEM;
     if (hipMalloc((void**)cold, sizeof(ipxg_flow_record) * (size_t)cap) != hipSuccess) {
