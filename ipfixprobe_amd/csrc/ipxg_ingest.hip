@@ -158,7 +158,9 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint32
         const uint32_t pos = hist[part] + rk[q];
         const uint32_t idx = LISTED ? ix[q] : tile + (uint32_t)q * IPXG_BLOCK + threadIdx.x;
         if (pos < bv.seg_cap) {
+#ifndef IPXG_EXP_NOEMIT  // timing experiment: records dropped
             bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
+#endif
         } else {  // segment full: accumulate straight into the table
             spilled++;
             const uint64_t lo = ((uint64_t)r1[q] << 32) | r0[q];
@@ -170,7 +172,11 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint32
 
 // the block's record counts per partition (its column of bv.count)
 __device__ __forceinline__ void seg_counts(const uint32_t* fill, uint32_t P, const BinView& bv, uint32_t col) {
+#ifdef IPXG_EXP_NOEMIT
+    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + col] = 0;
+#else
     for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + col] = min(fill[q], bv.seg_cap);
+#endif
 }
 
 // rank one keyed, unfragmented packet in its partition and keep its record in slot j
@@ -181,8 +187,9 @@ __device__ __forceinline__ void tile_rank(uint32_t* hist, uint32_t pmask, const 
                                           uint32_t (&rk)[BIN_K], uint32_t (&ix)[BIN_K]) {
     uint64_t lo, hf;
     uint32_t cdir;
-#ifdef IPXG_EXP_NOHASH  // timing experiment only: results are wrong
-    lo = ((uint64_t)pk.sip[0] << 32) ^ pk.dip[0] ^ ((uint64_t)pk.src_port << 16) ^ pk.dst_port;
+#ifdef IPXG_EXP_NOHASH  // timing experiment only: one cheap mixer instead of 2x XXH64
+    lo = (((uint64_t)(pk.sip[0] ^ pk.dip[0]) << 32) | (uint32_t)(pk.src_port ^ pk.dst_port)) * 0x9E3779B97F4A7C15ull;
+    lo ^= lo >> 29;
     cdir = 0;
     hf = lo;
 #else
