@@ -49,6 +49,7 @@ namespace ipxg {
 constexpr int BIN_K = IPXG_BIN_K;                 // packets per lane per tile
 constexpr uint32_t BIN_TILE = BIN_K * IPXG_BLOCK;  // 2048 packets
 constexpr uint32_t NO_REC = 0xFFFFFFFFu;
+constexpr uint32_t BIN_SLOWBUF = 512;             // slow packets a k_bin tile lists in LDS
 constexpr uint32_t RED_U = IPXG_RED_U;            // records in flight per thread
 constexpr uint32_t RED_MAX_PROBE = 256;
 constexpr uint32_t RED_FAILED = 0x80000000u;      // FlowAgg::tflags bit: table probe failed
@@ -132,42 +133,63 @@ __device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_d
 // of the tile follow the ones of the block's earlier tiles in the block's own segment of
 // that partition (fill[part] = records so far), so no workgroup shares a write position
 // with another and no device atomic is needed (a shared counter per partition, hit once
-// per tile by every workgroup, saturated at the memory-side atomic rate: ~35 % of k_bin).
+// per tile by every workgroup, saturated at the memory-side atomic rate).  The records are
+// first grouped by partition in LDS (stage) and then written with consecutive lanes on
+// consecutive records of a run: written straight from the lanes, 64 lanes stored to 64
+// different lines per instruction and the stores cost a third of k_bin's time.
 // A full segment spills to direct accumulation.
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
 template <bool LISTED>
-__device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint32_t P, uint32_t pmask,
-                                          const BinView& bv, uint32_t col, const TableView& t, BatchCtl* ctl,
-                                          uint32_t* deferred_list, const uint32_t (&r0)[BIN_K],
+__device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4* stage, uint32_t* scan_s, uint32_t P,
+                                          uint32_t pmask, const BinView& bv, uint32_t col, const TableView& t,
+                                          BatchCtl* ctl, uint32_t* deferred_list, const uint32_t (&r0)[BIN_K],
                                           const uint32_t (&r1)[BIN_K], const uint32_t (&r2)[BIN_K],
                                           const uint32_t (&rk)[BIN_K], const uint32_t (&ix)[BIN_K], uint32_t tile,
                                           uint32_t& spilled) {
+    constexpr uint32_t PT = (1u << BIN_MAX_PART_BITS) / IPXG_BLOCK;  // partitions per thread
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) {
-        const uint32_t cnt = hist[q];
-        const uint32_t base = fill[q];
-        fill[q] = base + cnt;
-        hist[q] = base;
+    // tile-local exclusive prefix over the partitions: hist[q] <- start of q's run in stage
+    const uint32_t q0 = threadIdx.x * PT;
+    uint32_t cnt[PT], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+        cnt[k] = q0 + k < P ? hist[q0 + k] : 0;
+        sum += cnt[k];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<IPXG_BLOCK>(sum, scan_s, &total);
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+        if (q0 + k < P) hist[q0 + k] = run;
+        run += cnt[k];
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < BIN_K; ++q) {
         if (rk[q] == NO_REC) continue;
-        const uint32_t part = r1[q] & pmask;
-        const uint32_t pos = hist[part] + rk[q];
         const uint32_t idx = LISTED ? ix[q] : tile + (uint32_t)q * IPXG_BLOCK + threadIdx.x;
+        stage[hist[r1[q] & pmask] + rk[q]] = make_uint4(r0[q], r1[q], idx, r2[q]);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < total; k += IPXG_BLOCK) {
+        const uint4 r = stage[k];
+        const uint32_t part = r.y & pmask;
+        const uint32_t pos = fill[part] + (k - hist[part]);
         if (pos < bv.seg_cap) {
 #ifndef IPXG_EXP_NOEMIT  // timing experiment: records dropped
-            bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] = make_uint4(r0[q], r1[q], idx, r2[q]);
+            bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] = r;
 #endif
         } else {  // segment full: accumulate straight into the table
             spilled++;
-            const uint64_t lo = ((uint64_t)r1[q] << 32) | r0[q];
-            if (!merge_packet_atomic(t, lo, idx, r2[q], &ctl->new_keys)) defer_packet(ctl, deferred_list, idx, true);
+            if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
+                defer_packet(ctl, deferred_list, r.z, true);
         }
     }
     __syncthreads();  // hist is reset by the next tile
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k)
+        if (q0 + k < P) fill[q0 + k] += cnt[k];
 }
 
 // the block's record counts per partition (its column of bv.count)
@@ -225,9 +247,11 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, unsigned long long* stats) {
-    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / base
+    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: records in the block's segments
-    __shared__ uint32_t slowbuf[BIN_TILE];              // the tile's packets for k_bin_slow
+    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: the tile's records by partition
+    __shared__ uint32_t slowbuf[BIN_SLOWBUF];           // the tile's packets for k_bin_slow
+    __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t nslow, slow_base;
     const uint32_t tid = threadIdx.x;
     for (uint32_t q = tid; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
@@ -294,7 +318,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                 else
                     slow = true;
             }
-            if (slow) slowbuf[atomicAdd(&nslow, 1u)] = i;
+            if (slow) {
+                const uint32_t sp = atomicAdd(&nslow, 1u);
+                if (sp < BIN_SLOWBUF) slowbuf[sp] = i;
+                else slow_list[atomicAdd(&ctl->slow_count, 1u)] = i;  // a tile of mostly slow frames
+            }
             if (have) tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
             dc = dn;
             pc = pn;
@@ -304,12 +332,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
-        tile_emit<false>(hist, fill, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile,
-                         spilled);
+        tile_emit<false>(hist, fill, stage, scan_s, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, r0, r1, r2, rk,
+                         ix, tile, spilled);
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         // the tile's slow packets: one list reservation per tile
-        const uint32_t ns = nslow;
+        const uint32_t ns = min(nslow, BIN_SLOWBUF);
         if (tid == 0 && ns) slow_base = atomicAdd(&ctl->slow_count, ns);
         __syncthreads();
         for (uint32_t k = tid; k < ns; k += IPXG_BLOCK) slow_list[slow_base + k] = slowbuf[k];
@@ -349,6 +377,8 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];  // 32 KiB: one header column per lane
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB
+    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB
+    __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     const uint32_t ns = ctl->slow_count;  // final: k_bin has completed
     if (blockIdx.x * BIN_TILE >= ns) return;  // its column stays zero (memset per batch)
     for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
@@ -389,7 +419,8 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             }
             tile_rank<true>(hist, pmask, p, b, pk, d, i, j, r0, r1, r2, rk, ix);
         }
-        tile_emit<true>(hist, fill, P, pmask, bv, bcol, t, ctl, deferred_list, r0, r1, r2, rk, ix, tile, spilled);
+        tile_emit<true>(hist, fill, stage, scan_s, P, pmask, bv, bcol, t, ctl, deferred_list, r0, r1, r2, rk, ix,
+                        tile, spilled);
     }
     seg_counts(fill, P, bv, bcol);
     if (tid < ST_COUNT) hist[tid] = 0;
