@@ -43,12 +43,11 @@ struct ipxg_engine {
     // export buffer: records [ex_head, ex_count) are pending
     ipxg_flow_record* ex = nullptr;
     uint32_t ex_cap = 0;
-    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag
+    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag (inside the ctl block)
     uint32_t ex_count = 0, ex_head = 0;
-    uint32_t ex_host[2] = {0, 0};
     // control / stats
-    BatchCtl* ctl_d = nullptr;
-    BatchCtl* ctl_h = nullptr;  // pinned
+    BatchCtl* ctl_d = nullptr;  // device block: BatchCtl, then ex_count_d's two words
+    BatchCtl* ctl_h = nullptr;  // pinned mirror of the whole block
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
     // staging for host batches
@@ -132,7 +131,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     int rc;
     if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
     if ((rc = ensure(e, e->bin_count, (size_t)P * cols * sizeof(uint32_t)))) return rc;
-    HIPCHK(e, hipMemsetAsync(e->bin_count.p, 0, (size_t)P * cols * sizeof(uint32_t), e->st));
+    // no clearing: every k_bin / k_bin_slow workgroup writes its whole column of counts
     bv.rec = (uint4*)e->bin_rec.p;
     bv.count = (uint32_t*)e->bin_count.p;
     bv.seg_cap = (uint32_t)seg;
@@ -179,22 +178,32 @@ static int alloc_table(ipxg_engine* e, uint32_t cap, HotSlot** hot, ipxg_flow_re
     return IPXG_OK;
 }
 
-static int read_ex_count(ipxg_engine* e) {
-    HIPCHK(e, hipMemcpyAsync(e->ex_host, e->ex_count_d, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
-    return IPXG_OK;
+constexpr size_t CTL_EX_OFF = (sizeof(BatchCtl) + 15) & ~(size_t)15;  // ex_count_d inside the ctl block
+constexpr size_t CTL_BYTES = CTL_EX_OFF + 16;
+
+static const uint32_t* ex_host(const ipxg_engine* e) {
+    return reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(e->ctl_h) + CTL_EX_OFF);
+}
+
+// Wait for the stream by polling: the blocking wait (interrupt) added tens of microseconds of
+// idle GPU per batch; the engine's syncs are short.
+static hipError_t stream_wait(hipStream_t st) {
+    hipError_t r;
+    while ((r = hipStreamQuery(st)) == hipErrorNotReady) {
+    }
+    return r;
 }
 
 static int check_ex(ipxg_engine* e) {
-    e->ex_count = e->ex_host[0];
-    if (e->ex_host[1]) return set_err(e, IPXG_EDEVICE, "export buffer overflow (engine bug: capacity under-sized)");
+    e->ex_count = ex_host(e)[0];
+    if (ex_host(e)[1]) return set_err(e, IPXG_EDEVICE, "export buffer overflow (engine bug: capacity under-sized)");
     return IPXG_OK;
 }
 
+// one copy of the control block and the export counter into pinned memory, then wait
 static int sync_ctl(ipxg_engine* e) {
-    int rc;
-    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, sizeof(BatchCtl), hipMemcpyDeviceToHost, e->st));
-    if ((rc = read_ex_count(e))) return rc;
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, CTL_BYTES, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, stream_wait(e->st));
     return check_ex(e);
 }
 
@@ -305,9 +314,10 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->cap = cap;
     e->ex_cap = 1u << 16;
     if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
-    if (hipMalloc((void**)&e->ex_count_d, 2 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
-    if (hipMalloc((void**)&e->ctl_d, sizeof(BatchCtl)) != hipSuccess) return fail(IPXG_ENOMEM);
-    if (hipHostMalloc((void**)&e->ctl_h, sizeof(BatchCtl), hipHostMallocDefault) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipMalloc((void**)&e->ctl_d, CTL_BYTES) != hipSuccess) return fail(IPXG_ENOMEM);
+    e->ex_count_d = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(e->ctl_d) + CTL_EX_OFF);
+    if (hipHostMalloc((void**)&e->ctl_h, CTL_BYTES, hipHostMallocDefault) != hipSuccess) return fail(IPXG_ENOMEM);
+    std::memset(e->ctl_h, 0, CTL_BYTES);
     if (hipMalloc((void**)&e->misc_d, 16 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->stats_d, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long)) != hipSuccess)
         return fail(IPXG_ENOMEM);
@@ -330,7 +340,6 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->cold);
     hipFree(e->slot_rank);
     hipFree(e->ex);
-    hipFree(e->ex_count_d);
     hipFree(e->ctl_d);
     if (e->ctl_h) hipHostFree(e->ctl_h);
     hipFree(e->misc_d);
@@ -566,12 +575,11 @@ int ipxg_finish(ipxg_engine* e) {
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
     ev_rec(e, 9);
-    launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);
+    launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);  // also empties the table
     HIPCHK(e, hipGetLastError());
-    HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
     ev_rec(e, 10);
-    if ((rc = read_ex_count(e))) return rc;
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, CTL_BYTES, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, stream_wait(e->st));
     if ((rc = check_ex(e))) return rc;
     if (e->prof) {
         e->tm.finish_ms += ev_ms(e, 9);

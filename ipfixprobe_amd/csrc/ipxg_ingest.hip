@@ -380,9 +380,12 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     const uint32_t ns = ctl->slow_count;  // final: k_bin has completed
-    if (blockIdx.x * BIN_TILE >= ns) return;  // its column stays zero (memset per batch)
-    for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
+    if (blockIdx.x * BIN_TILE >= ns) {      // no work: an empty column
+        for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + bcol] = 0;
+        return;
+    }
+    for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;

@@ -460,7 +460,8 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
     hipLaunchKernelGGL(k_expire, dim3(scan_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats);
 }
 
-// Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288).
+// Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288) and empty the
+// table (every slot it scans is zeroed).
 __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
                                                 unsigned long long* stats) {
     __shared__ uint32_t scratch[8];
@@ -475,6 +476,8 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
             mask |= 1u << j;
             c++;
         }
+        uint4* z = reinterpret_cast<uint4*>(&t.hot[s]);
+        z[0] = z[1] = z[2] = z[3] = make_uint4(0, 0, 0, 0);
     }
     uint32_t total;
     const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
