@@ -508,6 +508,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     const uint32_t tid = threadIdx.x;
     const uint32_t cols = bv.cols;
     const uint32_t* cnts = bv.count + (size_t)part * cols;
+    PROBE_T(q0t);
     // segment lengths -> exclusive prefix (cols <= RED_MAX_COLS = 4 per thread)
     uint32_t v[RED_MAX_COLS / RED_THREADS], my = 0;
 #pragma unroll
@@ -532,6 +533,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     }
     if (tid < C_N) cnt[tid] = 0;
     __syncthreads();
+    PROBE_T(q1t);
     const uint4* segs = bv.rec + (size_t)part * cols * bv.seg_cap;
     for (uint32_t k0 = 0; k0 < total; k0 += RED_THREADS * RED_U) {
         uint4 r[RED_U];
@@ -555,6 +557,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         }
     }
     __syncthreads();
+    PROBE_T(q2t);
     // Nothing else of this batch can touch these flows when no packet went to the fragment or
     // deferred paths (spilled packets were accumulated by k_bin, before this kernel): then the
     // merged slot is complete and goes on the finalise list (k_fin_list).
@@ -602,6 +605,14 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     if (n_keys) atomicAdd(&cnt[C_KEYS], n_keys);
     if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
     __syncthreads();
+    PROBE_T(q3t);
+#ifdef IPXG_PROBE
+    if (tid == 0) {
+        atomicAdd((unsigned long long*)&ctl->probe[4], (unsigned long long)(q1t - q0t));
+        atomicAdd((unsigned long long*)&ctl->probe[5], (unsigned long long)(q2t - q1t));
+        atomicAdd((unsigned long long*)&ctl->probe[6], (unsigned long long)(q3t - q2t));
+    }
+#endif
     if (cnt[C_FAIL]) {  // defer the packets of the flows that found no slot
         for (uint32_t k = tid; k < total; k += RED_THREADS) {
             const uint4 r = seg_record(segs, pre, cols, bv.seg_cap, k);

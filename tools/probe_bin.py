@@ -29,6 +29,10 @@ def main():
     for k, nme in enumerate(names):
         print("%-12s %12.0f cycles/wave  %5.1f %%" % (nme, int(pc[k]) / waves, 100.0 * int(pc[k]) / max(tot, 1)))
     print("k_bin avg %.4f ms" % (tm["ingest_ms"] / tm["ingest_launches"]))
+    blocks = 256  # k_reduce workgroups (partitions) of the bench batch
+    for k, nme in ((4, "red: prefix+zero"), (5, "red: aggregate"), (6, "red: merge+list")):
+        print("%-18s %10.0f cycles/workgroup" % (nme, int(pc[k]) / blocks))
+    print("k_reduce avg %.4f ms" % (tm["reduce_ms"] / max(tm["reduce_launches"], 1)))
 
 
 if __name__ == "__main__":
