@@ -494,6 +494,21 @@ __device__ __forceinline__ uint4 seg_record(const uint4* segs, const uint32_t* p
     return segs[(size_t)lo * seg_cap + (k - pre[lo])];
 }
 
+// Fold one record into the workgroup's LDS flow table (or straight into the device table
+// when the LDS table is full).
+__device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
+                                           uint32_t* cnt, const uint4& r) {
+    if (r.z == NO_REC) return;
+    const uint64_t lo = ((uint64_t)r.y << 32) | r.x;
+    const int e = lds_slot(ht, lo, true);
+    if (e >= 0) {
+        lds_fold(ht[e], r.z, r.w);
+    } else {
+        atomicAdd(&cnt[C_SPILL], 1u);
+        if (!merge_packet_atomic(t, lo, r.z, r.w, &ctl->new_keys)) defer_packet(ctl, deferred_list, r.z, false);
+    }
+}
+
 // One workgroup per partition: the partition's records sit in one segment per k_bin /
 // k_bin_slow workgroup (bv.count gives their lengths); a prefix sum over the segment lengths
 // in LDS maps the partition's record k to its segment.
@@ -501,6 +516,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                                                         uint32_t* deferred_list) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
     __shared__ uint32_t pre[RED_MAX_COLS + 1];
+    __shared__ uint32_t ne[RED_MAX_COLS];  // non-empty segments
     __shared__ uint32_t cnt[C_N];
     __shared__ uint32_t scan_s[RED_THREADS / 64 + 1];
     __shared__ uint32_t fin_base;
@@ -520,13 +536,21 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     uint32_t total;
     uint32_t run = block_exclusive_scan<RED_THREADS>(my, scan_s, &total);
     if (total == 0) return;  // uniform over the workgroup
+    uint32_t ne_n = 0;
 #pragma unroll
     for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
         const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
         if (c < cols) pre[c] = run;
         run += v[q];
+        ne_n += v[q] ? 1 : 0;
     }
     if (tid == 0) pre[cols] = total;
+    // the non-empty segments, listed in column order
+    uint32_t nseg;
+    uint32_t at = block_exclusive_scan<RED_THREADS>(ne_n, scan_s, &nseg);
+#pragma unroll
+    for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q)
+        if (v[q]) ne[at++] = tid * (RED_MAX_COLS / RED_THREADS) + q;
     {
         uint4* z = reinterpret_cast<uint4*>(ht);
         for (uint32_t q = tid; q < sizeof(ht) / 16; q += RED_THREADS) z[q] = make_uint4(0, 0, 0, 0);
@@ -535,24 +559,29 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __syncthreads();
     PROBE_T(q1t);
     const uint4* segs = bv.rec + (size_t)part * cols * bv.seg_cap;
-    for (uint32_t k0 = 0; k0 < total; k0 += RED_THREADS * RED_U) {
+    // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
+    // loads, no search); a segment longer than a wave loops (wave-uniform).
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    constexpr uint32_t NW = RED_THREADS / 64;
+    for (uint32_t s0 = wave; s0 < nseg; s0 += NW * RED_U) {
         uint4 r[RED_U];
+        uint32_t sc[RED_U], sl[RED_U];
 #pragma unroll
         for (uint32_t u = 0; u < RED_U; ++u) {
-            const uint32_t k = k0 + u * RED_THREADS + tid;
-            r[u] = k < total ? seg_record(segs, pre, cols, bv.seg_cap, k) : make_uint4(0, 0, NO_REC, 0);
+            const uint32_t si = s0 + u * NW;
+            sc[u] = si < nseg ? ne[si] : 0;
+            sl[u] = si < nseg ? pre[sc[u] + 1] - pre[sc[u]] : 0;
+            const bool ok = lane < sl[u];
+            r[u] = segs[(size_t)sc[u] * bv.seg_cap + (ok ? lane : 0)];  // unconditional load
+            if (!ok) r[u].z = NO_REC;
         }
 #pragma unroll
         for (uint32_t u = 0; u < RED_U; ++u) {
-            if (r[u].z == NO_REC) continue;
-            const uint64_t lo = ((uint64_t)r[u].y << 32) | r[u].x;
-            const int e = lds_slot(ht, lo, true);
-            if (e >= 0) {
-                lds_fold(ht[e], r[u].z, r[u].w);
-            } else {  // LDS table full: straight into the device table
-                atomicAdd(&cnt[C_SPILL], 1u);
-                if (!merge_packet_atomic(t, lo, r[u].z, r[u].w, &ctl->new_keys))
-                    defer_packet(ctl, deferred_list, r[u].z, false);
+            red_record(ht, t, ctl, deferred_list, cnt, r[u]);
+            for (uint32_t off = 64; off < sl[u]; off += 64) {  // long segment (uniform over the wave)
+                uint4 x = segs[(size_t)sc[u] * bv.seg_cap + (off + lane < sl[u] ? off + lane : 0)];
+                if (off + lane >= sl[u]) x.z = NO_REC;
+                red_record(ht, t, ctl, deferred_list, cnt, x);
             }
         }
     }
