@@ -221,7 +221,7 @@ def pmc_traffic(kernel="k_bin"):
         except (OSError, ValueError):
             continue
         for name, v in js.items():
-            if kernel in name and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            if name.split("::")[-1].split("<")[0] == kernel and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                 best = (p, (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0)
     return best
 

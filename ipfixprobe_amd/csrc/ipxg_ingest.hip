@@ -32,7 +32,7 @@ namespace ipxg {
 #define IPXG_BIN_K 8
 #endif
 #ifndef IPXG_BIN_WAVES
-#define IPXG_BIN_WAVES 4
+#define IPXG_BIN_WAVES 3  // = the LDS limit (3 workgroups of 51 KiB per CU): up to 168 VGPRs
 #endif
 #ifndef IPXG_RED_U
 #define IPXG_RED_U 4
@@ -239,9 +239,9 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 }
 
 // Every packet of the batch, in tiles of BIN_K x 256.  Software-pipelined: the descriptors of
-// the packet two steps ahead (and of its predecessor, for the timestamp order check) and the
-// 48-byte head of the next packet are in flight while a packet is parsed; the loop issues no
-// other global memory operation.  Frames the register parser does not take go to the slow
+// the packet three steps ahead (and of its predecessor, for the timestamp order check) and the
+// 48-byte heads of the next two packets are in flight while a packet is parsed; the loop
+// issues no other global memory operation.  Frames the register parser does not take go to the slow
 // list for k_bin_slow.  No LDS header staging here: LDS holds only the partition histogram
 // and the tile's slow list, so occupancy is set by registers.
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
@@ -291,21 +291,24 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
-        // pipeline prologue: descriptors of steps 0 and 1, head of step 0
+        // pipeline prologue: descriptors of steps 0..2, heads of steps 0 and 1
         uint32_t i = tile + tid;
         ipxg_pkt_desc dc = b.desc[min(i, last)];
         uint64_t pc = prev_ts(min(i, last));
         ipxg_pkt_desc dn = b.desc[min(i + IPXG_BLOCK, last)];
         uint64_t pn = prev_ts(min(i + IPXG_BLOCK, last));
+        ipxg_pkt_desc dnn = b.desc[min(i + 2 * IPXG_BLOCK, last)];
+        uint64_t pnn = prev_ts(min(i + 2 * IPXG_BLOCK, last));
         Head48 hc = load_head(b, dc, fast_ok && i < b.n && fast_shape(dc));
+        Head48 hn = load_head(b, dn, fast_ok && i + IPXG_BLOCK < b.n && fast_shape(dn));
 #pragma unroll 1
         for (int j = 0; j < BIN_K; ++j, i += IPXG_BLOCK) {
-            // issue: descriptors two steps ahead, then the next head (its descriptor, dn, was
-            // issued a step ago: waiting for it does not wait for the current head)
-            const uint32_t i2 = min(i + 2 * IPXG_BLOCK, last);
-            const ipxg_pkt_desc dnn = b.desc[i2];
-            const uint64_t pnn = prev_ts(i2);
-            const Head48 hn = load_head(b, dn, fast_ok && i + IPXG_BLOCK < b.n && fast_shape(dn));
+            // issue: descriptors three steps ahead, then the head two steps ahead (its
+            // descriptor was issued a step ago: waiting for it leaves both heads in flight)
+            const uint32_t i3 = min(i + 3 * IPXG_BLOCK, last);
+            const ipxg_pkt_desc d3 = b.desc[i3];
+            const uint64_t p3 = prev_ts(i3);
+            const Head48 h2 = load_head(b, dnn, fast_ok && i + 2 * IPXG_BLOCK < b.n && fast_shape(dnn));
             // this step's packet: dc, pc and hc were loaded at least one step ago
             const bool act = i < b.n;
             const uint64_t ts = ((uint64_t)dc.ts_sec << 32) | dc.ts_usec;
@@ -326,9 +329,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             if (have) tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
             dc = dn;
             pc = pn;
+            hc = hn;
             dn = dnn;
             pn = pnn;
-            hc = hn;
+            hn = h2;
+            dnn = d3;
+            pnn = p3;
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
