@@ -255,7 +255,7 @@ def main():
     flows = gen_flows(args.flows, rank, world, args.seed)
     frames, desc = build_batch(flows, args.packets, args.seed + rank, device)
     torch.cuda.synchronize()
-    eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(4 * args.flows)))), args.ingest),
+    eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(2 * args.flows)))), args.ingest),
                  device_id=local)
 
     def step():

@@ -61,53 +61,6 @@ __device__ __forceinline__ void defer_packet(BatchCtl* ctl, uint32_t* list, uint
 }
 
 // ---- phase A ------------------------------------------------------------------------------
-// The common frame shape -- Ethernet (no VLAN tag), IPv4 with IHL 5, UDP or TCP without
-// options -- read straight from its first 48 bytes in registers: exactly the fields, checks
-// and counters parse_frame produces for such a frame (parse_eth_hdr parser.cpp:68-155,
-// parse_ipv4_hdr :311-356, parse_tcp_hdr :469-543 with doff <= 5, parse_udp_hdr :552-573),
-// without staging it in LDS.  Returns false for any other shape, a TCP header cut by caplen,
-// or a fragment when the fragmentation cache is on: the caller then takes the general
-// path.  c0..c2 = bytes 0..47, caplen >= 48.
-__device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, const uint4& c2, uint32_t caplen,
-                                           bool frag_enable, DevPkt& p, ParseCounts& c) {
-    if ((c0.w & 0xFFFF) != 0x0008) return false;          // ethertype 0x0800 at bytes 12-13
-    if (((c0.w >> 16) & 0xFF) != 0x45) return false;      // version 4, IHL 5
-    const uint32_t proto = c1.y >> 24;                     // byte 23
-    if (proto == 47) return false;                         // GRE: the general parser recurses
-    const uint32_t fo = bswap16(c1.y);                     // bytes 20-21
-    const uint32_t frag_off = fo & 0x1FFF;
-    if (frag_enable && (fo & 0x3FFF)) return false;        // a fragment: the fragmentation-cache path
-    uint32_t ports = 0, flags = 0;
-    if (frag_off == 0 && proto == 6) {
-        if (caplen < 54) return false;                     // 20 > data_len: the general path drops it
-        if (((c2.w >> 20) & 0xF) > 5) return false;        // TCP options: the general option walk
-        flags = c2.w >> 24;                                // byte 47
-    }
-    if (frag_off == 0 && (proto == 6 || proto == 17)) ports = (c2.x >> 16) | (c2.y << 16);  // bytes 34-37
-    p.ip_version = 4;
-    p.ip_proto = (uint8_t)proto;
-    p.tcp_flags = (uint8_t)flags;
-    p.ethertype = 0x0800;
-    p.ip_len = bswap16(c1.x);                              // bytes 16-17
-    p.frag_id = bswap16(c1.x >> 16);                       // bytes 18-19
-    p.frag_off = (uint16_t)frag_off;
-    p.more_fragments = (fo & 0x2000) ? 1 : 0;
-    p.src_port = bswap16(ports);
-    p.dst_port = bswap16(ports >> 16);
-    p.vlan_id = 0;
-    p.sip[0] = (c1.z >> 16) | (c1.w << 16);                // bytes 26-29, memory order
-    p.dip[0] = (c1.w >> 16) | (c2.x << 16);                // bytes 30-33
-    p.sip[1] = p.sip[2] = p.sip[3] = 0;
-    p.dip[1] = p.dip[2] = p.dip[3] = 0;
-    c.seen++;
-    c.parsed++;
-    c.ipv4++;
-    c.ipv4_bytes += caplen;
-    if (frag_off == 0 && proto == 6) c.tcp++;
-    if (frag_off == 0 && proto == 17) c.udp++;
-    return true;
-}
-
 // A readable 48-byte frame of zeros: the loads below are issued unconditionally (a lane with
 // nothing to load reads this), so the number of loads in flight is the same on every path
 // and the compiler's s_waitcnt can wait for exactly the one it needs (a conditional load
@@ -117,8 +70,6 @@ __device__ uint4 g_zero_head[3];
 struct Head48 {  // bytes 0..47 of a frame
     uint4 c0, c1, c2;
 };
-
-__device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.offset & 15) == 0 && d.caplen >= 48; }
 
 __device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_desc& d, bool ok) {
     const uint4* fr = ok ? reinterpret_cast<const uint4*>(b.arena + d.offset) : g_zero_head;
@@ -376,21 +327,21 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 // and its extension headers, IPv4 options, TCP options, SLL/SLL2/raw link types, truncated
 // or unaligned frames): staged in the lane's LDS column, parsed by parse_frame, ranked and
 // emitted exactly like k_bin's records.  The list length is read on the device.
-// 128 VGPRs (4 waves/SIMD = the LDS limit of 4 workgroups per CU)
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+// 168 VGPRs (3 waves/SIMD = the LDS limit of 3 workgroups per CU)
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
                 const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
-    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];  // 32 KiB: one header column per lane
+    // the header columns (parse) and the tile's records (emit) are never live together:
+    // one 32 KiB area, 48 KiB in all (3 workgroups per CU)
+    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: records / header columns
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB
-    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
+    static_assert(sizeof(stage) >= IPXG_WIN_DW * IPXG_BLOCK * 4, "header columns exceed the stage");
+    uint32_t* win = reinterpret_cast<uint32_t*>(stage);
     const uint32_t ns = ctl->slow_count;  // final: k_bin has completed
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
-    if (blockIdx.x * BIN_TILE >= ns) {      // no work: an empty column
-        for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + bcol] = 0;
-        return;
-    }
+    if (blockIdx.x * BIN_TILE >= ns) return;  // no work: k_reduce does not read the column
     for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
@@ -528,8 +479,11 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __shared__ uint32_t fin_base;
     const uint32_t part = blockIdx.x;
     const uint32_t tid = threadIdx.x;
-    const uint32_t cols = bv.cols;
-    const uint32_t* cnts = bv.count + (size_t)part * cols;
+    // the columns written: every k_bin workgroup's, and those of the k_bin_slow workgroups
+    // that had slow packets (the others return without writing theirs)
+    const uint32_t slow_cols = min(bv.bin_grid, (ctl->slow_count + BIN_TILE - 1) / BIN_TILE);
+    const uint32_t cols = bv.bin_grid + slow_cols;
+    const uint32_t* cnts = bv.count + (size_t)part * bv.cols;
     PROBE_T(q0t);
     // segment lengths -> exclusive prefix (cols <= RED_MAX_COLS = 4 per thread)
     uint32_t v[RED_MAX_COLS / RED_THREADS], my = 0;
@@ -564,7 +518,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     if (tid < C_N) cnt[tid] = 0;
     __syncthreads();
     PROBE_T(q1t);
-    const uint4* segs = bv.rec + (size_t)part * cols * bv.seg_cap;
+    const uint4* segs = bv.rec + (size_t)part * bv.cols * bv.seg_cap;
     // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
     // loads, no search); a segment longer than a wave loops (wave-uniform).
     const uint32_t lane = tid & 63, wave = tid >> 6;

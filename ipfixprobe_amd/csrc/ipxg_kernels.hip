@@ -461,7 +461,7 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
 }
 
 // Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288) and empty the
-// table (every slot it scans is zeroed).
+// table (every occupied slot it scans is zeroed).
 __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
                                                 unsigned long long* stats) {
     __shared__ uint32_t scratch[8];
@@ -472,7 +472,8 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const uint32_t s = base + j * 256 + threadIdx.x;
         if (s >= cap) continue;
-        if (t.hot[s].key != 0 && (t.hot[s].state & SLOT_LIVE)) {
+        if (t.hot[s].key == 0) continue;  // an empty slot is all zero already
+        if (t.hot[s].state & SLOT_LIVE) {
             mask |= 1u << j;
             c++;
         }

@@ -293,6 +293,57 @@ __device__ __forceinline__ void apply_frag_ports(const Params& p, const FragView
     }
 }
 
+// ---- register parser for the common frame shape -------------------------------------------
+// The common frame shape -- Ethernet (no VLAN tag), IPv4 with IHL 5, UDP or TCP without
+// options -- read straight from its first 48 bytes in registers: exactly the fields, checks
+// and counters parse_frame produces for such a frame (parse_eth_hdr parser.cpp:68-155,
+// parse_ipv4_hdr :311-356, parse_tcp_hdr :469-543 with doff <= 5, parse_udp_hdr :552-573),
+// without staging it in LDS.  Returns false for any other shape, a TCP header cut by caplen,
+// or a fragment when the fragmentation cache is on: the caller then takes the general
+// path.  c0..c2 = bytes 0..47, caplen >= 48.
+__device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, const uint4& c2, uint32_t caplen,
+                                           bool frag_enable, DevPkt& p, ParseCounts& c) {
+    if ((c0.w & 0xFFFF) != 0x0008) return false;          // ethertype 0x0800 at bytes 12-13
+    if (((c0.w >> 16) & 0xFF) != 0x45) return false;      // version 4, IHL 5
+    const uint32_t proto = c1.y >> 24;                     // byte 23
+    if (proto == 47) return false;                         // GRE: the general parser recurses
+    const uint32_t fo = bswap16(c1.y);                     // bytes 20-21
+    const uint32_t frag_off = fo & 0x1FFF;
+    if (frag_enable && (fo & 0x3FFF)) return false;        // a fragment: the fragmentation-cache path
+    uint32_t ports = 0, flags = 0;
+    if (frag_off == 0 && proto == 6) {
+        if (caplen < 54) return false;                     // 20 > data_len: the general path drops it
+        if (((c2.w >> 20) & 0xF) > 5) return false;        // TCP options: the general option walk
+        flags = c2.w >> 24;                                // byte 47
+    }
+    if (frag_off == 0 && (proto == 6 || proto == 17)) ports = (c2.x >> 16) | (c2.y << 16);  // bytes 34-37
+    p.ip_version = 4;
+    p.ip_proto = (uint8_t)proto;
+    p.tcp_flags = (uint8_t)flags;
+    p.ethertype = 0x0800;
+    p.ip_len = bswap16(c1.x);                              // bytes 16-17
+    p.frag_id = bswap16(c1.x >> 16);                       // bytes 18-19
+    p.frag_off = (uint16_t)frag_off;
+    p.more_fragments = (fo & 0x2000) ? 1 : 0;
+    p.src_port = bswap16(ports);
+    p.dst_port = bswap16(ports >> 16);
+    p.vlan_id = 0;
+    p.sip[0] = (c1.z >> 16) | (c1.w << 16);                // bytes 26-29, memory order
+    p.dip[0] = (c1.w >> 16) | (c2.x << 16);                // bytes 30-33
+    p.sip[1] = p.sip[2] = p.sip[3] = 0;
+    p.dip[1] = p.dip[2] = p.dip[3] = 0;
+    c.seen++;
+    c.parsed++;
+    c.ipv4++;
+    c.ipv4_bytes += caplen;
+    if (frag_off == 0 && proto == 6) c.tcp++;
+    if (frag_off == 0 && proto == 17) c.udp++;
+    return true;
+}
+
+// a frame the register parser may take: 16-byte aligned in the arena, 48 bytes captured
+__device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.offset & 15) == 0 && d.caplen >= 48; }
+
 // ---- header staging into LDS ------------------------------------------------------------
 // Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
 // zero-masked past caplen, plus one zero chunk so straddling reads see zeros.
@@ -360,9 +411,26 @@ template <bool FULL>
 __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p, const FragView& f,
                                             uint32_t idx, uint32_t* col, DevPkt& pk, ipxg_pkt_desc& d) {
     d = b.desc[idx];
+    ParseCounts dummy = {};
+    if ((p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB) && fast_shape(d)) {  // the common shape: registers only
+        const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
+        const uint4 c0 = fr[0], c1 = fr[1], c2 = fr[2];
+        if (parse_fast(c0, c1, c2, d.caplen, p.frag_enable, pk, dummy)) {
+            if (FULL) {  // parse_eth_hdr's MAC copy; the rest of the FULL-only fields stay zero
+                pk.mac_lo = c0.x;
+                pk.mac_mid = c0.y;
+                pk.mac_hi = c0.z;
+                pk.mpls_top = pk.tcp_seq = pk.tcp_ack = pk.tcp_mss = 0;
+                pk.tcp_options = 0;
+                pk.tcp_window = 0;
+                pk.ip_ttl = pk.ip_tos = pk.ip_flags = 0;
+            }
+            apply_frag_ports(p, f, idx, pk);
+            return true;
+        }
+    }
     stage_frame(col, b.arena, d.offset, d.caplen);
     LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-    ParseCounts dummy = {};
     if (!parse_frame<FULL>(S, d.caplen, p.dlt, pk, dummy)) return false;
     apply_frag_ports(p, f, idx, pk);
     return true;
