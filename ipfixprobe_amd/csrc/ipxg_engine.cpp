@@ -56,7 +56,8 @@ struct ipxg_engine {
     DevBuf defer_a, defer_b, frag_list, frag_sorted, frag_ports, sort_tmp;
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
-    DevBuf slow_list, fin_list;          // k_bin -> k_bin_slow, k_reduce -> k_fin_list
+    uint32_t bin_slots = 0;              // k_bin workgroups resident at once (its grid)
+    DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
@@ -123,7 +124,12 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
     const uint32_t P = 1u << bits;
     const uint64_t tiles = ((uint64_t)n + 2047) / 2048;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, 1024);
+    if (!e->bin_slots) {
+        e->bin_slots = bin_resident_blocks(e->cfg.device_id);
+        if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
+            e->bin_slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
+    }
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->bin_slots);
     const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * 2048, n);
     const double mean = (double)per_block / P;
     const uint64_t seg = ((uint64_t)(mean * 1.5 + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
@@ -131,6 +137,12 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     int rc;
     if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
     if ((rc = ensure(e, e->bin_count, (size_t)P * cols * sizeof(uint32_t)))) return rc;
+    // each k_bin workgroup's slow list holds every packet of its tiles
+    const uint64_t slow_stride = (tiles + grid - 1) / grid * 2048;
+    if ((rc = ensure(e, e->slow_list, (size_t)grid * slow_stride * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(e, e->slow_cnt, (size_t)grid * sizeof(uint32_t)))) return rc;
+    bv.slow_stride = (uint32_t)slow_stride;
+    bv.slow_cnt = (uint32_t*)e->slow_cnt.p;  // written by every k_bin workgroup
     // no clearing: every k_bin / k_bin_slow workgroup writes its whole column of counts
     bv.rec = (uint4*)e->bin_rec.p;
     bv.count = (uint32_t*)e->bin_count.p;
@@ -350,7 +362,7 @@ int ipxg_destroy(ipxg_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->frag_list, &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
-                      &e->bin_count, &e->slow_list, &e->fin_list})
+                      &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -372,6 +384,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     BatchView bv;
     bv.n = n;
+    bv.arena_lim = (uint32_t)std::min<uint64_t>(batch->arena_len, 0xFFFFFF00ull);
     if (batch->flags & IPXG_BATCH_DEVICE) {
         bv.arena = batch->arena;
         bv.desc = batch->desc;
@@ -401,7 +414,6 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     BinView bins = {};
     if (binned) {
         if ((rc = setup_bins(e, n, bins))) return rc;
-        if ((rc = ensure(e, e->slow_list, (size_t)n * 4))) return rc;
         if ((rc = ensure(e, e->fin_list, (size_t)n * 4))) return rc;
     }
     ev_rec(e, 0);
@@ -716,6 +728,7 @@ int ipxg_parse_batch(ipxg_engine* e, const ipxg_batch* batch, ipxg_parsed_pkt* o
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     BatchView bv;
     bv.n = n;
+    bv.arena_lim = (uint32_t)std::min<uint64_t>(batch->arena_len, 0xFFFFFF00ull);
     bv.base_sec = 0;
     if (batch->flags & IPXG_BATCH_DEVICE) {
         bv.arena = batch->arena;

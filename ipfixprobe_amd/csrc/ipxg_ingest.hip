@@ -49,7 +49,6 @@ namespace ipxg {
 constexpr int BIN_K = IPXG_BIN_K;                 // packets per lane per tile
 constexpr uint32_t BIN_TILE = BIN_K * IPXG_BLOCK;  // 2048 packets
 constexpr uint32_t NO_REC = 0xFFFFFFFFu;
-constexpr uint32_t BIN_SLOWBUF = 512;             // slow packets a k_bin tile lists in LDS
 constexpr uint32_t RED_U = IPXG_RED_U;            // records in flight per thread
 constexpr uint32_t RED_MAX_PROBE = 256;
 constexpr uint32_t RED_FAILED = 0x80000000u;      // FlowAgg::tflags bit: table probe failed
@@ -61,23 +60,41 @@ __device__ __forceinline__ void defer_packet(BatchCtl* ctl, uint32_t* list, uint
 }
 
 // ---- phase A ------------------------------------------------------------------------------
-// A readable 48-byte frame of zeros: the loads below are issued unconditionally (a lane with
-// nothing to load reads this), so the number of loads in flight is the same on every path
-// and the compiler's s_waitcnt can wait for exactly the one it needs (a conditional load
-// made it wait for all of them, vmcnt(0), defeating the prefetch).
-__device__ uint4 g_zero_head[3];
+// k_bin's loads are buffer loads through two wave-uniform resource descriptors (the
+// descriptor array and the frame arena): each is one 16-byte (or 8-byte) load instruction,
+// where a plain load was narrowed by the compiler to the bytes used (4 instructions for a
+// 48-byte head); a lane with nothing to load gives an offset past the buffer's end and gets
+// zeros, with no memory traffic.  The loads are unconditional, so the number in flight is
+// the same on every path and s_waitcnt waits for exactly the one it needs.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t BUF_OOB = 0xFFFFFF00u;  // an offset past every buffer (arena_lim <= BUF_OOB)
 
 struct Head48 {  // bytes 0..47 of a frame
     uint4 c0, c1, c2;
 };
 
-__device__ __forceinline__ Head48 load_head(const BatchView& b, const ipxg_pkt_desc& d, bool ok) {
-    const uint4* fr = ok ? reinterpret_cast<const uint4*>(b.arena + d.offset) : g_zero_head;
+__device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
+__device__ __forceinline__ Head48 load_head(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok) {
+    const uint32_t o = ok ? d.offset : BUF_OOB;
     Head48 h;
-    h.c0 = fr[0];
-    h.c1 = fr[1];
-    h.c2 = fr[2];
+    h.c0 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o, 0, 0));
+    h.c1 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 16, 0, 0));
+    h.c2 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 32, 0, 0));
     return h;
+}
+
+// descriptor i (zeros past the batch's end)
+__device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, uint32_t i) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, 0);
+    ipxg_pkt_desc d;
+    d.offset = v.x;
+    d.caplen = (uint16_t)v.y;
+    d.wirelen = (uint16_t)(v.y >> 16);
+    d.ts_sec = v.z;
+    d.ts_usec = v.w;
+    return d;
 }
 
 // After every lane ranked its records of the tile in hist[part]: each partition's records
@@ -123,7 +140,12 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4*
         stage[hist[r1[q] & pmask] + rk[q]] = make_uint4(r0[q], r1[q], idx, r2[q]);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < total; k += IPXG_BLOCK) {
+    // fixed trip count (no loop in k_bin's tile body: a loop there made the compiler drain
+    // every load in flight before it)
+#pragma unroll
+    for (uint32_t kk = 0; kk < BIN_TILE / IPXG_BLOCK; ++kk) {
+        const uint32_t k = kk * IPXG_BLOCK + threadIdx.x;
+        if (k >= total) break;
         const uint4 r = stage[k];
         const uint32_t part = r.y & pmask;
         const uint32_t pos = fill[part] + (k - hist[part]);
@@ -189,23 +211,27 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
     f.list[pos] = ((uint64_t)bucket << 24) | i;
 }
 
-// Every packet of the batch, in tiles of BIN_K x 256.  Software-pipelined: the descriptors of
-// the packet three steps ahead (and of its predecessor, for the timestamp order check) and the
-// 48-byte heads of the next two packets are in flight while a packet is parsed; the loop
-// issues no other global memory operation.  Frames the register parser does not take go to the slow
-// list for k_bin_slow.  No LDS header staging here: LDS holds only the partition histogram
-// and the tile's slow list, so occupancy is set by registers.
+// Every packet of the batch, in tiles of BIN_K x 256, parsed in registers by parse_fast
+// from buffer loads software-pipelined across the tiles (below).  Frames the register parser
+// does not take go to the slow list for k_bin_slow.  No LDS header staging here: LDS holds
+// the partition histogram, the block's segment fill counts, the tile's record stage and its
+// slow list.
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: records in the block's segments
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: the tile's records by partition
-    __shared__ uint32_t slowbuf[BIN_SLOWBUF];           // the tile's packets for k_bin_slow
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
-    __shared__ uint32_t nslow, slow_base;
+    __shared__ uint32_t nslow[2];  // slow packets of the tile (by tile parity)
     const uint32_t tid = threadIdx.x;
     for (uint32_t q = tid; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
+    if (tid < 2) nslow[tid] = 0;
+    // the block's slow list: every packet of its tiles fits, so a slow packet is stored at
+    // its rank without any device atomic (a returning one inside the pipelined loop made the
+    // compiler drain every load in flight)
+    uint32_t* const my_slow = slow_list + (size_t)blockIdx.x * bv.slow_stride;
+    uint32_t slow_fill = 0, par = 0;
     if (b.n == 0) return;
     const uint32_t last = b.n - 1;
     const uint32_t base_sec = b.base_sec == BASE_FROM_DESC0 ? b.desc[0].ts_sec : b.base_sec;
@@ -216,11 +242,15 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     ParseCounts c = {};
     uint32_t spilled = 0;
     bool nonmono = false;
-    // ts of the packet before i (packet 0 compares with itself; its predecessor, the previous
-    // batch's last packet, is checked once below) -- an unconditional load
-    auto prev_ts = [&](uint32_t i) -> uint64_t {
-        const uint2 w = *reinterpret_cast<const uint2*>(&b.desc[i - (i != 0)].ts_sec);
-        return ((uint64_t)w.x << 32) | w.y;
+    const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const bool lane0 = (tid & 63) == 0;
+    // lane 0's predecessor packet (the previous wave's last one): its timestamp, for the order
+    // check; the other lanes take their predecessor's from the lane below (DPP)
+    auto prev_ts0 = [&](uint32_t i) -> u32x2 {
+        return __builtin_amdgcn_raw_buffer_load_b64(rs_desc, lane0 && i != 0 ? i * 16u - 8u : BUF_OOB, 0, 0);
     };
     if (blockIdx.x == 0 && tid == 0 && p.prev_valid) {
         const ipxg_pkt_desc d0 = b.desc[0];
@@ -229,11 +259,35 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 #ifdef IPXG_PROBE
     uint64_t probe_acc[4] = {0, 0, 0, 0};
 #endif
-    for (uint32_t tile = blockIdx.x * BIN_TILE; tile < b.n; tile += gridDim.x * BIN_TILE) {
+    // The block's tiles are blockIdx.x, blockIdx.x + grid, ...; its step g is step g % BIN_K of
+    // its tile g / BIN_K (one packet per lane).  Software pipeline across the tiles: step g
+    // issues the descriptor of step g + DA and the head of step g + HA (whose descriptor
+    // arrived during the DA - HA steps since it was issued), so the loads stay in flight
+    // through the tile's emit phase and its barriers.  The tile's steps are unrolled and
+    // BIN_K is a multiple of DA and HA: every ring slot is a fixed register set.
+    constexpr int DA = 4, HA = 2;
+    static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
+    const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
+    ipxg_pkt_desc Dr[DA];
+    u32x2 Pr[DA];
+    Head48 Hr[HA];
+#pragma unroll
+    for (int k = 0; k < DA; ++k) {
+        const uint32_t i = blockIdx.x * BIN_TILE + k * IPXG_BLOCK + tid;
+        Dr[k] = load_desc(rs_desc, i);
+        Pr[k] = prev_ts0(i);
+    }
+#pragma unroll
+    for (int k = 0; k < HA; ++k) Hr[k] = load_head(rs_arena, Dr[k], fast_ok && fast_shape(Dr[k]));
+    for (uint32_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+        const uint32_t tile = tile_id * BIN_TILE;
+        const uint32_t next = (tile_id + gridDim.x) * BIN_TILE;  // past the batch: loads give zeros
         PROBE_T(t0);
-        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
-        if (tid == 0) nslow = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << BIN_MAX_PART_BITS) / IPXG_BLOCK; ++k)
+            if (k * IPXG_BLOCK + tid < P) hist[k * IPXG_BLOCK + tid] = 0;
         __syncthreads();
+        if (tid == 0) nslow[par ^ 1] = 0;  // the next tile's (last read before this barrier)
         PROBE_T(t1);
         PROBE_ADD(0, t0, t1);
         uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
@@ -242,50 +296,42 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
-        // pipeline prologue: descriptors of steps 0..2, heads of steps 0 and 1
-        uint32_t i = tile + tid;
-        ipxg_pkt_desc dc = b.desc[min(i, last)];
-        uint64_t pc = prev_ts(min(i, last));
-        ipxg_pkt_desc dn = b.desc[min(i + IPXG_BLOCK, last)];
-        uint64_t pn = prev_ts(min(i + IPXG_BLOCK, last));
-        ipxg_pkt_desc dnn = b.desc[min(i + 2 * IPXG_BLOCK, last)];
-        uint64_t pnn = prev_ts(min(i + 2 * IPXG_BLOCK, last));
-        Head48 hc = load_head(b, dc, fast_ok && i < b.n && fast_shape(dc));
-        Head48 hn = load_head(b, dn, fast_ok && i + IPXG_BLOCK < b.n && fast_shape(dn));
-#pragma unroll 1
-        for (int j = 0; j < BIN_K; ++j, i += IPXG_BLOCK) {
-            // issue: descriptors three steps ahead, then the head two steps ahead (its
-            // descriptor was issued a step ago: waiting for it leaves both heads in flight)
-            const uint32_t i3 = min(i + 3 * IPXG_BLOCK, last);
-            const ipxg_pkt_desc d3 = b.desc[i3];
-            const uint64_t p3 = prev_ts(i3);
-            const Head48 h2 = load_head(b, dnn, fast_ok && i + 2 * IPXG_BLOCK < b.n && fast_shape(dnn));
-            // this step's packet: dc, pc and hc were loaded at least one step ago
+#pragma unroll
+        for (int j = 0; j < BIN_K; ++j) {
+            const uint32_t i = tile + j * IPXG_BLOCK + tid;
+            // this step's packet, loaded HA (head) and DA (descriptor) steps ago
+            const ipxg_pkt_desc dc = Dr[j % DA];
+            const u32x2 pc = Pr[j % DA];
+            const Head48 hc = Hr[j % HA];
+            // bytes 40-43 are not parsed: keep their register live until here, or the compiler
+            // reuses it while the load is in flight and must drain every load to do so
+            asm volatile("" ::"v"(hc.c2.z));
+            // issue: the descriptor DA steps ahead, the head HA steps ahead
+            const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
+            Dr[j % DA] = load_desc(rs_desc, ia);
+            Pr[j % DA] = prev_ts0(ia);
+            const ipxg_pkt_desc dh = Dr[(j + HA) % DA];
+            Hr[j % HA] = load_head(rs_arena, dh, fast_ok && fast_shape(dh));
             const bool act = i < b.n;
-            const uint64_t ts = ((uint64_t)dc.ts_sec << 32) | dc.ts_usec;
-            if (act && ts < pc) nonmono = true;
+            // the predecessor's timestamp: lane 0's was loaded, the others' is the lane below's
+            const uint32_t ps = (uint32_t)__builtin_amdgcn_update_dpp((int)pc.x, (int)dc.ts_sec, 0x138, 0xF, 0xF, false);
+            const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp((int)pc.y, (int)dc.ts_usec, 0x138, 0xF, 0xF, false);
+            if (act && (dc.ts_sec < ps || (dc.ts_sec == ps && dc.ts_usec < pu))) nonmono = true;
             DevPkt pk;
             bool have = false, slow = false;
+#ifdef IPXG_EXP_LOADONLY  // timing experiment only: the loads, no parse/rank
+            if (act) c.seen += hc.c0.x ^ hc.c1.y ^ hc.c2.z ^ hc.c0.w ^ hc.c1.x ^ hc.c2.y;
+            if (false) {
+#else
             if (act) {
+#endif
                 if (fast_ok && fast_shape(dc) && parse_fast(hc.c0, hc.c1, hc.c2, dc.caplen, p.frag_enable, pk, c))
                     have = true;
                 else
                     slow = true;
             }
-            if (slow) {
-                const uint32_t sp = atomicAdd(&nslow, 1u);
-                if (sp < BIN_SLOWBUF) slowbuf[sp] = i;
-                else slow_list[atomicAdd(&ctl->slow_count, 1u)] = i;  // a tile of mostly slow frames
-            }
+            if (slow) my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] = i;
             if (have) tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
-            dc = dn;
-            pc = pn;
-            hc = hn;
-            dn = dnn;
-            pn = pnn;
-            hn = h2;
-            dnn = d3;
-            pnn = p3;
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
@@ -293,11 +339,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                          ix, tile, spilled);
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
-        // the tile's slow packets: one list reservation per tile
-        const uint32_t ns = min(nslow, BIN_SLOWBUF);
-        if (tid == 0 && ns) slow_base = atomicAdd(&ctl->slow_count, ns);
-        __syncthreads();
-        for (uint32_t k = tid; k < ns; k += IPXG_BLOCK) slow_list[slow_base + k] = slowbuf[k];
+        slow_fill += nslow[par];  // final: read after the tile's barriers
+        par ^= 1;
         PROBE_T(t4);
         PROBE_ADD(3, t3, t4);
     }
@@ -311,6 +354,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         ctl->last_usec = d.ts_usec;
     }
     if (nonmono) ctl->nonmono = 1;
+    if (tid == 0) {
+        bv.slow_cnt[blockIdx.x] = slow_fill;
+        if (slow_fill) atomicAdd(&ctl->slow_count, slow_fill);
+    }
+    __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, blockIdx.x);
     // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
@@ -339,9 +387,11 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     static_assert(sizeof(stage) >= IPXG_WIN_DW * IPXG_BLOCK * 4, "header columns exceed the stage");
     uint32_t* win = reinterpret_cast<uint32_t*>(stage);
-    const uint32_t ns = ctl->slow_count;  // final: k_bin has completed
+    // k_bin workgroup b's slow packets, into segment column bin_grid + b
+    const uint32_t ns = bv.slow_cnt[blockIdx.x];  // final: k_bin has completed
+    const uint32_t* const list = slow_list + (size_t)blockIdx.x * bv.slow_stride;
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
-    if (blockIdx.x * BIN_TILE >= ns) return;  // no work: k_reduce does not read the column
+    if (ns == 0) return;  // no work: k_reduce does not read the column
     for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
@@ -349,7 +399,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     ParseCounts c = {};
     uint32_t keyless = 0, frags = 0, spilled = 0;
     uint32_t* col = &win[tid];
-    for (uint32_t tile = blockIdx.x * BIN_TILE; tile < ns; tile += gridDim.x * BIN_TILE) {
+    for (uint32_t tile = 0; tile < ns; tile += BIN_TILE) {
         for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
         __syncthreads();
         uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
@@ -362,7 +412,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         for (int j = 0; j < BIN_K; ++j) {
             const uint32_t k = tile + (uint32_t)j * IPXG_BLOCK + tid;
             if (k >= ns) continue;
-            const uint32_t i = slow_list[k];
+            const uint32_t i = list[k];
             const ipxg_pkt_desc d = b.desc[i];
             stage_frame(col, b.arena, d.offset, d.caplen);
             LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
@@ -382,6 +432,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         tile_emit<true>(hist, fill, stage, scan_s, P, pmask, bv, bcol, t, ctl, deferred_list, r0, r1, r2, rk, ix,
                         tile, spilled);
     }
+    __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, bcol);
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
@@ -391,6 +442,14 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         atomicAdd(&ctl->spilled, spilled);
         ctl->pending = 1;
     }
+}
+
+uint32_t bin_resident_blocks(int device) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bin, IPXG_BLOCK, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    return (uint32_t)std::max(1, std::min(cus * per_cu, (int)BIN_MAX_GRID));
 }
 
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
@@ -481,8 +540,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     const uint32_t tid = threadIdx.x;
     // the columns written: every k_bin workgroup's, and those of the k_bin_slow workgroups
     // that had slow packets (the others return without writing theirs)
-    const uint32_t slow_cols = min(bv.bin_grid, (ctl->slow_count + BIN_TILE - 1) / BIN_TILE);
-    const uint32_t cols = bv.bin_grid + slow_cols;
+    const uint32_t cols = bv.cols;
     const uint32_t* cnts = bv.count + (size_t)part * bv.cols;
     PROBE_T(q0t);
     // segment lengths -> exclusive prefix (cols <= RED_MAX_COLS = 4 per thread)
@@ -490,7 +548,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
     for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
         const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
-        v[q] = c < cols ? cnts[c] : 0;
+        v[q] = c < bv.bin_grid || (c < cols && bv.slow_cnt[c - bv.bin_grid]) ? cnts[c] : 0;
         my += v[q];
     }
     uint32_t total;

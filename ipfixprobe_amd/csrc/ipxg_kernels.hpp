@@ -48,7 +48,7 @@ struct BatchCtl {
     uint32_t exported;       // records exported while applying this batch
     uint32_t touched;        // flow aggregates built by k_reduce (partition sizing)
     uint32_t spilled;        // packets that fell back to direct atomic accumulation
-    uint32_t slow_count;     // packets k_bin left for k_bin_slow
+    uint32_t slow_count;     // packets k_bin left for k_bin_slow (statistics)
     uint32_t fin_count;      // slots k_reduce listed for k_fin_list
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
@@ -100,7 +100,8 @@ struct BatchView {
     const uint8_t* arena;
     const ipxg_pkt_desc* desc;
     uint32_t n;
-    uint32_t base_sec;  // tbits bucket origin (first packet's seconds), or BASE_FROM_DESC0
+    uint32_t base_sec;   // tbits bucket origin (first packet's seconds), or BASE_FROM_DESC0
+    uint32_t arena_lim;  // min(arena bytes, 0xFFFFFF00): the range of k_bin's buffer loads
 };
 constexpr uint32_t BASE_FROM_DESC0 = 0xFFFFFFFFu;
 
@@ -124,6 +125,8 @@ struct BinView {
     uint32_t cols;       // 2 * bin_grid: k_bin's columns, then k_bin_slow's
     uint32_t bin_grid;   // workgroups of k_bin (and of k_bin_slow)
     uint32_t part_bits;  // parts = 1 << part_bits
+    uint32_t slow_stride;  // k_bin workgroup b lists its slow packets at slow_list[b * slow_stride ...]
+    uint32_t* slow_cnt;    // bin_grid: slow packets listed by each k_bin workgroup
 };
 constexpr uint32_t BIN_MAX_PART_BITS = 11;  // <= 2048 partitions (LDS histograms of k_bin)
 constexpr uint32_t BIN_MAX_GRID = 2048;     // k_bin workgroups (persistent over the tiles)
@@ -141,6 +144,8 @@ struct ComplexView {
 };
 
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
+// k_bin workgroups resident on the whole device at once (its persistent grid)
+uint32_t bin_resident_blocks(int device);
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats);
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,

@@ -1,0 +1,88 @@
+// Read-bandwidth microbenchmark for k_bin's access pattern on one MI355X:
+//   contig : each wave reads consecutive 16-byte chunks (a float4 stream)
+//   frame  : lane = packet; a 16-byte descriptor, then the frame's first 48 bytes at the
+//            descriptor's offset (3 x 16-byte loads, dependent on the descriptor)
+//   frame_nodesc : the same 48 bytes at i * stride, no descriptor
+// Usage: membench <n_packets> <stride> <blocks>
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <vector>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+struct Desc { uint32_t off, len, s, us; };
+
+__global__ __launch_bounds__(256) void k_contig(const uint4* __restrict__ a, size_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256 * 4;
+    for (size_t base = (size_t)blockIdx.x * 256 * 4 + threadIdx.x; base < n16; base += stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = base + k * 256 < n16 ? a[base + k * 256] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <bool DESC>
+__global__ __launch_bounds__(256) void k_frame(const uint8_t* __restrict__ arena, const Desc* __restrict__ desc,
+                                               uint32_t n, uint32_t fstride, uint32_t* out) {
+    uint32_t acc = 0;
+    const uint32_t step = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256 * 4 + threadIdx.x; i0 < n; i0 += step * 4) {
+        uint32_t off[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = min(i0 + k * 256, n - 1);
+            if (DESC) { const Desc d = desc[i]; off[k] = d.off; acc ^= d.len ^ d.s; }
+            else off[k] = i * fstride;
+        }
+        uint4 h[4][3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) h[k][c] = *reinterpret_cast<const uint4*>(arena + off[k] + 16 * c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc ^= h[k][c].x ^ h[k][c].y ^ h[k][c].z ^ h[k][c].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char** argv) {
+    const uint32_t n = argc > 1 ? atoi(argv[1]) : 10000000;
+    const uint32_t fs = argc > 2 ? atoi(argv[2]) : 64;
+    const int blocks = argc > 3 ? atoi(argv[3]) : 2048;
+    const size_t abytes = (size_t)n * fs + 64;
+    uint8_t* arena; Desc* desc; uint32_t* out;
+    CHK(hipMalloc(&arena, abytes));
+    CHK(hipMalloc(&desc, (size_t)n * sizeof(Desc)));
+    CHK(hipMalloc(&out, 16));
+    CHK(hipMemset(arena, 1, abytes));
+    std::vector<Desc> hd(n);
+    for (uint32_t i = 0; i < n; ++i) hd[i] = Desc{i * fs, 64, i, 0};
+    CHK(hipMemcpy(desc, hd.data(), (size_t)n * sizeof(Desc), hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+    auto run = [&](const char* name, double bytes, auto launch) {
+        for (int w = 0; w < 3; ++w) launch();
+        CHK(hipDeviceSynchronize());
+        const int reps = 20;
+        CHK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) launch();
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= reps;
+        printf("%-14s blocks %5d  %8.1f us  %7.0f GB/s (%.0f MB)\n", name, blocks, ms * 1e3, bytes / (ms * 1e-3) / 1e9, bytes / 1e6);
+    };
+    const size_t n16 = (size_t)n * fs / 16;
+    run("contig", (double)n16 * 16, [&] { hipLaunchKernelGGL(k_contig, dim3(blocks), dim3(256), 0, 0, (const uint4*)arena, n16, out); });
+    run("frame", (double)n * (48 + 16), [&] { hipLaunchKernelGGL(k_frame<true>, dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    run("frame_nodesc", (double)n * 48, [&] { hipLaunchKernelGGL(k_frame<false>, dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    return 0;
+}
