@@ -226,6 +226,35 @@ def pmc_traffic(kernel="k_bin"):
     return best
 
 
+def end_to_end(eng, frames, desc, packets, reps=3):
+    """PCIe-inclusive rate (never `value`): the same batch from pinned host memory through
+    ipxg_submit (hipMemcpyAsync H2D of arena + descriptors, then the kernels), ipxg_finish and
+    the D2H poll of every exported record, one batch after another (no overlap)."""
+    import torch
+    hf = frames.cpu().pin_memory()
+    hd = desc.cpu().pin_memory()
+
+    def one():
+        eng.submit(hf, hd)
+        eng.finish()
+        return len(eng.poll())
+
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nrec = 0
+    for _ in range(reps):
+        nrec = one()
+    dt = time.perf_counter() - t0
+    h2d = hf.numel() + hd.numel() * hd.element_size()
+    return {"value": round(packets * reps / dt / 1e6, 2), "unit": "Mpkts/s",
+            "ms_per_batch": round(dt / reps * 1e3, 3),
+            "h2d_bytes_per_batch": h2d, "h2d_GBs_effective": round(h2d * reps / dt / 1e9, 2),
+            "records_per_batch": nrec,
+            "path": "pinned host batch -> H2D copy -> kernels -> finish -> D2H poll of the records, "
+                    "batches back to back (no copy/compute overlap)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -238,6 +267,7 @@ def main():
     ap.add_argument("--verify", action="store_true", help="check the records against the oracle")
     ap.add_argument("--ingest", default="binned", choices=["binned", "atomic"])
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host batch) rate")
     args = ap.parse_args()
 
     import torch
@@ -308,6 +338,9 @@ def main():
     stage = alg / ((bin_ms + red_ms) / 1e3) / 1e9 if bin_ms > 0 else 0.0
     kname = "k_bin" if args.ingest == "binned" else "k_ingest"
     pmc = pmc_traffic(kname)
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = end_to_end(eng, frames, desc, args.packets)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -338,6 +371,7 @@ def main():
                                   for k in ("ingest", "ingest_slow", "reduce", "fin", "finalize", "slow",
                                             "finish")},
             "flows_exported_per_step": int(st["end_forced"] // max(st["batches"], 1)),
+            "e2e_pcie": e2e,
             "spilled_packets": int(st["spilled_packets"]),
             "cpu_baseline": cpu,
         }

@@ -202,12 +202,13 @@ class Engine:
     @staticmethod
     def _batch(arena, desc, device=False):
         b = Batch()
-        if device:  # torch tensors on cuda
+        if device or hasattr(arena, "data_ptr"):  # torch tensors: on the GPU, or (pinned) host
             b.arena = arena.data_ptr()
             b.arena_len = arena.numel() * arena.element_size()
             b.desc = desc.data_ptr()
             b.n = desc.numel() * desc.element_size() // 16
-            b.flags = BATCH_DEVICE
+            b.flags = BATCH_DEVICE if device else 0
+            b._keep = (arena, desc)
         else:
             arena = np.ascontiguousarray(arena, dtype=np.uint8)
             desc = np.ascontiguousarray(desc)

@@ -27,7 +27,7 @@ if [ "${PROFILE:-1}" = "1" ]; then
   echo "== rocprofv3 kernel trace"; date
   export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
+      python3 bench.py --steps ${PROF_STEPS:-30} --warmup 2 --no-cpu-baseline > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
   rc=$?; tail -2 $OUT/prof_$TAG.err; stop_on_fault $rc rocprof
   find $OUT/prof_$TAG -name "*stats*" | head
 fi
