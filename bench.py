@@ -311,7 +311,10 @@ def main():
         diff = flowcmp.diff(got, want)
         print("verify: %d records, %s" % (len(got), "bit-exact vs oracle" if not diff else diff),
               file=sys.stderr)
-    eng.profile(True)
+    # timed region: HIP events around the ingest kernel only (the roofline's launch time);
+    # every-stage events cost ~35 us of host time per step, so the stage breakdown comes
+    # from a separate pass below
+    eng.profile(2)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -322,16 +325,20 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
-    tm = eng.timing()
+    tm_bin = eng.timing()
     st = eng.stats()
+    eng.profile(1)  # stage breakdown (untimed)
+    for _ in range(min(args.steps, 10)):
+        step()
+    tm = eng.timing()
+    stage_steps = min(args.steps, 10)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     total_pkts = args.packets * args.steps * world
     value = total_pkts / dt / 1e6
-    per_launch = lambda k: tm[k + "_ms"] / max(tm[k + "_launches"], 1)  # noqa: E731
-    bin_ms = per_launch("ingest")
+    bin_ms = tm_bin["ingest_ms"] / max(tm_bin["ingest_launches"], 1)
     red_ms = (tm["ingest_slow_ms"] + tm["reduce_ms"] + tm["fin_ms"]) / max(tm["reduce_launches"], 1)
     alg = ALG_BYTES_PER_PKT * args.packets
     achieved = alg / (bin_ms / 1e3) / 1e9 if bin_ms > 0 else 0.0
@@ -367,7 +374,7 @@ def main():
                                    "achieved": round(stage, 1),
                                    "frac": round(stage / HBM_PEAK_GBS, 4),
                                    "avg_ms": round(bin_ms + red_ms, 4)}},
-            "stage_ms_per_step": {k: round(tm[k + "_ms"] / max(args.steps, 1), 4)
+            "stage_ms_per_step": {k: round(tm[k + "_ms"] / stage_steps, 4)
                                   for k in ("ingest", "ingest_slow", "reduce", "fin", "finalize", "slow",
                                             "finish")},
             "flows_exported_per_step": int(st["end_forced"] // max(st["batches"], 1)),

@@ -254,7 +254,8 @@ typedef struct ipxg_timing {
 /* Per-phase shader-clock sums of the last batch's k_bin (8 values; all zero unless the
  * library was built with -DIPXG_PROBE -- a tuning aid). */
 int ipxg_probe_counters(ipxg_engine* eng, uint64_t* out);
-/* Enable (1) / disable (0) event timing; enabling also zeroes the accumulators. */
+/* Event timing: 1 = every stage, 2 = the ingest kernel only (two events per batch, the
+ * least host overhead), 0 = off; enabling also zeroes the accumulators. */
 int ipxg_profile(ipxg_engine* eng, int enable);
 int ipxg_get_timing(ipxg_engine* eng, ipxg_timing* out);
 

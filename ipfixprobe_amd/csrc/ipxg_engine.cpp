@@ -67,6 +67,7 @@ struct ipxg_engine {
     uint32_t prev_sec = 0, prev_usec = 0;
     // stage timing
     bool prof = false;
+    int prof_level = 0;  // 1: every stage, 2: the ingest kernel only
     hipEvent_t ev[11] = {};
     ipxg_timing tm = {};
 };
@@ -74,7 +75,8 @@ struct ipxg_engine {
 // events: 0 | k_bin | 1 | k_bin_slow | 2 | k_reduce | 3 | k_fin_list | 4;
 //         [5,6] slow paths, [7,8] k_finalize, [9,10] finish
 static void ev_rec(ipxg_engine* e, int i) {
-    if (e->prof) (void)hipEventRecord(e->ev[i], e->st);
+    // level 2: only the events around k_bin / k_ingest (0, 1): the others cost host time
+    if (e->prof && (e->prof_level == 1 || i <= 1)) (void)hipEventRecord(e->ev[i], e->st);
 }
 static double ev_ms(ipxg_engine* e, int a) {
     float ms = 0.f;
@@ -440,7 +442,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
-        if (binned) {
+        if (binned && e->prof_level == 1) {
             e->tm.ingest_slow_ms += ev_ms(e, 1);
             e->tm.reduce_ms += ev_ms(e, 2);
             e->tm.fin_ms += ev_ms(e, 3);
@@ -485,7 +487,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     if (slow) {
         ev_rec(e, 6);
         HIPCHK(e, hipStreamSynchronize(e->st));
-        if (e->prof) {
+        if (e->prof && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
         }
@@ -500,7 +502,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         ev_rec(e, 8);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
-        if (e->prof) {
+        if (e->prof && e->prof_level == 1) {
             e->tm.finalize_ms += ev_ms(e, 7);
             e->tm.finalize_launches++;
         }
@@ -536,7 +538,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         ev_rec(e, 6);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
-        if (e->prof) {
+        if (e->prof && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
         }
@@ -593,7 +595,7 @@ int ipxg_finish(ipxg_engine* e) {
     HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, CTL_BYTES, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, stream_wait(e->st));
     if ((rc = check_ex(e))) return rc;
-    if (e->prof) {
+    if (e->prof && e->prof_level == 1) {
         e->tm.finish_ms += ev_ms(e, 9);
         e->tm.finish_launches++;
     }
@@ -710,6 +712,7 @@ int ipxg_profile(ipxg_engine* e, int enable) {
     if (enable && !e->ev[0])
         for (hipEvent_t& ev : e->ev) HIPCHK(e, hipEventCreate(&ev));
     e->prof = enable != 0;
+    e->prof_level = enable == 2 ? 2 : (enable ? 1 : 0);
     if (enable) e->tm = ipxg_timing{};
     return IPXG_OK;
 }

@@ -15,7 +15,7 @@ def main():
     dev = torch.device("cuda", 0)
     flows = bench.gen_flows(100_000, 0, 1, 1234)
     frames, desc = bench.build_batch(flows, 10_000_000, 1234, dev)
-    eng = Engine("s=%d" % int(math.ceil(math.log2(4 * 100_000))))
+    eng = Engine("s=%d" % int(math.ceil(math.log2(2 * 100_000))))
     eng.profile(True)
     for _ in range(3):
         eng.submit(frames, desc, device=True)
