@@ -124,6 +124,8 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     if (est == 0 || est > n) est = n;
     uint32_t bits = 0;
     while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
+    if (const char* pb = std::getenv("IPXG_PART_BITS"))  // tuning knob (experiments only)
+        bits = std::min<uint32_t>((uint32_t)std::atoi(pb), BIN_MAX_PART_BITS);
     const uint32_t P = 1u << bits;
     const uint64_t tiles = ((uint64_t)n + 2047) / 2048;
     if (!e->bin_slots) {

@@ -97,6 +97,9 @@ __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, 
     return d;
 }
 
+// the target of stores that carry no record (tile_emit; k_bin's prologue)
+__device__ uint4 g_dummy_rec[32 * 64];
+
 // After every lane ranked its records of the tile in hist[part]: each partition's records
 // of the tile follow the ones of the block's earlier tiles in the block's own segment of
 // that partition (fill[part] = records so far), so no workgroup shares a write position
@@ -140,20 +143,26 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4*
         stage[hist[r1[q] & pmask] + rk[q]] = make_uint4(r0[q], r1[q], idx, r2[q]);
     }
     __syncthreads();
-    // fixed trip count (no loop in k_bin's tile body: a loop there made the compiler drain
-    // every load in flight before it)
+    // Fixed trip count and one store per iteration, always issued (a record that does not go
+    // to a segment is stored to a dummy line instead): on gfx950 stores count in vmcnt, and
+    // with a variable number of them the compiler's waits for the next tile's prefetched
+    // loads had to assume none were issued -- every later wait then also waited for the
+    // stores.  (A loop here made it drain every load in flight before it.)
 #pragma unroll
     for (uint32_t kk = 0; kk < BIN_TILE / IPXG_BLOCK; ++kk) {
         const uint32_t k = kk * IPXG_BLOCK + threadIdx.x;
-        if (k >= total) break;
-        const uint4 r = stage[k];
+        const bool valid = k < total;
+        const uint4 r = stage[valid ? k : 0];
         const uint32_t part = r.y & pmask;
         const uint32_t pos = fill[part] + (k - hist[part]);
-        if (pos < bv.seg_cap) {
-#ifndef IPXG_EXP_NOEMIT  // timing experiment: records dropped
-            bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] = r;
+        const bool seg = valid && pos < bv.seg_cap;
+#ifdef IPXG_EXP_NOEMIT  // timing experiment: records dropped
+        uint4* dst = &g_dummy_rec[threadIdx.x & 63];
+#else
+        uint4* dst = seg ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] : &g_dummy_rec[threadIdx.x & 63];
 #endif
-        } else {  // segment full: accumulate straight into the table
+        *dst = r;
+        if (valid && !seg) {  // segment full: accumulate straight into the table
             spilled++;
             if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
                 defer_packet(ctl, deferred_list, r.z, true);
@@ -271,14 +280,25 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     ipxg_pkt_desc Dr[DA];
     u32x2 Pr[DA];
     Head48 Hr[HA];
+    // The prologue issues its loads in the order the last DA steps of a tile do, with dummy
+    // stores where a tile issues heads of its own steps and its record stores: the loop's
+    // first waits are shared by the first tile and all later ones, and the compiler sizes
+    // them for the path with the fewest memory operations after each load.
 #pragma unroll
     for (int k = 0; k < DA; ++k) {
         const uint32_t i = blockIdx.x * BIN_TILE + k * IPXG_BLOCK + tid;
         Dr[k] = load_desc(rs_desc, i);
         Pr[k] = prev_ts0(i);
+        if (k >= DA - HA) {
+            const int h = k - (DA - HA);
+            Hr[h] = load_head(rs_arena, Dr[h], fast_ok && fast_shape(Dr[h]));
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) g_dummy_rec[(k * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
+        }
     }
 #pragma unroll
-    for (int k = 0; k < HA; ++k) Hr[k] = load_head(rs_arena, Dr[k], fast_ok && fast_shape(Dr[k]));
+    for (int q = 0; q < BIN_TILE / IPXG_BLOCK; ++q) g_dummy_rec[(DA * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
     for (uint32_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
         const uint32_t tile = tile_id * BIN_TILE;
         const uint32_t next = (tile_id + gridDim.x) * BIN_TILE;  // past the batch: loads give zeros
