@@ -47,7 +47,8 @@ struct ipxg_engine {
     uint32_t ex_count = 0, ex_head = 0;
     // control / stats
     BatchCtl* ctl_d = nullptr;  // device block: BatchCtl, then ex_count_d's two words
-    BatchCtl* ctl_h = nullptr;  // pinned mirror of the whole block
+    BatchCtl* ctl_h = nullptr;  // host-mapped mirror of the whole block
+    uint32_t* ctl_hd = nullptr;  // its device address
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
     // staging for host batches
@@ -216,9 +217,17 @@ static int check_ex(ipxg_engine* e) {
     return IPXG_OK;
 }
 
-// one copy of the control block and the export counter into pinned memory, then wait
+// the control block and the export counter into host-mapped memory (a one-block kernel on
+// the stream: cheaper than a D2H copy command), then wait
+static int publish_ctl(ipxg_engine* e) {
+    launch_publish(e->st, reinterpret_cast<const uint32_t*>(e->ctl_d), e->ctl_hd, (uint32_t)(CTL_BYTES / 4));
+    HIPCHK(e, hipGetLastError());
+    return IPXG_OK;
+}
+
 static int sync_ctl(ipxg_engine* e) {
-    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, CTL_BYTES, hipMemcpyDeviceToHost, e->st));
+    int rc;
+    if ((rc = publish_ctl(e))) return rc;
     HIPCHK(e, stream_wait(e->st));
     return check_ex(e);
 }
@@ -332,8 +341,10 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->ctl_d, CTL_BYTES) != hipSuccess) return fail(IPXG_ENOMEM);
     e->ex_count_d = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(e->ctl_d) + CTL_EX_OFF);
-    if (hipHostMalloc((void**)&e->ctl_h, CTL_BYTES, hipHostMallocDefault) != hipSuccess) return fail(IPXG_ENOMEM);
+    if (hipHostMalloc((void**)&e->ctl_h, CTL_BYTES, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(IPXG_ENOMEM);
     std::memset(e->ctl_h, 0, CTL_BYTES);
+    if (hipHostGetDevicePointer((void**)&e->ctl_hd, e->ctl_h, 0) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMalloc((void**)&e->misc_d, 16 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->stats_d, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long)) != hipSuccess)
         return fail(IPXG_ENOMEM);
@@ -594,9 +605,7 @@ int ipxg_finish(ipxg_engine* e) {
     launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);  // also empties the table
     HIPCHK(e, hipGetLastError());
     ev_rec(e, 10);
-    HIPCHK(e, hipMemcpyAsync(e->ctl_h, e->ctl_d, CTL_BYTES, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, stream_wait(e->st));
-    if ((rc = check_ex(e))) return rc;
+    if ((rc = sync_ctl(e))) return rc;
     if (e->prof && e->prof_level == 1) {
         e->tm.finish_ms += ev_ms(e, 9);
         e->tm.finish_launches++;

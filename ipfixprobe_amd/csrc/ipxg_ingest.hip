@@ -274,7 +274,13 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // arrived during the DA - HA steps since it was issued), so the loads stay in flight
     // through the tile's emit phase and its barriers.  The tile's steps are unrolled and
     // BIN_K is a multiple of DA and HA: every ring slot is a fixed register set.
-    constexpr int DA = 4, HA = 2;
+#ifndef IPXG_BIN_DA
+#define IPXG_BIN_DA 4
+#endif
+#ifndef IPXG_BIN_HA
+#define IPXG_BIN_HA 2
+#endif
+    constexpr int DA = IPXG_BIN_DA, HA = IPXG_BIN_HA;
     static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
     const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
     ipxg_pkt_desc Dr[DA];
@@ -639,16 +645,14 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         listed[q] = NO_REC;
         if (a.key) {
             n_touch++;
-            uint4 head;
+            HotSlot h;
             bool claimed;
-            HotSlot* hp = probe_insert(t, a.key, head, claimed);
-            if (claimed) n_keys++;
+            HotSlot* hp = probe_insert_full(t, a.key, h, claimed);  // this workgroup is the
+            if (claimed) n_keys++;                                  // slot's only writer here
             if (!hp) {
                 ht[e].tflags = a.tflags | RED_FAILED;
                 failed = true;
             } else {
-                HotSlot h = *hp;  // this workgroup is the slot's only writer in this kernel
-                h.key = a.key;
                 agg_fold(h, a);
                 *hp = h;
                 if (fuse) {

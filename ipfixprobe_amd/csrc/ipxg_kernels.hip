@@ -407,7 +407,8 @@ void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, Ta
 }
 
 // ---- maintenance: export_expired / finish / rehash / count ------------------------------
-constexpr uint32_t SCAN_PER_THREAD = 8;  // slots per thread in the export scans
+constexpr uint32_t SCAN_PER_THREAD = 1;  // slots per thread in the export scans (more made the
+                                         // cold-record loads wait on the previous export stores)
 
 static inline uint32_t scan_grid(uint32_t cap) {
     const uint32_t per = 256 * SCAN_PER_THREAD;
@@ -415,7 +416,7 @@ static inline uint32_t scan_grid(uint32_t cap) {
 }
 
 // Export every live record idle for >= inactive seconds at `now` (export_expired,
-// cache.cpp:508-523, over the whole table).  Slots [blk*2048, +2048), 8 per thread; one
+// cache.cpp:508-523, over the whole table).  Slots [blk*256*SCAN_PER_THREAD, ...); one
 // export-buffer reservation per block (a single counter saturates at ~88 returning
 // atomics/us: MI355X_MICROARCH.md "dequeue").
 __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t cap, int64_t now,
@@ -490,6 +491,17 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         if (mask >> j & 1) store_export(ex, pos++, t.cold[base + j * 256 + threadIdx.x], IPXG_FLOW_END_FORCED);
     if (threadIdx.x == 0 && total)
         atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + ST_END_FORCED], (unsigned long long)total);
+}
+
+// Copy the control block (+ export counter) into host-mapped memory: the host reads it after
+// the stream has drained, without a D2H copy command of its own.
+__global__ __launch_bounds__(64) void k_publish(const uint32_t* src, uint32_t* dst, uint32_t words) {
+    for (uint32_t i = threadIdx.x; i < words; i += 64) dst[i] = src[i];
+    __threadfence_system();
+}
+
+void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, src, dst, words);
 }
 
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats) {

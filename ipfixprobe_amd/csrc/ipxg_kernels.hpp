@@ -173,6 +173,7 @@ void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, Ta
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
                    ExportView ex, unsigned long long* stats);
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats);
+void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words);
 void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail);
 void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl);
 void launch_parse_batch(hipStream_t st, const BatchView& b, uint32_t dlt, ipxg_parsed_pkt* out);

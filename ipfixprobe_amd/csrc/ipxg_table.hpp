@@ -153,6 +153,35 @@ __device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo
     return nullptr;
 }
 
+// probe_insert for a caller that needs the whole slot: each probe reads the 64-byte slot
+// (one line), so a found slot needs no second read and a claimed one is known empty.  For
+// k_reduce, whose workgroup is the only writer of its keys' slots in that kernel.
+__device__ __forceinline__ HotSlot* probe_insert_full(const TableView& t, uint64_t lo, HotSlot& h, bool& claimed) {
+    uint32_t s = (uint32_t)lo & t.mask;
+    claimed = false;
+    for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
+        HotSlot* p = &t.hot[s];
+        h = *p;
+        if (h.key == 0) {
+            const unsigned long long old = atomicCAS((unsigned long long*)&p->key, 0ull, (unsigned long long)lo);
+            if (old == 0) {
+                h = HotSlot{};
+                h.key = lo;
+                claimed = true;
+                return p;
+            }
+            if (old == lo) {  // inserted meanwhile by another path: read it again
+                h = *p;
+                return p;
+            }
+        } else if (h.key == lo) {
+            return p;
+        }
+        s = (s + 1) & t.mask;
+    }
+    return nullptr;
+}
+
 __device__ __forceinline__ int64_t probe_find(const TableView& t, uint64_t lo) {
     uint32_t s = (uint32_t)lo & t.mask;
     for (uint32_t probe = 0; probe <= t.mask; ++probe) {
