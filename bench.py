@@ -37,7 +37,7 @@ ALG_BYTES_PER_PKT = 80  # 64 B frame + 16 B descriptor
 
 def gen_flows(F, rank, world, seed):
     """F distinct biflows whose canonical hash falls in this rank's range."""
-    from ipfixprobe_amd import Engine
+    from ipfixprobe_amd import Engine, shard
     rng = np.random.default_rng(seed)
     out = {k: [] for k in ("sip", "dip", "sport", "dport")}
     have = 0
@@ -63,9 +63,8 @@ def gen_flows(F, rank, world, seed):
                     k[:, 10 + q] = (b >> (24 - 8 * q)) & 0xFF
             hf = e.xxh64(keys.reshape(-1), 16)
             hi = e.xxh64(inv.reshape(-1), 16)
-            lo = np.minimum(hf, hi)
-            owner = ((lo >> np.uint64(32)) * np.uint64(world)) >> np.uint64(32)
-            for j in np.nonzero(owner == rank)[0]:
+            own = shard.owner(shard.canonical(hf, hi), world)
+            for j in np.nonzero(own == rank)[0]:
                 t = (int(sip[j]), int(dip[j]), int(sp[j]), int(dp[j]))
                 if t in seen or (t[1], t[0], t[3], t[2]) in seen:
                     continue
@@ -134,31 +133,13 @@ class _DevArray:
 
 
 def gather_exports(eng, rank, world, device):
-    """RCCL gather of every rank's device export buffer into rank 0 (counts first)."""
+    """RCCL gather of every rank's device export buffer into rank 0 (ipfixprobe_amd.shard)."""
     import torch
-    import torch.distributed as dist
+    from ipfixprobe_amd.shard import gather_records
     ptr, n = eng.device_exports()
-    cnt = torch.tensor([n], dtype=torch.int64, device=device)
-    counts = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(counts, cnt)
-    counts = [int(c.item()) for c in counts]
-    mine = torch.as_tensor(_DevArray(ptr, max(n, 1) * 128), device=device)[: n * 128]
-    total = 0
-    if rank == 0:
-        out = torch.empty(sum(counts) * 128, dtype=torch.uint8, device=device)
-        out[: n * 128].copy_(mine)
-        off = n * 128
-        reqs = []
-        for r in range(1, world):
-            if counts[r]:
-                reqs.append(dist.irecv(out[off: off + counts[r] * 128], src=r))
-            off += counts[r] * 128
-        for q in reqs:
-            q.wait()
-        total = sum(counts)
-    elif n:
-        dist.send(mine.contiguous(), dst=0)
-    return total
+    buf = torch.as_tensor(_DevArray(ptr, max(n, 1) * 128), device=device)
+    out = gather_records(buf, n, rank, world, device)
+    return 0 if out is None else out.numel() // 128
 
 
 def cpu_baseline(frames, desc, flows_per_shard, threads=16, reps=3):
