@@ -259,6 +259,25 @@ int ipxg_probe_counters(ipxg_engine* eng, uint64_t* out);
 int ipxg_profile(ipxg_engine* eng, int enable);
 int ipxg_get_timing(ipxg_engine* eng, ipxg_timing* out);
 
+/* ---- IPFIX export formatting --------------------------------------
+ * Data records of the reference IPFIX output plugin's basic templates (BASIC_TMPLT_V4 /
+ * BASIC_TMPLT_V6, include/ipfixprobe/ipfix-elements.hpp:328-366) as
+ * IPFIXExporter::fill_basic_flow writes them (src/plugins/output/ipfix/src/ipfix.cpp:1470-1516,
+ * field encoding IPFIX_FILL_FIELD :77-96): big-endian, flow times as 64-bit NTP timestamps
+ * (MK_NTP_TS, ipfix-elements.hpp:50-60), INPUT_INTERFACE = the exporter's dir_bit_field.
+ * IPXG_IPFIX_V4_LEN bytes for ip_version 4, IPXG_IPFIX_V6_LEN otherwise, back to back in
+ * record order.  Formatted on the device. */
+#define IPXG_IPFIX_V4_LEN 81
+#define IPXG_IPFIX_V6_LEN 105
+/* n host records -> out (>= n * 105 bytes), offsets[n + 1] byte offsets (offsets[n] = total). */
+int ipxg_ipfix_basic(ipxg_engine* eng, const ipxg_flow_record* recs, size_t n, uint32_t dir_bit_field,
+                     uint8_t* out, uint64_t* offsets);
+/* The pending exports straight from the device export buffer, consumed like
+ * ipxg_poll_exports: the longest prefix of whole records fitting `cap` bytes; *n records,
+ * *bytes written. */
+int ipxg_poll_ipfix(ipxg_engine* eng, uint32_t dir_bit_field, uint8_t* out, size_t cap, size_t* n,
+                    size_t* bytes);
+
 /* ---- stateless device entry points (parity tests, tools) ---------------------------- */
 /* Run the device parser on a batch; out receives n records (host pointer). */
 int ipxg_parse_batch(ipxg_engine* eng, const ipxg_batch* batch, ipxg_parsed_pkt* out);

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -59,6 +60,7 @@ struct ipxg_engine {
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
     uint32_t bin_slots = 0;              // k_bin workgroups resident at once (its grid)
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
+    DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
@@ -377,7 +379,8 @@ int ipxg_destroy(ipxg_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->frag_list, &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
-                      &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list})
+                      &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
+                      &e->ipf_tot, &e->ipf_off})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -652,6 +655,65 @@ int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t*
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     *n = k;
+    return IPXG_OK;
+}
+
+// IPFIX basic-template records of n device records at `rec` into the scratch buffers
+// (ipf_out: the bytes, ipf_off: n + 1 offsets); no host sync.
+static int ipfix_format(ipxg_engine* e, const ipxg_flow_record* rec, uint32_t n, uint32_t dir) {
+    int rc;
+    const size_t nb = (n + 255) / 256;
+    if ((rc = ensure(e, e->ipf_out, (size_t)n * 105 + 16))) return rc;
+    if ((rc = ensure(e, e->ipf_tot, (nb + 1) * sizeof(uint64_t)))) return rc;
+    if ((rc = ensure(e, e->ipf_off, ((size_t)n + 1) * sizeof(uint64_t)))) return rc;
+    launch_ipfix_basic(e->st, rec, n, dir, (uint64_t*)e->ipf_tot.p, (uint8_t*)e->ipf_out.p, (uint64_t*)e->ipf_off.p);
+    HIPCHK(e, hipGetLastError());
+    return IPXG_OK;
+}
+
+int ipxg_ipfix_basic(ipxg_engine* e, const ipxg_flow_record* recs, size_t n, uint32_t dir_bit_field, uint8_t* out,
+                     uint64_t* offsets) {
+    if (!e || (n && (!recs || !out || !offsets))) return IPXG_EINVAL;
+    if (offsets) offsets[0] = 0;
+    if (n == 0) return IPXG_OK;
+    if (n > IPXG_MAX_BATCH) return set_err(e, IPXG_ETOOBIG, "more records than IPXG_MAX_BATCH");
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if ((rc = ensure(e, e->ipf_rec, n * sizeof(ipxg_flow_record)))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->ipf_rec.p, recs, n * sizeof(ipxg_flow_record), hipMemcpyHostToDevice, e->st));
+    if ((rc = ipfix_format(e, (const ipxg_flow_record*)e->ipf_rec.p, (uint32_t)n, dir_bit_field))) return rc;
+    HIPCHK(e, hipMemcpyAsync(offsets, e->ipf_off.p, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipMemcpyAsync(out, e->ipf_out.p, offsets[n], hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return IPXG_OK;
+}
+
+int ipxg_poll_ipfix(ipxg_engine* e, uint32_t dir_bit_field, uint8_t* out, size_t cap, size_t* n, size_t* bytes) {
+    if (!e || !n || !bytes || (cap && !out)) return IPXG_EINVAL;
+    *n = *bytes = 0;
+    const uint32_t pend = e->ex_count - e->ex_head;
+    if (pend == 0) return IPXG_OK;
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if ((rc = ipfix_format(e, e->ex + e->ex_head, pend, dir_bit_field))) return rc;
+    std::vector<uint64_t> off((size_t)pend + 1);
+    HIPCHK(e, hipMemcpyAsync(off.data(), e->ipf_off.p, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    // whole records only: the longest prefix that fits `cap`
+    const size_t k = (size_t)(std::upper_bound(off.begin(), off.end(), (uint64_t)cap) - off.begin()) - 1;
+    if (k) {
+        HIPCHK(e, hipMemcpyAsync(out, e->ipf_out.p, off[k], hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    e->ex_head += (uint32_t)k;
+    if (e->ex_head == e->ex_count) {
+        e->ex_head = e->ex_count = 0;
+        HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    *n = k;
+    *bytes = off[k];
     return IPXG_OK;
 }
 

@@ -161,7 +161,14 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4*
 #else
         uint4* dst = seg ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] : &g_dummy_rec[threadIdx.x & 63];
 #endif
+#ifdef IPXG_NT_REC_STORE  // tuning knob: streaming (non-temporal) record stores
+        __builtin_nontemporal_store(r.x, &dst->x);
+        __builtin_nontemporal_store(r.y, &dst->y);
+        __builtin_nontemporal_store(r.z, &dst->z);
+        __builtin_nontemporal_store(r.w, &dst->w);
+#else
         *dst = r;
+#endif
         if (valid && !seg) {  // segment full: accumulate straight into the table
             spilled++;
             if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))

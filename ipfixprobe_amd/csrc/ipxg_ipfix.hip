@@ -1,0 +1,149 @@
+// IPFIX export formatting on the device: the data records of the
+// reference IPFIX output plugin's basic templates, BASIC_TMPLT_V4 / BASIC_TMPLT_V6
+// (include/ipfixprobe/ipfix-elements.hpp:328-366), filled exactly as
+// IPFIXExporter::fill_basic_flow (src/plugins/output/ipfix/src/ipfix.cpp:1470-1516) with
+// IPFIX_FILL_FIELD (ipfix.cpp:77-96): 1-byte fields copied, 2-byte fields htons, the IPv4
+// addresses copied in network order, other 4-byte fields htonl, 8-byte fields byte-swapped,
+// everything else (IPv6 addresses, MACs) copied.  Times are 64-bit NTP (MK_NTP_TS,
+// ipfix-elements.hpp:50-60); INPUT_INTERFACE is the exporter's dir_bit_field.
+//
+// Records are written back to back in export order (81 B for ip_version 4, 105 B otherwise:
+// the v6 template, as get_template picks it, ipfix.cpp:287-291).  Three kernels: per-block
+// byte totals, one exclusive scan over the blocks, then each block stages its records in
+// LDS and writes its byte range with consecutive lanes on consecutive bytes.
+#include "ipxg_kernels.hpp"
+
+namespace ipxg {
+
+constexpr uint32_t IPFIX_BLOCK = 256;
+constexpr uint32_t IPFIX_V4_LEN = 81, IPFIX_V6_LEN = 105;
+constexpr uint64_t NTP_EPOCH_DIFF = 2208988800ULL;  // ipfix-elements.hpp:50
+
+__device__ __forceinline__ uint32_t ipfix_len(const ipxg_flow_record& r) {
+    return r.ip_version == 4 ? IPFIX_V4_LEN : IPFIX_V6_LEN;
+}
+
+__device__ __forceinline__ uint64_t ntp_ts(uint32_t sec, uint32_t usec) {  // MK_NTP_TS
+    return (((uint64_t)sec + NTP_EPOCH_DIFF) << 32) | (uint32_t)(((uint64_t)usec << 32) / 1000000u);
+}
+
+__device__ __forceinline__ void put_be(uint8_t* p, uint64_t v, int n) {
+    for (int k = 0; k < n; ++k) p[k] = (uint8_t)(v >> (8 * (n - 1 - k)));
+}
+
+// one record's basic-template bytes at p (fill_basic_flow's field order)
+__device__ __forceinline__ void fill_basic(uint8_t* p, const ipxg_flow_record& r, uint32_t dir) {
+    p[0] = r.end_reason;                                   // FLOW_END_REASON   (0, 136, 1)
+    put_be(p + 1, r.src_bytes, 8);                         // BYTES             (0, 1, 8)
+    put_be(p + 9, r.dst_bytes, 8);                         // BYTES_REV         (29305, 1, 8)
+    put_be(p + 17, (uint64_t)r.src_packets, 8);            // PACKETS           (0, 2, 8)
+    put_be(p + 25, (uint64_t)r.dst_packets, 8);            // PACKETS_REV       (29305, 2, 8)
+    put_be(p + 33, ntp_ts(r.time_first_sec, r.time_first_usec), 8);  // FLOW_START_USEC (0, 154, 8)
+    put_be(p + 41, ntp_ts(r.time_last_sec, r.time_last_usec), 8);    // FLOW_END_USEC   (0, 155, 8)
+    p[49] = r.ip_version;                                  // L3_PROTO          (0, 60, 1)
+    p[50] = r.ip_proto;                                    // L4_PROTO          (0, 4, 1)
+    p[51] = r.src_tcp_flags;                               // L4_TCP_FLAGS      (0, 6, 1)
+    p[52] = r.dst_tcp_flags;                               // L4_TCP_FLAGS_REV  (29305, 6, 1)
+    put_be(p + 53, r.src_port, 2);                         // L4_PORT_SRC       (0, 7, 2)
+    put_be(p + 55, r.dst_port, 2);                         // L4_PORT_DST       (0, 11, 2)
+    put_be(p + 57, dir, 4);                                // INPUT_INTERFACE   (0, 10, 4)
+    const int na = r.ip_version == 4 ? 4 : 16;             // L3_IPV4/6_ADDR_SRC/DST: as stored
+    for (int k = 0; k < na; ++k) {
+        p[61 + k] = r.src_ip[k];
+        p[61 + na + k] = r.dst_ip[k];
+    }
+    uint8_t* m = p + 61 + 2 * na;
+    for (int k = 0; k < 6; ++k) {
+        m[k] = r.src_mac[k];                               // L2_SRC_MAC        (0, 56, 6)
+        m[6 + k] = r.dst_mac[k];                           // L2_DST_MAC        (0, 80, 6)
+    }
+}
+
+__global__ __launch_bounds__(IPFIX_BLOCK) void k_ipfix_sizes(const ipxg_flow_record* rec, uint32_t n,
+                                                             uint64_t* block_tot) {
+    __shared__ uint32_t part[IPFIX_BLOCK / 64];
+    const uint32_t i = blockIdx.x * IPFIX_BLOCK + threadIdx.x;
+    uint32_t v = i < n ? (rec[i].ip_version == 4 ? IPFIX_V4_LEN : IPFIX_V6_LEN) : 0;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < IPFIX_BLOCK / 64; ++w) t += part[w];
+        block_tot[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of nb block totals in place (one workgroup); total at block_tot[nb]
+__global__ __launch_bounds__(1024) void k_ipfix_scan(uint64_t* block_tot, uint32_t nb) {
+    __shared__ uint64_t part[1024];
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per;
+    uint64_t s = 0;
+    for (uint32_t k = 0; k < per; ++k)
+        if (b0 + k < nb) s += block_tot[b0 + k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele over the 1024 sums
+        const uint64_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (uint32_t k = 0; k < per; ++k) {
+        if (b0 + k < nb) {
+            const uint64_t t = block_tot[b0 + k];
+            block_tot[b0 + k] = run;
+            run += t;
+        }
+    }
+    if (threadIdx.x == 1023) block_tot[nb] = part[1023];
+}
+
+__global__ __launch_bounds__(IPFIX_BLOCK) void k_ipfix_fill(const ipxg_flow_record* rec, uint32_t n, uint32_t dir,
+                                                            const uint64_t* block_base, uint8_t* out,
+                                                            uint64_t* offsets) {
+    __shared__ uint8_t stage[IPFIX_BLOCK * IPFIX_V6_LEN];  // 26.25 KiB
+    __shared__ uint32_t wsum[IPFIX_BLOCK / 64];
+    const uint32_t i = blockIdx.x * IPFIX_BLOCK + threadIdx.x;
+    ipxg_flow_record r;
+    uint32_t len = 0;
+    if (i < n) {
+        r = rec[i];
+        len = ipfix_len(r);
+    }
+    // block exclusive scan of the record lengths
+    uint32_t x = len;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (uint32_t k = 0; k < IPFIX_BLOCK / 64; ++k) {
+        if (k < w) wbase += wsum[k];
+        total += wsum[k];
+    }
+    const uint32_t local = wbase + x - len;
+    const uint64_t base = block_base[blockIdx.x];
+    if (i < n) {
+        fill_basic(stage + local, r, dir);
+        offsets[i] = base + local;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offsets[n] = block_base[gridDim.x];
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < total; k += IPFIX_BLOCK) out[base + k] = stage[k];
+}
+
+void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,
+                        uint8_t* out, uint64_t* offsets) {
+    const uint32_t nb = (n + IPFIX_BLOCK - 1) / IPFIX_BLOCK;
+    hipLaunchKernelGGL(k_ipfix_sizes, dim3(nb), dim3(IPFIX_BLOCK), 0, st, rec, n, block_tot);
+    hipLaunchKernelGGL(k_ipfix_scan, dim3(1), dim3(1024), 0, st, block_tot, nb);
+    hipLaunchKernelGGL(k_ipfix_fill, dim3(nb), dim3(IPFIX_BLOCK), 0, st, rec, n, dir, block_tot, out, offsets);
+}
+
+}  // namespace ipxg

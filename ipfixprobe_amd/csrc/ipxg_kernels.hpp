@@ -174,6 +174,8 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
                    ExportView ex, unsigned long long* stats);
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats);
 void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words);
+void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,
+                        uint8_t* out, uint64_t* offsets);
 void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail);
 void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl);
 void launch_parse_batch(hipStream_t st, const BatchView& b, uint32_t dlt, ipxg_parsed_pkt* out);

@@ -78,13 +78,15 @@ class Capture(ctypes.Structure):
                 ("desc", ctypes.c_void_p), ("n", ctypes.c_uint32), ("datalink", ctypes.c_uint32)]
 
 
+IPFIX_V4_LEN, IPFIX_V6_LEN = 81, 105  # IPXG_IPFIX_V4_LEN / _V6_LEN
+
 EXPORTED_SYMBOLS = [
     "ipxg_config_default", "ipxg_config_parse", "ipxg_create", "ipxg_destroy",
     "ipxg_last_error", "ipxg_stream", "ipxg_submit", "ipxg_expire", "ipxg_finish",
     "ipxg_reset", "ipxg_pending_exports", "ipxg_poll_exports", "ipxg_device_exports",
     "ipxg_clear_exports", "ipxg_get_stats", "ipxg_parse_batch", "ipxg_xxh64_batch",
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
-    "ipxg_probe_counters",
+    "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix",
 ]
 
 _LIB = None
@@ -133,6 +135,8 @@ def lib():
         L.ipxg_profile.argtypes = [vp, ctypes.c_int]
         L.ipxg_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
         L.ipxg_probe_counters.argtypes = [vp, vp]
+        L.ipxg_ipfix_basic.argtypes = [vp, vp, sz, u32, vp, vp]
+        L.ipxg_poll_ipfix.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         for name in EXPORTED_SYMBOLS:
             if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default",
                             "ipxg_capture_free"):
@@ -279,6 +283,26 @@ class Engine:
         out = np.zeros(8, dtype=np.uint64)
         self._check(lib().ipxg_probe_counters(self._h, out.ctypes.data), "ipxg_probe_counters")
         return out
+
+    def ipfix_basic(self, recs, dir_bit_field=0):
+        """IPFIX basic-template data records of `recs` (FLOW_DTYPE) formatted on the device:
+        (bytes uint8 array, offsets[n + 1])."""
+        recs = np.ascontiguousarray(recs, dtype=FLOW_DTYPE)
+        out = np.zeros(max(len(recs), 1) * IPFIX_V6_LEN, dtype=np.uint8)
+        off = np.zeros(len(recs) + 1, dtype=np.uint64)
+        self._check(lib().ipxg_ipfix_basic(self._h, recs.ctypes.data, len(recs), dir_bit_field,
+                                           out.ctypes.data, off.ctypes.data), "ipxg_ipfix_basic")
+        return out[: int(off[-1])], off
+
+    def poll_ipfix(self, dir_bit_field=0, cap=None):
+        """Pending exports as IPFIX basic-template records (consumed): (bytes, records)."""
+        if cap is None:
+            cap = self.pending() * IPFIX_V6_LEN
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n, nb = ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(lib().ipxg_poll_ipfix(self._h, dir_bit_field, out.ctypes.data, cap, ctypes.byref(n),
+                                          ctypes.byref(nb)), "ipxg_poll_ipfix")
+        return out[: nb.value], n.value
 
     def parse(self, arena, desc):
         b = self._batch(arena, desc)

@@ -1008,3 +1008,111 @@ void oracle_cache_stats(const oracle_cache* c, ipxg_stats* out)
     out->flows_in_cache = c->flows_in_cache;
     out->table_capacity = c->cache_size;
 }
+
+/* ===================================================================================== */
+/* IPFIX basic templates -- src/plugins/output/ipfix/src/ipfix.cpp,                       */
+/* include/ipfixprobe/ipfix-elements.hpp                                                  */
+/* ===================================================================================== */
+/* One template element: enterprise number, element id, length (ipfix-elements.hpp FIELD
+ * macro order) and which Flow member it reads. */
+enum ipfix_src {
+    S_END_REASON, S_BYTES, S_BYTES_REV, S_PACKETS, S_PACKETS_REV, S_START, S_END, S_L3, S_L4,
+    S_FLAGS, S_FLAGS_REV, S_SPORT, S_DPORT, S_DIR, S_SRC4, S_DST4, S_SRC6, S_DST6, S_SMAC, S_DMAC
+};
+typedef struct {
+    uint32_t en, id;
+    int len;
+    enum ipfix_src src;
+} ipfix_elem;
+
+/* BASIC_TMPLT_V4 / _V6 (ipfix-elements.hpp:328-366) with the element definitions of
+ * ipfix-elements.hpp:71-119 (FLOW_START/END are the USEC variants, IPXP_TS_MSEC unset). */
+static const ipfix_elem basic_v4[] = {
+    {0, 136, 1, S_END_REASON}, {0, 1, 8, S_BYTES},       {29305, 1, 8, S_BYTES_REV},
+    {0, 2, 8, S_PACKETS},      {29305, 2, 8, S_PACKETS_REV}, {0, 154, 8, S_START},
+    {0, 155, 8, S_END},        {0, 60, 1, S_L3},         {0, 4, 1, S_L4},
+    {0, 6, 1, S_FLAGS},        {29305, 6, 1, S_FLAGS_REV}, {0, 7, 2, S_SPORT},
+    {0, 11, 2, S_DPORT},       {0, 10, 4, S_DIR},        {0, 8, 4, S_SRC4},
+    {0, 12, 4, S_DST4},        {0, 56, 6, S_SMAC},       {0, 80, 6, S_DMAC}};
+static const ipfix_elem basic_v6[] = {
+    {0, 136, 1, S_END_REASON}, {0, 1, 8, S_BYTES},       {29305, 1, 8, S_BYTES_REV},
+    {0, 2, 8, S_PACKETS},      {29305, 2, 8, S_PACKETS_REV}, {0, 154, 8, S_START},
+    {0, 155, 8, S_END},        {0, 60, 1, S_L3},         {0, 4, 1, S_L4},
+    {0, 6, 1, S_FLAGS},        {29305, 6, 1, S_FLAGS_REV}, {0, 7, 2, S_SPORT},
+    {0, 11, 2, S_DPORT},       {0, 10, 4, S_DIR},        {0, 27, 16, S_SRC6},
+    {0, 28, 16, S_DST6},       {0, 56, 6, S_SMAC},       {0, 80, 6, S_DMAC}};
+
+/* MK_NTP_TS (ipfix-elements.hpp:50-60): (tv_sec + EPOCH_DIFF) << 32 | usec * 2^32 / 1e6 */
+static uint64_t ntp_ts(uint32_t sec, uint32_t usec)
+{
+    return (((uint64_t)sec + 2208988800ULL) << 32) | (uint64_t)(uint32_t)(((uint64_t)usec << 32) / 1000000);
+}
+
+/* the element's source value in host byte order (integers) or its bytes (addresses, MACs),
+ * as the FIELD macro's SRC pointer would read it */
+static void ipfix_source(const ipxg_flow_record* r, uint32_t dir, enum ipfix_src s, uint64_t* v,
+                         const uint8_t** bytes)
+{
+    *bytes = NULL;
+    switch (s) {
+    case S_END_REASON: *v = r->end_reason; break;
+    case S_BYTES: *v = r->src_bytes; break;
+    case S_BYTES_REV: *v = r->dst_bytes; break;
+    case S_PACKETS: *v = (uint64_t)r->src_packets; break;  /* temp = (uint64_t) flow.src_packets */
+    case S_PACKETS_REV: *v = (uint64_t)r->dst_packets; break;
+    case S_START: *v = ntp_ts(r->time_first_sec, r->time_first_usec); break;
+    case S_END: *v = ntp_ts(r->time_last_sec, r->time_last_usec); break;
+    case S_L3: *v = r->ip_version; break;
+    case S_L4: *v = r->ip_proto; break;
+    case S_FLAGS: *v = r->src_tcp_flags; break;
+    case S_FLAGS_REV: *v = r->dst_tcp_flags; break;
+    case S_SPORT: *v = r->src_port; break;
+    case S_DPORT: *v = r->dst_port; break;
+    case S_DIR: *v = dir; break;                               /* &this->dir_bit_field */
+    case S_SRC4: case S_SRC6: *bytes = r->src_ip; break;        /* network order in memory */
+    case S_DST4: case S_DST6: *bytes = r->dst_ip; break;
+    case S_SMAC: *bytes = r->src_mac; break;
+    case S_DMAC: *bytes = r->dst_mac; break;
+    }
+}
+
+/* IPFIX_FILL_FIELD (ipfix.cpp:77-96): len 1 copy; len 2 htons; the IPv4 addresses (en 0,
+ * ids 8/12) copied as stored; other len 4 htonl; len 8 byte swap; anything else memcpy. */
+static uint8_t* ipfix_fill_field(uint8_t* t, const ipfix_elem* e, const ipxg_flow_record* r, uint32_t dir)
+{
+    uint64_t v = 0;
+    const uint8_t* b;
+    ipfix_source(r, dir, e->src, &v, &b);
+    if (e->len == 1) {
+        t[0] = (uint8_t)v;
+    } else if (e->len == 2) {
+        t[0] = (uint8_t)(v >> 8);
+        t[1] = (uint8_t)v;
+    } else if (e->en == 0 && (e->id == 8 || e->id == 12)) {
+        memcpy(t, b, 4);
+    } else if (e->len == 4) {
+        for (int k = 0; k < 4; ++k) t[k] = (uint8_t)(v >> (24 - 8 * k));
+    } else if (e->len == 8) {
+        for (int k = 0; k < 8; ++k) t[k] = (uint8_t)(v >> (56 - 8 * k));
+    } else {
+        memcpy(t, b, (size_t)e->len);
+    }
+    return t + e->len;
+}
+
+/* fill_basic_flow: ip_version == IP::v4 selects BASIC_TMPLT_V4, anything else _V6
+ * (ipfix.cpp:1478-1509; get_template :289 likewise) */
+void oracle_ipfix_basic(const ipxg_flow_record* recs, size_t n, uint32_t dir_bit_field, uint8_t* out,
+                        uint64_t* offsets)
+{
+    uint8_t* p = out;
+    offsets[0] = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const ipxg_flow_record* r = &recs[i];
+        const ipfix_elem* t = r->ip_version == 4 ? basic_v4 : basic_v6;
+        const size_t ne = r->ip_version == 4 ? sizeof(basic_v4) / sizeof(basic_v4[0])
+                                             : sizeof(basic_v6) / sizeof(basic_v6[0]);
+        for (size_t k = 0; k < ne; ++k) p = ipfix_fill_field(p, &t[k], r, dir_bit_field);
+        offsets[i + 1] = (uint64_t)(p - out);
+    }
+}

@@ -61,6 +61,11 @@ size_t oracle_cache_pending(const oracle_cache* c);
 size_t oracle_cache_take(oracle_cache* c, ipxg_flow_record* out, size_t cap);
 void oracle_cache_stats(const oracle_cache* c, ipxg_stats* out);
 
+/* IPFIXExporter::fill_basic_flow (ipfix.cpp:1470-1516) for each of n records: the basic
+ * template's data records back to back into out, byte offsets into offsets[n + 1]. */
+void oracle_ipfix_basic(const ipxg_flow_record* recs, size_t n, uint32_t dir_bit_field, uint8_t* out,
+                        uint64_t* offsets);
+
 #ifdef __cplusplus
 }
 #endif

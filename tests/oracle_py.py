@@ -38,6 +38,7 @@ def lib():
         L.oracle_cache_pending.argtypes = [vp]
         L.oracle_cache_take.restype = ctypes.c_size_t
         L.oracle_cache_take.argtypes = [vp, vp, ctypes.c_size_t]
+        L.oracle_ipfix_basic.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
         L.oracle_cache_stats.argtypes = [vp, vp]
         _LIB = L
     return _LIB
@@ -119,6 +120,15 @@ class OracleCache:
             self.close()
         except Exception:
             pass
+
+
+def ipfix_basic(recs, dir_bit_field=0):
+    """IPFIXExporter::fill_basic_flow restated (oracle): (bytes uint8 array, offsets[n+1])."""
+    recs = np.ascontiguousarray(recs, dtype=FLOW_DTYPE)
+    out = np.zeros(max(len(recs), 1) * 105, dtype=np.uint8)
+    off = np.zeros(len(recs) + 1, dtype=np.uint64)
+    lib().oracle_ipfix_basic(recs.ctypes.data, len(recs), dir_bit_field, out.ctypes.data, off.ctypes.data)
+    return out[: int(off[-1])], off
 
 
 def run_capture(arena, desc, datalink=1, finish=True, **kw):
