@@ -270,7 +270,7 @@ def main():
                  device_id=local)
 
     def step():
-        eng.submit(frames, desc, device=True)
+        eng.submit(frames, desc, device=True, asynchronous=True)  # finish follows right behind
         eng.finish()
         if world > 1:
             gather_exports(eng, rank, world, device)

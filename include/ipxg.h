@@ -71,6 +71,11 @@ typedef struct ipxg_pkt_desc {
 } ipxg_pkt_desc;
 
 #define IPXG_BATCH_DEVICE 0x1u /* arena and desc are device pointers (already in HBM)   */
+#define IPXG_BATCH_ASYNC 0x2u  /* with IPXG_BATCH_DEVICE: ipxg_submit may return before the
+                                * batch is applied (its kernels enqueued); the batch's
+                                * buffers must stay unchanged until the next call on the
+                                * engine, which completes it (ipxg_finish right behind it
+                                * then costs one host round trip instead of two)            */
 
 typedef struct ipxg_batch {
     const uint8_t* arena;       /* frame bytes                                          */

@@ -59,6 +59,14 @@ struct ipxg_engine {
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
     uint32_t bin_slots = 0;              // k_bin workgroups resident at once (its grid)
+    // an IPXG_BATCH_ASYNC batch whose kernels are enqueued but whose control block the host
+    // has not read yet (completed by the next call on the engine)
+    struct {
+        bool on = false;
+        BatchView bv;
+        Params p;
+        uint32_t n = 0;
+    } inflight;
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
@@ -391,6 +399,20 @@ const char* ipxg_last_error(const ipxg_engine* e) { return e ? e->err.c_str() : 
 
 void* ipxg_stream(ipxg_engine* e) { return e ? (void*)e->st : nullptr; }
 
+static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool binned, bool finishing);
+
+// The in-flight asynchronous batch, if any: wait for its kernels and run post_batch.  Every
+// entry point that reads or changes engine state calls this first.
+static int complete_batch(ipxg_engine* e) {
+    if (!e->inflight.on) return IPXG_OK;
+    e->inflight.on = false;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    HIPCHK(e, stream_wait(e->st));
+    int rc;
+    if ((rc = check_ex(e))) return rc;
+    return post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, false);
+}
+
 int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     if (!e || !batch) return IPXG_EINVAL;
     const uint32_t n = batch->n;
@@ -399,6 +421,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     if (batch->arena_len > (1ull << 32)) return set_err(e, IPXG_ETOOBIG, "arena larger than 4 GiB");
     if (!batch->arena || !batch->desc) return set_err(e, IPXG_EINVAL, "null arena/desc");
     int rc;
+    if ((rc = complete_batch(e))) return rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     BatchView bv;
     bv.n = n;
@@ -452,7 +475,24 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         ev_rec(e, 1);
     }
     HIPCHK(e, hipGetLastError());
+    if ((batch->flags & IPXG_BATCH_ASYNC) && (batch->flags & IPXG_BATCH_DEVICE) && binned) {
+        if ((rc = publish_ctl(e))) return rc;  // read by the next call (complete_batch)
+        e->inflight.on = true;
+        e->inflight.bv = bv;
+        e->inflight.p = p;
+        e->inflight.n = n;
+        return IPXG_OK;
+    }
     if ((rc = sync_ctl(e))) return rc;
+    return post_batch(e, bv, p, n, binned, false);
+}
+
+// Everything after the batch's main kernels, from the control block in e->ctl_h: timing,
+// the fragment, deferral, table-scan and complex paths when the batch needs them, then the
+// host's accounting.  `finishing`: a finish follows at once (no table growth needed).
+static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool binned, bool finishing) {
+    int rc;
+    FragView fv = frag_view(e);
     const BatchCtl c1 = *e->ctl_h;
     if (e->prof) {
         e->tm.ingest_ms += ev_ms(e, 0);
@@ -575,7 +615,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     e->prev_usec = c2.last_usec;
     e->batches++;
     // keep the load factor <= 1/2 for the next batch (dead slots are dropped by the rebuild)
-    if ((uint64_t)e->keys * 2 > e->cap) {
+    if (!finishing && (uint64_t)e->keys * 2 > e->cap) {
         uint32_t ncap = pow2_at_least((uint64_t)e->live * 4 + 1);
         if (ncap < e->cap) ncap = e->cap;
         if ((rc = rehash(e, ncap))) return rc;
@@ -586,6 +626,10 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 
 int ipxg_expire(ipxg_engine* e, int64_t now_sec) {
     if (!e) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
@@ -603,6 +647,32 @@ int ipxg_finish(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (e->inflight.on) {
+        // Enqueue the finish right behind the batch, guarded on the device (k_finish_guard):
+        // one host round trip for batch + finish when the batch needs nothing from the host.
+        launch_finish_guard(e->st, e->ctl_d, e->ex_count_d, e->ex_cap, e->live);
+        ev_rec(e, 9);
+        launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d, e->ctl_d);
+        HIPCHK(e, hipGetLastError());
+        ev_rec(e, 10);
+        if ((rc = publish_ctl(e))) return rc;
+        HIPCHK(e, stream_wait(e->st));
+        if ((rc = check_ex(e))) return rc;
+        e->inflight.on = false;
+        const bool held = e->ctl_h->hold != 0;
+        HIPCHK(e, hipMemsetAsync(&e->ctl_d->hold, 0, sizeof(uint32_t), e->st));
+        if ((rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, !held))) return rc;
+        if (!held) {
+            if (e->prof && e->prof_level == 1) {
+                e->tm.finish_ms += ev_ms(e, 9);
+                e->tm.finish_launches++;
+            }
+            e->keys = e->live = 0;
+            e->prev_valid = false;
+            return IPXG_OK;
+        }
+        // the guard held k_finish back: the batch is complete now, finish normally
+    }
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
     ev_rec(e, 9);
     launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);  // also empties the table
@@ -620,6 +690,10 @@ int ipxg_finish(ipxg_engine* e) {
 
 int ipxg_reset(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
     const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
@@ -635,12 +709,20 @@ int ipxg_reset(ipxg_engine* e) {
 
 int ipxg_pending_exports(ipxg_engine* e, size_t* n) {
     if (!e || !n) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     *n = e->ex_count - e->ex_head;
     return IPXG_OK;
 }
 
 int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t* n) {
     if (!e || !n || (cap && !out)) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     size_t k = std::min<size_t>(cap, e->ex_count - e->ex_head);
     if (k) {
         HIPCHK(e, hipSetDevice(e->cfg.device_id));
@@ -674,6 +756,10 @@ static int ipfix_format(ipxg_engine* e, const ipxg_flow_record* rec, uint32_t n,
 int ipxg_ipfix_basic(ipxg_engine* e, const ipxg_flow_record* recs, size_t n, uint32_t dir_bit_field, uint8_t* out,
                      uint64_t* offsets) {
     if (!e || (n && (!recs || !out || !offsets))) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     if (offsets) offsets[0] = 0;
     if (n == 0) return IPXG_OK;
     if (n > IPXG_MAX_BATCH) return set_err(e, IPXG_ETOOBIG, "more records than IPXG_MAX_BATCH");
@@ -691,6 +777,10 @@ int ipxg_ipfix_basic(ipxg_engine* e, const ipxg_flow_record* recs, size_t n, uin
 
 int ipxg_poll_ipfix(ipxg_engine* e, uint32_t dir_bit_field, uint8_t* out, size_t cap, size_t* n, size_t* bytes) {
     if (!e || !n || !bytes || (cap && !out)) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     *n = *bytes = 0;
     const uint32_t pend = e->ex_count - e->ex_head;
     if (pend == 0) return IPXG_OK;
@@ -719,6 +809,10 @@ int ipxg_poll_ipfix(ipxg_engine* e, uint32_t dir_bit_field, uint8_t* out, size_t
 
 int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n) {
     if (!e || !dptr || !n) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     *dptr = e->ex + e->ex_head;
     *n = e->ex_count - e->ex_head;
     return IPXG_OK;
@@ -726,6 +820,10 @@ int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n
 
 int ipxg_clear_exports(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     e->ex_head = e->ex_count = 0;
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));  // ordered on the stream
     return IPXG_OK;
@@ -733,6 +831,10 @@ int ipxg_clear_exports(ipxg_engine* e) {
 
 int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     if (!e || !out) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     unsigned long long h[STAT_SHARDS * ST_COUNT];
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     HIPCHK(e, hipMemcpyAsync(h, e->stats_d, sizeof(h), hipMemcpyDeviceToHost, e->st));
@@ -775,12 +877,20 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
 
 int ipxg_probe_counters(ipxg_engine* e, uint64_t* out) {
     if (!e || !out) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     for (int k = 0; k < 8; ++k) out[k] = e->ctl_h->probe[k];
     return IPXG_OK;
 }
 
 int ipxg_profile(ipxg_engine* e, int enable) {
     if (!e) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if (enable && !e->ev[0])
         for (hipEvent_t& ev : e->ev) HIPCHK(e, hipEventCreate(&ev));
@@ -792,12 +902,20 @@ int ipxg_profile(ipxg_engine* e, int enable) {
 
 int ipxg_get_timing(ipxg_engine* e, ipxg_timing* out) {
     if (!e || !out) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     *out = e->tm;
     return IPXG_OK;
 }
 
 int ipxg_parse_batch(ipxg_engine* e, const ipxg_batch* batch, ipxg_parsed_pkt* out) {
     if (!e || !batch || !out) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     const uint32_t n = batch->n;
     if (!n) return IPXG_OK;
     int rc;
@@ -833,6 +951,10 @@ int ipxg_parse_batch(ipxg_engine* e, const ipxg_batch* batch, ipxg_parsed_pkt* o
 int ipxg_xxh64_batch(ipxg_engine* e, const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
                      uint64_t* out) {
     if (!e || (n && (!keys || !out))) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
     if (!n) return IPXG_OK;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     uint8_t* dk;

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("IPXG_LIB") or os.path.join(_HERE, "libipxg.so")
 
 DLT_EN10MB, DLT_RAW, DLT_LINUX_SLL, DLT_LINUX_SLL2 = 1, 12, 113, 276
 BATCH_DEVICE = 0x1
+BATCH_ASYNC = 0x2
 MAX_BATCH = 16 * 1024 * 1024 - 1
 
 DESC_DTYPE = np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"),
@@ -204,14 +205,14 @@ class Engine:
         return lib().ipxg_stream(self._h)
 
     @staticmethod
-    def _batch(arena, desc, device=False):
+    def _batch(arena, desc, device=False, asynchronous=False):
         b = Batch()
         if device or hasattr(arena, "data_ptr"):  # torch tensors: on the GPU, or (pinned) host
             b.arena = arena.data_ptr()
             b.arena_len = arena.numel() * arena.element_size()
             b.desc = desc.data_ptr()
             b.n = desc.numel() * desc.element_size() // 16
-            b.flags = BATCH_DEVICE if device else 0
+            b.flags = (BATCH_DEVICE | (BATCH_ASYNC if asynchronous else 0)) if device else 0
             b._keep = (arena, desc)
         else:
             arena = np.ascontiguousarray(arena, dtype=np.uint8)
@@ -224,8 +225,11 @@ class Engine:
             b._keep = (arena, desc)
         return b
 
-    def submit(self, arena, desc, device=False):
-        b = self._batch(arena, desc, device)
+    def submit(self, arena, desc, device=False, asynchronous=False):
+        """asynchronous (device batches): may return before the batch is applied; keep the
+        tensors alive and unchanged until the next call on the engine."""
+        b = self._batch(arena, desc, device, asynchronous)
+        self._keep_async = b._keep if (device and asynchronous) else None
         self._check(lib().ipxg_submit(self._h, ctypes.byref(b)), "ipxg_submit")
 
     def submit_all(self, arena, desc, batch=None):
