@@ -648,11 +648,10 @@ int ipxg_finish(ipxg_engine* e) {
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if (e->inflight.on) {
-        // Enqueue the finish right behind the batch, guarded on the device (k_finish_guard):
+        // Enqueue the finish right behind the batch, guarded on the device (k_finish's guard):
         // one host round trip for batch + finish when the batch needs nothing from the host.
-        launch_finish_guard(e->st, e->ctl_d, e->ex_count_d, e->ex_cap, e->live);
         ev_rec(e, 9);
-        launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d, e->ctl_d);
+        launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d, e->ctl_d, e->ex_count, e->live);
         HIPCHK(e, hipGetLastError());
         ev_rec(e, 10);
         if ((rc = publish_ctl(e))) return rc;

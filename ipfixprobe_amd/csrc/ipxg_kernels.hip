@@ -463,11 +463,23 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
 
 // Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288) and empty the
 // table (every occupied slot it scans is zeroed).
+// guard != nullptr: a finish enqueued right behind a batch before the host has read the
+// batch's control block.  It must not run when the batch left work for the host (fragments,
+// deferred packets, the table scan, complex flows) or when the export buffer might not hold
+// every live record; every workgroup decides alike from fields k_finish does not change,
+// workgroup 0 reports it (guard->hold) and the host then completes the batch and finishes
+// again.
 __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
-                                                unsigned long long* stats, const BatchCtl* guard) {
+                                                unsigned long long* stats, BatchCtl* guard, uint32_t ex_before,
+                                                uint32_t live_before) {
     __shared__ uint32_t scratch[8];
     __shared__ uint32_t bbase;
-    if (guard && guard->hold) return;  // speculative finish behind a batch that needs the host
+    if (guard) {
+        const bool hold = guard->frag_count || guard->deferred || guard->pending || guard->complex_count ||
+                          (uint64_t)ex_before + guard->exported + live_before + guard->new_live > ex.cap;
+        if (blockIdx.x == 0 && threadIdx.x == 0) guard->hold = hold ? 1u : 0u;
+        if (hold) return;
+    }
     const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
     uint32_t mask = 0, c = 0;
 #pragma unroll
@@ -498,7 +510,6 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
 // the stream has drained, without a D2H copy command of its own.
 __global__ __launch_bounds__(64) void k_publish(const uint32_t* src, uint32_t* dst, uint32_t words) {
     for (uint32_t i = threadIdx.x; i < words; i += 64) dst[i] = src[i];
-    __threadfence_system();
 }
 
 void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words) {
@@ -506,24 +517,9 @@ void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t
 }
 
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
-                   const BatchCtl* guard) {
-    hipLaunchKernelGGL(k_finish, dim3(scan_grid(cap)), dim3(256), 0, st, t, cap, ex, stats, guard);
-}
-
-// Decide, on the device, whether a finish enqueued right behind a batch (before the host has
-// seen the batch's control block) may run: not when the batch left work for the host
-// (fragments, deferred packets, the table scan, complex flows) or when the export buffer
-// might not hold every live record.  k_finish then returns at once and the host completes
-// the batch and finishes again.
-__global__ void k_finish_guard(BatchCtl* ctl, const uint32_t* ex_count, uint32_t ex_cap, uint32_t live_before) {
-    const bool host = ctl->frag_count || ctl->deferred || ctl->pending || ctl->complex_count;
-    const uint64_t need = (uint64_t)ex_count[0] + live_before + ctl->new_live;
-    ctl->hold = (host || need > ex_cap) ? 1u : 0u;
-}
-
-void launch_finish_guard(hipStream_t st, BatchCtl* ctl, const uint32_t* ex_count, uint32_t ex_cap,
-                         uint32_t live_before) {
-    hipLaunchKernelGGL(k_finish_guard, dim3(1), dim3(1), 0, st, ctl, ex_count, ex_cap, live_before);
+                   BatchCtl* guard, uint32_t ex_before, uint32_t live_before) {
+    hipLaunchKernelGGL(k_finish, dim3(scan_grid(cap)), dim3(256), 0, st, t, cap, ex, stats, guard, ex_before,
+                       live_before);
 }
 
 __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_cap, TableView to,

@@ -50,7 +50,7 @@ struct BatchCtl {
     uint32_t spilled;        // packets that fell back to direct atomic accumulation
     uint32_t slow_count;     // packets k_bin left for k_bin_slow (statistics)
     uint32_t fin_count;      // slots k_reduce listed for k_fin_list
-    uint32_t hold;           // k_finish_guard: a speculative finish must not run
+    uint32_t hold;           // set by a guarded k_finish that did not run (see k_finish)
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -174,9 +174,7 @@ void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, Ta
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
                    ExportView ex, unsigned long long* stats);
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
-                   const BatchCtl* guard = nullptr);
-void launch_finish_guard(hipStream_t st, BatchCtl* ctl, const uint32_t* ex_count, uint32_t ex_cap,
-                         uint32_t live_before);
+                   BatchCtl* guard = nullptr, uint32_t ex_before = 0, uint32_t live_before = 0);
 void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words);
 void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,
                         uint8_t* out, uint64_t* offsets);

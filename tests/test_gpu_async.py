@@ -1,6 +1,6 @@
 """IPXG_BATCH_ASYNC: ipxg_submit of a device batch returns with the kernels enqueued; the next
 call completes the batch (ipxg_finish runs speculatively behind it, held back on the device
-by k_finish_guard when the batch needs the host).  Records must equal the synchronous path's
+by its guard when the batch needs the host).  Records must equal the synchronous path's
 and the oracle's in every case: plain batches, batches that need the host (fragments,
 deferrals, non-monotonic time, complex flows), and every entry point after an async batch."""
 import os
