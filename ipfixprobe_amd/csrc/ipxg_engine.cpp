@@ -407,9 +407,8 @@ static int complete_batch(ipxg_engine* e) {
     if (!e->inflight.on) return IPXG_OK;
     e->inflight.on = false;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
-    HIPCHK(e, stream_wait(e->st));
     int rc;
-    if ((rc = check_ex(e))) return rc;
+    if ((rc = sync_ctl(e))) return rc;
     return post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, false);
 }
 
@@ -476,8 +475,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     }
     HIPCHK(e, hipGetLastError());
     if ((batch->flags & IPXG_BATCH_ASYNC) && (batch->flags & IPXG_BATCH_DEVICE) && binned) {
-        if ((rc = publish_ctl(e))) return rc;  // read by the next call (complete_batch)
-        e->inflight.on = true;
+        e->inflight.on = true;  // the next call publishes and reads the control block
         e->inflight.bv = bv;
         e->inflight.p = p;
         e->inflight.n = n;
