@@ -1,29 +1,32 @@
-// ipxg_ingest.hip -- the per-batch ingest of the packet -> biflow engine, in two phases with
-// no per-packet device-scope atomics (those execute at the memory side on CDNA4, ~20 G/s
-// chip-wide for lane-scattered addresses: MI355X_MICROARCH.md "Global float atomics").
+// ipxg_ingest.hip -- the per-batch ingest of the packet -> biflow engine (the binned
+// pipeline), with no per-packet device-scope atomics (those execute at the memory side on
+// CDNA4, ~20 G/s chip-wide for lane-scattered addresses: MI355X_MICROARCH.md "Global float
+// atomics").
 //
-//   k_bin     BIN_K packets per lane per tile: stage <= 128 header bytes in the lane's LDS
-//             column, parse (parse_packet, parser.cpp:673-805), build key + inverse key and
-//             2x XXH64 (create_hash_key + XXH64, cache.cpp:525-574, xxhash.h:2885-2901),
-//             then append a 16-byte record {canonical hash, packet index, contribution} to
-//             the region of its partition (bits 32.. of the canonical hash).  A tile ranks
-//             its records per partition with LDS atomics and reserves room with one
-//             coalesced device atomic per 64 partitions, so a partition's records of one
-//             tile land in one run.                                     (HBM-bound)
-//   k_bin_slow  the frames k_bin's register parser does not take, through the general
-//             LDS-staged parser (parse_frame), emitted the same way.
-//   k_reduce  one 1024-thread workgroup per partition chunk: aggregates the chunk's records
+//   k_bin     persistent workgroups over tiles of BIN_K x 256 packets (one per lane per
+//             step), buffer loads software-pipelined across the tiles: parse_fast reads
+//             Eth/IPv4/UDP|TCP headers from registers (parse_packet, parser.cpp:673-805, for
+//             that shape), key + inverse key and 2x XXH64 (create_hash_key + XXH64,
+//             cache.cpp:525-574, xxhash.h:2885-2901) give the canonical hash, and a 16-byte
+//             record {canonical hash, packet index, contribution} is ranked in its partition
+//             (bits 32.. of the hash) with an LDS atomic.  At the tile's end the records are
+//             sorted by partition in LDS and each run is written coalesced into the
+//             workgroup's own segment of the partition.  Other frame shapes go to the
+//             workgroup's slow list.                                        (HBM-bound)
+//   k_bin_slow  the slow lists through the general LDS-staged parser (parse_frame), ranked
+//             and emitted the same way into segment columns of their own.
+//   k_reduce  one 1024-thread workgroup per partition: aggregates the partition's records
 //             per flow in an LDS hash table (LDS atomics), then merges each flow into its
-//             slot of the device table once -- a plain read-modify-write when the workgroup
-//             holds all of the partition's records, atomics otherwise -- and, when nothing
-//             else of the batch can touch the flow any more, lists the slot for k_fin_list.
+//             slot of the device table with plain stores (the workgroup owns its keys) and,
+//             when nothing else of the batch can touch the flow, lists the slot for
+//             k_fin_list.
 //   k_fin_list  applies the reference's split rules to the listed slots (finalize_slot), so
 //             the table is not scanned per batch.
 //
-// Records that do not fit (partition region full, LDS table full) fall back to direct
-// atomic accumulation (merge_packet_atomic); the engine then runs the k_finalize scan for
-// the batch (ctl->pending).  Both paths are order-independent reductions keyed by packet
-// index, so the result does not depend on which lane or workgroup runs first.
+// Records that do not fit (segment full, LDS table full) fall back to direct atomic
+// accumulation (merge_packet_atomic); the engine then runs the k_finalize scan for the
+// batch (ctl->pending).  Both paths are order-independent reductions keyed by packet index,
+// so the result does not depend on which lane or workgroup runs first.
 #include "ipxg_table.hpp"
 
 namespace ipxg {
