@@ -106,3 +106,32 @@ def test_engine_shards_union_equals_whole_capture():
     parts = [run_capture(arena, np.ascontiguousarray(desc[own == r]))[0] for r in range(2)]
     d = flowcmp.diff(np.concatenate(parts), want)
     assert not d, d
+
+
+@pytest.mark.gpu
+def test_rccl_gather_single_rank_aliases_device_exports():
+    """bench.py's N > 1 step on one rank: the export buffer aliased zero-copy as a torch tensor
+    (__cuda_array_interface__) and gathered over RCCL (world size 1) equals ipxg_poll_exports."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    import bench
+    from ipfixprobe_amd import Engine
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        arena, desc = _capture(seed=24)
+        with Engine() as e:
+            e.submit(arena, desc)
+            e.finish()
+            ptr, n = e.device_exports()
+            buf = torch.as_tensor(bench._DevArray(ptr, max(n, 1) * 128), device=dev)
+            out = shard.gather_records(buf, n, 0, 1, dev)
+            got = out.cpu().numpy().view(FLOW_DTYPE)
+            want = e.poll()
+        assert n == len(want) > 0
+        assert got.tobytes() == want.tobytes()
+    finally:
+        dist.destroy_process_group()
