@@ -35,14 +35,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 ALG_BYTES_PER_PKT = 80  # 64 B frame + 16 B descriptor
 
 
-def gen_flows(F, rank, world, seed):
-    """F distinct biflows whose canonical hash falls in this rank's range."""
+def gen_flows(F, rank, world, seed, device_id=0):
+    """F distinct biflows whose canonical hash falls in this rank's range (hashed on this
+    rank's GPU)."""
     from ipfixprobe_amd import Engine, shard
     rng = np.random.default_rng(seed)
     out = {k: [] for k in ("sip", "dip", "sport", "dport")}
     have = 0
     seen = set()
-    with Engine() as e:
+    with Engine(device_id=device_id) as e:
         while have < F:
             m = max(2 * (F - have) * world, 1024)
             sip = (10 << 24) | rng.integers(0, 1 << 24, m, dtype=np.uint64)
@@ -263,7 +264,7 @@ def main():
     torch.cuda.set_device(device)
 
     from ipfixprobe_amd import Engine
-    flows = gen_flows(args.flows, rank, world, args.seed)
+    flows = gen_flows(args.flows, rank, world, args.seed, device_id=local)
     frames, desc = build_batch(flows, args.packets, args.seed + rank, device)
     torch.cuda.synchronize()
     eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(2 * args.flows)))), args.ingest),
