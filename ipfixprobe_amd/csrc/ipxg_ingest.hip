@@ -243,6 +243,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: the tile's records by partition
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t nslow[2];  // slow packets of the tile (by tile parity)
+    // timestamps (sec << 32 | usec) of each step's first and last packet per wave: the order
+    // check across wave boundaries, done once per tile (within a wave it is a DPP shift)
+    __shared__ uint64_t bnd_first[BIN_K][IPXG_BLOCK / 64], bnd_last[BIN_K][IPXG_BLOCK / 64];
     const uint32_t tid = threadIdx.x;
     for (uint32_t q = tid; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     if (tid < 2) nslow[tid] = 0;
@@ -265,12 +268,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
-    const bool lane0 = (tid & 63) == 0;
-    // lane 0's predecessor packet (the previous wave's last one): its timestamp, for the order
-    // check; the other lanes take their predecessor's from the lane below (DPP)
-    auto prev_ts0 = [&](uint32_t i) -> u32x2 {
-        return __builtin_amdgcn_raw_buffer_load_b64(rs_desc, lane0 && i != 0 ? i * 16u - 8u : BUF_OOB, 0, 0);
-    };
+    const uint32_t lane = tid & 63, wave = tid >> 6;
     if (blockIdx.x == 0 && tid == 0 && p.prev_valid) {
         const ipxg_pkt_desc d0 = b.desc[0];
         if ((((uint64_t)d0.ts_sec << 32) | d0.ts_usec) < ts_before) nonmono = true;
@@ -294,7 +292,6 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
     const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
     ipxg_pkt_desc Dr[DA];
-    u32x2 Pr[DA];
     Head48 Hr[HA];
     // The prologue issues its loads in the order the last DA steps of a tile do, with dummy
     // stores where a tile issues heads of its own steps and its record stores: the loop's
@@ -304,7 +301,6 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     for (int k = 0; k < DA; ++k) {
         const uint32_t i = blockIdx.x * BIN_TILE + k * IPXG_BLOCK + tid;
         Dr[k] = load_desc(rs_desc, i);
-        Pr[k] = prev_ts0(i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
             Hr[h] = load_head(rs_arena, Dr[h], fast_ok && fast_shape(Dr[h]));
@@ -318,6 +314,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     for (uint32_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
         const uint32_t tile = tile_id * BIN_TILE;
         const uint32_t next = (tile_id + gridDim.x) * BIN_TILE;  // past the batch: loads give zeros
+        // the timestamp of the packet before the tile (another workgroup's tile), for the
+        // tile's first packet; consumed after the tile (zeros for the batch's first tile)
+        const u32x2 tpred = __builtin_amdgcn_raw_buffer_load_b64(rs_desc, tile ? tile * 16u - 8u : BUF_OOB, 0, 0);
         PROBE_T(t0);
 #pragma unroll
         for (uint32_t k = 0; k < (1u << BIN_MAX_PART_BITS) / IPXG_BLOCK; ++k)
@@ -337,7 +336,6 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t i = tile + j * IPXG_BLOCK + tid;
             // this step's packet, loaded HA (head) and DA (descriptor) steps ago
             const ipxg_pkt_desc dc = Dr[j % DA];
-            const u32x2 pc = Pr[j % DA];
             const Head48 hc = Hr[j % HA];
             // bytes 40-43 are not parsed: keep their register live until here, or the compiler
             // reuses it while the load is in flight and must drain every load to do so
@@ -345,14 +343,17 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             // issue: the descriptor DA steps ahead, the head HA steps ahead
             const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
             Dr[j % DA] = load_desc(rs_desc, ia);
-            Pr[j % DA] = prev_ts0(ia);
             const ipxg_pkt_desc dh = Dr[(j + HA) % DA];
             Hr[j % HA] = load_head(rs_arena, dh, fast_ok && fast_shape(dh));
             const bool act = i < b.n;
-            // the predecessor's timestamp: lane 0's was loaded, the others' is the lane below's
-            const uint32_t ps = (uint32_t)__builtin_amdgcn_update_dpp((int)pc.x, (int)dc.ts_sec, 0x138, 0xF, 0xF, false);
-            const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp((int)pc.y, (int)dc.ts_usec, 0x138, 0xF, 0xF, false);
+            // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
+            // with itself here and with the previous wave's last packet after the tile)
+            const uint32_t ps = (uint32_t)__builtin_amdgcn_update_dpp((int)dc.ts_sec, (int)dc.ts_sec, 0x138, 0xF, 0xF, false);
+            const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp((int)dc.ts_usec, (int)dc.ts_usec, 0x138, 0xF, 0xF, false);
             if (act && (dc.ts_sec < ps || (dc.ts_sec == ps && dc.ts_usec < pu))) nonmono = true;
+            const uint64_t ts = ((uint64_t)dc.ts_sec << 32) | dc.ts_usec;
+            if (lane == 0) bnd_first[j][wave] = ts;
+            if (lane == 63) bnd_last[j][wave] = ts;
             DevPkt pk;
             bool have = false, slow = false;
 #ifdef IPXG_EXP_LOADONLY  // timing experiment only: the loads, no parse/rank
@@ -377,6 +378,13 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         PROBE_ADD(2, t2, t3);
         slow_fill += nslow[par];  // final: read after the tile's barriers
         par ^= 1;
+        if (tid < BIN_K * (IPXG_BLOCK / 64)) {  // the wave boundaries of the tile
+            const uint32_t j = tid / (IPXG_BLOCK / 64), w = tid % (IPXG_BLOCK / 64);
+            const uint32_t i0 = tile + j * IPXG_BLOCK + w * 64;
+            const uint64_t pred = w ? bnd_last[j][w - 1]
+                                    : (j ? bnd_last[j - 1][IPXG_BLOCK / 64 - 1] : ((uint64_t)tpred.x << 32) | tpred.y);
+            if (i0 != 0 && i0 < b.n && bnd_first[j][w] < pred) nonmono = true;
+        }
         PROBE_T(t4);
         PROBE_ADD(3, t3, t4);
     }

@@ -324,3 +324,21 @@ def test_flows_fuzz_corpus(seed):
     for k in ("seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",
               "tcp_packets", "udp_packets", "vlan_packets", "keyless_packets"):
         assert gst[k] == wst[k], k
+
+
+@pytest.mark.parametrize("at", [1, 63, 64, 256, 2047, 2048, 2048 * 5 + 192])
+def test_nonmonotonic_detected_at_wave_and_tile_boundaries(at):
+    """One timestamp going backwards, at a lane / wave / tile boundary of k_bin: the batch is
+    handled on the order-preserving path (every flow complex) and matches the oracle."""
+    from ipfixprobe_amd import run_capture
+    rng = np.random.default_rng(41)
+    arena, desc = _udp_batch(rng, rng.integers(0, 50, 12000), 50)  # no order-dependent flows
+    d2 = desc.copy()
+    d2["ts_sec"][at] = d2["ts_sec"][at - 1] - 1  # before its predecessor
+    want, _ = oracle_py.run_capture(arena, d2, 1, cache_exp=20)
+    got, st = run_capture(arena, d2)
+    assert st["complex_flows"] > 0
+    d = flowcmp.diff(got, want)
+    assert not d, d
+    _, st0 = run_capture(arena, desc)
+    assert st0["complex_flows"] == 0
