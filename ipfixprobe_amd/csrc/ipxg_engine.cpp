@@ -127,8 +127,8 @@ static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_c
 
 // Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
 // (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
-// than the batch's packets.  k_bin runs bin_grid persistent workgroups over the 2048-packet
-// tiles; each owns one segment per partition, sized for 1.5x its mean share of records plus
+// than the batch's packets.  k_bin runs bin_grid persistent workgroups over tiles of
+// BIN_TILE_PKTS packets; each owns one segment per partition, sized for 1.5x its mean share of records plus
 // 4 standard deviations (binomial) and a margin; what does not fit spills to atomics.
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
@@ -138,14 +138,14 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     if (const char* pb = std::getenv("IPXG_PART_BITS"))  // tuning knob (experiments only)
         bits = std::min<uint32_t>((uint32_t)std::atoi(pb), BIN_MAX_PART_BITS);
     const uint32_t P = 1u << bits;
-    const uint64_t tiles = ((uint64_t)n + 2047) / 2048;
+    const uint64_t tiles = ((uint64_t)n + BIN_TILE_PKTS - 1) / BIN_TILE_PKTS;
     if (!e->bin_slots) {
         e->bin_slots = bin_resident_blocks(e->cfg.device_id);
         if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
             e->bin_slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
     }
     const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->bin_slots);
-    const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * 2048, n);
+    const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * BIN_TILE_PKTS, n);
     const double mean = (double)per_block / P;
     const uint64_t seg = ((uint64_t)(mean * 1.5 + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
     const uint32_t cols = 2 * grid;
@@ -153,7 +153,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
     if ((rc = ensure(e, e->bin_count, (size_t)P * cols * sizeof(uint32_t)))) return rc;
     // each k_bin workgroup's slow list holds every packet of its tiles
-    const uint64_t slow_stride = (tiles + grid - 1) / grid * 2048;
+    const uint64_t slow_stride = (tiles + grid - 1) / grid * BIN_TILE_PKTS;
     if ((rc = ensure(e, e->slow_list, (size_t)grid * slow_stride * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(e, e->slow_cnt, (size_t)grid * sizeof(uint32_t)))) return rc;
     bv.slow_stride = (uint32_t)slow_stride;

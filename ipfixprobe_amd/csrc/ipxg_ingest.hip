@@ -31,9 +31,6 @@
 
 namespace ipxg {
 
-#ifndef IPXG_BIN_K
-#define IPXG_BIN_K 8
-#endif
 #ifndef IPXG_BIN_WAVES
 #define IPXG_BIN_WAVES 3  // = the LDS limit (3 workgroups of 51 KiB per CU): up to 168 VGPRs
 #endif
@@ -50,7 +47,8 @@ namespace ipxg {
 #define PROBE_ADD(k, a, b)
 #endif
 constexpr int BIN_K = IPXG_BIN_K;                 // packets per lane per tile
-constexpr uint32_t BIN_TILE = BIN_K * IPXG_BLOCK;  // 2048 packets
+constexpr uint32_t BIN_TILE = BIN_TILE_PKTS;       // 2048 packets
+static_assert(BIN_TILE == BIN_K * IPXG_BLOCK, "k_bin tile = one packet per lane per step");
 constexpr uint32_t NO_REC = 0xFFFFFFFFu;
 constexpr uint32_t RED_U = IPXG_RED_U;            // records in flight per thread
 constexpr uint32_t RED_MAX_PROBE = 256;

@@ -129,10 +129,20 @@ struct BinView {
     uint32_t slow_stride;  // k_bin workgroup b lists its slow packets at slow_list[b * slow_stride ...]
     uint32_t* slow_cnt;    // bin_grid: slow packets listed by each k_bin workgroup
 };
-constexpr uint32_t BIN_MAX_PART_BITS = 11;  // <= 2048 partitions (LDS histograms of k_bin)
+#ifndef IPXG_BIN_K
+#define IPXG_BIN_K 8  // packets per lane per k_bin tile
+#endif
+constexpr uint32_t BIN_TILE_PKTS = IPXG_BIN_K * 256u;  // packets per k_bin tile (256-lane workgroups)
+#ifndef IPXG_BIN_MAX_PART_BITS
+#define IPXG_BIN_MAX_PART_BITS 11
+#endif
+constexpr uint32_t BIN_MAX_PART_BITS = IPXG_BIN_MAX_PART_BITS;  // <= 2048 partitions (LDS histograms of k_bin)
 constexpr uint32_t BIN_MAX_GRID = 2048;     // k_bin workgroups (persistent over the tiles)
 constexpr uint32_t RED_THREADS = 1024;      // k_reduce workgroup
-constexpr uint32_t RED_ENTRIES = 2048;      // k_reduce LDS flow table (56 B entries)
+#ifndef IPXG_RED_ENTRIES
+#define IPXG_RED_ENTRIES 2048
+#endif
+constexpr uint32_t RED_ENTRIES = IPXG_RED_ENTRIES;  // k_reduce LDS flow table (56 B entries)
 constexpr uint32_t RED_TARGET_FLOWS = 600;  // flows per partition the host sizes for
 
 struct ComplexView {
