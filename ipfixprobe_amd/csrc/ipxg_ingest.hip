@@ -77,18 +77,26 @@ struct Head48 {  // bytes 0..47 of a frame
 
 __device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
+// Cache policy of the frame and descriptor loads: non-temporal (aux bit 1, `nt`).  Every
+// frame and descriptor is read exactly once, so streaming them keeps L2 and the Infinity
+// Cache for the 160 MB of partition records that k_reduce reads back right after: measured
+// A/B on one box, k_bin -3 % and k_reduce -12 % against default-policy loads (sc0 alone:
+// no change; sc0|nt: as nt).
+#ifndef IPXG_LOAD_AUX
+#define IPXG_LOAD_AUX 2
+#endif
 __device__ __forceinline__ Head48 load_head(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok) {
     const uint32_t o = ok ? d.offset : BUF_OOB;
     Head48 h;
-    h.c0 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o, 0, 0));
-    h.c1 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 16, 0, 0));
-    h.c2 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 32, 0, 0));
+    h.c0 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o, 0, IPXG_LOAD_AUX));
+    h.c1 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 16, 0, IPXG_LOAD_AUX));
+    h.c2 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 32, 0, IPXG_LOAD_AUX));
     return h;
 }
 
 // descriptor i (zeros past the batch's end)
 __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, uint32_t i) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, 0);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, IPXG_LOAD_AUX);
     ipxg_pkt_desc d;
     d.offset = v.x;
     d.caplen = (uint16_t)v.y;
