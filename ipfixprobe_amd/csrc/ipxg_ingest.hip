@@ -640,7 +640,12 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
             sc[u] = si < nseg ? ne[si] : 0;
             sl[u] = si < nseg ? pre[sc[u] + 1] - pre[sc[u]] : 0;
             const bool ok = lane < sl[u];
+#ifdef IPXG_RED_NT  // tuning knob: streaming loads of the records (read once)
+            r[u] = u4(__builtin_nontemporal_load(
+                reinterpret_cast<const u32x4*>(&segs[(size_t)sc[u] * bv.seg_cap + (ok ? lane : 0)])));
+#else
             r[u] = segs[(size_t)sc[u] * bv.seg_cap + (ok ? lane : 0)];  // unconditional load
+#endif
             if (!ok) r[u].z = NO_REC;
         }
 #pragma unroll
