@@ -1,27 +1,39 @@
 """bench.py -- device-resident packet->biflow throughput on MI355X.
 
-Workload (BASELINE.json configs[1]): per GPU, 10M synthetic 64 B Ethernet/IPv4/UDP frames
-(tot_len 50) over 100k distinct biflows (src 10/8, dst 192.168/16, sport 1024-65535, dport
-1-1023; each packet picks a direction at random), timestamps 1 us apart (10 s span, so no
-inactive/active timeout fires).  A step is one pass of the hot path over that batch with
-the frames already in HBM: ipxg_submit (parse + 2x XXH64 + biflow-table update) followed by
-ipxg_finish (every flow exported FORCED into the device export buffer).  With N GPUs each
-rank owns a disjoint range of the canonical flow hash (the NIC-RSS analogue),
-so there is no collective in the data path; at N > 1 the per-GPU export buffers are gathered
-to rank 0 over RCCL inside the step (the path's only exchange).
+Workloads (BASELINE.json configs; `--workload`):
+  udp64  configs[1] (default, the metric's config): per GPU, 10M synthetic 64 B
+         Ethernet/IPv4/UDP frames (tot_len 50) over 100k distinct biflows (src 10/8, dst
+         192.168/16, sport 1024-65535, dport 1-1023; each packet picks a direction at random).
+         `--mode cold` (default): a step = ipxg_submit + ipxg_finish of the batch (every flow
+         exported FORCED), timestamps 1 us apart.  `--mode stream`: a step = one batch of a
+         continuing stream (timestamps 100 ns apart, batch k starts where k-1 ended), flows
+         carried across batches, plus ipxg_expire(now) on the virtual clock -- the steady state.
+  imix   configs[2]: IMIX 64/594/1518 B (7:4:1), Zipf(1.1) popularity over 1M flows, TCP (most
+         with timestamp options) / UDP, TLS/HTTP/DNS payload prefixes, some IPv6 and 802.1Q
+         (tools/synth); a step = 100M packets as 10 batches of 10M submitted back to back
+         (flows carried across batches) + finish.  The TLS/HTTP/DNS process plugins run on the
+         host above the C-ABI and are not part of this device measurement.
+  quic   configs[4]: QUIC-heavy variable-length mix over 1M flows (60 % UDP/443 QUIC, 40 %
+         802.1Q/QinQ/MPLS/IPv6-ext/PPPoE/GRE encapsulations; tools/synth); a step = 4 batches of
+         5M + finish.
+With N GPUs each rank owns a disjoint range of the canonical flow hash (the NIC-RSS analogue,
+SURVEY 8(e)): every rank generates packets of its own flows only, so the data path has no
+collective; at N > 1 the per-GPU export buffers are gathered to rank 0 over RCCL inside the step
+(the path's only exchange).
 
-Prints one JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch of the
-dominant kernel k_bin (64 B frame + 16 B descriptor per packet) / its average
-duration, timed with HIP events on the engine's stream; roofline.stage gives the same bytes
-over the whole ingest (k_bin + k_bin_slow + k_reduce + k_fin_list).  roofline.traffic is the HBM bytes per k_bin launch
-from the newest committed rocprofv3 PMC summary (profiles/*/pmc_summary.json, collected by
-tools/gpu_pmc.sh), or null when none covers k_bin.
+Prints one JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch of the dominant
+ingest kernel (min(caplen, 128) + 16 B descriptor per packet, 80 B for 64 B frames)
+/ its average duration from HIP events on the engine's stream; roofline.step = the same bytes
+over the whole step (every kernel, the host round trips, the finish).  roofline.traffic is the
+HBM bytes per launch of that kernel from the newest committed rocprofv3 PMC summary
+(profiles/*/pmc_summary*.json for this workload, collected by tools/gpu_pmc.sh), or null.
 """
 import argparse
 import glob
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -32,12 +44,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpkts/s device-resident, 64B synthetic mix, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-ALG_BYTES_PER_PKT = 80  # 64 B frame + 16 B descriptor
+DESC_NP = np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"), ("ts_sec", "<u4"), ("ts_usec", "<u4")])
 
 
 def gen_flows(F, rank, world, seed, device_id=0):
-    """F distinct biflows whose canonical hash falls in this rank's range (hashed on this
-    rank's GPU)."""
+    """F distinct 64 B-UDP biflows whose canonical hash falls in this rank's range (hashed on
+    this rank's GPU)."""
     from ipfixprobe_amd import Engine, shard
     rng = np.random.default_rng(seed)
     out = {k: [] for k in ("sip", "dip", "sport", "dport")}
@@ -78,8 +90,9 @@ def gen_flows(F, rank, world, seed, device_id=0):
     return {k: np.array(v, dtype=np.int64) for k, v in out.items()}
 
 
-def build_batch(flows, P, seed, device):
-    """64 B frames (P, 64) uint8 and descriptors (P, 16) uint8, generated on the GPU."""
+def build_batch(flows, P, seed, device, dt_ns=1000, t0_pkt=0):
+    """64 B frames (P, 64) uint8 and descriptors (P, 16) uint8, generated on the GPU; packet i
+    is stamped 1_700_000_000 s + (t0_pkt + i) * dt_ns."""
     import torch
     F = len(flows["sip"])
     g = torch.Generator(device=device)
@@ -116,13 +129,20 @@ def build_batch(flows, P, seed, device):
     put(34, sp, 2)
     put(36, dp, 2)
     fr[:, 39] = 30  # UDP length
+    return fr.reshape(-1).contiguous(), stamp_desc(P, device, dt_ns, t0_pkt)
+
+
+def stamp_desc(P, device, dt_ns, t0_pkt):
+    """Descriptors of P consecutive 64 B frames, packet i at 1_700_000_000 s + (t0_pkt + i) * dt_ns."""
+    import torch
     i = torch.arange(P, device=device, dtype=torch.int64)
+    us = (t0_pkt + i) * dt_ns // 1000
     desc = torch.zeros((P, 4), dtype=torch.int32, device=device)
     desc[:, 0] = (i * 64).to(torch.int32)
     desc[:, 1] = 64 | (64 << 16)
-    desc[:, 2] = (1_700_000_000 + i // 1_000_000).to(torch.int32)
-    desc[:, 3] = (i % 1_000_000).to(torch.int32)
-    return fr.reshape(-1).contiguous(), desc.reshape(-1).view(torch.uint8).contiguous()
+    desc[:, 2] = (1_700_000_000 + us // 1_000_000).to(torch.int32)
+    desc[:, 3] = (us % 1_000_000).to(torch.int32)
+    return desc.reshape(-1).view(torch.uint8).contiguous()
 
 
 class _DevArray:
@@ -134,76 +154,95 @@ class _DevArray:
 
 
 def gather_exports(eng, rank, world, device):
-    """RCCL gather of every rank's device export buffer into rank 0 (ipfixprobe_amd.shard)."""
+    """RCCL gather of every rank's device export buffer into rank 0 (ipfixprobe_amd.shard).
+    Ordering: the engine's stream is idle here (ipxg_device_exports completes the batch); the
+    engine's stream waits for the gather before its next kernels can overwrite the buffer."""
     import torch
     from ipfixprobe_amd.shard import gather_records
     ptr, n = eng.device_exports()
     buf = torch.as_tensor(_DevArray(ptr, max(n, 1) * 128), device=device)
     out = gather_records(buf, n, rank, world, device)
+    torch.cuda.ExternalStream(eng.stream(), device=device).wait_stream(torch.cuda.current_stream(device))
     return 0 if out is None else out.numel() // 128
 
 
-def cpu_baseline(frames, desc, flows_per_shard, threads=16, reps=3):
-    """The oracle (CPU restatement of the reference path) on the same packets, one pipeline
-    per core as the reference scales (one input thread + private NHTFlowCache per RSS queue,
-    ipfixprobe.cpp:381-464): packets are dealt to `threads` shards by a symmetric hash of the
-    IP pair (the NIC's symmetric RSS on IPs, dpdkDevice.cpp:230-262 -- not timed), each shard
-    runs parse_packet + put_pkt + finish in its own thread (ctypes drops the GIL)."""
-    import threading
+# ---- CPU baseline (BASELINE.md 2) ---------------------------------------------------------------
+def host_cores():
+    """nproc (honours the box's CPU share: OMP_NUM_THREADS / cgroup), the CPUs to pin to, the model."""
+    try:
+        n = int(subprocess.run(["nproc"], stdout=subprocess.PIPE, text=True, check=True).stdout.strip())
+    except (OSError, ValueError, subprocess.CalledProcessError):
+        n = os.cpu_count() or 1
+    cpus = sorted(os.sched_getaffinity(0))[:n]
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, cpus, model
+
+
+def cpu_baseline(arena_np, desc_np, canon_lo, flows, reps=3, label=""):
+    """The oracle (oracle/ipxg_oracle.c, the reference path restated in C, gcc -O3) on the same
+    packets, driven by oracle/cpu_baseline.c: one pinned pipeline thread per host core, each
+    with its own cache over its shard of the packets -- the reference's scaling (one input
+    thread + private NHTFlowCache per RSS queue, ipfixprobe.cpp:381-464); shards by the
+    direction-symmetric canonical flow hash (the NIC's symmetric RSS, dpdkDevice.cpp:230-262;
+    not timed).  Also one thread over the whole sample.  Median of `reps` each."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py
-    arena = frames.cpu().numpy()
-    d = desc.cpu().numpy().view(np.uint8).view(
-        np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"),
-                  ("ts_sec", "<u4"), ("ts_usec", "<u4")]))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    fr = arena.reshape(-1, 64)
-    ip = lambda c: fr[:, c:c + 4].view(">u4").reshape(-1).astype(np.uint64)  # noqa: E731
-    sym = (ip(26) ^ ip(30)) * np.uint64(0x9E3779B97F4A7C15)
-    shard = ((sym >> np.uint64(40)) % np.uint64(threads)).astype(np.int64)
-    parts = [np.ascontiguousarray(d[shard == k]) for k in range(threads)]
-    s_exp = min(30, int(math.ceil(math.log2(max(flows_per_shard // threads, 2)))) + 4)
-    caches = [oracle_py.OracleCache(cache_exp=s_exp) for _ in range(threads)]
-    counts = [0] * threads
-
-    def work(k):
-        for _ in range(reps):
-            caches[k].run(arena, parts[k], 1)
-            caches[k].finish()
-            counts[k] += len(caches[k].take())
-
-    ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
-    t0 = time.perf_counter()
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    dt = time.perf_counter() - t0
-    no_res = sum(c.stats()["end_no_res"] for c in caches)
-    for c in caches:
-        c.close()
-    pkts = len(d) * reps
-    return {"value": round(pkts / dt / 1e6, 3), "unit": "Mpkts/s", "cores": threads, "kind": "port",
-            "sample": "the bench batch (%d packets, %d flows) x%d passes through oracle/ipxg_oracle.c "
-                      "(parse_packet + NHTFlowCache::put_pkt + finish restated in C, gcc -O2), "
-                      "%d threads each owning a symmetric-IP-hash shard with its own cache (s=%d), "
-                      "%.2f s wall; %d records, NO_RES evictions %d"
-                      % (len(d), flows_per_shard, reps, threads, s_exp, dt, sum(counts), no_res)}
+    n, cpus, model = host_cores()
+    shard = ((canon_lo & np.uint64(0xFFFFFFFF)) * np.uint64(n) >> np.uint64(32)).astype(np.int64)
+    s_all = min(30, int(math.ceil(math.log2(max(flows // n, 2)))) + 4)
+    s_one = min(30, int(math.ceil(math.log2(max(flows, 2)))) + 4)
+    multi, single = [], []
+    nrec = no_res = 0
+    for _ in range(reps):
+        dt, nrec, no_res = oracle_py.bench_mt(arena_np, desc_np, shard, n, cpus, s_all)
+        multi.append(dt)
+    for _ in range(reps):
+        dt1, rec1, nr1 = oracle_py.bench_mt(arena_np, desc_np, np.zeros(len(desc_np), np.int64), 1, cpus[:1], s_one)
+        single.append(dt1)
+    pk = len(desc_np)
+    mt, st = float(np.median(multi)), float(np.median(single))
+    return {"value": round(pk / mt / 1e6, 3), "unit": "Mpkts/s", "cores": n, "nproc": n, "cpu_model": model,
+            "single_core": round(pk / st / 1e6, 3), "kind": "port",
+            "sample": "%s%d packets x %d runs (median): oracle/ipxg_oracle.c (parse_packet + NHTFlowCache::"
+                      "put_pkt + finish restated in C, gcc -O3) in oracle/cpu_baseline.c, %d pinned threads each "
+                      "over its canonical-hash shard with its own cache (s=%d), %.3f s; single core: one thread, "
+                      "s=%d, %.2f s; %d records, NO_RES %d"
+                      % (label, pk, reps, n, s_all, mt, s_one, st, nrec, no_res)}
 
 
-def pmc_traffic(kernel="k_bin"):
-    """HBM bytes per launch of `kernel` from the newest profiles/*/pmc_summary.json:
+def canon_of(eng, arena_np, desc_np):
+    """Canonical (direction-free) flow hash per packet from the device parser (RSS stand-in)."""
+    from ipfixprobe_amd import shard
+    out = np.zeros(len(desc_np), dtype=np.uint64)
+    step = 2_000_000
+    for s in range(0, len(desc_np), step):
+        p = eng.parse(arena_np, desc_np[s:s + step])
+        out[s:s + step] = shard.canonical(p["hash_fwd"], p["hash_inv"])
+    return out
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest profiles/*/pmc_summary[_<workload>].json:
     FETCH_SIZE (KiB; doubled -- gfx950 tallies wide streaming reads at half, MI355X_MICROARCH.md
     'HBM') + WRITE_SIZE (KiB), both per launch."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json"))):
+    name = "pmc_summary.json" if workload == "udp64" else "pmc_summary_%s.json" % workload
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name))):
         try:
             with open(p) as f:
                 js = json.load(f)
         except (OSError, ValueError):
             continue
-        for name, v in js.items():
-            if name.split("::")[-1].split("<")[0] == kernel and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        for kn, v in js.items():
+            if kn.split("::")[-1].split("<")[0] == kernel and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                 best = (p, (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0)
     return best
 
@@ -237,20 +276,142 @@ def end_to_end(eng, frames, desc, packets, reps=3):
                     "batches back to back (no copy/compute overlap)"}
 
 
+# ---- workloads -------------------------------------------------------------------------------------
+def torch_int32():
+    import torch
+    return torch.int32
+
+
+class Workload:
+    """Device-resident batches and how a step walks them."""
+
+    def __init__(self, name, batches, flows, per_step, finish, description):
+        self.name, self.batches, self.flows = name, batches, flows
+        self.per_step = per_step        # batches submitted per step
+        self.finish = finish            # ipxg_finish at the end of each step
+        self.description = description
+        self.alg = [self._alg(d) for _, d in batches]
+        self.packets = [d.numel() // 16 for _, d in batches]
+        self.last_sec = [int(d[-16:].view(torch_int32())[2].item()) for _, d in batches]  # virtual clock
+
+    @staticmethod
+    def _alg(desc):
+        import torch
+        cl = desc.view(-1, 16)[:, 4:6].contiguous().view(torch.int16).to(torch.int64) & 0xFFFF
+        return int(torch.clamp(cl, max=128).sum().item()) + 16 * desc.numel() // 16
+
+
+def make_workload(args, rank, world, device, local):
+    import torch
+    if args.workload == "udp64":
+        flows = gen_flows(args.flows, rank, world, args.seed, device_id=local)
+        if args.mode == "cold":
+            fr, de = build_batch(flows, args.packets, args.seed + rank, device)
+            desc = ("configs[1]: %d synthetic 64B Eth/IPv4/UDP packets over %d distinct biflows per GPU; step = "
+                    "parse + XXH64 + biflow-cache update + finish (all flows exported)" % (args.packets, args.flows))
+            return Workload("udp64", [(fr, de)], args.flows, 1, True, desc)
+        # stream: one frame arena, one descriptor array per step with advancing timestamps
+        fr, d0 = build_batch(flows, args.packets, args.seed + rank, device, dt_ns=100)
+        nb = args.warmup + args.steps + min(args.steps, 10) + 1
+        batches = [(fr, d0)] + [(fr, stamp_desc(args.packets, device, 100, k * args.packets)) for k in range(1, nb)]
+        desc = ("configs[1] streaming: %d synthetic 64B Eth/IPv4/UDP packets per step over %d distinct biflows per "
+                "GPU, 100 ns apart, flows carried across steps; step = parse + XXH64 + biflow-cache update of one "
+                "batch + ipxg_expire(now)" % (args.packets, args.flows))
+        return Workload("udp64-stream", batches, args.flows, 1, False, desc)
+    sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
+    import synthgen
+    zipf = args.zipf if args.zipf is not None else (1.1 if args.workload == "imix" else None)
+    mix = synthgen.Mix(args.workload, args.flows * world if world > 1 else args.flows, seed=args.seed, zipf=zipf)
+    if world > 1:  # this rank's flows only (flow-hash-range shards, the NIC-RSS analogue)
+        own = rank_flows(mix, rank, world, local)
+        mix.flows = mix.flows[own]
+        if mix.cdf is not None:
+            mix.cdf, mix.rank_flow = zipf_cdf(len(mix.flows), zipf), np.random.default_rng(args.seed).permutation(
+                len(mix.flows)).astype(np.uint32)
+    gen = synthgen.Generator(mix, device, seed=args.seed + 7919 * rank)
+    batches = [gen.batch(k * args.packets, args.packets) for k in range(args.batches)]
+    torch.cuda.synchronize()
+    desc = ("%s: %s mix, %d packets per GPU per step (%d batches of %d, flows carried across batches) over %d "
+            "flows%s; step = parse + XXH64 + biflow-cache update of every batch + finish"
+            % ({"imix": "configs[2]", "quic": "configs[4]"}[args.workload], args.workload,
+               args.packets * args.batches, args.batches, args.packets, len(mix.flows),
+               " (Zipf %.2f popularity)" % zipf if zipf else " (uniform popularity)"))
+    return Workload(args.workload, batches, len(mix.flows), args.batches, True, desc)
+
+
+def zipf_cdf(F, s):
+    w = np.arange(1, F + 1, dtype=np.float64) ** (-float(s))
+    c = np.cumsum(w)
+    c /= c[-1]
+    cdf = np.floor(c * 18446744073709549568.0).astype(np.uint64)
+    cdf[-1] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    return cdf
+
+
+def rank_flows(mix, rank, world, local):
+    """Indices of the mix's flows whose canonical hash this rank owns."""
+    from ipfixprobe_amd import Engine, shard
+    F = len(mix.flows)
+    owner = np.zeros(F, dtype=np.int64)
+    with Engine(device_id=local) as e:
+        for s in range(0, F, 1 << 20):
+            sub = mix.flows[s:s + (1 << 20)]
+            owner[s:s + len(sub)] = shard.owner(flow_canon(e, mix, sub), world)
+    return np.nonzero(owner == rank)[0]
+
+
+def flow_canon(e, mix, fl):
+    """Canonical hash of each flow of a synthetic mix from its packed keys (cache.hpp:29-46)."""
+    from ipfixprobe_amd import shard
+    lay = mix.layouts[fl["layout"].astype(np.int64)]
+    v6 = lay["addr_len"] == 16
+    proto = np.where(lay["tcp_flags_off"] > 0, 6, 17).astype(np.uint8)
+    out = np.zeros(len(fl), dtype=np.uint64)
+    for is6, klen in ((False, 16), (True, 40)):
+        sel = np.nonzero(v6 == is6)[0]
+        if not len(sel):
+            continue
+        al = 16 if is6 else 4
+        kf = np.zeros((len(sel), klen), dtype=np.uint8)
+        ki = np.zeros((len(sel), klen), dtype=np.uint8)
+        f = fl[sel]
+        vl = np.where(lay["vlan_off"][sel] > 0, f["vlan"], 0).astype(np.uint16)
+        for k, (a, b, pa, pb) in ((kf, (f["sip"], f["dip"], f["sport"], f["dport"])),
+                                  (ki, (f["dip"], f["sip"], f["dport"], f["sport"]))):
+            k[:, 0:2] = pa.astype("<u2").view(np.uint8).reshape(-1, 2)
+            k[:, 2:4] = pb.astype("<u2").view(np.uint8).reshape(-1, 2)
+            k[:, 4] = proto[sel]
+            k[:, 5] = 6 if is6 else 4
+            k[:, 6:6 + al] = a[:, :al]
+            k[:, 6 + al:6 + 2 * al] = b[:, :al]
+            k[:, 6 + 2 * al:8 + 2 * al] = vl.view(np.uint8).reshape(-1, 2)
+        out[sel] = shard.canonical(e.xxh64(kf.reshape(-1), klen), e.xxh64(ki.reshape(-1), klen))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--packets", type=int, default=10_000_000)
-    ap.add_argument("--flows", type=int, default=100_000)
+    ap.add_argument("--workload", default="udp64", choices=["udp64", "imix", "quic"])
+    ap.add_argument("--mode", default="cold", choices=["cold", "stream"], help="udp64 only")
+    ap.add_argument("--packets", type=int, default=None, help="packets per batch")
+    ap.add_argument("--batches", type=int, default=None, help="batches per step (imix / quic)")
+    ap.add_argument("--flows", type=int, default=None)
+    ap.add_argument("--zipf", type=float, default=None)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="check the records against the oracle")
+    ap.add_argument("--verify", action="store_true", help="check one step's records against the oracle")
     ap.add_argument("--ingest", default="binned", choices=["binned", "atomic"])
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host batch) rate")
     args = ap.parse_args()
+    dflt = {"udp64": (10_000_000, 1, 100_000, 20), "imix": (10_000_000, 10, 1_000_000, 5),
+            "quic": (5_000_000, 4, 1_000_000, 10)}[args.workload]
+    args.packets = args.packets or dflt[0]
+    args.batches = args.batches or dflt[1]
+    args.flows = args.flows or dflt[2]
+    args.steps = args.steps or dflt[3]
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,39 +425,41 @@ def main():
     torch.cuda.set_device(device)
 
     from ipfixprobe_amd import Engine
-    flows = gen_flows(args.flows, rank, world, args.seed, device_id=local)
-    frames, desc = build_batch(flows, args.packets, args.seed + rank, device)
+    wl = make_workload(args, rank, world, device, local)
     torch.cuda.synchronize()
-    eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(2 * args.flows)))), args.ingest),
+    eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest),
                  device_id=local)
+    cursor = [0]
+    gather_ms = [0.0]
 
     def step():
-        eng.submit(frames, desc, device=True, asynchronous=True)  # finish follows right behind
-        eng.finish()
+        if wl.finish:
+            for k in range(wl.per_step):
+                fr, de = wl.batches[k]
+                # back to back; finish right behind (the batches were synchronised after generation)
+                eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+            eng.finish()
+        else:
+            fr, de = wl.batches[cursor[0]]
+            cursor[0] += 1
+            eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+            eng.expire(wl.last_sec[cursor[0] - 1])  # the virtual clock: idle flows out (none idle here)
         if world > 1:
+            t0 = time.perf_counter()
             gather_exports(eng, rank, world, device)
+            gather_ms[0] += (time.perf_counter() - t0) * 1e3
         eng.clear_exports()
 
     for _ in range(args.warmup):
         step()
-    if args.verify and rank == 0:
-        eng.submit(frames, desc, device=True)
-        eng.finish()
-        got = eng.poll()
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import flowcmp
-        import oracle_py
-        d = desc.cpu().numpy().view(np.uint8).view(
-            np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"),
-                      ("ts_sec", "<u4"), ("ts_usec", "<u4")]))
-        want, _ = oracle_py.run_capture(frames.cpu().numpy(), d, 1, cache_exp=21)
-        diff = flowcmp.diff(got, want)
-        print("verify: %d records, %s" % (len(got), "bit-exact vs oracle" if not diff else diff),
-              file=sys.stderr)
-    # timed region: HIP events around the ingest kernel only (the roofline's launch time);
-    # every-stage events cost ~35 us of host time per step, so the stage breakdown comes
-    # from a separate pass below
-    eng.profile(2)
+    verify = None
+    if args.verify and rank == 0 and wl.finish:
+        verify = verify_step(eng, wl)
+    # timed region: HIP events around the ingest kernels only (k_bin, k_bin_slow); the
+    # every-stage events cost ~35 us of host time per step, so the stage breakdown comes from a
+    # separate pass below
+    eng.profile(3)
+    gather_ms[0] = 0.0
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -307,67 +470,103 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
-    tm_bin = eng.timing()
+    tm_in = eng.timing()
     st = eng.stats()
+    gms = gather_ms[0] / args.steps
     eng.profile(1)  # stage breakdown (untimed)
-    for _ in range(min(args.steps, 10)):
+    stage_steps = min(args.steps, 10)
+    for _ in range(stage_steps):
         step()
     tm = eng.timing()
-    stage_steps = min(args.steps, 10)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-    total_pkts = args.packets * args.steps * world
+    pk_step = sum(wl.packets[:wl.per_step]) if wl.finish else wl.packets[0]
+    alg_step = sum(wl.alg[:wl.per_step]) if wl.finish else wl.alg[0]
+    total_pkts = pk_step * args.steps * world
     value = total_pkts / dt / 1e6
-    bin_ms = tm_bin["ingest_ms"] / max(tm_bin["ingest_launches"], 1)
-    red_ms = (tm["ingest_slow_ms"] + tm["reduce_ms"] + tm["fin_ms"]) / max(tm["reduce_launches"], 1)
-    alg = ALG_BYTES_PER_PKT * args.packets
-    achieved = alg / (bin_ms / 1e3) / 1e9 if bin_ms > 0 else 0.0
-    stage = alg / ((bin_ms + red_ms) / 1e3) / 1e9 if bin_ms > 0 else 0.0
+    launches = max(tm_in["ingest_launches"], 1)
+    bin_ms = tm_in["ingest_ms"] / launches
+    slow_ms = tm_in["ingest_slow_ms"] / launches
+    alg_launch = alg_step / (wl.per_step if wl.finish else 1)
     kname = "k_bin" if args.ingest == "binned" else "k_ingest"
-    pmc = pmc_traffic(kname)
+    if args.ingest == "binned" and slow_ms > bin_ms:
+        kname, kms = "k_bin_slow", slow_ms
+    else:
+        kms = bin_ms
+    achieved = alg_launch / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+    ingest_gbs = alg_launch / ((bin_ms + slow_ms) / 1e3) / 1e9 if bin_ms > 0 else 0.0
+    step_ms = dt / args.steps * 1e3
+    step_gbs = alg_step * world / (step_ms / 1e3) / 1e9
+    pmc = pmc_traffic(kname, wl.name if wl.name != "udp64-stream" else "stream")
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = end_to_end(eng, frames, desc, args.packets)
+    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "udp64" and args.mode == "cold":
+        e2e = end_to_end(eng, wl.batches[0][0], wl.batches[0][1], wl.packets[0])
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        fr, de = wl.batches[0]
+        arena_np = fr.cpu().numpy()
+        desc_np = de.cpu().numpy().view(DESC_NP)
+        canon = canon_of(eng, arena_np, desc_np)
+        cpu = cpu_baseline(arena_np, desc_np, canon, wl.flows,
+                           label="the first batch of the workload, ")
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(frames, desc, args.flows, threads=args.cpu_threads)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpkts/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (generated on device, seed %d)" % args.seed,
-            "config": {"workload": "configs[1]: %d synthetic 64B Eth/IPv4/UDP packets over %d distinct "
-                                   "biflows per GPU; step = parse + XXH64 + biflow-cache update + "
-                                   "finish (all flows exported)" % (args.packets, args.flows),
-                       "packets_per_gpu": args.packets, "flows_per_gpu": args.flows,
-                       "ingest": args.ingest,
+            "config": {"workload": wl.description, "name": wl.name,
+                       "packets_per_gpu_per_step": pk_step, "flows_per_gpu": wl.flows,
+                       "batches_per_step": wl.per_step, "ingest": args.ingest,
                        "parallelism": "flow-hash-range shards x%d, RCCL gather of export buffers"
                                       % world if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(pmc[1]) if pmc else None,
                          "traffic_source": os.path.relpath(pmc[0], ROOT) if pmc else None,
-                         "algorithmic_bytes_per_launch": alg,
-                         "avg_launch_ms": round(bin_ms, 4),
-                         "stage": {"kernels": "k_bin+k_bin_slow+k_reduce+k_fin_list",
-                                   "achieved": round(stage, 1),
-                                   "frac": round(stage / HBM_PEAK_GBS, 4),
-                                   "avg_ms": round(bin_ms + red_ms, 4)}},
+                         "algorithmic_bytes_per_launch": alg_launch,
+                         "algorithmic_bytes_per_packet": round(alg_step / pk_step, 2),
+                         "avg_launch_ms": round(kms, 4),
+                         "ingest": {"kernels": "k_bin+k_bin_slow", "avg_ms": round(bin_ms + slow_ms, 4),
+                                    "achieved": round(ingest_gbs, 1), "frac": round(ingest_gbs / HBM_PEAK_GBS, 4)},
+                         "step": {"what": "algorithmic bytes of the step / the whole step (every kernel, host "
+                                          "round trips, finish)",
+                                  "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
+                         "step_frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(tm[k + "_ms"] / stage_steps, 4)
                                   for k in ("ingest", "ingest_slow", "reduce", "fin", "finalize", "slow",
                                             "finish")},
-            "flows_exported_per_step": int(st["end_forced"] // max(st["batches"], 1)),
+            "flows_exported_per_step": int(st["total_exported"] // max(st["batches"] // max(wl.per_step, 1), 1)),
+            "slow_path_packets_share": round(st["slow_path_packets"] / max(st["parsed_packets"], 1), 4),
             "e2e_pcie": e2e,
             "spilled_packets": int(st["spilled_packets"]),
+            "complex_flows": int(st["complex_flows"]),
+            "gather_ms_per_step": round(gms, 4) if world > 1 else None,
+            "verify": verify,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     eng.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def verify_step(eng, wl):
+    """One step of the workload against the oracle (the first batch only for multi-batch steps,
+    in its own engine state): bit-exact flow records or the first differences."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import flowcmp
+    import oracle_py
+    fr, de = wl.batches[0]
+    eng.submit(fr, de, device=True)
+    eng.finish()
+    got = eng.poll()
+    d = de.cpu().numpy().view(DESC_NP)
+    want, _ = oracle_py.run_capture(fr.cpu().numpy(), d, 1, cache_exp=min(30, int(math.ceil(math.log2(2 * wl.flows))) + 2))
+    diff = flowcmp.diff(got, want)
+    return "%d records, %s" % (len(got), "bit-exact vs oracle" if not diff else diff[:500])
 
 
 if __name__ == "__main__":

@@ -200,6 +200,7 @@ typedef struct ipxg_stats {
     uint64_t batches;
     uint64_t spilled_packets; /* packets that fell back from the binned ingest to direct
                                  device atomics (partition region or LDS table full)    */
+    uint64_t slow_path_packets; /* packets k_bin left to the general parser (k_bin_slow)  */
 } ipxg_stats;
 
 typedef struct ipxg_engine ipxg_engine;
@@ -260,7 +261,8 @@ typedef struct ipxg_timing {
  * library was built with -DIPXG_PROBE -- a tuning aid). */
 int ipxg_probe_counters(ipxg_engine* eng, uint64_t* out);
 /* Event timing: 1 = every stage, 2 = the ingest kernel only (two events per batch, the
- * least host overhead), 0 = off; enabling also zeroes the accumulators. */
+ * least host overhead), 3 = k_bin and k_bin_slow (three events), 0 = off; enabling also
+ * zeroes the accumulators. */
 int ipxg_profile(ipxg_engine* eng, int enable);
 int ipxg_get_timing(ipxg_engine* eng, ipxg_timing* out);
 

@@ -56,6 +56,7 @@ struct ipxg_engine {
     DevBuf arena, desc;
     // scratch
     DevBuf defer_a, defer_b, frag_list, frag_sorted, frag_ports, sort_tmp;
+    DevBuf adefer_a, adefer_b;           // deferred tile aggregates (3 x 16 B each)
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
     uint32_t bin_slots = 0;              // k_bin workgroups resident at once (its grid)
@@ -70,15 +71,17 @@ struct ipxg_engine {
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
+    double skew = 1.0;                   // previous batch: most loaded partition / mean partition
+    uint32_t part_bits_last = 0;         // partitions of the last binned batch (log2)
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
     // host-side counters
-    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0;
+    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0;
     bool prev_valid = false;
     uint32_t prev_sec = 0, prev_usec = 0;
     // stage timing
     bool prof = false;
-    int prof_level = 0;  // 1: every stage, 2: the ingest kernel only
+    int prof_level = 0;  // 1: every stage, 2: k_bin only, 3: k_bin and k_bin_slow
     hipEvent_t ev[11] = {};
     ipxg_timing tm = {};
 };
@@ -86,8 +89,10 @@ struct ipxg_engine {
 // events: 0 | k_bin | 1 | k_bin_slow | 2 | k_reduce | 3 | k_fin_list | 4;
 //         [5,6] slow paths, [7,8] k_finalize, [9,10] finish
 static void ev_rec(ipxg_engine* e, int i) {
-    // level 2: only the events around k_bin / k_ingest (0, 1): the others cost host time
-    if (e->prof && (e->prof_level == 1 || i <= 1)) (void)hipEventRecord(e->ev[i], e->st);
+    // level 2: only the events around k_bin / k_ingest (0, 1), level 3 also k_bin_slow (2):
+    // the others cost host time
+    if (e->prof && (e->prof_level == 1 || i <= 1 || (e->prof_level == 3 && i == 2)))
+        (void)hipEventRecord(e->ev[i], e->st);
 }
 static double ev_ms(ipxg_engine* e, int a) {
     float ms = 0.f;
@@ -128,8 +133,12 @@ static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_c
 // Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
 // (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
 // than the batch's packets.  k_bin runs bin_grid persistent workgroups over tiles of
-// BIN_TILE_PKTS packets; each owns one segment per partition, sized for 1.5x its mean share of records plus
-// 4 standard deviations (binomial) and a margin; what does not fit spills to atomics.
+// BIN_TILE_PKTS packets; each owns one segment per partition, sized for its mean share of the
+// packets times max(3, 1.25 x the previous batch's most loaded partition / mean), plus 4
+// standard deviations (binomial) and a margin; what does not fit spills to atomics.  Memory
+// is plentiful (288 GB of HBM) and only the slots written are read, so the margin is generous:
+// skewed traffic (tile aggregation leaves the configs[2] Zipf mix at ~2.4x) never spills after
+// its first batch.
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
     if (est == 0 || est > n) est = n;
@@ -147,7 +156,8 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->bin_slots);
     const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * BIN_TILE_PKTS, n);
     const double mean = (double)per_block / P;
-    const uint64_t seg = ((uint64_t)(mean * 1.5 + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
+    const double factor = std::max(3.0, 1.25 * e->skew);
+    const uint64_t seg = ((uint64_t)(mean * factor + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
     const uint32_t cols = 2 * grid;
     int rc;
     if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
@@ -165,6 +175,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     bv.cols = cols;
     bv.bin_grid = grid;
     bv.part_bits = bits;
+    e->part_bits_last = bits;
     return IPXG_OK;
 }
 
@@ -385,7 +396,8 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->frag_cnt);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->frag_list, &e->frag_sorted,
+    for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
+                      &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
                       &e->ipf_tot, &e->ipf_off})
@@ -441,6 +453,9 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     // per-batch scratch sized for the worst case (every packet deferred / a fragment)
     if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
     if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
+    // deferred aggregates: each covers >= TAGG_MIN (3) packets, 48 bytes
+    if ((rc = ensure(e, e->adefer_a, ((size_t)n / 3 + 1) * 48))) return rc;
+    if ((rc = ensure(e, e->adefer_b, ((size_t)n / 3 + 1) * 48))) return rc;
     if (e->cfg.frag_enable) {
         if ((rc = ensure(e, e->frag_list, (size_t)n * 8))) return rc;
         if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
@@ -461,11 +476,12 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         uint32_t* dl = (uint32_t*)e->defer_a.p;
         uint32_t* sl = (uint32_t*)e->slow_list.p;
         uint32_t* fl = (uint32_t*)e->fin_list.p;
-        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, e->stats_d);
+        uint4* al = (uint4*)e->adefer_a.p;
+        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 1);
-        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, e->stats_d);
+        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 2);
-        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl);
+        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
         ev_rec(e, 3);
         launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n);
         ev_rec(e, 4);
@@ -496,6 +512,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
+        if (binned && e->prof_level == 3) e->tm.ingest_slow_ms += ev_ms(e, 1);
         if (binned && e->prof_level == 1) {
             e->tm.ingest_slow_ms += ev_ms(e, 1);
             e->tm.reduce_ms += ev_ms(e, 2);
@@ -506,7 +523,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     bool slow = false;
 
     // fragmentation cache: order fragments by (bucket, arrival) and replay the rings
-    uint32_t ndef = c1.deferred;
+    uint32_t ndef = c1.deferred, nadef = c1.agg_deferred;
     if (c1.frag_count) {
         if (!slow) ev_rec(e, 5);
         slow = true;
@@ -524,19 +541,27 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         ndef = e->ctl_h->deferred;
+        nadef = e->ctl_h->agg_deferred;
     }
-    // table overflow: grow and re-apply the deferred packets
-    while (ndef) {
+    // table overflow: grow and re-apply the deferred packets and tile aggregates
+    while (ndef || nadef) {
         if (!slow) ev_rec(e, 5);
         slow = true;
         if ((rc = rehash(e, e->cap * 2))) return rc;
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->deferred, 0, sizeof(uint32_t), e->st));
-        launch_deferred(e->st, bv, p, table_view(e), frag_view(e), (const uint32_t*)e->defer_a.p, ndef,
-                        e->ctl_d, (uint32_t*)e->defer_b.p);
+        HIPCHK(e, hipMemsetAsync(&e->ctl_d->agg_deferred, 0, sizeof(uint32_t), e->st));
+        if (ndef)
+            launch_deferred(e->st, bv, p, table_view(e), frag_view(e), (const uint32_t*)e->defer_a.p, ndef,
+                            e->ctl_d, (uint32_t*)e->defer_b.p);
+        if (nadef)
+            launch_deferred_agg(e->st, table_view(e), (const uint4*)e->adefer_a.p, nadef, e->ctl_d,
+                                (uint4*)e->adefer_b.p);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         ndef = e->ctl_h->deferred;
+        nadef = e->ctl_h->agg_deferred;
         std::swap(e->defer_a, e->defer_b);
+        std::swap(e->adefer_a, e->adefer_b);
     }
     if (slow) {
         ev_rec(e, 6);
@@ -548,7 +573,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     }
     // slots k_reduce could not finalise (fragments, deferrals, spills, multi-workgroup
     // partitions; every slot in the atomic ingest mode): the full-table scan
-    const bool scan = !binned || c1.pending || c1.frag_count || c1.deferred;
+    const bool scan = !binned || c1.pending || c1.frag_count || c1.deferred || c1.agg_deferred;
     if (scan) {
         p.force_complex = p.force_complex || c1.nonmono;
         ev_rec(e, 7);
@@ -607,7 +632,12 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     }
     e->live += c2.cx_new_live;
     e->last_touched = c2.touched;
+    if (binned && c2.total_slots) {  // the next batch's segment sizing
+        const uint32_t P = 1u << e->part_bits_last;
+        e->skew = (double)c2.max_part * P / c2.total_slots;
+    }
     e->spilled += c2.spilled;
+    e->slow_pkts += c2.slow_count;
     e->prev_valid = true;
     e->prev_sec = c2.last_sec;
     e->prev_usec = c2.last_usec;
@@ -869,6 +899,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->table_rehashes = e->rehashes;
     out->batches = e->batches;
     out->spilled_packets = e->spilled;
+    out->slow_path_packets = e->slow_pkts;
     return IPXG_OK;
 }
 
@@ -892,7 +923,7 @@ int ipxg_profile(ipxg_engine* e, int enable) {
     if (enable && !e->ev[0])
         for (hipEvent_t& ev : e->ev) HIPCHK(e, hipEventCreate(&ev));
     e->prof = enable != 0;
-    e->prof_level = enable == 2 ? 2 : (enable ? 1 : 0);
+    e->prof_level = (enable == 2 || enable == 3) ? enable : (enable ? 1 : 0);
     if (enable) e->tm = ipxg_timing{};
     return IPXG_OK;
 }

@@ -32,7 +32,7 @@
 namespace ipxg {
 
 #ifndef IPXG_BIN_WAVES
-#define IPXG_BIN_WAVES 3  // = the LDS limit (3 workgroups of 51 KiB per CU): up to 168 VGPRs
+#define IPXG_BIN_WAVES 2  // = the LDS limit (2 workgroups of 76 KiB per CU)
 #endif
 #ifndef IPXG_RED_U
 #define IPXG_RED_U 4
@@ -59,6 +59,40 @@ __device__ __forceinline__ void defer_packet(BatchCtl* ctl, uint32_t* list, uint
     list[pos] = idx;
     if (from_bin) atomicAdd(&ctl->a_deferred, 1u);
 }
+
+// ---- per-tile flow aggregation (LDS) --------------------------------------------------------
+// Skewed traffic (Zipf popularity: the top flow of the configs[2] mix carries 12 % of all
+// packets) would put most of a tile's records into one partition: its segments overflow and
+// the overflow lands on one table slot with device atomics, and k_reduce's workgroup for that
+// partition serialises on one LDS entry.  So every tile first counts its packets per flow in an
+// LDS hash (keys in the stage area, which is free until the records are staged), and a flow
+// with >= TAGG_MIN packets in the tile is folded into an LDS aggregate and emitted as one
+// 3-slot aggregate record (ipxg_table.hpp) in place of its packet records: in the configs[2]
+// mix a tile then emits ~1200 slots instead of 2048, and the most loaded partition carries
+// 2.4x the mean instead of 32x.  With uniform traffic nearly every flow has one packet per
+// tile and the records are exactly the packet records as before.
+constexpr uint32_t TAGG_HASH = 4096;  // tile hash entries (2 per packet of the tile)
+constexpr uint32_t TAGG_CAP = 128;    // aggregates per tile (a flow past the cap stays packets)
+
+struct TileAgg {  // 64 B, LDS
+    unsigned long long key;
+    unsigned long long acc[2];
+    uint32_t first_n, last1, tbits, tflags;
+    uint32_t syn1[2], fin_n[2];
+    uint32_t part, rank;
+};
+
+// The LDS arrays of a k_bin / k_bin_slow workgroup that the tile phases share.
+struct BinLds {
+    uint32_t* hist;     // per partition: rank counter, then the run start in the tile
+    uint32_t* fill;     // per partition: slots in the workgroup's segment so far
+    uint4* stage;       // BIN_TILE slots: the tile hash's keys, then the staged records
+    uint32_t* cnt;      // TAGG_HASH: packets per tile-hash entry | (aggregate + 1) << 16
+    TileAgg* agg;       // TAGG_CAP
+    uint16_t* part_of;  // BIN_TILE: the partition of each staged slot
+    uint32_t* scan_s;
+    uint32_t* nagg;
+};
 
 // ---- phase A ------------------------------------------------------------------------------
 // k_bin's loads are buffer loads through two wave-uniform resource descriptors (the
@@ -109,25 +143,28 @@ __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, 
 // the target of stores that carry no record (tile_emit; k_bin's prologue)
 __device__ uint4 g_dummy_rec[32 * 64];
 
-// After every lane ranked its records of the tile in hist[part]: each partition's records
-// of the tile follow the ones of the block's earlier tiles in the block's own segment of
-// that partition (fill[part] = records so far), so no workgroup shares a write position
-// with another and no device atomic is needed (a shared counter per partition, hit once
-// per tile by every workgroup, saturated at the memory-side atomic rate).  The records are
+// After tile_aggregate ranked the tile's packet records and aggregates in hist[part]: each
+// partition's slots of the tile follow the ones of the block's earlier tiles in the block's own
+// segment of that partition (fill[part] = slots so far), so no workgroup shares a write
+// position with another and no device atomic is needed (a shared counter per partition, hit
+// once per tile by every workgroup, saturated at the memory-side atomic rate).  The slots are
 // first grouped by partition in LDS (stage) and then written with consecutive lanes on
-// consecutive records of a run: written straight from the lanes, 64 lanes stored to 64
-// different lines per instruction and the stores cost a third of k_bin's time.
-// A full segment spills to direct accumulation.
+// consecutive slots of a run: written straight from the lanes, 64 lanes stored to 64 different
+// lines per instruction and the stores cost a third of k_bin's time.
+// A full segment spills to direct accumulation (an aggregate spills whole: its slots that
+// would fit become NO_REC fillers, so k_reduce never reads half an aggregate).
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
 template <bool LISTED>
-__device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4* stage, uint32_t* scan_s, uint32_t P,
-                                          uint32_t pmask, const BinView& bv, uint32_t col, const TableView& t,
-                                          BatchCtl* ctl, uint32_t* deferred_list, const uint32_t (&r0)[BIN_K],
-                                          const uint32_t (&r1)[BIN_K], const uint32_t (&r2)[BIN_K],
-                                          const uint32_t (&rk)[BIN_K], const uint32_t (&ix)[BIN_K], uint32_t tile,
-                                          uint32_t& spilled) {
+__device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t pmask, const BinView& bv, uint32_t col,
+                                          const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
+                                          uint4* agg_list, const uint32_t (&r0)[BIN_K], const uint32_t (&r1)[BIN_K],
+                                          const uint32_t (&r2)[BIN_K], const uint32_t (&rk)[BIN_K],
+                                          const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& spilled) {
     constexpr uint32_t PT = (1u << BIN_MAX_PART_BITS) / IPXG_BLOCK;  // partitions per thread
+    uint32_t* const hist = L.hist;
+    uint32_t* const fill = L.fill;
+    uint4* const stage = L.stage;
     __syncthreads();
     // tile-local exclusive prefix over the partitions: hist[q] <- start of q's run in stage
     const uint32_t q0 = threadIdx.x * PT;
@@ -138,7 +175,7 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4*
         sum += cnt[k];
     }
     uint32_t total;
-    uint32_t run = block_exclusive_scan<IPXG_BLOCK>(sum, scan_s, &total);
+    uint32_t run = block_exclusive_scan<IPXG_BLOCK>(sum, L.scan_s, &total);
 #pragma unroll
     for (uint32_t k = 0; k < PT; ++k) {
         if (q0 + k < P) hist[q0 + k] = run;
@@ -149,26 +186,53 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4*
     for (int q = 0; q < BIN_K; ++q) {
         if (rk[q] == NO_REC) continue;
         const uint32_t idx = LISTED ? ix[q] : tile + (uint32_t)q * IPXG_BLOCK + threadIdx.x;
-        stage[hist[r1[q] & pmask] + rk[q]] = make_uint4(r0[q], r1[q], idx, r2[q]);
+        const uint32_t part = r1[q] & pmask;
+        const uint32_t k = hist[part] + rk[q];
+        stage[k] = make_uint4(r0[q], r1[q], idx, r2[q]);
+        L.part_of[k] = (uint16_t)part;
+    }
+    const uint32_t na = min(*L.nagg, TAGG_CAP);
+    for (uint32_t a = threadIdx.x; a < na; a += IPXG_BLOCK) {
+        const TileAgg& g = L.agg[a];
+        FlowAgg f;
+        f.key = g.key;
+        f.acc[0] = g.acc[0];
+        f.acc[1] = g.acc[1];
+        f.first_n = g.first_n;
+        f.last1 = g.last1;
+        f.tbits = g.tbits;
+        f.tflags = g.tflags;
+        f.syn1[0] = g.syn1[0];
+        f.syn1[1] = g.syn1[1];
+        f.fin_n[0] = g.fin_n[0];
+        f.fin_n[1] = g.fin_n[1];
+        const uint32_t k = hist[g.part] + g.rank;
+        agg_encode(f, stage[k], stage[k + 1], stage[k + 2]);
+        L.part_of[k] = L.part_of[k + 1] = L.part_of[k + 2] = (uint16_t)g.part;
     }
     __syncthreads();
-    // Fixed trip count and one store per iteration, always issued (a record that does not go
-    // to a segment is stored to a dummy line instead): on gfx950 stores count in vmcnt, and
-    // with a variable number of them the compiler's waits for the next tile's prefetched
-    // loads had to assume none were issued -- every later wait then also waited for the
-    // stores.  (A loop here made it drain every load in flight before it.)
+    // Fixed trip count and one store per iteration, always issued (a slot that does not go to
+    // a segment is stored to a dummy line instead): on gfx950 stores count in vmcnt, and with a
+    // variable number of them the compiler's waits for the next tile's prefetched loads had to
+    // assume none were issued -- every later wait then also waited for the stores.  (A loop
+    // here made it drain every load in flight before it.)
 #pragma unroll
     for (uint32_t kk = 0; kk < BIN_TILE / IPXG_BLOCK; ++kk) {
         const uint32_t k = kk * IPXG_BLOCK + threadIdx.x;
         const bool valid = k < total;
-        const uint4 r = stage[valid ? k : 0];
-        const uint32_t part = r.y & pmask;
+        uint4 r = stage[valid ? k : 0];
+        const uint32_t part = L.part_of[valid ? k : 0];
         const uint32_t pos = fill[part] + (k - hist[part]);
-        const bool seg = valid && pos < bv.seg_cap;
+        const bool agg = rec_is_agg(r);
+        const uint32_t ai = agg ? rec_agg_slot(r) : 0;
+        const bool fits = valid && (pos - ai + (agg ? 3 : 1) <= bv.seg_cap);
+        const bool filler = valid && !fits && pos < bv.seg_cap;  // part of an aggregate that spills
+        if (filler) r = make_uint4(0, 0, NO_REC, 0);
 #ifdef IPXG_EXP_NOEMIT  // timing experiment: records dropped
         uint4* dst = &g_dummy_rec[threadIdx.x & 63];
 #else
-        uint4* dst = seg ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos] : &g_dummy_rec[threadIdx.x & 63];
+        uint4* dst = (fits || filler) ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos]
+                                      : &g_dummy_rec[threadIdx.x & 63];
 #endif
 #ifdef IPXG_NT_REC_STORE  // tuning knob: streaming (non-temporal) record stores
         __builtin_nontemporal_store(r.x, &dst->x);
@@ -178,10 +242,18 @@ __device__ __forceinline__ void tile_emit(uint32_t* hist, uint32_t* fill, uint4*
 #else
         *dst = r;
 #endif
-        if (valid && !seg) {  // segment full: accumulate straight into the table
+        if (valid && !fits && ai == 0) {  // segment full: accumulate straight into the table
             spilled++;
-            if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
-                defer_packet(ctl, deferred_list, r.z, true);
+            if (!agg) {
+                if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
+                    defer_packet(ctl, deferred_list, r.z, true);
+            } else {
+                const uint4 s0 = stage[k], s1 = stage[k + 1], s2 = stage[k + 2];
+                if (!merge_agg_probe(t, agg_decode(s0, s1, s2), &ctl->new_keys)) {
+                    defer_agg(&ctl->agg_deferred, agg_list, s0, s1, s2);
+                    atomicAdd(&ctl->a_deferred, 1u);
+                }
+            }
         }
     }
     __syncthreads();  // hist is reset by the next tile
@@ -199,12 +271,12 @@ __device__ __forceinline__ void seg_counts(const uint32_t* fill, uint32_t P, con
 #endif
 }
 
-// rank one keyed, unfragmented packet in its partition and keep its record in slot j
+// keep one keyed, unfragmented packet's record in slot j (ranked in tile_aggregate)
 template <bool LISTED>
-__device__ __forceinline__ void tile_rank(uint32_t* hist, uint32_t pmask, const Params& p, const BatchView& b,
-                                          const DevPkt& pk, const ipxg_pkt_desc& d, uint32_t i, int j,
-                                          uint32_t (&r0)[BIN_K], uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K],
-                                          uint32_t (&rk)[BIN_K], uint32_t (&ix)[BIN_K]) {
+__device__ __forceinline__ void tile_rank(const Params& p, const BatchView& b, const DevPkt& pk,
+                                          const ipxg_pkt_desc& d, uint32_t i, int j, uint32_t (&r0)[BIN_K],
+                                          uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
+                                          uint32_t (&ix)[BIN_K]) {
     uint64_t lo, hf;
     uint32_t cdir;
 #ifdef IPXG_EXP_NOHASH  // timing experiment only: one cheap mixer instead of 2x XXH64
@@ -216,17 +288,96 @@ __device__ __forceinline__ void tile_rank(uint32_t* hist, uint32_t pmask, const 
     canon(pk, p, lo, cdir, hf);
 #endif
     const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
-    const uint32_t rank = atomicAdd(&hist[(uint32_t)(lo >> 32) & pmask], 1u);
 #pragma unroll
     for (int q = 0; q < BIN_K; ++q) {  // registers indexed by compile-time q only
         if (q == j) {
             r0[q] = (uint32_t)lo;
             r1[q] = (uint32_t)(lo >> 32);
             r2[q] = m;
-            rk[q] = rank;
+            rk[q] = 0;
             if (LISTED) ix[q] = i;
         }
     }
+}
+
+// After the tile's packet loop (rk[q] != NO_REC: record q of this lane holds a packet):
+// count the packets per flow in the LDS hash, fold the flows with >= TAGG_MIN packets into
+// LDS aggregates, and rank the remaining packet records (rk[q] <- rank in its partition) and
+// the aggregates (3 slots each) in the tile's partition histogram.
+template <bool LISTED>
+__device__ __forceinline__ void tile_aggregate(const BinLds& L, uint32_t pmask, uint32_t (&r0)[BIN_K],
+                                               uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
+                                               const uint32_t (&ix)[BIN_K], uint32_t tile) {
+    const uint32_t tid = threadIdx.x;
+    unsigned long long* hk = reinterpret_cast<unsigned long long*>(L.stage);
+    static_assert(TAGG_HASH * 8 <= BIN_TILE * 16, "tile hash keys live in the stage area");
+    __syncthreads();  // the stage area is free (the previous tile's emit, k_bin_slow's headers)
+    for (uint32_t k = tid; k < TAGG_HASH; k += IPXG_BLOCK) {
+        hk[k] = 0ull;
+        L.cnt[k] = 0;
+    }
+    if (tid == 0) *L.nagg = 0;
+    __syncthreads();
+    uint32_t ent[BIN_K], lead = 0;
+#pragma unroll
+    for (int q = 0; q < BIN_K; ++q) {
+        ent[q] = 0;
+        if (rk[q] == NO_REC) continue;
+        const unsigned long long lo = ((unsigned long long)r1[q] << 32) | r0[q];
+        uint32_t e = r0[q] & (TAGG_HASH - 1);
+        while (true) {  // <= 2048 keys in 4096 entries: terminates
+            unsigned long long k = hk[e];
+            if (k == 0ull) {
+                k = atomicCAS(&hk[e], 0ull, lo);
+                if (k == 0ull) break;
+            }
+            if (k == lo) break;
+            e = (e + 1) & (TAGG_HASH - 1);
+        }
+        ent[q] = e;
+        if (atomicAdd(&L.cnt[e], 1u) == 0) lead |= 1u << q;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BIN_K; ++q) {  // one leader per flow: an aggregate for a frequent flow
+        if (!((lead >> q) & 1) || L.cnt[ent[q]] < TAGG_MIN) continue;
+        const uint32_t a = atomicAdd(L.nagg, 1u);
+        if (a >= TAGG_CAP) continue;
+        TileAgg& g = L.agg[a];
+        g.key = ((unsigned long long)r1[q] << 32) | r0[q];
+        g.acc[0] = g.acc[1] = 0ull;
+        g.first_n = g.last1 = g.tbits = g.tflags = 0;
+        g.syn1[0] = g.syn1[1] = g.fin_n[0] = g.fin_n[1] = 0;
+        g.part = r1[q] & pmask;
+        L.cnt[ent[q]] |= (a + 1) << 16;  // only the leader writes its entry in this phase
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BIN_K; ++q) {
+        if (rk[q] == NO_REC) continue;
+        const uint32_t v = L.cnt[ent[q]];
+        if (v >> 16) {  // fold into the flow's aggregate (lds_fold's reductions)
+            TileAgg& g = L.agg[(v >> 16) - 1];
+            const uint32_t idx = LISTED ? ix[q] : tile + (uint32_t)q * IPXG_BLOCK + tid, m = r2[q];
+            const uint32_t cdir = misc_dir(m);
+            atomicAdd(&g.acc[cdir], (1ull << 40) | (unsigned long long)misc_len(m));
+            atomicMax(&g.last1, idx + 1);
+            atomicMax(&g.first_n, ~idx);
+            atomicOr(&g.tbits, 1u << misc_tb(m));
+            const uint32_t fl = misc_flags(m);
+            if (misc_tcp(m) && fl) {
+                atomicOr(&g.tflags, fl << (8 * cdir));
+                if (fl & 0x02) atomicMax(&g.syn1[cdir], idx + 1);
+                if (fl & 0x05) atomicMax(&g.fin_n[cdir], ~idx);
+            }
+            rk[q] = NO_REC;
+        } else {
+            rk[q] = atomicAdd(&L.hist[r1[q] & pmask], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t na = min(*L.nagg, TAGG_CAP);
+    for (uint32_t a = tid; a < na; a += IPXG_BLOCK) L.agg[a].rank = atomicAdd(&L.hist[L.agg[a].part], 3u);
 }
 
 __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& p, const FragView& f, BatchCtl* ctl,
@@ -243,11 +394,16 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 // slow list.
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
-           uint32_t* deferred_list, unsigned long long* stats) {
+           uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
-    __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: records in the block's segments
-    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: the tile's records by partition
+    __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: slots in the block's segments
+    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: tile hash keys, then the slots by partition
+    __shared__ uint32_t tcnt[TAGG_HASH];                // 16 KiB: tile hash counts / aggregate ids
+    __shared__ TileAgg tagg[TAGG_CAP];                  // 8 KiB
+    __shared__ uint16_t part_of[BIN_TILE];              // 4 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
+    __shared__ uint32_t nagg;
+    const BinLds L = {hist, fill, stage, tcnt, tagg, part_of, scan_s, &nagg};
     __shared__ uint32_t nslow[2];  // slow packets of the tile (by tile parity)
     // timestamps (sec << 32 | usec) of each step's first and last packet per wave: the order
     // check across wave boundaries, done once per tile (within a wave it is a DPP shift)
@@ -374,12 +530,13 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                     slow = true;
             }
             if (slow) my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] = i;
-            if (have) tile_rank<false>(hist, pmask, p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
+            if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
-        tile_emit<false>(hist, fill, stage, scan_s, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, r0, r1, r2, rk,
-                         ix, tile, spilled);
+        tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile);
+        tile_emit<false>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile,
+                         spilled);
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         slow_fill += nslow[par];  // final: read after the tile's barriers
@@ -426,15 +583,20 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 // or unaligned frames): staged in the lane's LDS column, parsed by parse_frame, ranked and
 // emitted exactly like k_bin's records.  The list length is read on the device.
 // 168 VGPRs (3 waves/SIMD = the LDS limit of 3 workgroups per CU)
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
-                const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
-    // the header columns (parse) and the tile's records (emit) are never live together:
-    // one 32 KiB area, 48 KiB in all (3 workgroups per CU)
-    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: records / header columns
+                const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
+    // the header columns (parse), the tile hash and the tile's slots (emit) are never live
+    // together: one 32 KiB area; 76 KiB in all (2 workgroups per CU)
+    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: header columns / tile hash / slots
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB
+    __shared__ uint32_t tcnt[TAGG_HASH];                // 16 KiB
+    __shared__ TileAgg tagg[TAGG_CAP];                  // 8 KiB
+    __shared__ uint16_t part_of[BIN_TILE];              // 4 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
+    __shared__ uint32_t nagg;
+    const BinLds L = {hist, fill, stage, tcnt, tagg, part_of, scan_s, &nagg};
     static_assert(sizeof(stage) >= IPXG_WIN_DW * IPXG_BLOCK * 4, "header columns exceed the stage");
     uint32_t* win = reinterpret_cast<uint32_t*>(stage);
     // k_bin workgroup b's slow packets, into segment column bin_grid + b
@@ -477,10 +639,10 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
                 divert_fragment(pk, p, f, ctl, i);
                 continue;
             }
-            tile_rank<true>(hist, pmask, p, b, pk, d, i, j, r0, r1, r2, rk, ix);
+            tile_rank<true>(p, b, pk, d, i, j, r0, r1, r2, rk, ix);
         }
-        tile_emit<true>(hist, fill, stage, scan_s, P, pmask, bv, bcol, t, ctl, deferred_list, r0, r1, r2, rk, ix,
-                        tile, spilled);
+        tile_aggregate<true>(L, pmask, r0, r1, r2, rk, ix, tile);
+        tile_emit<true>(L, P, pmask, bv, bcol, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile, spilled);
     }
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, bcol);
@@ -503,15 +665,17 @@ uint32_t bin_resident_blocks(int device) {
 }
 
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
+                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                unsigned long long* stats) {
     hipLaunchKernelGGL(k_bin, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
-                       deferred_list, stats);
+                       deferred_list, agg_list, stats);
 }
 
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats) {
+                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                     unsigned long long* stats) {
     hipLaunchKernelGGL(k_bin_slow, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
-                       deferred_list, stats);
+                       deferred_list, agg_list, stats);
 }
 
 // ---- phase B ------------------------------------------------------------------------------
@@ -560,11 +724,38 @@ __device__ __forceinline__ uint4 seg_record(const uint4* segs, const uint32_t* p
     return segs[(size_t)lo * seg_cap + (k - pre[lo])];
 }
 
-// Fold one record into the workgroup's LDS flow table (or straight into the device table
-// when the LDS table is full).
+__device__ __forceinline__ void lds_fold_agg(FlowAgg& e, const FlowAgg& a) {
+    if (a.acc[0]) atomicAdd(&e.acc[0], a.acc[0]);
+    if (a.acc[1]) atomicAdd(&e.acc[1], a.acc[1]);
+    atomicMax(&e.last1, a.last1);
+    atomicMax(&e.first_n, a.first_n);
+    atomicOr(&e.tbits, a.tbits);
+    if (a.tflags) atomicOr(&e.tflags, a.tflags);
+    for (int d = 0; d < 2; ++d) {
+        if (a.syn1[d]) atomicMax(&e.syn1[d], a.syn1[d]);
+        if (a.fin_n[d]) atomicMax(&e.fin_n[d], a.fin_n[d]);
+    }
+}
+
+// Fold one record slot into the workgroup's LDS flow table (or straight into the device table
+// when the LDS table is full).  rp = the slot's address (an aggregate's head reads its two
+// payload slots after it; the payload slots themselves are skipped).
 __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
-                                           uint32_t* cnt, const uint4& r) {
+                                           uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp) {
     if (r.z == NO_REC) return;
+    if (rec_is_agg(r)) {
+        if (rec_agg_slot(r) != 0) return;
+        const uint4 s1 = rp[1], s2 = rp[2];
+        const FlowAgg a = agg_decode(r, s1, s2);
+        const int e = lds_slot(ht, a.key, true);
+        if (e >= 0) {
+            lds_fold_agg(ht[e], a);
+        } else {
+            atomicAdd(&cnt[C_SPILL], 1u);
+            if (!merge_agg_probe(t, a, &ctl->new_keys)) defer_agg(&ctl->agg_deferred, agg_list, r, s1, s2);
+        }
+        return;
+    }
     const uint64_t lo = ((uint64_t)r.y << 32) | r.x;
     const int e = lds_slot(ht, lo, true);
     if (e >= 0) {
@@ -579,7 +770,7 @@ __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, Batc
 // k_bin_slow workgroup (bv.count gives their lengths); a prefix sum over the segment lengths
 // in LDS maps the partition's record k to its segment.
 __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
-                                                        uint32_t* deferred_list) {
+                                                        uint32_t* deferred_list, uint4* agg_list) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
     __shared__ uint32_t pre[RED_MAX_COLS + 1];
     __shared__ uint32_t ne[RED_MAX_COLS];  // non-empty segments
@@ -604,6 +795,10 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     uint32_t total;
     uint32_t run = block_exclusive_scan<RED_THREADS>(my, scan_s, &total);
     if (total == 0) return;  // uniform over the workgroup
+    if (tid == 0) {  // the partition's load (segment sizing of the next batch)
+        atomicMax(&ctl->max_part, total);
+        atomicAdd(&ctl->total_slots, total);
+    }
     uint32_t ne_n = 0;
 #pragma unroll
     for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
@@ -650,11 +845,12 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         }
 #pragma unroll
         for (uint32_t u = 0; u < RED_U; ++u) {
-            red_record(ht, t, ctl, deferred_list, cnt, r[u]);
+            const uint4* sg = segs + (size_t)sc[u] * bv.seg_cap;
+            red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], sg + lane);
             for (uint32_t off = 64; off < sl[u]; off += 64) {  // long segment (uniform over the wave)
-                uint4 x = segs[(size_t)sc[u] * bv.seg_cap + (off + lane < sl[u] ? off + lane : 0)];
+                uint4 x = sg[off + lane < sl[u] ? off + lane : 0];
                 if (off + lane >= sl[u]) x.z = NO_REC;
-                red_record(ht, t, ctl, deferred_list, cnt, x);
+                red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane);
             }
         }
     }
@@ -713,11 +909,17 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         atomicAdd((unsigned long long*)&ctl->probe[6], (unsigned long long)(q3t - q2t));
     }
 #endif
-    if (cnt[C_FAIL]) {  // defer the packets of the flows that found no slot
+    if (cnt[C_FAIL]) {  // defer the packets (and aggregates) of the flows that found no slot
         for (uint32_t k = tid; k < total; k += RED_THREADS) {
             const uint4 r = seg_record(segs, pre, cols, bv.seg_cap, k);
+            if (r.z == NO_REC || (rec_is_agg(r) && rec_agg_slot(r) != 0)) continue;
             const int e = lds_slot(ht, ((uint64_t)r.y << 32) | r.x, false);
-            if (e >= 0 && (ht[e].tflags & RED_FAILED)) defer_packet(ctl, deferred_list, r.z, false);
+            if (e < 0 || !(ht[e].tflags & RED_FAILED)) continue;
+            if (rec_is_agg(r))  // its payload slots follow it in the same segment
+                defer_agg(&ctl->agg_deferred, agg_list, r, seg_record(segs, pre, cols, bv.seg_cap, k + 1),
+                          seg_record(segs, pre, cols, bv.seg_cap, k + 2));
+            else
+                defer_packet(ctl, deferred_list, r.z, false);
         }
     }
     if (tid == 0) {
@@ -729,9 +931,9 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 }
 
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
-                   uint32_t* deferred_list) {
+                   uint32_t* deferred_list, uint4* agg_list) {
     hipLaunchKernelGGL(k_reduce, dim3(1u << bv.part_bits), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list,
-                       deferred_list);
+                       deferred_list, agg_list);
 }
 
 // ---- finalisation of the flows k_reduce completed -----------------------------------------

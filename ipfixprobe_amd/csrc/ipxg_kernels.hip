@@ -245,6 +245,20 @@ void launch_deferred(hipStream_t st, const BatchView& b, const Params& p, TableV
                        ctl, out_list);
 }
 
+// Re-apply deferred tile aggregates (3 slots each) after the table has grown.
+__global__ __launch_bounds__(256) void k_deferred_agg(TableView t, const uint4* in_list, uint32_t n_in, BatchCtl* ctl,
+                                                      uint4* out_list) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_in) return;
+    const uint4 s0 = in_list[3 * (size_t)j], s1 = in_list[3 * (size_t)j + 1], s2 = in_list[3 * (size_t)j + 2];
+    if (!merge_agg_probe(t, agg_decode(s0, s1, s2), &ctl->new_keys)) defer_agg(&ctl->agg_deferred, out_list, s0, s1, s2);
+}
+
+void launch_deferred_agg(hipStream_t st, TableView t, const uint4* in_list, uint32_t n_in, BatchCtl* ctl,
+                         uint4* out_list) {
+    hipLaunchKernelGGL(k_deferred_agg, dim3((n_in + 255) / 256), dim3(256), 0, st, t, in_list, n_in, ctl, out_list);
+}
+
 __device__ __forceinline__ void reason_count(uint32_t* sc, uint8_t reason) {
     atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
 }
@@ -475,7 +489,8 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     __shared__ uint32_t scratch[8];
     __shared__ uint32_t bbase;
     if (guard) {
-        const bool hold = guard->frag_count || guard->deferred || guard->pending || guard->complex_count ||
+        const bool hold = guard->frag_count || guard->deferred || guard->agg_deferred || guard->pending ||
+                          guard->complex_count ||
                           (uint64_t)ex_before + guard->exported + live_before + guard->new_live > ex.cap;
         if (blockIdx.x == 0 && threadIdx.x == 0) guard->hold = hold ? 1u : 0u;
         if (hold) return;

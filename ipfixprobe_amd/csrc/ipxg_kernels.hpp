@@ -51,6 +51,10 @@ struct BatchCtl {
     uint32_t slow_count;     // packets k_bin left for k_bin_slow (statistics)
     uint32_t fin_count;      // slots k_reduce listed for k_fin_list
     uint32_t hold;           // set by a guarded k_finish that did not run (see k_finish)
+    uint32_t agg_deferred;   // tile aggregates whose table probe failed (3-slot list length)
+    uint32_t max_part;       // most record slots in one partition (segment sizing, k_reduce)
+    uint32_t total_slots;    // record slots over all partitions (k_reduce)
+    uint32_t pad_;
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -157,12 +161,16 @@ struct ComplexView {
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid)
 uint32_t bin_resident_blocks(int device);
+// deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
+// 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats);
+                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                unsigned long long* stats);
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, unsigned long long* stats);
+                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                     unsigned long long* stats);
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
-                   uint32_t* deferred_list);
+                   uint32_t* deferred_list, uint4* agg_list);
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, const uint32_t* fin_list, unsigned long long* stats, uint32_t max_n);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
@@ -173,6 +181,8 @@ void launch_frag_accumulate(hipStream_t st, const BatchView& b, const Params& p,
                             FragView f, uint32_t nfrag, BatchCtl* ctl, uint32_t* deferred_list);
 void launch_deferred(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                      const uint32_t* in_list, uint32_t n_in, BatchCtl* ctl, uint32_t* out_list);
+void launch_deferred_agg(hipStream_t st, TableView t, const uint4* in_list, uint32_t n_in, BatchCtl* ctl,
+                         uint4* out_list);
 void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                      ExportView ex, BatchCtl* ctl, unsigned long long* stats);
 void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap);

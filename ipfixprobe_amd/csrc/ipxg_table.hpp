@@ -243,6 +243,51 @@ __device__ __forceinline__ void agg_fold(HotSlot& h, const FlowAgg& a) {
     h.syn1[1] = max(h.syn1[1], a.syn1[1]);
 }
 
+// ---- tile aggregates (k_bin / k_bin_slow -> k_reduce) ------------------------------------
+// A flow with >= TAGG_MIN packets in one k_bin tile travels as one aggregate of its packets
+// instead of one 16-byte record per packet: three consecutive record slots in the partition
+// segment, each marked with bit 31 of word w (a packet record's w = pack_misc() leaves bit 31
+// clear) and its slot index in bits 29-30.  Fields (indices absolute in the batch):
+//   s0 = {lo low, lo high, first | tflags dir0 << 24, last | MARK | 0 << 29}
+//   s1 = {bytes0 | packets0 low 5 << 27, bytes1 | packets1 low 5 << 27, tbits,
+//         packets0 >> 5 | (packets1 >> 5) << 7 | tflags dir1 << 14 | MARK | 1 << 29}
+//   s2 = {syn1[0], syn1[1], fin1[0], fin1[1] | MARK | 2 << 29}   (index + 1, 0 = none)
+// A tile has 2048 packets: packets <= 2048 (12 bits), bytes <= 2048 * 65535 < 2^27.
+constexpr uint32_t AGG_MARK = 0x80000000u;
+constexpr uint32_t TAGG_MIN = 3;  // below this, packet records are smaller than one aggregate
+
+__device__ __forceinline__ bool rec_is_agg(const uint4& r) { return (r.w & AGG_MARK) != 0; }
+__device__ __forceinline__ uint32_t rec_agg_slot(const uint4& r) { return (r.w >> 29) & 3; }
+
+__device__ __forceinline__ void agg_encode(const FlowAgg& a, uint4& s0, uint4& s1, uint4& s2) {
+    const uint32_t p0 = (uint32_t)(a.acc[0] >> 40), p1 = (uint32_t)(a.acc[1] >> 40);
+    const uint32_t b0 = (uint32_t)(a.acc[0] & ACC_BYTES_MASK), b1 = (uint32_t)(a.acc[1] & ACC_BYTES_MASK);
+    const uint32_t f1[2] = {a.fin_n[0] ? ~a.fin_n[0] + 1 : 0u, a.fin_n[1] ? ~a.fin_n[1] + 1 : 0u};
+    s0 = make_uint4((uint32_t)a.key, (uint32_t)(a.key >> 32), (~a.first_n) | ((a.tflags & 0xFF) << 24),
+                    (a.last1 - 1) | AGG_MARK);
+    s1 = make_uint4(b0 | (p0 << 27), b1 | (p1 << 27), a.tbits,
+                    (p0 >> 5) | ((p1 >> 5) << 7) | (((a.tflags >> 8) & 0xFF) << 14) | AGG_MARK | (1u << 29));
+    s2 = make_uint4(a.syn1[0], a.syn1[1], f1[0], f1[1] | AGG_MARK | (2u << 29));
+}
+
+__device__ __forceinline__ FlowAgg agg_decode(const uint4& s0, const uint4& s1, const uint4& s2) {
+    FlowAgg a;
+    a.key = ((unsigned long long)s0.y << 32) | s0.x;
+    const uint64_t p0 = (s1.x >> 27) | ((s1.w & 0x7F) << 5), p1 = (s1.y >> 27) | (((s1.w >> 7) & 0x7F) << 5);
+    a.acc[0] = (p0 << 40) | (s1.x & 0x07FFFFFFu);
+    a.acc[1] = (p1 << 40) | (s1.y & 0x07FFFFFFu);
+    a.first_n = ~(s0.z & 0xFFFFFF);
+    a.last1 = (s0.w & 0xFFFFFF) + 1;
+    a.tbits = s1.z;
+    a.tflags = (s0.z >> 24) | (((s1.w >> 14) & 0xFF) << 8);
+    a.syn1[0] = s2.x;
+    a.syn1[1] = s2.y;
+    const uint32_t f0 = s2.z, f1 = s2.w & 0xFFFFFF;
+    a.fin_n[0] = f0 ? ~(f0 - 1) : 0u;
+    a.fin_n[1] = f1 ? ~(f1 - 1) : 0u;
+    return a;
+}
+
 // atomic merge of an aggregate into a slot (when other workgroups may touch it too)
 __device__ __forceinline__ void agg_merge_atomic(HotSlot* h, const FlowAgg& a) {
     if (a.acc[0]) atomicAdd((unsigned long long*)&h->acc[0], a.acc[0]);
@@ -255,6 +300,27 @@ __device__ __forceinline__ void agg_merge_atomic(HotSlot* h, const FlowAgg& a) {
         if (a.fin_n[d]) atomicMax(&h->fin_n[d], a.fin_n[d]);
         if (a.syn1[d]) atomicMax(&h->syn1[d], a.syn1[d]);
     }
+}
+
+// probe/claim the aggregate's slot and merge it with device atomics; false when the probe
+// failed (the caller defers the aggregate until the table has grown)
+__device__ __forceinline__ bool merge_agg_probe(const TableView& t, const FlowAgg& a, uint32_t* new_keys) {
+    uint4 head;
+    bool claimed;
+    HotSlot* h = probe_insert(t, a.key, head, claimed);
+    if (!h) return false;
+    if (claimed) atomicAdd(new_keys, 1u);
+    agg_merge_atomic(h, a);
+    return true;
+}
+
+// deferred aggregates: 3 record slots each, after the per-packet deferral list's counter
+__device__ __forceinline__ void defer_agg(uint32_t* count, uint4* list, const uint4& s0, const uint4& s1,
+                                          const uint4& s2) {
+    const uint32_t pos = atomicAdd(count, 1u);
+    list[3 * (size_t)pos] = s0;
+    list[3 * (size_t)pos + 1] = s1;
+    list[3 * (size_t)pos + 2] = s2;
 }
 
 // ---- flow record construction (FlowRecord::create/update, cache.cpp:94-152) ---------------

@@ -51,7 +51,7 @@ STATS_FIELDS = [
     "vlan_packets", "ipv4_bytes", "ipv6_bytes", "end_inactive", "end_active", "end_eof",
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
-    "table_rehashes", "batches", "spilled_packets",
+    "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
 ]
 
 
@@ -225,9 +225,19 @@ class Engine:
             b._keep = (arena, desc)
         return b
 
-    def submit(self, arena, desc, device=False, asynchronous=False):
+    def submit(self, arena, desc, device=False, asynchronous=False, wait_producer=True):
         """asynchronous (device batches): may return before the batch is applied; keep the
-        tensors alive and unchanged until the next call on the engine."""
+        tensors alive and unchanged until the next call on the engine.  wait_producer (device
+        torch tensors): the engine's stream first waits for the work queued so far on torch's
+        current stream (the kernels that wrote the batch) -- the engine's stream is a
+        non-blocking stream, unordered with respect to torch's; pass False when the caller has
+        synchronised already."""
+        if device and wait_producer and hasattr(arena, "data_ptr"):
+            import torch
+            dev = arena.device
+            if getattr(self, "_ext_stream", None) is None:
+                self._ext_stream = torch.cuda.ExternalStream(self.stream(), device=dev)
+            self._ext_stream.wait_stream(torch.cuda.current_stream(dev))
         b = self._batch(arena, desc, device, asynchronous)
         self._keep_async = b._keep if (device and asynchronous) else None
         self._check(lib().ipxg_submit(self._h, ctypes.byref(b)), "ipxg_submit")

@@ -40,6 +40,9 @@ def lib():
         L.oracle_cache_take.argtypes = [vp, vp, ctypes.c_size_t]
         L.oracle_ipfix_basic.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
         L.oracle_cache_stats.argtypes = [vp, vp]
+        L.oracle_bench_mt.restype = ctypes.c_double
+        L.oracle_bench_mt.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         _LIB = L
     return _LIB
 
@@ -140,3 +143,22 @@ def run_capture(arena, desc, datalink=1, finish=True, **kw):
     st = c.stats()
     c.close()
     return recs, st
+
+
+def bench_mt(arena, desc, shard, nshards, cpus=None, cache_exp=17, datalink=1):
+    """oracle/cpu_baseline.c: nshards pinned threads, thread k runs parse + put_pkt + finish
+    over the packets with shard == k (in arrival order) with its own cache.  Returns
+    (wall seconds, records, NO_RES exports)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    order = np.argsort(shard, kind="stable")
+    grouped = np.ascontiguousarray(desc[order])
+    count = np.bincount(shard, minlength=nshards).astype(np.uint64)
+    first = np.concatenate([[0], np.cumsum(count)[:-1]]).astype(np.uint64)
+    cp = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.int32)
+    rec, nr = ctypes.c_uint64(), ctypes.c_uint64()
+    dt = lib().oracle_bench_mt(arena.ctypes.data, grouped.ctypes.data, first.ctypes.data, count.ctypes.data,
+                               nshards, None if cp is None else cp.ctypes.data, cache_exp, datalink,
+                               ctypes.byref(rec), ctypes.byref(nr))
+    if dt < 0:
+        raise RuntimeError("oracle_bench_mt failed")
+    return dt, rec.value, nr.value

@@ -59,7 +59,7 @@ STATS_FIELDS = [
     "vlan_packets", "ipv4_bytes", "ipv6_bytes", "end_inactive", "end_active", "end_eof",
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
-    "table_rehashes", "batches", "spilled_packets",
+    "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
 ]
 
 
