@@ -201,6 +201,7 @@ typedef struct ipxg_stats {
     uint64_t spilled_packets; /* packets that fell back from the binned ingest to direct
                                  device atomics (partition region or LDS table full)    */
     uint64_t slow_path_packets; /* packets k_bin left to the general parser (k_bin_slow)  */
+    uint64_t aggregated_packets; /* packets folded into per-tile flow aggregates (skew)   */
 } ipxg_stats;
 
 typedef struct ipxg_engine ipxg_engine;
@@ -284,6 +285,43 @@ int ipxg_ipfix_basic(ipxg_engine* eng, const ipxg_flow_record* recs, size_t n, u
  * *bytes written. */
 int ipxg_poll_ipfix(ipxg_engine* eng, uint32_t dir_bit_field, uint8_t* out, size_t cap, size_t* n,
                     size_t* bytes);
+
+/* ---- IPFIX messages: the IPFIX output plugin's wire format ---------
+ * The message stream IPFIXExporter (src/plugins/output/ipfix/src/ipfix.cpp) sends for a run of
+ * export_flow() calls followed by flush(): the template message (the basic templates, ids 258
+ * for IPv4 and 259 for IPv6, create_template ipfix.cpp:537-656, create_template_packet
+ * :671-728) once per exporter, then data messages of at most `mtu` bytes, each a 16-byte
+ * header (fill_ipfix_header :475-486: version 10, length, export time, sequence number =
+ * records in earlier data messages, observation domain) and one data set per template whose
+ * buffer fits (create_data_packet :739-795), a template's buffer flushing when its next record
+ * would pass mtu - 16 bytes (fill_basic_flow :1470-1516, export_flow :385-398).  The records
+ * are fed to that exporter in export-buffer order with the IPv4 records first (a stable
+ * partition by template -- export order is not part of the flow contract), formatted and
+ * packed on the device.  The caller keeps the exporter state. */
+#define IPXG_IPFIX_DEFAULT_MTU 1458 /* ipfix.hpp:34 */
+typedef struct ipxg_ipfix_exporter {
+    uint32_t odid;            /* observationDomainId (ipfix plugin id=)                    */
+    uint32_t dir_bit_field;   /* INPUT_INTERFACE value (ipfix plugin dir=)                 */
+    uint32_t export_time;     /* header exportTime (the reference: time(NULL) at send)     */
+    uint32_t sequence;        /* in/out: records carried by earlier data messages          */
+    uint16_t mtu;             /* message size limit, >= 125 (ipfix plugin mtu=)            */
+    uint16_t templates_sent;  /* in/out: the template message has gone out                 */
+} ipxg_ipfix_exporter;
+
+void ipxg_ipfix_exporter_init(ipxg_ipfix_exporter* x);
+/* Upper bound of the message bytes for n records (templates included). */
+uint64_t ipxg_ipfix_bound(uint64_t n);
+/* n host records, in this order, through the exporter -> out (cap bytes, IPXG_ETOOBIG and
+ * nothing written if short); *bytes written, *msgs messages. */
+int ipxg_ipfix_export(ipxg_engine* eng, ipxg_ipfix_exporter* x, const ipxg_flow_record* recs, size_t n,
+                      uint8_t* out, size_t cap, size_t* bytes, size_t* msgs);
+/* The pending exports (consumed, like ipxg_poll_exports) as messages into host memory. */
+int ipxg_poll_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, uint8_t* out, size_t cap, size_t* n_records,
+                             size_t* bytes, size_t* msgs);
+/* The same into a device buffer owned by the engine (valid until the next engine call): for
+ * gathering the per-GPU message streams with RCCL. */
+int ipxg_device_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, const uint8_t** dptr, size_t* n_records,
+                               size_t* bytes, size_t* msgs);
 
 /* ---- stateless device entry points (parity tests, tools) ---------------------------- */
 /* Run the device parser on a batch; out receives n records (host pointer). */

@@ -69,6 +69,7 @@ bool read_pcapng(const std::vector<uint8_t>& d, std::vector<Pkt>& out, int& dlt)
     struct Iface {
         int dlt;
         uint64_t res;  // units per second
+        bool dec;      // a power of ten (else a power of two)
     };
     std::vector<Iface> ifs;
     bool swap = false;
@@ -87,16 +88,19 @@ bool read_pcapng(const std::vector<uint8_t>& d, std::vector<Pkt>& out, int& dlt)
         const uint8_t* body = &d[o + 8];
         size_t blen = bl - 12;
         if (bt == 1 && blen >= 8) {  // IDB
-            Iface f{map_linktype(rd16(body, swap)), 1000000};
+            Iface f{map_linktype(rd16(body, swap)), 1000000, true};
             size_t p = 8;
             while (p + 4 <= blen) {
                 uint16_t code = rd16(body + p, swap), ol = rd16(body + p + 2, swap);
                 if (code == 0) break;
-                if (code == 9 && ol >= 1) {
-                    uint8_t v = body[p + 4];
-                    f.res = (v & 0x80) ? (1ull << (v & 0x7F)) : 1;
-                    if (!(v & 0x80))
-                        for (int i = 0; i < v; ++i) f.res *= 10;
+                if (code == 9 && ol >= 1 && p + 5 <= blen) {  // if_tsresol
+                    const uint8_t v = body[p + 4], ex = v & 0x7F;
+                    f.dec = !(v & 0x80);
+                    // a resolution that does not fit 64 bits (10^20, 2^64) cannot be a
+                    // timestamp unit: reject the capture instead of dividing by zero
+                    if (f.dec ? ex > 19 : ex > 63) return false;
+                    f.res = 1;
+                    for (int i = 0; i < ex; ++i) f.res *= f.dec ? 10 : 2;
                 }
                 p += 4 + ((ol + 3u) & ~3u);
             }
@@ -109,10 +113,12 @@ bool read_pcapng(const std::vector<uint8_t>& d, std::vector<Pkt>& out, int& dlt)
             p.caplen = rd32(body + 12, swap);
             p.wirelen = rd32(body + 16, swap);
             if (iid >= ifs.size() || 20 + (size_t)p.caplen > blen) break;
-            uint64_t res = ifs[iid].res;
+            // libpcap's conversion to microseconds: a decimal resolution finer than 1 us divides
+            // by the power of ten, anything else scales frac * 10^6 / res (128-bit: exact)
+            const uint64_t res = ifs[iid].res;
             uint64_t sec = t / res, frac = t % res;
-            if (res > 1000000) frac /= (res / 1000000);
-            else if (res < 1000000) frac = frac * 1000000 / res;
+            if (ifs[iid].dec && res >= 1000000) frac /= (res / 1000000);
+            else frac = (uint64_t)((unsigned __int128)frac * 1000000u / res);
             p.sec = (uint32_t)sec;
             p.usec = (uint32_t)frac;
             p.off = (size_t)(body + 20 - d.data());

@@ -59,7 +59,8 @@ struct ipxg_engine {
     DevBuf adefer_a, adefer_b;           // deferred tile aggregates (3 x 16 B each)
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
-    uint32_t bin_slots = 0;              // k_bin workgroups resident at once (its grid)
+    uint32_t bin_slots[2] = {0, 0};      // k_bin workgroups resident at once (its grid), [agg]
+    bool tile_agg = true;                // the next batch aggregates frequent flows per tile
     // an IPXG_BATCH_ASYNC batch whose kernels are enqueued but whose control block the host
     // has not read yet (completed by the next call on the engine)
     struct {
@@ -70,13 +71,14 @@ struct ipxg_engine {
     } inflight;
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
+    DevBuf ipf_msg, ipf_plan;                   // IPFIX messages: output, plan (sets + messages)
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
     double skew = 1.0;                   // previous batch: most loaded partition / mean partition
     uint32_t part_bits_last = 0;         // partitions of the last binned batch (log2)
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
     // host-side counters
-    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0;
+    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0;
     bool prev_valid = false;
     uint32_t prev_sec = 0, prev_usec = 0;
     // stage timing
@@ -134,11 +136,11 @@ static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_c
 // (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
 // than the batch's packets.  k_bin runs bin_grid persistent workgroups over tiles of
 // BIN_TILE_PKTS packets; each owns one segment per partition, sized for its mean share of the
-// packets times max(3, 1.25 x the previous batch's most loaded partition / mean), plus 4
-// standard deviations (binomial) and a margin; what does not fit spills to atomics.  Memory
-// is plentiful (288 GB of HBM) and only the slots written are read, so the margin is generous:
-// skewed traffic (tile aggregation leaves the configs[2] Zipf mix at ~2.4x) never spills after
-// its first batch.
+// packets times max(3 when aggregating else 1.5, 1.25 x the previous batch's most loaded
+// partition / mean), plus 4 standard deviations (binomial) and a margin; what does not fit
+// spills to atomics.  Memory is plentiful (288 GB of HBM) and only the slots written are
+// read, so the margin is generous: skewed traffic (tile aggregation leaves the configs[2] Zipf
+// mix at ~2.4x) does not spill after its first batch.
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
     if (est == 0 || est > n) est = n;
@@ -148,15 +150,18 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
         bits = std::min<uint32_t>((uint32_t)std::atoi(pb), BIN_MAX_PART_BITS);
     const uint32_t P = 1u << bits;
     const uint64_t tiles = ((uint64_t)n + BIN_TILE_PKTS - 1) / BIN_TILE_PKTS;
-    if (!e->bin_slots) {
-        e->bin_slots = bin_resident_blocks(e->cfg.device_id);
+    const int ag = e->tile_agg ? 1 : 0;
+    if (!e->bin_slots[ag]) {
+        e->bin_slots[ag] = bin_resident_blocks(e->cfg.device_id, ag != 0);
         if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
-            e->bin_slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
+            e->bin_slots[ag] = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
     }
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->bin_slots);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->bin_slots[ag]);
     const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * BIN_TILE_PKTS, n);
     const double mean = (double)per_block / P;
-    const double factor = std::max(3.0, 1.25 * e->skew);
+    // aggregating batches follow a skewed one (the most loaded partition ~2.4x the mean with
+    // the configs[2] Zipf mix); the others spill only if the skew changed since the last batch
+    const double factor = std::max(e->tile_agg ? 3.0 : 1.5, 1.25 * e->skew);
     const uint64_t seg = ((uint64_t)(mean * factor + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
     const uint32_t cols = 2 * grid;
     int rc;
@@ -198,6 +203,7 @@ static Params params(ipxg_engine* e) {
     p.prev_valid = e->prev_valid;
     p.prev_sec = e->prev_sec;
     p.prev_usec = e->prev_usec;
+    p.tile_agg = e->tile_agg ? 1 : 0;
     return p;
 }
 
@@ -400,7 +406,7 @@ int ipxg_destroy(ipxg_engine* e) {
                       &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
-                      &e->ipf_tot, &e->ipf_off})
+                      &e->ipf_tot, &e->ipf_off, &e->ipf_msg, &e->ipf_plan})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -636,6 +642,15 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         const uint32_t P = 1u << e->part_bits_last;
         e->skew = (double)c2.max_part * P / c2.total_slots;
     }
+    // Tile aggregation for the next batch: kept while it folds >= 2 % of the packets, switched
+    // on when the partitions' loads show skew (the most loaded > 2x the mean); the first batch
+    // aggregates.  Uniform traffic folds nothing and skips the aggregation's LDS passes.
+    e->agg_pkts += c2.agg_packets;
+    if (binned) {
+        if (p.tile_agg) e->tile_agg = (uint64_t)c2.agg_packets * 50 >= n;
+        else e->tile_agg = e->skew > 2.0;
+        if (const char* a = std::getenv("IPXG_TILE_AGG")) e->tile_agg = std::atoi(a) != 0;  // experiments
+    }
     e->spilled += c2.spilled;
     e->slow_pkts += c2.slow_count;
     e->prev_valid = true;
@@ -682,10 +697,12 @@ int ipxg_finish(ipxg_engine* e) {
         launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d, e->ctl_d, e->ex_count, e->live);
         HIPCHK(e, hipGetLastError());
         ev_rec(e, 10);
+        // the batch is consumed here whatever happens next: an error below must not make the
+        // next call run post_batch again on a table k_finish may already have emptied
+        e->inflight.on = false;
         if ((rc = publish_ctl(e))) return rc;
         HIPCHK(e, stream_wait(e->st));
         if ((rc = check_ex(e))) return rc;
-        e->inflight.on = false;
         const bool held = e->ctl_h->hold != 0;
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->hold, 0, sizeof(uint32_t), e->st));
         if ((rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, !held))) return rc;
@@ -834,6 +851,237 @@ int ipxg_poll_ipfix(ipxg_engine* e, uint32_t dir_bit_field, uint8_t* out, size_t
     return IPXG_OK;
 }
 
+// ---- IPFIX messages ---------------------------------------------------------------------
+// The reference exporter's buffer logic (src/plugins/output/ipfix/src/ipfix.cpp) replayed over
+// whole data sets: n4 IPv4-template records, then n6 IPv6-template records, then flush().
+// A template buffer takes records while 4 + (k + 1) * len <= mtu - 16 (fill_basic_flow
+// :1479/:1497, tmpltMaxBufferSize = mtu - IPFIX_HEADER_SIZE); the record that does not fit
+// flushes (export_flow :385-398): the template message if not sent yet (create_template_packet
+// :671-728), then data messages (create_data_packet :739-795: walk the template list, newest
+// template -- IPv6, 259 -- first, and add every non-empty buffer that still fits the message).
+namespace {
+constexpr uint32_t IPFIX_LEN[2] = {81, 105};
+constexpr uint32_t IPFIX_TMPL_REC = 88;                    // 4 + 18 fields * 4 + 3 enterprise numbers * 4
+constexpr uint32_t IPFIX_TMPL_MSG = 16 + 4 + 2 * IPFIX_TMPL_REC;
+
+struct IpfixPlan {
+    std::vector<IpfixSet> sets[2];
+    std::vector<IpfixMsg> msgs;
+    uint64_t bytes = 0;
+    bool tmpl = false;  // the template message leads the stream
+    uint32_t seq_end = 0;
+};
+
+IpfixPlan ipfix_plan(uint64_t n4, uint64_t n6, const ipxg_ipfix_exporter& x) {
+    IpfixPlan P;
+    const uint32_t mtu = x.mtu;
+    uint64_t b[2] = {0, 0}, emitted[2] = {0, 0};
+    uint32_t seq = x.sequence;
+    bool tmpl_sent = x.templates_sent != 0;
+    auto flush = [&]() {
+        if (!tmpl_sent) {
+            P.tmpl = true;
+            P.bytes += IPFIX_TMPL_MSG;
+            tmpl_sent = true;
+        }
+        for (;;) {
+            uint32_t size = 16, flows = 0;
+            for (int c : {1, 0}) {  // the template list: IPv6 (259) first, then IPv4 (258)
+                const uint32_t sz = 4 + (uint32_t)b[c] * IPFIX_LEN[c];
+                if (b[c] > 0 && size + sz <= mtu) {
+                    P.sets[c].push_back(IpfixSet{(uint32_t)c, (uint32_t)b[c], emitted[c], P.bytes + size});
+                    emitted[c] += b[c];
+                    flows += (uint32_t)b[c];
+                    size += sz;
+                    b[c] = 0;
+                }
+            }
+            if (size == 16) break;
+            P.msgs.push_back(IpfixMsg{P.bytes, size, seq});
+            P.bytes += size;
+            seq += flows;
+        }
+    };
+    const uint64_t n[2] = {n4, n6};
+    for (int c : {0, 1}) {
+        const uint64_t cap = (mtu - 20) / IPFIX_LEN[c];
+        uint64_t rem = n[c];
+        while (rem) {
+            if (b[c] == cap) flush();
+            const uint64_t take = std::min(rem, cap - b[c]);
+            b[c] += take;
+            rem -= take;
+        }
+    }
+    if (n4 + n6) flush();
+    P.seq_end = seq;
+    return P;
+}
+
+// the template message: header, template set, the IPv6 then the IPv4 basic template records
+// (create_template :537-656 with the elements of ipfix-elements.hpp:328-366)
+void ipfix_template_msg(uint8_t* m, const ipxg_ipfix_exporter& x) {
+    static const uint32_t F[2][18][3] = {
+        {{0, 136, 1}, {0, 1, 8}, {29305, 1, 8}, {0, 2, 8}, {29305, 2, 8}, {0, 154, 8}, {0, 155, 8}, {0, 60, 1},
+         {0, 4, 1}, {0, 6, 1}, {29305, 6, 1}, {0, 7, 2}, {0, 11, 2}, {0, 10, 4}, {0, 8, 4}, {0, 12, 4}, {0, 56, 6},
+         {0, 80, 6}},
+        {{0, 136, 1}, {0, 1, 8}, {29305, 1, 8}, {0, 2, 8}, {29305, 2, 8}, {0, 154, 8}, {0, 155, 8}, {0, 60, 1},
+         {0, 4, 1}, {0, 6, 1}, {29305, 6, 1}, {0, 7, 2}, {0, 11, 2}, {0, 10, 4}, {0, 27, 16}, {0, 28, 16},
+         {0, 56, 6}, {0, 80, 6}}};
+    auto be16 = [](uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; };
+    auto be32 = [](uint8_t* p, uint32_t v) { for (int k = 0; k < 4; ++k) p[k] = (uint8_t)(v >> (24 - 8 * k)); };
+    be16(m, 10);
+    be16(m + 2, IPFIX_TMPL_MSG);
+    be32(m + 4, x.export_time);
+    be32(m + 8, x.sequence);
+    be32(m + 12, x.odid);
+    be16(m + 16, 2);  // TEMPLATE_SET_ID
+    be16(m + 18, IPFIX_TMPL_MSG - 16);
+    uint32_t p = 20;
+    for (int c : {1, 0}) {
+        be16(m + p, c ? 259 : 258);
+        be16(m + p + 2, 18);
+        p += 4;
+        for (const auto& f : F[c]) {
+            be16(m + p, f[1] | (f[0] ? 0x8000 : 0));
+            be16(m + p + 2, f[2]);
+            p += 4;
+            if (f[0]) {
+                be32(m + p, f[0]);
+                p += 4;
+            }
+        }
+    }
+}
+}  // namespace
+
+// n device records at rec -> messages in e->ipf_msg; *bytes, *msgs; updates *x.
+static int ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flow_record* rec, uint32_t n,
+                          size_t* bytes, size_t* msgs) {
+    if (x->mtu < 16 + 4 + 105) return set_err(e, IPXG_EINVAL, "IPFIX mtu below one IPv6 basic record");
+    int rc;
+    const size_t nb = (n + 255) / 256;
+    uint64_t n6 = 0;
+    if (n) {
+        if ((rc = ensure(e, e->ipf_tot, (nb + 1) * sizeof(uint64_t)))) return rc;
+        launch_ipfix_count6(e->st, rec, n, (uint64_t*)e->ipf_tot.p);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipMemcpyAsync(&n6, (uint64_t*)e->ipf_tot.p + nb, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    const IpfixPlan P = ipfix_plan(n - n6, n6, *x);
+    const size_t ns4 = P.sets[0].size(), ns6 = P.sets[1].size(), nm = P.msgs.size();
+    std::vector<uint8_t> plan((ns4 + ns6) * sizeof(IpfixSet) + nm * sizeof(IpfixMsg) + IPFIX_TMPL_MSG);
+    std::memcpy(plan.data(), P.sets[0].data(), ns4 * sizeof(IpfixSet));
+    std::memcpy(plan.data() + ns4 * sizeof(IpfixSet), P.sets[1].data(), ns6 * sizeof(IpfixSet));
+    const size_t moff = (ns4 + ns6) * sizeof(IpfixSet), toff = moff + nm * sizeof(IpfixMsg);
+    std::memcpy(plan.data() + moff, P.msgs.data(), nm * sizeof(IpfixMsg));
+    ipfix_template_msg(plan.data() + toff, *x);
+    if ((rc = ensure(e, e->ipf_plan, plan.size()))) return rc;
+    if ((rc = ensure(e, e->ipf_msg, P.bytes + 16))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->ipf_plan.p, plan.data(), plan.size(), hipMemcpyHostToDevice, e->st));
+    uint8_t* out = (uint8_t*)e->ipf_msg.p;
+    if (P.tmpl)
+        HIPCHK(e, hipMemcpyAsync(out, (uint8_t*)e->ipf_plan.p + toff, IPFIX_TMPL_MSG, hipMemcpyDeviceToDevice, e->st));
+    const IpfixSet* sets = (const IpfixSet*)e->ipf_plan.p;
+    const IpfixMsg* m = (const IpfixMsg*)((uint8_t*)e->ipf_plan.p + moff);
+    launch_ipfix_messages(e->st, rec, n, x->dir_bit_field, (const uint64_t*)e->ipf_tot.p, sets, (uint32_t)ns4,
+                          (uint32_t)ns6, m, (uint32_t)nm, x->odid, x->export_time, out);
+    HIPCHK(e, hipGetLastError());
+    // the plan's host copy must outlive the asynchronous upload
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    if (P.tmpl) x->templates_sent = 1;
+    x->sequence = P.seq_end;
+    *bytes = P.bytes;
+    *msgs = nm + (P.tmpl ? 1 : 0);
+    return IPXG_OK;
+}
+
+void ipxg_ipfix_exporter_init(ipxg_ipfix_exporter* x) {
+    if (!x) return;
+    std::memset(x, 0, sizeof(*x));
+    x->mtu = IPXG_IPFIX_DEFAULT_MTU;
+}
+
+uint64_t ipxg_ipfix_bound(uint64_t n) {
+    // every record in a message of its own is the worst case: 16 + 4 + 105 per record
+    return IPFIX_TMPL_MSG + n * (16 + 4 + 105);
+}
+
+int ipxg_ipfix_export(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flow_record* recs, size_t n, uint8_t* out,
+                      size_t cap, size_t* bytes, size_t* msgs) {
+    if (!e || !x || !bytes || !msgs || (n && (!recs || !out))) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
+    if (n > 0xFFFFFFF0ull) return set_err(e, IPXG_ETOOBIG, "too many records");
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (n) {
+        if ((rc = ensure(e, e->ipf_rec, n * sizeof(ipxg_flow_record)))) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->ipf_rec.p, recs, n * sizeof(ipxg_flow_record), hipMemcpyHostToDevice, e->st));
+    }
+    ipxg_ipfix_exporter y = *x;
+    size_t nbytes = 0, nm = 0;
+    if ((rc = ipfix_messages(e, &y, (const ipxg_flow_record*)e->ipf_rec.p, (uint32_t)n, &nbytes, &nm))) return rc;
+    if (nbytes > cap) return set_err(e, IPXG_ETOOBIG, "output buffer too small for the messages");
+    if (nbytes) {
+        HIPCHK(e, hipMemcpyAsync(out, e->ipf_msg.p, nbytes, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    *x = y;
+    *bytes = nbytes;
+    *msgs = nm;
+    return IPXG_OK;
+}
+
+int ipxg_device_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const uint8_t** dptr, size_t* n_records,
+                               size_t* bytes, size_t* msgs) {
+    if (!e || !x || !dptr || !n_records || !bytes || !msgs) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    const uint32_t pend = e->ex_count - e->ex_head;
+    int rc;
+    if ((rc = ipfix_messages(e, x, e->ex + e->ex_head, pend, bytes, msgs))) return rc;
+    *dptr = (const uint8_t*)e->ipf_msg.p;
+    *n_records = pend;
+    e->ex_head = e->ex_count = 0;  // consumed
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    return IPXG_OK;
+}
+
+int ipxg_poll_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, uint8_t* out, size_t cap, size_t* n_records,
+                             size_t* bytes, size_t* msgs) {
+    if (!e || !x || !n_records || !bytes || !msgs || (cap && !out)) return IPXG_EINVAL;
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    const uint32_t pend = e->ex_count - e->ex_head;
+    ipxg_ipfix_exporter y = *x;
+    size_t nbytes = 0, nm = 0;
+    int rc;
+    if ((rc = ipfix_messages(e, &y, e->ex + e->ex_head, pend, &nbytes, &nm))) return rc;
+    if (nbytes > cap) return set_err(e, IPXG_ETOOBIG, "output buffer too small for the messages");
+    if (nbytes) {
+        HIPCHK(e, hipMemcpyAsync(out, e->ipf_msg.p, nbytes, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    e->ex_head = e->ex_count = 0;
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    *x = y;
+    *n_records = pend;
+    *bytes = nbytes;
+    *msgs = nm;
+    return IPXG_OK;
+}
+
 int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n) {
     if (!e || !dptr || !n) return IPXG_EINVAL;
     {
@@ -900,6 +1148,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->batches = e->batches;
     out->spilled_packets = e->spilled;
     out->slow_path_packets = e->slow_pkts;
+    out->aggregated_packets = e->agg_pkts;
     return IPXG_OK;
 }
 

@@ -143,6 +143,20 @@ __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, 
 // the target of stores that carry no record (tile_emit; k_bin's prologue)
 __device__ uint4 g_dummy_rec[32 * 64];
 
+// one device atomic per wave for a per-lane count (convergent: every lane calls it)
+__device__ __forceinline__ void add_wave_sum(uint32_t* counter, uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane_id() == 0 && v) atomicAdd(counter, v);
+}
+
+// Without tile aggregation: rank every packet record in its partition.
+__device__ __forceinline__ void tile_rank_all(uint32_t* hist, uint32_t pmask, const uint32_t (&r1)[BIN_K],
+                                              uint32_t (&rk)[BIN_K]) {
+#pragma unroll
+    for (int q = 0; q < BIN_K; ++q)
+        if (rk[q] != NO_REC) rk[q] = atomicAdd(&hist[r1[q] & pmask], 1u);
+}
+
 // After tile_aggregate ranked the tile's packet records and aggregates in hist[part]: each
 // partition's slots of the tile follow the ones of the block's earlier tiles in the block's own
 // segment of that partition (fill[part] = slots so far), so no workgroup shares a write
@@ -155,7 +169,7 @@ __device__ uint4 g_dummy_rec[32 * 64];
 // would fit become NO_REC fillers, so k_reduce never reads half an aggregate).
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
-template <bool LISTED>
+template <bool LISTED, bool AGG>
 __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t pmask, const BinView& bv, uint32_t col,
                                           const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
                                           uint4* agg_list, const uint32_t (&r0)[BIN_K], const uint32_t (&r1)[BIN_K],
@@ -189,9 +203,9 @@ __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t 
         const uint32_t part = r1[q] & pmask;
         const uint32_t k = hist[part] + rk[q];
         stage[k] = make_uint4(r0[q], r1[q], idx, r2[q]);
-        L.part_of[k] = (uint16_t)part;
+        if (AGG) L.part_of[k] = (uint16_t)part;
     }
-    const uint32_t na = min(*L.nagg, TAGG_CAP);
+    const uint32_t na = AGG ? min(*L.nagg, TAGG_CAP) : 0;
     for (uint32_t a = threadIdx.x; a < na; a += IPXG_BLOCK) {
         const TileAgg& g = L.agg[a];
         FlowAgg f;
@@ -221,9 +235,9 @@ __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t 
         const uint32_t k = kk * IPXG_BLOCK + threadIdx.x;
         const bool valid = k < total;
         uint4 r = stage[valid ? k : 0];
-        const uint32_t part = L.part_of[valid ? k : 0];
+        const uint32_t part = AGG ? L.part_of[valid ? k : 0] : (r.y & pmask);
         const uint32_t pos = fill[part] + (k - hist[part]);
-        const bool agg = rec_is_agg(r);
+        const bool agg = AGG && rec_is_agg(r);
         const uint32_t ai = agg ? rec_agg_slot(r) : 0;
         const bool fits = valid && (pos - ai + (agg ? 3 : 1) <= bv.seg_cap);
         const bool filler = valid && !fits && pos < bv.seg_cap;  // part of an aggregate that spills
@@ -307,7 +321,7 @@ __device__ __forceinline__ void tile_rank(const Params& p, const BatchView& b, c
 template <bool LISTED>
 __device__ __forceinline__ void tile_aggregate(const BinLds& L, uint32_t pmask, uint32_t (&r0)[BIN_K],
                                                uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
-                                               const uint32_t (&ix)[BIN_K], uint32_t tile) {
+                                               const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& folded) {
     const uint32_t tid = threadIdx.x;
     unsigned long long* hk = reinterpret_cast<unsigned long long*>(L.stage);
     static_assert(TAGG_HASH * 8 <= BIN_TILE * 16, "tile hash keys live in the stage area");
@@ -371,6 +385,7 @@ __device__ __forceinline__ void tile_aggregate(const BinLds& L, uint32_t pmask, 
                 if (fl & 0x05) atomicMax(&g.fin_n[cdir], ~idx);
             }
             rk[q] = NO_REC;
+            folded++;
         } else {
             rk[q] = atomicAdd(&L.hist[r1[q] & pmask], 1u);
         }
@@ -392,18 +407,22 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 // does not take go to the slow list for k_bin_slow.  No LDS header staging here: LDS holds
 // the partition histogram, the block's segment fill counts, the tile's record stage and its
 // slow list.
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_BIN_WAVES)))
+// AGG: with the per-tile flow aggregation (76 KiB of LDS, 2 workgroups per CU); without it
+// 51 KiB (3 per CU).  The host picks the variant per batch (ipxg_engine.cpp setup_bins).
+template <bool AGG>
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG ? 2 : 3)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: slots in the block's segments
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: tile hash keys, then the slots by partition
-    __shared__ uint32_t tcnt[TAGG_HASH];                // 16 KiB: tile hash counts / aggregate ids
-    __shared__ TileAgg tagg[TAGG_CAP];                  // 8 KiB
-    __shared__ uint16_t part_of[BIN_TILE];              // 4 KiB
+    __shared__ uint32_t tcnt[AGG ? TAGG_HASH : 1];      // 16 KiB: tile hash counts / aggregate ids
+    __shared__ TileAgg tagg[AGG ? TAGG_CAP : 1];        // 8 KiB
+    __shared__ uint16_t part_of[AGG ? BIN_TILE : 1];    // 4 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t nagg;
     const BinLds L = {hist, fill, stage, tcnt, tagg, part_of, scan_s, &nagg};
+    uint32_t folded = 0;
     __shared__ uint32_t nslow[2];  // slow packets of the tile (by tile parity)
     // timestamps (sec << 32 | usec) of each step's first and last packet per wave: the order
     // check across wave boundaries, done once per tile (within a wave it is a DPP shift)
@@ -534,9 +553,10 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
-        tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile);
-        tile_emit<false>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile,
-                         spilled);
+        if (AGG) tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
+        else tile_rank_all(hist, pmask, r1, rk);
+        tile_emit<false, AGG>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix,
+                              tile, spilled);
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         slow_fill += nslow[par];  // final: read after the tile's barriers
@@ -576,6 +596,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         atomicAdd(&ctl->spilled, spilled);
         ctl->pending = 1;
     }
+    if (AGG) add_wave_sum(&ctl->agg_packets, folded);
 }
 
 // The frames k_bin left for the general parser (VLAN/QinQ, MPLS, PPPoE, GRE, TRILL, IPv6
@@ -583,20 +604,23 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 // or unaligned frames): staged in the lane's LDS column, parsed by parse_frame, ranked and
 // emitted exactly like k_bin's records.  The list length is read on the device.
 // 168 VGPRs (3 waves/SIMD = the LDS limit of 3 workgroups per CU)
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
+template <bool AGG>
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG ? 2 : 3)))
 void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
                 const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     // the header columns (parse), the tile hash and the tile's slots (emit) are never live
-    // together: one 32 KiB area; 76 KiB in all (2 workgroups per CU)
+    // together: one 32 KiB area; 76 KiB in all with aggregation (2 workgroups per CU), 48 KiB
+    // without (3 per CU)
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: header columns / tile hash / slots
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB
-    __shared__ uint32_t tcnt[TAGG_HASH];                // 16 KiB
-    __shared__ TileAgg tagg[TAGG_CAP];                  // 8 KiB
-    __shared__ uint16_t part_of[BIN_TILE];              // 4 KiB
+    __shared__ uint32_t tcnt[AGG ? TAGG_HASH : 1];      // 16 KiB
+    __shared__ TileAgg tagg[AGG ? TAGG_CAP : 1];        // 8 KiB
+    __shared__ uint16_t part_of[AGG ? BIN_TILE : 1];    // 4 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t nagg;
     const BinLds L = {hist, fill, stage, tcnt, tagg, part_of, scan_s, &nagg};
+    uint32_t folded = 0;
     static_assert(sizeof(stage) >= IPXG_WIN_DW * IPXG_BLOCK * 4, "header columns exceed the stage");
     uint32_t* win = reinterpret_cast<uint32_t*>(stage);
     // k_bin workgroup b's slow packets, into segment column bin_grid + b
@@ -641,8 +665,10 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             }
             tile_rank<true>(p, b, pk, d, i, j, r0, r1, r2, rk, ix);
         }
-        tile_aggregate<true>(L, pmask, r0, r1, r2, rk, ix, tile);
-        tile_emit<true>(L, P, pmask, bv, bcol, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile, spilled);
+        if (AGG) tile_aggregate<true>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
+        else tile_rank_all(hist, pmask, r1, rk);
+        tile_emit<true, AGG>(L, P, pmask, bv, bcol, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile,
+                             spilled);
     }
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, bcol);
@@ -654,12 +680,15 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         atomicAdd(&ctl->spilled, spilled);
         ctl->pending = 1;
     }
+    if (AGG) add_wave_sum(&ctl->agg_packets, folded);
 }
 
-uint32_t bin_resident_blocks(int device) {
+uint32_t bin_resident_blocks(int device, bool agg) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bin, IPXG_BLOCK, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, agg ? k_bin<true> : k_bin<false>, IPXG_BLOCK, 0) !=
+            hipSuccess ||
+        per_cu < 1)
         per_cu = 1;
     return (uint32_t)std::max(1, std::min(cus * per_cu, (int)BIN_MAX_GRID));
 }
@@ -667,15 +696,23 @@ uint32_t bin_resident_blocks(int device) {
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats) {
-    hipLaunchKernelGGL(k_bin, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
-                       deferred_list, agg_list, stats);
+    if (p.tile_agg)
+        hipLaunchKernelGGL(k_bin<true>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
+                           deferred_list, agg_list, stats);
+    else
+        hipLaunchKernelGGL(k_bin<false>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
+                           deferred_list, agg_list, stats);
 }
 
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                      BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
                      unsigned long long* stats) {
-    hipLaunchKernelGGL(k_bin_slow, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
-                       deferred_list, agg_list, stats);
+    if (p.tile_agg)
+        hipLaunchKernelGGL(k_bin_slow<true>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
+                           slow_list, deferred_list, agg_list, stats);
+    else
+        hipLaunchKernelGGL(k_bin_slow<false>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
+                           slow_list, deferred_list, agg_list, stats);
 }
 
 // ---- phase B ------------------------------------------------------------------------------

@@ -11,6 +11,8 @@
 // the v6 template, as get_template picks it, ipfix.cpp:287-291).  Three kernels: per-block
 // byte totals, one exclusive scan over the blocks, then each block stages its records in
 // LDS and writes its byte range with consecutive lanes on consecutive bytes.
+#include <algorithm>
+
 #include "ipxg_kernels.hpp"
 
 namespace ipxg {
@@ -136,6 +138,100 @@ __global__ __launch_bounds__(IPFIX_BLOCK) void k_ipfix_fill(const ipxg_flow_reco
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offsets[n] = block_base[gridDim.x];
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < total; k += IPFIX_BLOCK) out[base + k] = stage[k];
+}
+
+// ---- messages (ipxg_device_ipfix_messages): the exporter's message stream ----------------
+// Records feed the exporter v4-first (stable): a record's place is its rank among the records
+// of its template (class 0 = IPv4 template, 1 = IPv6).  The host plans the messages from the
+// two counts (IpfixSet / IpfixMsg below, a restatement of IPFIXExporter's buffer logic at the
+// granularity of whole data sets) and these kernels write every byte on the device.
+
+// per block: records of class 1 (IPv6 template)
+__global__ __launch_bounds__(IPFIX_BLOCK) void k_ipfix_count6(const ipxg_flow_record* rec, uint32_t n,
+                                                              uint64_t* block_tot) {
+    __shared__ uint32_t part[IPFIX_BLOCK / 64];
+    const uint32_t i = blockIdx.x * IPFIX_BLOCK + threadIdx.x;
+    const uint64_t m = __ballot(i < n && rec[i].ip_version == 6);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < IPFIX_BLOCK / 64; ++w) t += part[w];
+        block_tot[blockIdx.x] = t;
+    }
+}
+
+// one record per lane: its rank in its class -> its data set (binary search over the class's
+// sets, in rank order) -> its bytes
+__global__ __launch_bounds__(IPFIX_BLOCK) void k_ipfix_msg_fill(const ipxg_flow_record* rec, uint32_t n, uint32_t dir,
+                                                                const uint64_t* block_pre6, const IpfixSet* sets,
+                                                                uint32_t nsets4, uint32_t nsets6, uint8_t* out) {
+    __shared__ uint32_t wcnt[IPFIX_BLOCK / 64];
+    const uint32_t i = blockIdx.x * IPFIX_BLOCK + threadIdx.x;
+    const bool act = i < n;
+    const bool v6 = act && rec[i].ip_version == 6;
+    const uint64_t m = __ballot(v6);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t below6 = (uint32_t)__popcll(lane ? (m & (~0ull >> (64 - lane))) : 0ull);
+    for (uint32_t k = 0; k < w; ++k) below6 += wcnt[k];
+    if (!act) return;
+    const uint64_t pre6 = block_pre6[blockIdx.x] + below6;             // IPv6 records before i
+    const uint64_t ord = v6 ? pre6 : (uint64_t)i - pre6;                // rank in the class
+    const IpfixSet* s = v6 ? sets + nsets4 : sets;
+    uint32_t lo = 0, hi = v6 ? nsets6 : nsets4;                        // last set with ord0 <= ord
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s[mid].ord0 <= ord) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t len = v6 ? IPFIX_V6_LEN : IPFIX_V4_LEN;
+    uint8_t b[IPFIX_V6_LEN];
+    fill_basic(b, rec[i], dir);
+    uint8_t* p = out + s[lo].off + 4 + (ord - s[lo].ord0) * len;
+    for (uint32_t k = 0; k < len; ++k) p[k] = b[k];
+}
+
+// message headers (fill_ipfix_header) and data set headers (template id, length)
+__global__ __launch_bounds__(256) void k_ipfix_msg_headers(const IpfixMsg* msgs, uint32_t nmsgs, const IpfixSet* sets,
+                                                           uint32_t nsets, uint32_t odid, uint32_t export_time,
+                                                           uint8_t* out) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j < nmsgs) {
+        uint8_t* p = out + msgs[j].off;
+        put_be(p, 10, 2);
+        put_be(p + 2, msgs[j].len, 2);
+        put_be(p + 4, export_time, 4);
+        put_be(p + 8, msgs[j].seq, 4);
+        put_be(p + 12, odid, 4);
+    }
+    if (j < nsets) {
+        const IpfixSet& s = sets[j];
+        uint8_t* p = out + s.off;
+        put_be(p, s.cls ? 259 : 258, 2);
+        put_be(p + 2, 4 + s.count * (s.cls ? IPFIX_V6_LEN : IPFIX_V4_LEN), 2);
+    }
+}
+
+void launch_ipfix_count6(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint64_t* block_tot) {
+    const uint32_t nb = (n + IPFIX_BLOCK - 1) / IPFIX_BLOCK;
+    hipLaunchKernelGGL(k_ipfix_count6, dim3(nb), dim3(IPFIX_BLOCK), 0, st, rec, n, block_tot);
+    hipLaunchKernelGGL(k_ipfix_scan, dim3(1), dim3(1024), 0, st, block_tot, nb);
+}
+
+void launch_ipfix_messages(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir,
+                           const uint64_t* block_pre6, const IpfixSet* sets, uint32_t nsets4, uint32_t nsets6,
+                           const IpfixMsg* msgs, uint32_t nmsgs, uint32_t odid, uint32_t export_time, uint8_t* out) {
+    if (n) {
+        const uint32_t nb = (n + IPFIX_BLOCK - 1) / IPFIX_BLOCK;
+        hipLaunchKernelGGL(k_ipfix_msg_fill, dim3(nb), dim3(IPFIX_BLOCK), 0, st, rec, n, dir, block_pre6, sets, nsets4,
+                           nsets6, out);
+    }
+    const uint32_t nh = std::max(nmsgs, nsets4 + nsets6);
+    if (nh)
+        hipLaunchKernelGGL(k_ipfix_msg_headers, dim3((nh + 255) / 256), dim3(256), 0, st, msgs, nmsgs, sets,
+                           nsets4 + nsets6, odid, export_time, out);
 }
 
 void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,

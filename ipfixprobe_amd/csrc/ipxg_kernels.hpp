@@ -54,7 +54,7 @@ struct BatchCtl {
     uint32_t agg_deferred;   // tile aggregates whose table probe failed (3-slot list length)
     uint32_t max_part;       // most record slots in one partition (segment sizing, k_reduce)
     uint32_t total_slots;    // record slots over all partitions (k_reduce)
-    uint32_t pad_;
+    uint32_t agg_packets;    // packets folded into tile aggregates (k_bin / k_bin_slow)
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -99,6 +99,7 @@ struct Params {
     uint32_t force_complex;  // route every touched flow to the sequential path
     uint32_t prev_valid;     // prev_sec/prev_usec hold the previous batch's last timestamp
     uint32_t prev_sec, prev_usec;
+    uint32_t tile_agg;       // k_bin / k_bin_slow aggregate frequent flows per tile (skewed traffic)
 };
 
 struct BatchView {
@@ -159,8 +160,9 @@ struct ComplexView {
 };
 
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
-// k_bin workgroups resident on the whole device at once (its persistent grid)
-uint32_t bin_resident_blocks(int device);
+// k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
+// tile-aggregating variant (more LDS)
+uint32_t bin_resident_blocks(int device, bool agg);
 // deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
 // 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
@@ -198,6 +200,22 @@ void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, uns
 void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words);
 void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,
                         uint8_t* out, uint64_t* offsets);
+// IPFIX message plan (host, ipxg_engine.cpp): data sets in rank order per class (class 0 = the
+// IPv4 template's records, then class 1 = IPv6), and the messages.
+struct IpfixSet {
+    uint32_t cls, count;
+    uint64_t ord0;  // rank (in its class) of the set's first record
+    uint64_t off;   // byte offset of the set header in the output
+};
+struct IpfixMsg {
+    uint64_t off;
+    uint32_t len, seq;
+};
+// block_tot[nb + 1] <- exclusive prefix of the IPv6-template records per 256-record block (+ total)
+void launch_ipfix_count6(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint64_t* block_tot);
+void launch_ipfix_messages(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir,
+                           const uint64_t* block_pre6, const IpfixSet* sets, uint32_t nsets4, uint32_t nsets6,
+                           const IpfixMsg* msgs, uint32_t nmsgs, uint32_t odid, uint32_t export_time, uint8_t* out);
 void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail);
 void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl);
 void launch_parse_batch(hipStream_t st, const BatchView& b, uint32_t dlt, ipxg_parsed_pkt* out);

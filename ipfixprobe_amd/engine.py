@@ -52,6 +52,7 @@ STATS_FIELDS = [
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
     "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
+    "aggregated_packets",
 ]
 
 
@@ -81,13 +82,20 @@ class Capture(ctypes.Structure):
 
 IPFIX_V4_LEN, IPFIX_V6_LEN = 81, 105  # IPXG_IPFIX_V4_LEN / _V6_LEN
 
+
+class IpfixExporter(ctypes.Structure):
+    """ipxg_ipfix_exporter: the IPFIX exporter's state (include/ipxg.h)."""
+    _fields_ = [("odid", ctypes.c_uint32), ("dir_bit_field", ctypes.c_uint32), ("export_time", ctypes.c_uint32),
+                ("sequence", ctypes.c_uint32), ("mtu", ctypes.c_uint16), ("templates_sent", ctypes.c_uint16)]
+
 EXPORTED_SYMBOLS = [
     "ipxg_config_default", "ipxg_config_parse", "ipxg_create", "ipxg_destroy",
     "ipxg_last_error", "ipxg_stream", "ipxg_submit", "ipxg_expire", "ipxg_finish",
     "ipxg_reset", "ipxg_pending_exports", "ipxg_poll_exports", "ipxg_device_exports",
     "ipxg_clear_exports", "ipxg_get_stats", "ipxg_parse_batch", "ipxg_xxh64_batch",
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
-    "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix",
+    "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
+    "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
 ]
 
 _LIB = None
@@ -138,9 +146,19 @@ def lib():
         L.ipxg_probe_counters.argtypes = [vp, vp]
         L.ipxg_ipfix_basic.argtypes = [vp, vp, sz, u32, vp, vp]
         L.ipxg_poll_ipfix.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        px = ctypes.POINTER(IpfixExporter)
+        L.ipxg_ipfix_exporter_init.argtypes = [px]
+        L.ipxg_ipfix_exporter_init.restype = None
+        L.ipxg_ipfix_bound.argtypes = [ctypes.c_uint64]
+        L.ipxg_ipfix_bound.restype = ctypes.c_uint64
+        L.ipxg_ipfix_export.argtypes = [vp, px, vp, sz, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.ipxg_poll_ipfix_messages.argtypes = [vp, px, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz),
+                                               ctypes.POINTER(sz)]
+        L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
+                                                 ctypes.POINTER(sz), ctypes.POINTER(sz)]
         for name in EXPORTED_SYMBOLS:
             if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default",
-                            "ipxg_capture_free"):
+                            "ipxg_capture_free", "ipxg_ipfix_exporter_init", "ipxg_ipfix_bound"):
                 getattr(L, name).restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -317,6 +335,42 @@ class Engine:
         self._check(lib().ipxg_poll_ipfix(self._h, dir_bit_field, out.ctypes.data, cap, ctypes.byref(n),
                                           ctypes.byref(nb)), "ipxg_poll_ipfix")
         return out[: nb.value], n.value
+
+    @staticmethod
+    def ipfix_exporter(odid=0, dir_bit_field=0, export_time=0, mtu=1458):
+        x = IpfixExporter()
+        lib().ipxg_ipfix_exporter_init(ctypes.byref(x))
+        x.odid, x.dir_bit_field, x.export_time, x.mtu = odid, dir_bit_field, export_time, mtu
+        return x
+
+    def ipfix_export(self, x, recs):
+        """Host records (FLOW_DTYPE) through the exporter state x: (message bytes, messages)."""
+        recs = np.ascontiguousarray(recs, dtype=FLOW_DTYPE)
+        cap = int(lib().ipxg_ipfix_bound(len(recs)))
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        nb, nm = ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(lib().ipxg_ipfix_export(self._h, ctypes.byref(x), recs.ctypes.data if len(recs) else None,
+                                            len(recs), out.ctypes.data, cap, ctypes.byref(nb), ctypes.byref(nm)),
+                    "ipxg_ipfix_export")
+        return out[:nb.value], nm.value
+
+    def poll_ipfix_messages(self, x):
+        """Pending exports as IPFIX messages (consumed): (bytes, records, messages)."""
+        cap = int(lib().ipxg_ipfix_bound(self.pending()))
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        nr, nb, nm = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(lib().ipxg_poll_ipfix_messages(self._h, ctypes.byref(x), out.ctypes.data, cap, ctypes.byref(nr),
+                                                   ctypes.byref(nb), ctypes.byref(nm)), "ipxg_poll_ipfix_messages")
+        return out[:nb.value], nr.value, nm.value
+
+    def device_ipfix_messages(self, x):
+        """Pending exports as IPFIX messages in an engine-owned device buffer (consumed):
+        (device pointer, bytes, records, messages); valid until the next engine call."""
+        p = ctypes.c_void_p()
+        nr, nb, nm = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(lib().ipxg_device_ipfix_messages(self._h, ctypes.byref(x), ctypes.byref(p), ctypes.byref(nr),
+                                                     ctypes.byref(nb), ctypes.byref(nm)), "ipxg_device_ipfix_messages")
+        return p.value, nb.value, nr.value, nm.value
 
     def parse(self, arena, desc):
         b = self._batch(arena, desc)

@@ -1116,3 +1116,161 @@ void oracle_ipfix_basic(const ipxg_flow_record* recs, size_t n, uint32_t dir_bit
         offsets[i + 1] = (uint64_t)(p - out);
     }
 }
+
+/* ===================================================================================== */
+/* IPFIX messages -- IPFIXExporter (src/plugins/output/ipfix/src/ipfix.cpp) over the       */
+/* basic templates, TCP transport (templates sent once, no refresh: ipfix.hpp:52,66)      */
+/* ===================================================================================== */
+typedef struct {
+    uint16_t id;
+    uint8_t rec[128]; /* templateRecord */
+    uint16_t rec_size;
+    uint8_t buf[65536]; /* template buffer: data set header + records */
+    uint32_t buf_size, count;
+    int exported;
+} otmpl;
+
+typedef struct {
+    ipxg_ipfix_exporter* x;
+    otmpl t[2];  /* the template list: [0] = IPv6 (259, created second, list head), [1] = IPv4 */
+    int have;    /* templates created (get_template on the first flow) */
+    uint8_t* out;
+    size_t cap, len, msgs;
+    int overflow;
+} oexp;
+
+static void be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+static void be32(uint8_t* p, uint32_t v)
+{
+    for (int k = 0; k < 4; ++k) p[k] = (uint8_t)(v >> (24 - 8 * k));
+}
+
+/* create_template ipfix.cpp:537-656 (fields from the template-file table = ipfix-elements.hpp) */
+static void otmpl_create(otmpl* t, uint16_t id, const ipfix_elem* el, size_t ne, uint32_t mtu)
+{
+    memset(t, 0, sizeof(*t));
+    t->id = id;
+    be16(t->rec, id);
+    uint16_t sz = 4;
+    for (size_t k = 0; k < ne; ++k) {
+        be16(t->rec + sz, el[k].id | (el[k].en ? 0x8000 : 0));
+        be16(t->rec + sz + 2, (uint32_t)el[k].len);
+        sz += 4;
+        if (el[k].en) {
+            be32(t->rec + sz, el[k].en);
+            sz += 4;
+        }
+    }
+    be16(t->rec + 2, (uint32_t)ne);
+    t->rec_size = sz;
+    be16(t->buf, id); /* init_template_buffer :414-417 */
+    t->buf_size = 4;
+    (void)mtu;
+}
+
+static void oexp_emit(oexp* e, const uint8_t* msg, size_t n)
+{
+    if (e->len + n > e->cap) {
+        e->overflow = 1;
+    } else {
+        memcpy(e->out + e->len, msg, n);
+    }
+    e->len += n;
+    e->msgs++;
+}
+
+/* fill_ipfix_header :475-486 */
+static void ohdr(oexp* e, uint8_t* p, uint32_t size)
+{
+    be16(p, 10);
+    be16(p + 2, size);
+    be32(p + 4, e->x->export_time);
+    be32(p + 8, e->x->sequence);
+    be32(p + 12, e->x->odid);
+}
+
+/* flush :846-853 = send_templates (create_template_packet :671-728) + send_data
+ * (create_data_packet :739-795 until it returns 0); send_packet adds packet->flows to the
+ * sequence number (:945) */
+static void oexp_flush(oexp* e)
+{
+    static uint8_t msg[65536];
+    if (!e->have) return;
+    uint32_t total = 0;
+    for (int k = 0; k < 2; ++k)
+        if (!e->t[k].exported) total += e->t[k].rec_size;
+    if (total) {
+        total += 16 + 4;
+        ohdr(e, msg, total);
+        be16(msg + 16, 2); /* TEMPLATE_SET_ID */
+        be16(msg + 18, total - 16);
+        uint32_t p = 20;
+        for (int k = 0; k < 2; ++k)
+            if (!e->t[k].exported) {
+                memcpy(msg + p, e->t[k].rec, e->t[k].rec_size);
+                p += e->t[k].rec_size;
+                e->t[k].exported = 1;
+            }
+        oexp_emit(e, msg, total);
+        e->x->templates_sent = 1;
+    }
+    for (;;) {
+        uint32_t size = 16, flows = 0;
+        for (int k = 0; k < 2; ++k) {
+            otmpl* t = &e->t[k];
+            if (t->count > 0 && size + t->buf_size <= e->x->mtu) {
+                memcpy(msg + size, t->buf, t->buf_size);
+                be16(msg + size + 2, t->buf_size);
+                size += t->buf_size;
+                t->buf_size = 4;
+                flows += t->count;
+                t->count = 0;
+            }
+        }
+        if (size == 16) break;
+        ohdr(e, msg, size);
+        oexp_emit(e, msg, size);
+        e->x->sequence += flows;
+    }
+}
+
+/* fill_template :350-382 / fill_basic_flow :1470-1516: -1 when the record passes the buffer
+ * limit mtu - IPFIX_HEADER_SIZE */
+static int oexp_fill(oexp* e, otmpl* t, const ipxg_flow_record* r)
+{
+    const uint32_t len = r->ip_version == 4 ? 81 : 105;
+    if (t->buf_size + len > (uint32_t)e->x->mtu - 16) return -1;
+    uint64_t off[2];
+    oracle_ipfix_basic(r, 1, e->x->dir_bit_field, t->buf + t->buf_size, off);
+    t->buf_size += len;
+    t->count++;
+    return 0;
+}
+
+size_t oracle_ipfix_export(ipxg_ipfix_exporter* x, const ipxg_flow_record* recs, size_t n, uint8_t* out, size_t cap,
+                           size_t* msgs)
+{
+    static oexp e; /* test infrastructure: one exporter at a time */
+    memset(&e, 0, sizeof(e));
+    e.x = x;
+    e.out = out;
+    e.cap = cap;
+    /* get_template :287-323 creates both basic templates on the first flow: v4 first (id 258),
+     * then v6 (259), each pushed at the list head */
+    if (n) {
+        otmpl_create(&e.t[1], 258, basic_v4, sizeof(basic_v4) / sizeof(basic_v4[0]), x->mtu);
+        otmpl_create(&e.t[0], 259, basic_v6, sizeof(basic_v6) / sizeof(basic_v6[0]), x->mtu);
+        e.t[0].exported = e.t[1].exported = x->templates_sent;
+        e.have = 1;
+    }
+    for (size_t i = 0; i < n; ++i) { /* export_flow :385-398 */
+        otmpl* t = recs[i].ip_version == 6 ? &e.t[0] : &e.t[1];
+        if (oexp_fill(&e, t, &recs[i]) != 0) {
+            oexp_flush(&e);
+            oexp_fill(&e, t, &recs[i]);
+        }
+    }
+    oexp_flush(&e); /* the output worker's flush when its queue runs dry (workers.cpp:176-183) */
+    if (msgs) *msgs = e.msgs;
+    return e.overflow ? (size_t)-1 : e.len;
+}

@@ -66,6 +66,12 @@ void oracle_cache_stats(const oracle_cache* c, ipxg_stats* out);
 void oracle_ipfix_basic(const ipxg_flow_record* recs, size_t n, uint32_t dir_bit_field, uint8_t* out,
                         uint64_t* offsets);
 
+/* IPFIXExporter::export_flow for each record in order, then flush(): the message bytes into
+ * out (returns their length, (size_t)-1 if cap is short); updates x->sequence and
+ * x->templates_sent like the exporter's state. */
+size_t oracle_ipfix_export(ipxg_ipfix_exporter* x, const ipxg_flow_record* recs, size_t n, uint8_t* out, size_t cap,
+                           size_t* msgs);
+
 #ifdef __cplusplus
 }
 #endif

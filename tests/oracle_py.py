@@ -40,6 +40,8 @@ def lib():
         L.oracle_cache_take.argtypes = [vp, vp, ctypes.c_size_t]
         L.oracle_ipfix_basic.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
         L.oracle_cache_stats.argtypes = [vp, vp]
+        L.oracle_ipfix_export.restype = ctypes.c_size_t
+        L.oracle_ipfix_export.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_bench_mt.restype = ctypes.c_double
         L.oracle_bench_mt.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
@@ -132,6 +134,31 @@ def ipfix_basic(recs, dir_bit_field=0):
     off = np.zeros(len(recs) + 1, dtype=np.uint64)
     lib().oracle_ipfix_basic(recs.ctypes.data, len(recs), dir_bit_field, out.ctypes.data, off.ctypes.data)
     return out[: int(off[-1])], off
+
+
+class IpfixExporterState(ctypes.Structure):
+    """ipxg_ipfix_exporter (include/ipxg.h) for the oracle's exporter."""
+    _fields_ = [("odid", ctypes.c_uint32), ("dir_bit_field", ctypes.c_uint32), ("export_time", ctypes.c_uint32),
+                ("sequence", ctypes.c_uint32), ("mtu", ctypes.c_uint16), ("templates_sent", ctypes.c_uint16)]
+
+
+def ipfix_exporter(odid=0, dir_bit_field=0, export_time=0, mtu=1458):
+    x = IpfixExporterState()
+    x.odid, x.dir_bit_field, x.export_time, x.mtu = odid, dir_bit_field, export_time, mtu
+    return x
+
+
+def ipfix_export(x, recs):
+    """IPFIXExporter::export_flow per record in the given order, then flush() (oracle): (bytes,
+    messages); x (IpfixExporterState) is updated like the exporter's state."""
+    recs = np.ascontiguousarray(recs, dtype=FLOW_DTYPE)
+    cap = 196 + len(recs) * 125 + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    nm = ctypes.c_size_t()
+    n = lib().oracle_ipfix_export(ctypes.byref(x), recs.ctypes.data if len(recs) else None, len(recs),
+                                  out.ctypes.data, cap, ctypes.byref(nm))
+    assert n != ctypes.c_size_t(-1).value
+    return out[:n], nm.value
 
 
 def run_capture(arena, desc, datalink=1, finish=True, **kw):

@@ -60,6 +60,7 @@ STATS_FIELDS = [
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
     "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
+    "aggregated_packets",
 ]
 
 
@@ -111,7 +112,8 @@ def _read_pcapng(d):
             res = ifaces[iid][1]
             sec, frac = divmod(t, res)
             if res != 1000000:
-                frac = frac * 1000000 // res if res < 1000000 else frac // (res // 1000000)
+                dec = res == 10 ** (len(str(res)) - 1)
+                frac = frac // (res // 1000000) if (dec and res > 1000000) else frac * 1000000 // res
             pkts.append((sec, frac, cl, wl, body[20:20 + cl]))
         elif btype == 3:  # SPB
             wl = struct.unpack(e + "I", body[:4])[0]

@@ -74,3 +74,54 @@ def test_no_gpu_fails_loudly():
     from ipfixprobe_amd import Engine, IpxgError
     with pytest.raises(IpxgError):
         Engine()
+
+
+def _pcapng(path, tsresol, stamps):
+    """A little-endian pcapng: SHB, one Ethernet IDB with if_tsresol = tsresol (None: no
+    option), one EPB per raw timestamp in `stamps` (a 60-byte frame each)."""
+    import struct
+
+    def block(bt, body):
+        body = body + b"\0" * ((4 - len(body) % 4) % 4)
+        n = 12 + len(body)
+        return struct.pack("<II", bt, n) + body + struct.pack("<I", n)
+
+    out = block(0x0A0D0D0A, struct.pack("<IHHq", 0x1A2B3C4D, 1, 0, -1))
+    opts = b""
+    if tsresol is not None:
+        opts = struct.pack("<HH", 9, 1) + bytes([tsresol]) + b"\0\0\0" + struct.pack("<HH", 0, 0)
+    out += block(1, struct.pack("<HHI", 1, 0, 65535) + opts)
+    frame = bytes(12) + b"\x08\x00" + bytes(46)
+    for t in stamps:
+        out += block(6, struct.pack("<IIIII", 0, t >> 32, t & 0xFFFFFFFF, len(frame), len(frame)) + frame)
+    with open(path, "wb") as f:
+        f.write(out)
+
+
+@pytest.mark.parametrize("tsresol,unit", [(None, 10**6), (9, 10**9), (3, 10**3), (0x94, 2**20), (0x8A, 2**10),
+                                          (0xBF, 2**63)])
+def test_pcapng_tsresol_conversion(tmp_path, tsresol, unit):
+    """if_tsresol as libpcap converts it: a decimal resolution finer than 1 us divides by the
+    power of ten, anything else scales frac * 10^6 / resolution (binary 2^-20 was
+    left unscaled)."""
+    from ipfixprobe_amd import load_capture
+    stamps = [unit - 1, unit, unit + unit // 2 + 1, 3 * unit + 12345 % unit if unit < 2**62 else unit + 7]
+    p = str(tmp_path / "t.pcapng")
+    _pcapng(p, tsresol, stamps)
+    _, desc, _ = load_capture(p)
+    _, pk = pcaputil.read_capture(p)
+    want = [(t // unit, (t % unit) * 10**6 // unit) for t in stamps]
+    assert [(int(d["ts_sec"]), int(d["ts_usec"])) for d in desc] == want
+    assert [(k[0], k[1]) for k in pk] == want
+    assert all(u < 10**6 for _, u in want)
+
+
+@pytest.mark.parametrize("tsresol", [20, 64, 0x7F, 0xC0, 0xFF])
+def test_pcapng_tsresol_out_of_range_is_rejected(tmp_path, tsresol):
+    """A resolution of 10^20 or 2^64 and beyond does not fit 64 bits: the reader rejects the
+    capture (IPXG_EIO) instead of dividing by zero / shifting out of range."""
+    from ipfixprobe_amd import IpxgError, load_capture
+    p = str(tmp_path / "t.pcapng")
+    _pcapng(p, tsresol, [123456789])
+    with pytest.raises(IpxgError):
+        load_capture(p)

@@ -273,9 +273,10 @@ def _udp_batch(rng, flow_of_pkt, n_flows, reverse_share=0.5):
                             np.where(rev, dp[f], sp[f]), np.where(rev, sp[f], dp[f]))
 
 
-def test_elephant_flow_spills_and_multi_chunk():
-    """Half of 200k packets in one biflow: its partition overflows its region (spill to
-    device atomics) and spans several k_reduce workgroups (atomic merge, table scan)."""
+def test_elephant_flow_aggregated_per_tile():
+    """Half of 200k packets in one biflow: each k_bin tile folds the elephant's ~1000 packets
+    into one aggregate record (tile aggregation, first batch), so its partition's segments do
+    not overflow; the records match the oracle."""
     from ipfixprobe_amd import run_capture
     rng = np.random.default_rng(21)
     n, F = 200_000, 5000
@@ -283,7 +284,31 @@ def test_elephant_flow_spills_and_multi_chunk():
     arena, desc = _udp_batch(rng, fop, F)
     want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
     got, st = run_capture(arena, desc, params="s=16")
-    assert st["spilled_packets"] > 0
+    assert st["aggregated_packets"] >= n // 2 - 2000 and st["spilled_packets"] == 0
+    d = flowcmp.diff(got, want)
+    assert not d, d
+
+
+@pytest.mark.parametrize("agg", ["0", "1"])
+def test_elephant_flow_spill_path(monkeypatch, agg):
+    """The same elephant with the segments forced small (IPXG_TILE_AGG / IPXG_PART_BITS tuning
+    knobs are read per batch): records that do not fit their segment spill to device atomics
+    (packet records, or whole aggregates) and the records still match the oracle."""
+    from ipfixprobe_amd import Engine
+    rng = np.random.default_rng(23)
+    n, F = 200_000, 5000
+    fop = np.where(rng.random(n) < 0.5, 0, rng.integers(1, F, n))
+    arena, desc = _udp_batch(rng, fop, F)
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    monkeypatch.setenv("IPXG_TILE_AGG", agg)
+    monkeypatch.setenv("IPXG_PART_BITS", "8")
+    with Engine("s=16") as e:
+        e.submit(arena, desc[:1000])  # first batch: the knob takes effect from the next one
+        e.submit(arena, desc[1000:])
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert st["spilled_packets"] > 0 if agg == "0" else st["aggregated_packets"] > 0
     d = flowcmp.diff(got, want)
     assert not d, d
 

@@ -133,3 +133,118 @@ def _split(stream):
         k += n
     assert k == len(stream)
     return out
+
+
+# ---- IPFIX messages: templates + MTU-bounded data messages (ipfix.cpp:385-398, 537-795) ------
+import json  # noqa: E402
+
+import ipfixdec  # noqa: E402
+
+GOLDEN_TMPL = os.path.join(os.path.dirname(__file__), "golden", "ipfix_basic_templates.json")
+
+
+def _v4_first(recs):
+    return np.concatenate([recs[recs["ip_version"] != 6], recs[recs["ip_version"] == 6]])
+
+
+def test_oracle_templates_match_reference_header():
+    """The template message's records equal BASIC_TMPLT_V4/V6 as the reference header expands
+    them (tests/golden/gen_ipfix_template.py compiles ipfix-elements.hpp), ids 258 / 259."""
+    with open(GOLDEN_TMPL) as f:
+        gold = json.load(f)
+    recs = _random_records(2, seed=3)
+    recs["ip_version"] = [4, 6]
+    b, nm = oracle_py.ipfix_export(oracle_py.ipfix_exporter(), recs)
+    msgs, tmpl, _, _, _ = ipfixdec.decode(b)
+    assert msgs[0]["sets"][0][0] == 2 and len(msgs[0]["sets"]) == 1
+    assert [list(t) for t in tmpl[258]] == gold["BASIC_TMPLT_V4"]
+    assert [list(t) for t in tmpl[259]] == gold["BASIC_TMPLT_V6"]
+
+
+def test_oracle_ntp_matches_reference_macro():
+    with open(GOLDEN_TMPL) as f:
+        gold = json.load(f)
+    r = np.zeros(len(gold["MK_NTP_TS"]), dtype=FLOW_DTYPE)
+    r["ip_version"] = 4
+    r["time_first_sec"] = [g[0] for g in gold["MK_NTP_TS"]]
+    r["time_first_usec"] = [g[1] for g in gold["MK_NTP_TS"]]
+    got, off = oracle_py.ipfix_basic(r, 0)
+    for i, g in enumerate(gold["MK_NTP_TS"]):
+        o = int(off[i]) + 33  # FLOW_START after end reason, bytes x2, packets x2
+        assert bytes(got[o:o + 8]).hex() == g[2]
+
+
+@pytest.mark.parametrize("n,share6,mtu", [(0, 0.5, 1458), (1, 0.0, 1458), (17, 0.0, 1458), (18, 0.0, 1458),
+                                          (13, 1.0, 1458), (14, 1.0, 1458), (30, 0.3, 1458), (1000, 0.4, 1458),
+                                          (777, 0.5, 9000), (500, 0.5, 125), (300, 0.1, 1500)])
+def test_oracle_message_stream_structure(n, share6, mtu):
+    """Every message of the oracle's stream is well formed and <= mtu, the template message
+    comes once and first, sequence numbers count the records of earlier data messages, and the
+    records decode back to the input."""
+    rng = np.random.default_rng(n)
+    recs = _random_records(n, seed=n)
+    recs["ip_version"] = np.where(rng.random(n) < share6, 6, 4)
+    x = oracle_py.ipfix_exporter(odid=42, dir_bit_field=5, export_time=1_700_000_000, mtu=mtu)
+    b, nm = oracle_py.ipfix_export(x, recs)
+    if n == 0:
+        assert len(b) == 0 and nm == 0 and x.templates_sent == 0
+        return
+    msgs, tmpl, got, where, dirs = ipfixdec.decode(b)
+    assert len(msgs) == nm and x.templates_sent == 1 and x.sequence == n
+    assert msgs[0]["sets"][0][0] == 2 and all(s[0] != 2 for m in msgs[1:] for s in m["sets"])
+    seq = 0
+    for m in msgs:  # the template message is not bounded by mtu (create_template_packet :671-728)
+        assert (m["length"] <= mtu or m["sets"][0][0] == 2) and m["odid"] == 42 and m["export_time"] == 1_700_000_000
+        assert m["sequence"] == seq
+        seq += m["records"]
+    assert dirs == {5}
+    assert ipfixdec.basic_view(got) == ipfixdec.basic_view(recs)
+    # a second call: no template message, the sequence continues
+    b2, _ = oracle_py.ipfix_export(x, recs[:3])
+    m2, _, _, _, _ = ipfixdec.decode(b2, tmpl)
+    assert all(s[0] != 2 for m in m2 for s in m["sets"]) and m2[0]["sequence"] == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,share6,mtu", [(1, 0.0, 1458), (17, 0.0, 1458), (18, 0.0, 1458), (14, 1.0, 1458),
+                                          (30, 0.3, 1458), (1000, 0.4, 1458), (777, 0.5, 9000), (500, 0.5, 125),
+                                          (50_000, 0.2, 1458), (300_000, 0.5, 1500)])
+def test_device_messages_equal_oracle(n, share6, mtu):
+    """ipxg_ipfix_export (records fed v4-first, formatted and packed on the device) is byte
+    for byte the oracle exporter over the same record order, across two calls (exporter state
+    carried: templates once, sequence numbers continue)."""
+    from ipfixprobe_amd import Engine
+    rng = np.random.default_rng(n + 1)
+    recs = _random_records(n, seed=n + 1)
+    recs["ip_version"] = np.where(rng.random(n) < share6, 6, 4)
+    with Engine() as e:
+        xd = e.ipfix_exporter(odid=9, dir_bit_field=3, export_time=1_600_000_123, mtu=mtu)
+        xo = oracle_py.ipfix_exporter(odid=9, dir_bit_field=3, export_time=1_600_000_123, mtu=mtu)
+        for part in (recs, recs[: n // 3]):
+            got, gm = e.ipfix_export(xd, part)
+            want, wm = oracle_py.ipfix_export(xo, _v4_first(part))
+            assert gm == wm and len(got) == len(want)
+            assert bytes(got) == bytes(want)
+            assert (xd.sequence, xd.templates_sent) == (xo.sequence, xo.templates_sent)
+
+
+@pytest.mark.gpu
+def test_poll_ipfix_messages_from_flow_cache():
+    """A capture through the engine, exported as IPFIX messages straight from the device export
+    buffer: the decoded records are the oracle's flow records (basic fields)."""
+    from ipfixprobe_amd import Engine
+    arena, desc = synth.flow_stream(seed=21, n_flows=400, n_pkts=8000).batch()
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    with Engine() as e:
+        e.submit(arena, desc)
+        e.finish()
+        x = e.ipfix_exporter(odid=1, export_time=77)
+        b, nrec, nm = e.poll_ipfix_messages(x)
+        assert e.pending() == 0
+    msgs, _, got, _, _ = ipfixdec.decode(b)
+    assert nrec == len(want) == len(got) and nm == len(msgs)
+    w = want.copy()
+    w["end_reason"] = got["end_reason"][0]  # reasons differ by design (FORCED vs sweep), see flowcmp
+    g = got.copy()
+    g["end_reason"] = w["end_reason"][0]
+    assert ipfixdec.basic_view(g) == ipfixdec.basic_view(w)
