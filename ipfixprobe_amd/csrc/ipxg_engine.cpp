@@ -475,13 +475,13 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     BinView bins = {};
     if (binned) {
         if ((rc = setup_bins(e, n, bins))) return rc;
-        if ((rc = ensure(e, e->fin_list, (size_t)n * 4))) return rc;
+        if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
     }
     ev_rec(e, 0);
     if (binned) {
         uint32_t* dl = (uint32_t*)e->defer_a.p;
         uint32_t* sl = (uint32_t*)e->slow_list.p;
-        uint32_t* fl = (uint32_t*)e->fin_list.p;
+        HotSlot* fl = (HotSlot*)e->fin_list.p;
         uint4* al = (uint4*)e->adefer_a.p;
         launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 1);

@@ -376,7 +376,7 @@ __device__ __forceinline__ void tile_aggregate(const BinLds& L, uint32_t pmask, 
             const uint32_t cdir = misc_dir(m);
             atomicAdd(&g.acc[cdir], (1ull << 40) | (unsigned long long)misc_len(m));
             atomicMax(&g.last1, idx + 1);
-            atomicMax(&g.first_n, ~idx);
+            atomicMax(&g.first_n, first_key(idx, m));
             atomicOr(&g.tbits, 1u << misc_tb(m));
             const uint32_t fl = misc_flags(m);
             if (misc_tcp(m) && fl) {
@@ -736,7 +736,7 @@ __device__ __forceinline__ void lds_fold(FlowAgg& a, uint32_t idx, uint32_t m) {
     const uint32_t cdir = misc_dir(m);
     atomicAdd(&a.acc[cdir], (1ull << 40) | (unsigned long long)misc_len(m));
     atomicMax(&a.last1, idx + 1);
-    atomicMax(&a.first_n, ~idx);
+    atomicMax(&a.first_n, first_key(idx, m));
     atomicOr(&a.tbits, 1u << misc_tb(m));
     const uint32_t fl = misc_flags(m);
     if (misc_tcp(m) && fl) {
@@ -750,15 +750,19 @@ enum RedCount { C_KEYS, C_TOUCH, C_SPILL, C_FAIL, C_N };
 constexpr uint32_t RED_MAX_COLS = 2 * BIN_MAX_GRID;
 
 // record k (0 <= k < total) of the partition: in the segment s with pre[s] <= k < pre[s+1]
+__device__ __forceinline__ const uint4* seg_ptr(const uint4* segs, const uint32_t* pre, uint32_t cols,
+                                                uint32_t seg_cap, uint32_t k) {
+    uint32_t lo = 0;  // the last s with pre[s] <= k: a fixed number of steps, no branches
+#pragma unroll
+    for (uint32_t step = RED_MAX_COLS / 2; step; step >>= 1) {
+        const uint32_t m = lo + step;
+        lo = (m < cols && pre[m] <= k) ? m : lo;
+    }
+    return segs + (size_t)lo * seg_cap + (k - pre[lo]);
+}
 __device__ __forceinline__ uint4 seg_record(const uint4* segs, const uint32_t* pre, uint32_t cols,
                                             uint32_t seg_cap, uint32_t k) {
-    uint32_t lo = 0, hi = cols;  // pre[lo] <= k < pre[hi]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= k) lo = mid;
-        else hi = mid;
-    }
-    return segs[(size_t)lo * seg_cap + (k - pre[lo])];
+    return *seg_ptr(segs, pre, cols, seg_cap, k);
 }
 
 __device__ __forceinline__ void lds_fold_agg(FlowAgg& e, const FlowAgg& a) {
@@ -777,9 +781,11 @@ __device__ __forceinline__ void lds_fold_agg(FlowAgg& e, const FlowAgg& a) {
 // Fold one record slot into the workgroup's LDS flow table (or straight into the device table
 // when the LDS table is full).  rp = the slot's address (an aggregate's head reads its two
 // payload slots after it; the payload slots themselves are skipped).
+// ok: the slot exists (tested here, not by overwriting the loaded value: a write into the
+// load's destination made the compiler wait for each load as soon as it was issued)
 __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
-                                           uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp) {
-    if (r.z == NO_REC) return;
+                                           uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp, bool ok) {
+    if (!ok || r.z == NO_REC) return;
     if (rec_is_agg(r)) {
         if (rec_agg_slot(r) != 0) return;
         const uint4 s1 = rp[1], s2 = rp[2];
@@ -806,7 +812,7 @@ __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, Batc
 // One workgroup per partition: the partition's records sit in one segment per k_bin /
 // k_bin_slow workgroup (bv.count gives their lengths); a prefix sum over the segment lengths
 // in LDS maps the partition's record k to its segment.
-__global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
+__global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                                                         uint32_t* deferred_list, uint4* agg_list) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
     __shared__ uint32_t pre[RED_MAX_COLS + 1];
@@ -859,35 +865,59 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __syncthreads();
     PROBE_T(q1t);
     const uint4* segs = bv.rec + (size_t)part * bv.cols * bv.seg_cap;
-    // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
-    // loads, no search); a segment longer than a wave loops (wave-uniform).
     const uint32_t lane = tid & 63, wave = tid >> 6;
     constexpr uint32_t NW = RED_THREADS / 64;
-    for (uint32_t s0 = wave; s0 < nseg; s0 += NW * RED_U) {
-        uint4 r[RED_U];
-        uint32_t sc[RED_U], sl[RED_U];
+    if (total < nseg * 16) {
+        // Short segments (many partitions and workgroups for the batch: ~2-5 records per
+        // segment with 1M flows): a wave per segment would leave most lanes idle, so each
+        // thread takes record k of the partition, found by a binary search over the segment
+        // prefix in LDS (consecutive threads, consecutive records within a segment).
+        for (uint32_t k0 = 0; k0 < total; k0 += RED_THREADS * RED_U) {
+            uint4 r[RED_U];
+            const uint4* rp[RED_U];
 #pragma unroll
-        for (uint32_t u = 0; u < RED_U; ++u) {
-            const uint32_t si = s0 + u * NW;
-            sc[u] = si < nseg ? ne[si] : 0;
-            sl[u] = si < nseg ? pre[sc[u] + 1] - pre[sc[u]] : 0;
-            const bool ok = lane < sl[u];
-#ifdef IPXG_RED_NT  // tuning knob: streaming loads of the records (read once)
-            r[u] = u4(__builtin_nontemporal_load(
-                reinterpret_cast<const u32x4*>(&segs[(size_t)sc[u] * bv.seg_cap + (ok ? lane : 0)])));
-#else
-            r[u] = segs[(size_t)sc[u] * bv.seg_cap + (ok ? lane : 0)];  // unconditional load
-#endif
-            if (!ok) r[u].z = NO_REC;
+            for (uint32_t u = 0; u < RED_U; ++u) {
+                const uint32_t k = k0 + u * RED_THREADS + tid;
+                rp[u] = k < total ? seg_ptr(segs, pre, cols, bv.seg_cap, k) : segs;
+                r[u] = *rp[u];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < RED_U; ++u)
+                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], rp[u], k0 + u * RED_THREADS + tid < total);
         }
+    } else {
+        // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
+        // loads, no search); a segment longer than a wave loops (wave-uniform).  The segments'
+        // positions are wave-uniform (scalar), read before the loads are issued, so no branch
+        // separates a load from its use.
+        const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+        for (uint32_t s0 = wv; s0 < nseg; s0 += NW * RED_U) {
+            uint4 r[RED_U];
+            uint32_t sc[RED_U], sl[RED_U];
 #pragma unroll
-        for (uint32_t u = 0; u < RED_U; ++u) {
-            const uint4* sg = segs + (size_t)sc[u] * bv.seg_cap;
-            red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], sg + lane);
-            for (uint32_t off = 64; off < sl[u]; off += 64) {  // long segment (uniform over the wave)
-                uint4 x = sg[off + lane < sl[u] ? off + lane : 0];
-                if (off + lane >= sl[u]) x.z = NO_REC;
-                red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane);
+            for (uint32_t u = 0; u < RED_U; ++u) {
+                const uint32_t si = s0 + u * NW;
+                const uint32_t c = ne[si < nseg ? si : 0];
+                sc[u] = __builtin_amdgcn_readfirstlane(c);
+                sl[u] = __builtin_amdgcn_readfirstlane(si < nseg ? pre[c + 1] - pre[c] : 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < RED_U; ++u) {
+#ifdef IPXG_RED_NT  // tuning knob: streaming loads of the records (read once)
+                r[u] = u4(__builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4*>(&segs[(size_t)sc[u] * bv.seg_cap + (lane < sl[u] ? lane : 0)])));
+#else
+                r[u] = segs[(size_t)sc[u] * bv.seg_cap + (lane < sl[u] ? lane : 0)];  // unconditional load
+#endif
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < RED_U; ++u) {
+                const uint4* sg = segs + (size_t)sc[u] * bv.seg_cap;
+                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], sg + lane, lane < sl[u]);
+                for (uint32_t off = 64; off < sl[u]; off += 64) {  // long segment (uniform over the wave)
+                    const uint4 x = sg[off + lane < sl[u] ? off + lane : 0];
+                    red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane, off + lane < sl[u]);
+                }
             }
         }
     }
@@ -898,28 +928,31 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     // merged slot is complete and goes on the finalise list (k_fin_list).
     const bool fuse = ctl->frag_count == 0 && ctl->a_deferred == 0;
     uint32_t n_keys = 0, n_touch = 0, n_list = 0;
-    uint32_t listed[RED_ENTRIES / RED_THREADS];
+    constexpr uint32_t EPT = RED_ENTRIES / RED_THREADS;  // LDS entries per thread
+    HotSlot img[EPT];
+    bool listed[EPT];
     bool failed = false;
 #pragma unroll
-    for (uint32_t q = 0; q < RED_ENTRIES / RED_THREADS; ++q) {
+    for (uint32_t q = 0; q < EPT; ++q) {
         const uint32_t e = tid + q * RED_THREADS;
         const FlowAgg a = ht[e];
-        listed[q] = NO_REC;
+        listed[q] = false;
         if (a.key) {
             n_touch++;
-            HotSlot h;
             bool claimed;
-            HotSlot* hp = probe_insert_full(t, a.key, h, claimed);  // this workgroup is the
-            if (claimed) n_keys++;                                  // slot's only writer here
+            HotSlot* hp = probe_insert_full(t, a.key, img[q], claimed);  // this workgroup is the
+            if (claimed) n_keys++;                                       // slot's only writer here
             if (!hp) {
                 ht[e].tflags = a.tflags | RED_FAILED;
                 failed = true;
             } else {
-                agg_fold(h, a);
-                *hp = h;
-                if (fuse) {
-                    listed[q] = (uint32_t)(hp - t.hot);
+                agg_fold(img[q], a);
+                if (fuse) {  // the merged image goes to k_fin_list, which writes the slot back
+                    img[q].pad = (uint32_t)(hp - t.hot);
+                    listed[q] = true;
                     n_list++;
+                } else {
+                    *hp = img[q];
                 }
             }
         }
@@ -932,8 +965,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __syncthreads();
     pos += fin_base;
 #pragma unroll
-    for (uint32_t q = 0; q < RED_ENTRIES / RED_THREADS; ++q)
-        if (listed[q] != NO_REC) fin_list[pos++] = listed[q];
+    for (uint32_t q = 0; q < EPT; ++q)
+        if (listed[q]) fin_list[pos++] = img[q];
     if (failed) atomicOr(&cnt[C_FAIL], 1u);
     if (n_keys) atomicAdd(&cnt[C_KEYS], n_keys);
     if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
@@ -967,7 +1000,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     }
 }
 
-void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
+void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                    uint32_t* deferred_list, uint4* agg_list) {
     hipLaunchKernelGGL(k_reduce, dim3(1u << bv.part_bits), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list,
                        deferred_list, agg_list);
@@ -977,7 +1010,7 @@ void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint3
 // One lane per listed slot: finalize_slot with the creator's headers staged in the lane's
 // LDS column (256-thread blocks keep the register budget of the general parser).
 __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
-                                                         ExportView ex, BatchCtl* ctl, const uint32_t* fin_list,
+                                                         ExportView ex, BatchCtl* ctl, const HotSlot* fin_list,
                                                          unsigned long long* stats) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     __shared__ uint32_t sc[ST_COUNT];
@@ -996,8 +1029,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
         uint8_t reason = 0;
         ipxg_flow_record er;
         if (k < nf) {
-            const uint32_t s = fin_list[k];
-            const FinResult fr = finalize_slot<true>(b, p, t, f, s, t.hot[s], force_cx, &win[tid], er);
+            const HotSlot h = fin_list[k];  // the slot's merged image, its index in pad
+            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er);
             if (fr.status == FIN_COMPLEX) n_cx++;
             else if (fr.created) n_live++;
             do_export = fr.do_export;
@@ -1022,7 +1055,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
 }
 
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
-                     BatchCtl* ctl, const uint32_t* fin_list, unsigned long long* stats, uint32_t max_n) {
+                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n) {
     uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, ex, ctl, fin_list,

@@ -13,7 +13,7 @@ namespace ipxg {
 // Per-batch accumulators are folded into the cold record by k_finalize and re-zeroed.
 struct alignas(64) HotSlot {
     uint64_t key;      // 0  canonical flow hash: min(XXH64(key), XXH64(key_inv)); 0 = empty
-    uint32_t first_n;  // 8  ~(first packet index in this batch), max-reduced; 0 = none
+    uint32_t first_n;  // 8  the batch's first packet of the flow, max-reduced: first_key(); 0 = none
     uint32_t tbits;    // 12 occupancy of (inactive/2)-second buckets since the batch start,
                        //    bit 31 = beyond bucket 30
     uint64_t acc[2];   // 16 per canonical direction: packets << 40 | IP bytes
@@ -22,7 +22,7 @@ struct alignas(64) HotSlot {
     uint32_t fin_n[2]; // 40 ~(first FIN|RST packet index) per direction, max-reduced
     uint32_t syn1[2];  // 48 last SYN packet index + 1 per direction, max-reduced
     uint32_t state;    // 56 SLOT_LIVE | SLOT_COMPLEX
-    uint32_t pad;      // 60
+    uint32_t pad;      // 60 (a finalise-list image: the slot's index)
 };
 static_assert(sizeof(HotSlot) == 64, "hot slot must be one 64-byte line");
 
@@ -171,10 +171,11 @@ void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                      BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
                      unsigned long long* stats);
-void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, uint32_t* fin_list,
+// fin_list: the merged images of the slots k_reduce completed (HotSlot::pad = slot index)
+void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                    uint32_t* deferred_list, uint4* agg_list);
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
-                     BatchCtl* ctl, const uint32_t* fin_list, unsigned long long* stats, uint32_t max_n);
+                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
 void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,

@@ -123,6 +123,17 @@ __device__ __forceinline__ uint32_t misc_dir(uint32_t m) { return (m >> 24) & 1;
 __device__ __forceinline__ bool misc_tcp(uint32_t m) { return (m >> 25) & 1; }
 __device__ __forceinline__ uint32_t misc_tb(uint32_t m) { return (m >> 26) & 31; }
 
+// The batch's first packet of a flow, as one max-reduced word: (~index & 0xFFFFFF) << 8 (the
+// largest is the smallest index; indices are < 2^24 - 1, so a packet's key is never 0) and, in
+// the low bits, what the boundary checks of put_pkt_recursive need of that packet without
+// parsing it again: its SYN flag (cache.cpp:431) and its canonical direction (:428).
+__device__ __forceinline__ uint32_t first_key(uint32_t idx, uint32_t m) {
+    return ((~idx & 0xFFFFFFu) << 8) | (((misc_flags(m) >> 1) & 1u) << 1) | misc_dir(m);
+}
+__device__ __forceinline__ uint32_t first_idx(uint32_t fk) { return ~(fk >> 8) & 0xFFFFFFu; }
+__device__ __forceinline__ bool first_syn(uint32_t fk) { return (fk & 2u) != 0; }
+__device__ __forceinline__ uint32_t first_dir(uint32_t fk) { return fk & 1u; }
+
 // ---- flow-table probing (open addressing, linear probing, capacity 2^k) ------------------
 // Probe for (and if absent claim) the slot of canonical hash lo; nullptr after MAX_PROBE.
 // One 16-byte load per probe returns the key together with first_n and tbits, so the
@@ -207,7 +218,7 @@ __device__ __forceinline__ bool merge_packet_atomic(const TableView& t, uint64_t
     const uint32_t cdir = misc_dir(m);
     atomicAdd((unsigned long long*)&h->acc[cdir], (1ull << 40) | (uint64_t)misc_len(m));
     atomicMax(&h->last1, idx + 1);
-    const uint32_t fn = ~idx;
+    const uint32_t fn = first_key(idx, m);
     if (head.z < fn) atomicMax(&h->first_n, fn);
     const uint32_t tb = 1u << misc_tb(m);
     if (!(head.w & tb)) atomicOr(&h->tbits, tb);
@@ -248,7 +259,7 @@ __device__ __forceinline__ void agg_fold(HotSlot& h, const FlowAgg& a) {
 // instead of one 16-byte record per packet: three consecutive record slots in the partition
 // segment, each marked with bit 31 of word w (a packet record's w = pack_misc() leaves bit 31
 // clear) and its slot index in bits 29-30.  Fields (indices absolute in the batch):
-//   s0 = {lo low, lo high, first | tflags dir0 << 24, last | MARK | 0 << 29}
+//   s0 = {lo low, lo high, first | tflags dir0 << 24, last | first SYN, dir << 24 | MARK | 0 << 29}
 //   s1 = {bytes0 | packets0 low 5 << 27, bytes1 | packets1 low 5 << 27, tbits,
 //         packets0 >> 5 | (packets1 >> 5) << 7 | tflags dir1 << 14 | MARK | 1 << 29}
 //   s2 = {syn1[0], syn1[1], fin1[0], fin1[1] | MARK | 2 << 29}   (index + 1, 0 = none)
@@ -263,8 +274,8 @@ __device__ __forceinline__ void agg_encode(const FlowAgg& a, uint4& s0, uint4& s
     const uint32_t p0 = (uint32_t)(a.acc[0] >> 40), p1 = (uint32_t)(a.acc[1] >> 40);
     const uint32_t b0 = (uint32_t)(a.acc[0] & ACC_BYTES_MASK), b1 = (uint32_t)(a.acc[1] & ACC_BYTES_MASK);
     const uint32_t f1[2] = {a.fin_n[0] ? ~a.fin_n[0] + 1 : 0u, a.fin_n[1] ? ~a.fin_n[1] + 1 : 0u};
-    s0 = make_uint4((uint32_t)a.key, (uint32_t)(a.key >> 32), (~a.first_n) | ((a.tflags & 0xFF) << 24),
-                    (a.last1 - 1) | AGG_MARK);
+    s0 = make_uint4((uint32_t)a.key, (uint32_t)(a.key >> 32), first_idx(a.first_n) | ((a.tflags & 0xFF) << 24),
+                    (a.last1 - 1) | ((a.first_n & 3u) << 24) | AGG_MARK);
     s1 = make_uint4(b0 | (p0 << 27), b1 | (p1 << 27), a.tbits,
                     (p0 >> 5) | ((p1 >> 5) << 7) | (((a.tflags >> 8) & 0xFF) << 14) | AGG_MARK | (1u << 29));
     s2 = make_uint4(a.syn1[0], a.syn1[1], f1[0], f1[1] | AGG_MARK | (2u << 29));
@@ -276,7 +287,7 @@ __device__ __forceinline__ FlowAgg agg_decode(const uint4& s0, const uint4& s1, 
     const uint64_t p0 = (s1.x >> 27) | ((s1.w & 0x7F) << 5), p1 = (s1.y >> 27) | (((s1.w >> 7) & 0x7F) << 5);
     a.acc[0] = (p0 << 40) | (s1.x & 0x07FFFFFFu);
     a.acc[1] = (p1 << 40) | (s1.y & 0x07FFFFFFu);
-    a.first_n = ~(s0.z & 0xFFFFFF);
+    a.first_n = ((~s0.z & 0xFFFFFFu) << 8) | ((s0.w >> 24) & 3u);
     a.last1 = (s0.w & 0xFFFFFF) + 1;
     a.tbits = s1.z;
     a.tflags = (s0.z >> 24) | (((s1.w >> 14) & 0xFF) << 8);
@@ -541,39 +552,36 @@ struct FinResult {
 };
 
 // h = the slot's complete batch image (key, accumulators, state) with h.last1 != 0.
-// Re-parses the batch's first packet of the flow (the creator fields and the boundary
-// checks need it), applies the reference's SYN-after-FIN/RST, inactive and active checks
-// at the batch's first packet (cache.cpp:431-472), and decides whether a split could fall
-// strictly inside the batch (a SYN after a FIN/RST in the same direction, a gap >= inactive
-// -- detected conservatively as an empty inactive/2 bucket between busy ones --, or the
-// active limit inside the batch).  If so the slot is marked complex (k_complex_walk replays
-// the flow's packets sequentially); otherwise the accumulators are folded into the record
-// and the slot cleared.  Writes the slot (and its cold record) back.
+// Applies the reference's SYN-after-FIN/RST, inactive and active checks at the batch's first
+// packet of the flow (cache.cpp:431-472) -- from that packet's SYN flag and direction carried
+// in h.first_n and its descriptor's timestamp -- and decides whether a split could fall
+// strictly inside the batch (a SYN after a FIN/RST in the same direction, a gap >= inactive --
+// detected conservatively as an empty inactive/2 bucket between busy ones --, or the active
+// limit inside the batch).  If so the slot is marked complex (k_complex_walk replays the
+// flow's packets sequentially); otherwise the accumulators are folded into the record and the
+// slot cleared.  Only a flow that starts a record here (new, or split at the boundary)
+// re-parses its first packet (FlowRecord::create's fields, cache.cpp:94-133).  Writes the slot
+// (and its cold record) back.
 // LDSW: stage the creator's headers in the lane's LDS column `col` (else byte loads).
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
                                                    bool force_cx, uint32_t* col, ipxg_flow_record& er) {
     FinResult res = {FIN_DONE, false, false, 0};
-    const uint32_t first = ~h.first_n, last = h.last1 - 1;
+    const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
     ipxg_flow_record rec;
     if (live) rec = t.cold[s];
-    DevPkt fp;
-    ipxg_pkt_desc df;
-    if (LDSW) reparse_lds<true>(b, p, f, first, col, fp, df);
-    else reparse<true>(b, p, f, first, fp, df);
+    const ipxg_pkt_desc df = b.desc[first];
     const ipxg_pkt_desc dl = b.desc[last];
-    uint64_t lo, hf;
-    uint32_t cdf;
-    canon(fp, p, lo, cdf, hf);
+    const uint32_t cdf = p.split_biflow ? 0u : first_dir(h.first_n);
     const uint32_t I = p.inactive_s, A = p.active_s;
     uint8_t bsplit = 0;
     if (live) {
         const uint32_t creator = rec.reserved[0];
         const bool dsrc = p.split_biflow || cdf == creator;
         const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
-        if ((fp.tcp_flags & 0x02) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
+        if (first_syn(h.first_n) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
         else if ((int64_t)df.ts_sec - (int64_t)rec.time_last_sec >= (int64_t)I) bsplit = export_reason(rec);
         else if ((int64_t)df.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
     }
@@ -599,6 +607,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     if (cx) {
         HotSlot c = h;
         c.state = h.state | SLOT_COMPLEX;
+        c.pad = 0;
         t.hot[s] = c;
         res.status = FIN_COMPLEX;
         return res;
@@ -608,7 +617,16 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         res.reason = bsplit;
         er = rec;
     }
-    if (!cont) rec_create(rec, fp, df, hf, cdf);
+    if (!cont) {  // a record starts at the first packet: its fields from a re-parse
+        DevPkt fp;
+        ipxg_pkt_desc d2;
+        if (LDSW) reparse_lds<true>(b, p, f, first, col, fp, d2);
+        else reparse<true>(b, p, f, first, fp, d2);
+        uint64_t lo, hf;
+        uint32_t c2;
+        canon(fp, p, lo, c2, hf);
+        rec_create(rec, fp, df, hf, cdf);
+    }
     const uint32_t sd = rec.reserved[0];
     const uint64_t as = h.acc[sd], ad = h.acc[sd ^ 1];
     rec.src_packets += (uint32_t)(as >> 40);
