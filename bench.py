@@ -153,17 +153,55 @@ class _DevArray:
                                          "data": (ptr, False), "version": 3}
 
 
-def gather_exports(eng, rank, world, device):
-    """RCCL gather of every rank's device export buffer into rank 0 (ipfixprobe_amd.shard).
-    Ordering: the engine's stream is idle here (ipxg_device_exports completes the batch); the
-    engine's stream waits for the gather before its next kernels can overwrite the buffer."""
-    import torch
-    from ipfixprobe_amd.shard import gather_records
-    ptr, n = eng.device_exports()
-    buf = torch.as_tensor(_DevArray(ptr, max(n, 1) * 128), device=device)
-    out = gather_records(buf, n, rank, world, device)
-    torch.cuda.ExternalStream(eng.stream(), device=device).wait_stream(torch.cuda.current_stream(device))
-    return 0 if out is None else out.numel() // 128
+class ExportGather:
+    """The N > 1 step's only exchange (BASELINE.json configs[3]: "RCCL gather of per-GPU IPFIX
+    export buffers over xGMI"): each rank's exports leave as the IPFIX message stream of its
+    own observation domain (odid = rank), formatted on its GPU (ipxg_device_ipfix_messages,
+    no host round trip), copied into a fixed-size slot and gathered to rank 0 with one
+    dist.gather on a side stream -- behind the next step's kernels.  The engine's stream
+    waits only for the slot copy (its message buffer is then free); the slots alternate, and
+    the side stream is in order, so a slot is rewritten only after its gather."""
+
+    def __init__(self, eng, rank, world, device, max_records):
+        import torch
+        from ipfixprobe_amd import shard
+        self.eng, self.rank, self.world, self.device = eng, rank, world, device
+        self.x = eng.ipfix_exporter(odid=rank, export_time=1_700_000_000)
+        self.slot_bytes = shard.SLOT_HEADER + shard.ipfix_stream_bound(max_records)
+        self.slots = [torch.zeros(self.slot_bytes, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.side = torch.cuda.Stream(device=device)
+        self.eng_stream = torch.cuda.ExternalStream(eng.stream(), device=device)
+        self.events = []
+        self.k = 0
+        self.records = self.bytes = 0
+
+    def step(self):
+        import torch
+        from ipfixprobe_amd import shard
+        ptr, nb, nr, _ = self.eng.device_ipfix_messages(self.x)
+        src = torch.as_tensor(_DevArray(ptr, max(nb, 1)), device=self.device)
+        slot = self.slots[self.k % 2]
+        self.k += 1
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        copied = torch.cuda.Event()
+        self.side.wait_stream(self.eng_stream)
+        with torch.cuda.stream(self.side):
+            t0.record()
+            shard.pack_slot(slot, src, nb, nr)
+            copied.record()
+            shard.gather_slots(slot, self.rank, self.world)
+            t1.record()
+        self.eng_stream.wait_event(copied)
+        self.events.append((t0, t1))
+        self.records += nr
+        self.bytes += nb
+
+    def device_ms(self, reset=True):
+        """Side-stream time of the slot copies + gathers (synchronise first)."""
+        ms = sum(a.elapsed_time(b) for a, b in self.events)
+        if reset:
+            self.events = []
+        return ms
 
 
 # ---- CPU baseline (BASELINE.md 2) ---------------------------------------------------------------
@@ -430,7 +468,7 @@ def main():
     eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest),
                  device_id=local)
     cursor = [0]
-    gather_ms = [0.0]
+    gather = ExportGather(eng, rank, world, device, wl.flows * 2) if world > 1 else None
 
     def step():
         if wl.finish:
@@ -444,11 +482,10 @@ def main():
             cursor[0] += 1
             eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
             eng.expire(wl.last_sec[cursor[0] - 1])  # the virtual clock: idle flows out (none idle here)
-        if world > 1:
-            t0 = time.perf_counter()
-            gather_exports(eng, rank, world, device)
-            gather_ms[0] += (time.perf_counter() - t0) * 1e3
-        eng.clear_exports()
+        if gather is not None:
+            gather.step()  # IPFIX streams to rank 0 over RCCL, overlapped with the next step
+        else:
+            eng.clear_exports()
 
     for _ in range(args.warmup):
         step()
@@ -459,7 +496,9 @@ def main():
     # every-stage events cost ~35 us of host time per step, so the stage breakdown comes from a
     # separate pass below
     eng.profile(3)
-    gather_ms[0] = 0.0
+    if gather is not None:
+        torch.cuda.synchronize()
+        gather.device_ms()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -472,7 +511,7 @@ def main():
     dt = time.perf_counter() - t0
     tm_in = eng.timing()
     st = eng.stats()
-    gms = gather_ms[0] / args.steps
+    gms = gather.device_ms() / args.steps if gather is not None else None
     eng.profile(1)  # stage breakdown (untimed)
     stage_steps = min(args.steps, 10)
     for _ in range(stage_steps):
@@ -543,7 +582,11 @@ def main():
             "e2e_pcie": e2e,
             "spilled_packets": int(st["spilled_packets"]),
             "complex_flows": int(st["complex_flows"]),
-            "gather_ms_per_step": round(gms, 4) if world > 1 else None,
+            "gather": {"what": "per-rank IPFIX stream (odid = rank) -> fixed-size slot -> dist.gather to rank 0 "
+                               "(RCCL) on a side stream, overlapped with the next step",
+                       "device_ms_per_step": round(gms, 4), "slot_bytes": gather.slot_bytes,
+                       "rank0_receives_bytes_per_step": gather.slot_bytes * world,
+                       "stream_bytes_per_step": round(gather.bytes / max(gather.k, 1))} if gather is not None else None,
             "verify": verify,
             "cpu_baseline": cpu,
         }

@@ -44,8 +44,11 @@ struct ipxg_engine {
     // export buffer: records [ex_head, ex_count) are pending
     ipxg_flow_record* ex = nullptr;
     uint32_t ex_cap = 0;
-    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag (inside the ctl block)
+    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag, [2] IPv6 records (ctl block)
     uint32_t ex_count = 0, ex_head = 0;
+    uint32_t ex_count6 = 0;          // [2] at the last readback
+    bool ex6_valid = false;          // [2] counts exactly the records [0, ex_count) (ex_head == 0)
+    bool count6_on = false;          // kernels keep [2]: switched on by the first IPFIX message call
     // control / stats
     BatchCtl* ctl_d = nullptr;  // device block: BatchCtl, then ex_count_d's two words
     BatchCtl* ctl_h = nullptr;  // host-mapped mirror of the whole block
@@ -72,6 +75,9 @@ struct ipxg_engine {
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     DevBuf ipf_msg, ipf_plan;                   // IPFIX messages: output, plan (sets + messages)
+    uint8_t* plan_h = nullptr;                  // pinned staging of the plan (asynchronous upload)
+    size_t plan_h_bytes = 0;
+    hipEvent_t plan_ev = nullptr;               // the last plan upload
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
     double skew = 1.0;                   // previous batch: most loaded partition / mean partition
     uint32_t part_bits_last = 0;         // partitions of the last binned batch (log2)
@@ -130,7 +136,9 @@ static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
 
 static TableView table_view(ipxg_engine* e) { return TableView{e->hot, e->cold, e->slot_rank, e->cap - 1}; }
 
-static ExportView export_view(ipxg_engine* e) { return ExportView{e->ex, e->ex_count_d, e->ex_cap}; }
+static ExportView export_view(ipxg_engine* e) {
+    return ExportView{e->ex, e->ex_count_d, e->ex_cap, e->count6_on ? 1u : 0u};
+}
 
 // Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
 // (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
@@ -240,6 +248,7 @@ static hipError_t stream_wait(hipStream_t st) {
 
 static int check_ex(ipxg_engine* e) {
     e->ex_count = ex_host(e)[0];
+    e->ex_count6 = ex_host(e)[2];
     if (ex_host(e)[1]) return set_err(e, IPXG_EDEVICE, "export buffer overflow (engine bug: capacity under-sized)");
     return IPXG_OK;
 }
@@ -309,6 +318,7 @@ static int ensure_export(ipxg_engine* e, size_t extra) {
     }
     e->ex_head = 0;
     e->ex_count = (uint32_t)pending;
+    e->ex6_valid = false;  // [2] counted records that are gone now
     HIPCHK(e, hipMemcpyAsync(e->ex_count_d, &e->ex_count, sizeof(uint32_t), hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     return IPXG_OK;
@@ -379,7 +389,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (hipMalloc((void**)&e->frag_ent, (size_t)fs * 4 * sizeof(FragEntry)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->frag_cnt, (size_t)fs * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
-    if (hipMemsetAsync(e->ex_count_d, 0, 2 * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+    if (hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
         return fail(IPXG_EDEVICE);
     if (hipStreamSynchronize(e->st) != hipSuccess) return fail(IPXG_EDEVICE);
@@ -400,6 +410,8 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->stats_d);
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
+    if (e->plan_h) hipHostFree(e->plan_h);
+    if (e->plan_ev) (void)hipEventDestroy(e->plan_ev);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
@@ -742,9 +754,10 @@ int ipxg_reset(ipxg_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
     const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
     HIPCHK(e, hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st));
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 2 * sizeof(uint32_t), e->st));
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->ex_count = e->ex_head = 0;
+    e->ex6_valid = e->count6_on;
     e->keys = e->live = 0;
     e->last_touched = 0;
     e->prev_valid = false;
@@ -775,9 +788,11 @@ int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t*
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     e->ex_head += (uint32_t)k;
+    if (k) e->ex6_valid = false;
     if (e->ex_head == e->ex_count) {
         e->ex_head = e->ex_count = 0;
-        HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+        e->ex6_valid = e->count6_on;
+        HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     *n = k;
@@ -841,9 +856,11 @@ int ipxg_poll_ipfix(ipxg_engine* e, uint32_t dir_bit_field, uint8_t* out, size_t
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     e->ex_head += (uint32_t)k;
+    if (k) e->ex6_valid = false;
     if (e->ex_head == e->ex_count) {
         e->ex_head = e->ex_count = 0;
-        HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+        e->ex6_valid = e->count6_on;
+        HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     *n = k;
@@ -955,31 +972,50 @@ void ipfix_template_msg(uint8_t* m, const ipxg_ipfix_exporter& x) {
 }
 }  // namespace
 
-// n device records at rec -> messages in e->ipf_msg; *bytes, *msgs; updates *x.
+// n device records at rec -> messages in e->ipf_msg; *bytes, *msgs; updates *x.  n6 >= 0: the
+// IPv6-template records among them, known from the export counters (then nothing here waits
+// for the device); n6 < 0: counted first (one readback).
 static int ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flow_record* rec, uint32_t n,
-                          size_t* bytes, size_t* msgs) {
+                          int64_t n6, size_t* bytes, size_t* msgs) {
     if (x->mtu < 16 + 4 + 105) return set_err(e, IPXG_EINVAL, "IPFIX mtu below one IPv6 basic record");
     int rc;
     const size_t nb = (n + 255) / 256;
-    uint64_t n6 = 0;
     if (n) {
         if ((rc = ensure(e, e->ipf_tot, (nb + 1) * sizeof(uint64_t)))) return rc;
-        launch_ipfix_count6(e->st, rec, n, (uint64_t*)e->ipf_tot.p);
+        launch_ipfix_count6(e->st, rec, n, (uint64_t*)e->ipf_tot.p);  // per-block prefix (the fill needs it)
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipMemcpyAsync(&n6, (uint64_t*)e->ipf_tot.p + nb, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
-        HIPCHK(e, hipStreamSynchronize(e->st));
+        if (n6 < 0) {
+            uint64_t c = 0;
+            HIPCHK(e, hipMemcpyAsync(&c, (uint64_t*)e->ipf_tot.p + nb, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
+            HIPCHK(e, hipStreamSynchronize(e->st));
+            n6 = (int64_t)c;
+        }
+    } else {
+        n6 = 0;
     }
-    const IpfixPlan P = ipfix_plan(n - n6, n6, *x);
+    const IpfixPlan P = ipfix_plan(n - (uint64_t)n6, (uint64_t)n6, *x);
     const size_t ns4 = P.sets[0].size(), ns6 = P.sets[1].size(), nm = P.msgs.size();
-    std::vector<uint8_t> plan((ns4 + ns6) * sizeof(IpfixSet) + nm * sizeof(IpfixMsg) + IPFIX_TMPL_MSG);
-    std::memcpy(plan.data(), P.sets[0].data(), ns4 * sizeof(IpfixSet));
-    std::memcpy(plan.data() + ns4 * sizeof(IpfixSet), P.sets[1].data(), ns6 * sizeof(IpfixSet));
     const size_t moff = (ns4 + ns6) * sizeof(IpfixSet), toff = moff + nm * sizeof(IpfixMsg);
-    std::memcpy(plan.data() + moff, P.msgs.data(), nm * sizeof(IpfixMsg));
-    ipfix_template_msg(plan.data() + toff, *x);
-    if ((rc = ensure(e, e->ipf_plan, plan.size()))) return rc;
+    const size_t pbytes = toff + IPFIX_TMPL_MSG;
+    // the pinned staging buffer may still feed the previous plan's upload
+    if (e->plan_ev) HIPCHK(e, hipEventSynchronize(e->plan_ev));
+    else HIPCHK(e, hipEventCreateWithFlags(&e->plan_ev, hipEventDisableTiming));
+    if (e->plan_h_bytes < pbytes) {
+        if (e->plan_h) HIPCHK(e, hipHostFree(e->plan_h));
+        e->plan_h = nullptr;
+        e->plan_h_bytes = 0;
+        HIPCHK(e, hipHostMalloc((void**)&e->plan_h, pbytes * 2, hipHostMallocDefault));
+        e->plan_h_bytes = pbytes * 2;
+    }
+    uint8_t* plan = e->plan_h;
+    std::memcpy(plan, P.sets[0].data(), ns4 * sizeof(IpfixSet));
+    std::memcpy(plan + ns4 * sizeof(IpfixSet), P.sets[1].data(), ns6 * sizeof(IpfixSet));
+    std::memcpy(plan + moff, P.msgs.data(), nm * sizeof(IpfixMsg));
+    ipfix_template_msg(plan + toff, *x);
+    if ((rc = ensure(e, e->ipf_plan, pbytes))) return rc;
     if ((rc = ensure(e, e->ipf_msg, P.bytes + 16))) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->ipf_plan.p, plan.data(), plan.size(), hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->ipf_plan.p, plan, pbytes, hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipEventRecord(e->plan_ev, e->st));
     uint8_t* out = (uint8_t*)e->ipf_msg.p;
     if (P.tmpl)
         HIPCHK(e, hipMemcpyAsync(out, (uint8_t*)e->ipf_plan.p + toff, IPFIX_TMPL_MSG, hipMemcpyDeviceToDevice, e->st));
@@ -988,13 +1024,17 @@ static int ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flo
     launch_ipfix_messages(e->st, rec, n, x->dir_bit_field, (const uint64_t*)e->ipf_tot.p, sets, (uint32_t)ns4,
                           (uint32_t)ns6, m, (uint32_t)nm, x->odid, x->export_time, out);
     HIPCHK(e, hipGetLastError());
-    // the plan's host copy must outlive the asynchronous upload
-    HIPCHK(e, hipStreamSynchronize(e->st));
     if (P.tmpl) x->templates_sent = 1;
     x->sequence = P.seq_end;
     *bytes = P.bytes;
     *msgs = nm + (P.tmpl ? 1 : 0);
     return IPXG_OK;
+}
+
+static int64_t known_v6(ipxg_engine* e) {
+    const int64_t k = (e->ex6_valid && e->ex_head == 0) ? (int64_t)e->ex_count6 : -1;
+    e->count6_on = true;  // from now on the export kernels count (valid from the next reset)
+    return k;
 }
 
 void ipxg_ipfix_exporter_init(ipxg_ipfix_exporter* x) {
@@ -1024,7 +1064,7 @@ int ipxg_ipfix_export(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flow_re
     }
     ipxg_ipfix_exporter y = *x;
     size_t nbytes = 0, nm = 0;
-    if ((rc = ipfix_messages(e, &y, (const ipxg_flow_record*)e->ipf_rec.p, (uint32_t)n, &nbytes, &nm))) return rc;
+    if ((rc = ipfix_messages(e, &y, (const ipxg_flow_record*)e->ipf_rec.p, (uint32_t)n, -1, &nbytes, &nm))) return rc;
     if (nbytes > cap) return set_err(e, IPXG_ETOOBIG, "output buffer too small for the messages");
     if (nbytes) {
         HIPCHK(e, hipMemcpyAsync(out, e->ipf_msg.p, nbytes, hipMemcpyDeviceToHost, e->st));
@@ -1046,11 +1086,12 @@ int ipxg_device_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const uin
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     const uint32_t pend = e->ex_count - e->ex_head;
     int rc;
-    if ((rc = ipfix_messages(e, x, e->ex + e->ex_head, pend, bytes, msgs))) return rc;
+    if ((rc = ipfix_messages(e, x, e->ex + e->ex_head, pend, known_v6(e), bytes, msgs))) return rc;
     *dptr = (const uint8_t*)e->ipf_msg.p;
     *n_records = pend;
     e->ex_head = e->ex_count = 0;  // consumed
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    e->ex6_valid = e->count6_on;
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
     return IPXG_OK;
 }
 
@@ -1066,14 +1107,15 @@ int ipxg_poll_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, uint8_t* ou
     ipxg_ipfix_exporter y = *x;
     size_t nbytes = 0, nm = 0;
     int rc;
-    if ((rc = ipfix_messages(e, &y, e->ex + e->ex_head, pend, &nbytes, &nm))) return rc;
+    if ((rc = ipfix_messages(e, &y, e->ex + e->ex_head, pend, known_v6(e), &nbytes, &nm))) return rc;
     if (nbytes > cap) return set_err(e, IPXG_ETOOBIG, "output buffer too small for the messages");
     if (nbytes) {
         HIPCHK(e, hipMemcpyAsync(out, e->ipf_msg.p, nbytes, hipMemcpyDeviceToHost, e->st));
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     e->ex_head = e->ex_count = 0;
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));
+    e->ex6_valid = e->count6_on;
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     *x = y;
     *n_records = pend;
@@ -1100,7 +1142,8 @@ int ipxg_clear_exports(ipxg_engine* e) {
         if (rc0) return rc0;
     }
     e->ex_head = e->ex_count = 0;
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, sizeof(uint32_t), e->st));  // ordered on the stream
+    e->ex6_valid = e->count6_on;
+    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));  // ordered on the stream
     return IPXG_OK;
 }
 

@@ -1042,6 +1042,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
             atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
             n_ex++;
         }
+        count_v6_exports(ex, do_export && er.ip_version == 6);
     }
     if (n_live) atomicAdd(&cnt[0], n_live);
     if (n_cx) atomicAdd(&cnt[1], n_cx);

@@ -303,6 +303,7 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
             reason_count(sc, reason);
             ex_n++;
         }
+        count_v6_exports(ex, do_export && er.ip_version == 6);
     }
     atomicAdd(&cnt[0], keys);
     atomicAdd(&cnt[1], live_n);
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
             if (reason) {
                 uint32_t pos = atomicAdd(ex.count, 1u);
                 store_export(ex, pos, rec, reason);
+                if (ex.count6 && rec.ip_version == 6) atomicAdd(ex.count + 2, 1u);
                 atomicAdd(&stats[ST_END_INACTIVE + reason - 1], 1ull);
                 n_ex++;
                 live = false;
@@ -461,11 +463,15 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
     uint32_t pos = bbase + off;
 #pragma unroll
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
-        if (!(mask >> j & 1)) continue;
-        const ipxg_flow_record rec = t.cold[base + j * 256 + threadIdx.x];
-        const uint8_t reason = export_reason(rec);
-        store_export(ex, pos++, rec, reason);
-        reason_count(sc, reason);
+        const bool mine = mask >> j & 1;
+        ipxg_flow_record rec;
+        if (mine) {
+            rec = t.cold[base + j * 256 + threadIdx.x];
+            const uint8_t reason = export_reason(rec);
+            store_export(ex, pos++, rec, reason);
+            reason_count(sc, reason);
+        }
+        count_v6_exports(ex, mine && rec.ip_version == 6);
     }
     flush_block_stats(sc, stats);
 }
@@ -515,8 +521,15 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     __syncthreads();
     uint32_t pos = bbase + off;
 #pragma unroll
-    for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j)
-        if (mask >> j & 1) store_export(ex, pos++, t.cold[base + j * 256 + threadIdx.x], IPXG_FLOW_END_FORCED);
+    for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
+        const bool mine = mask >> j & 1;
+        ipxg_flow_record rec;
+        if (mine) {
+            rec = t.cold[base + j * 256 + threadIdx.x];
+            store_export(ex, pos++, rec, IPXG_FLOW_END_FORCED);
+        }
+        count_v6_exports(ex, mine && rec.ip_version == 6);
+    }
     if (threadIdx.x == 0 && total)
         atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + ST_END_FORCED], (unsigned long long)total);
 }

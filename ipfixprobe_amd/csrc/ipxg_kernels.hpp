@@ -85,8 +85,10 @@ struct TableView {
 
 struct ExportView {
     ipxg_flow_record* buf;
-    uint32_t* count;  // [0] records appended, [1] overflow flag (never set when sized right)
+    uint32_t* count;  // [0] records appended, [1] overflow flag (never set when sized right),
+                      // [2] of them IPv6-template records (ip_version 6), when count6
     uint32_t cap;
+    uint32_t count6;  // keep [2] (the engine's IPFIX message layer has been used)
 };
 
 struct Params {

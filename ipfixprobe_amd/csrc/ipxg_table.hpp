@@ -383,6 +383,14 @@ __device__ __forceinline__ void store_export(ExportView ex, uint32_t pos, const 
     ex.buf[pos] = o;
 }
 
+// ex.count[2] counts the exported records that take the IPv6 basic template (the IPFIX message
+// layout needs the split, ipxg_engine.cpp ipfix_plan).  Convergent: every lane of the wave.
+__device__ __forceinline__ void count_v6_exports(ExportView ex, bool v6) {
+    if (!ex.count6) return;  // uniform
+    const uint64_t m = __ballot(v6);
+    if (m && lane_id() == (uint32_t)__builtin_ctzll(m)) atomicAdd(ex.count + 2, (uint32_t)__popcll(m));
+}
+
 __device__ __forceinline__ void clear_slot(HotSlot* h, uint64_t key, uint32_t state) {
     HotSlot z = {};
     z.key = key;

@@ -6,6 +6,7 @@
 namespace ipxp {
 
 GpuFlowCache::GpuFlowCache(const std::string& params, ExportSink* sink) : m_sink(sink) {
+    ipxg_ipfix_exporter_init(&m_ipfix);
     init(params.c_str());
 }
 
@@ -76,6 +77,14 @@ void GpuFlowCache::drain() {
     size_t n = 0;
     check(ipxg_pending_exports(m_eng, &n), "ipxg_pending_exports");
     if (!n) return;
+    if (m_msg_sink) {  // IPFIX messages formatted and packed on the device
+        m_msg.resize(ipxg_ipfix_bound(n));
+        size_t recs = 0, bytes = 0, msgs = 0;
+        check(ipxg_poll_ipfix_messages(m_eng, &m_ipfix, m_msg.data(), m_msg.size(), &recs, &bytes, &msgs),
+              "ipxg_poll_ipfix_messages");
+        m_msg_sink->messages(m_msg.data(), bytes, recs, msgs);
+        return;
+    }
     m_out.resize(n);
     size_t got = 0;
     check(ipxg_poll_exports(m_eng, m_out.data(), n, &got), "ipxg_poll_exports");

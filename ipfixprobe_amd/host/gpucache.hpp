@@ -44,6 +44,14 @@ public:
     virtual void push(const ipxg_flow_record& rec) = 0;
 };
 
+// IPFIX output formatted on the device: the message stream the reference's IPFIX output
+// plugin would send for the exported flows (ipxg_poll_ipfix_messages), handed over whole.
+class MessageSink {
+public:
+    virtual ~MessageSink() {}
+    virtual void messages(const uint8_t* data, size_t bytes, size_t records, size_t msgs) = 0;
+};
+
 class GpuFlowCache {
 public:
     GpuFlowCache(const std::string& params, ExportSink* sink);
@@ -55,6 +63,11 @@ public:
     void export_expired(time_t ts);
     void finish();
     void set_queue(ExportSink* sink) { m_sink = sink; }
+    // exports go out as IPFIX messages (exporter state x: odid, mtu, dir, export time)
+    void set_ipfix(MessageSink* sink, const ipxg_ipfix_exporter& x) {
+        m_msg_sink = sink;
+        m_ipfix = x;
+    }
     ipxg_stats stats();
     // whole pre-built batch (arena + descriptors), bypassing the per-packet buffer
     void put_batch(const ipxg_batch& b);
@@ -67,6 +80,9 @@ private:
     ipxg_engine* m_eng = nullptr;
     ipxg_config m_cfg;
     ExportSink* m_sink = nullptr;
+    MessageSink* m_msg_sink = nullptr;
+    ipxg_ipfix_exporter m_ipfix;
+    std::vector<uint8_t> m_msg;
     std::vector<uint8_t> m_arena;
     std::vector<ipxg_pkt_desc> m_desc;
     std::vector<ipxg_flow_record> m_out;

@@ -1,17 +1,21 @@
 // ipxg_probe -- minimal pipeline driver: pcap/pcapng file -> gpucache -> flow records.
 //
-//   ipxg_probe -i FILE [-s "s=20;a=300;i=30;..."] [-o csv|unirec] [-q BLOCK]
+//   ipxg_probe -i FILE [-s "s=20;a=300;i=30;..."] [-o csv|csv-vlan|ipfix:PATH] [--odid N]
+//              [--export-time SEC] [--mtu N]
 //
 // The input side mirrors ipfixprobe's pcap plugin + input_storage_worker
 // (workers.cpp:40-140): packets are read in arrival order and handed to the storage plugin
 // one by one (put_pkt); at end of file the storage is finished (workers.cpp:136).  Output is
 // the basic biflow columns in the text form of the reference's functional tests (UniRec
-// logger, tests/functional/scripts/run_test.sh), one line per exported flow.
+// logger, tests/functional/scripts/run_test.sh), one line per exported flow, or (ipfix:PATH)
+// the IPFIX message stream of the reference's IPFIX output plugin (basic templates), written
+// to PATH as sent on the wire -- formatted and packed on the device.
 #include <arpa/inet.h>
 #include <sys/time.h>
 #include <time.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -55,8 +59,20 @@ struct CsvSink : ipxp::ExportSink {
     }
 };
 
+struct FileMessages : ipxp::MessageSink {
+    FILE* f;
+    size_t records = 0, msgs = 0;
+    explicit FileMessages(FILE* out) : f(out) {}
+    void messages(const uint8_t* data, size_t bytes, size_t n, size_t m) override {
+        if (bytes && fwrite(data, 1, bytes, f) != bytes) throw ipxp::PluginError("ipxg_probe: write failed");
+        records += n;
+        msgs += m;
+    }
+};
+
 void usage() {
-    fprintf(stderr, "usage: ipxg_probe -i FILE [-s CACHE_OPTIONS] [-o csv|csv-vlan] [--stats]\n");
+    fprintf(stderr, "usage: ipxg_probe -i FILE [-s CACHE_OPTIONS] [-o csv|csv-vlan|ipfix:PATH] [--odid N] "
+                    "[--export-time SEC] [--mtu N] [--stats]\n");
 }
 
 }  // namespace
@@ -64,11 +80,17 @@ void usage() {
 int main(int argc, char** argv) {
     std::string in, opts, fmt = "csv";
     bool stats = false;
+    ipxg_ipfix_exporter x;
+    ipxg_ipfix_exporter_init(&x);
+    x.export_time = (uint32_t)time(nullptr);
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         if (a == "-i" && i + 1 < argc) in = argv[++i];
         else if (a == "-s" && i + 1 < argc) opts = argv[++i];
         else if (a == "-o" && i + 1 < argc) fmt = argv[++i];
+        else if (a == "--odid" && i + 1 < argc) x.odid = (uint32_t)strtoul(argv[++i], nullptr, 0);
+        else if (a == "--export-time" && i + 1 < argc) x.export_time = (uint32_t)strtoul(argv[++i], nullptr, 0);
+        else if (a == "--mtu" && i + 1 < argc) x.mtu = (uint16_t)strtoul(argv[++i], nullptr, 0);
         else if (a == "--stats") stats = true;
         else {
             usage();
@@ -95,8 +117,19 @@ int main(int argc, char** argv) {
     }
     if (probe_cfg.datalink == 0) opts += (opts.empty() ? "" : ";") + std::string("dlt=") + std::to_string(cap->datalink);
     CsvSink sink(stdout, fmt == "csv-vlan");
+    FILE* ipfix_out = nullptr;
+    if (fmt.rfind("ipfix:", 0) == 0) {
+        ipfix_out = fopen(fmt.c_str() + 6, "wb");
+        if (!ipfix_out) {
+            fprintf(stderr, "ipxg_probe: cannot write %s\n", fmt.c_str() + 6);
+            ipxg_capture_free(cap);
+            return 1;
+        }
+    }
+    FileMessages msink(ipfix_out);
     try {
         ipxp::GpuFlowCache cache(opts, &sink);
+        if (ipfix_out) cache.set_ipfix(&msink, x);
         for (uint32_t i = 0; i < cap->n; ++i) {
             const ipxg_pkt_desc& d = cap->desc[i];
             ipxp::RawPacket p;
@@ -119,8 +152,13 @@ int main(int argc, char** argv) {
         }
     } catch (const ipxp::PluginError& e) {
         fprintf(stderr, "ipxg_probe: %s\n", e.what());
+        if (ipfix_out) fclose(ipfix_out);
         ipxg_capture_free(cap);
         return 1;
+    }
+    if (ipfix_out) {
+        fclose(ipfix_out);
+        if (stats) fprintf(stderr, "ipfix: %zu records in %zu messages\n", msink.records, msink.msgs);
     }
     ipxg_capture_free(cap);
     return 0;

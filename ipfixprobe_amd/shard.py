@@ -6,9 +6,11 @@ same queue (ipfixprobe.cpp:381-464, dpdkDevice.cpp:230-262); caches never exchan
 Here: one process and one engine per GPU, and the canonical flow hash
 `lo = min(XXH64(key), XXH64(key_inv))` (the table key, cache.cpp:84-92 / ipxg_table.hpp)
 picks the rank, so both directions of a biflow land on the same GPU.  The only exchange is
-the gather of the per-GPU export buffers to rank 0 (`gather_records`): an all-gather of the
-record counts, then point-to-point transfers (RCCL over xGMI on GPUs; gloo on CPU tensors
-in the tests).
+the gather of the per-GPU export buffers to rank 0: `gather_records` (an all-gather of the
+record counts, then point-to-point transfers) or, for IPFIX message streams formatted on each
+GPU, `gather_slots` (one fixed-size slot per rank -- the stream's length in its header -- so no
+rank waits on the host for the others' sizes and the gather can run on a side stream, behind
+the next step's kernels).  RCCL over xGMI on GPUs; gloo on CPU tensors in the tests.
 """
 import numpy as np
 
@@ -57,3 +59,52 @@ def gather_records(buf, n, rank, world, device):
     if n:
         dist.send(mine.contiguous(), dst=0)
     return None
+
+
+SLOT_HEADER = 16  # little-endian u64 stream bytes, u64 records
+
+
+def ipfix_stream_bound(records):
+    """Bytes of an IPFIX message stream of `records` basic records, templates included (at
+    least 13 records per message of 1458 bytes: 16 + 4 + 13 * 105; two more messages for the
+    template message and a flush that splits the two templates' sets)."""
+    return 196 + records * 105 + (records // 13 + 3) * 20
+
+
+def pack_slot(slot, stream, nbytes, records):
+    """Header + the first nbytes of `stream` (uint8 tensor) into `slot` (uint8 tensor of the
+    agreed slot size, same device), with stream-ordered copies (no host synchronisation)."""
+    if SLOT_HEADER + nbytes > slot.numel():
+        raise ValueError("IPFIX stream of %d bytes exceeds the slot (%d)" % (nbytes, slot.numel()))
+    hdr = slot[:SLOT_HEADER].view(torch_int64())  # two scalar fills on the device
+    hdr[0] = nbytes
+    hdr[1] = records
+    if nbytes:
+        slot[SLOT_HEADER:SLOT_HEADER + nbytes].copy_(stream[:nbytes])
+
+
+def torch_int64():
+    import torch
+    return torch.int64
+
+
+def gather_slots(slot, rank, world):
+    """Every rank's slot into rank 0 (dist.gather on the current stream): a list of world
+    tensors on rank 0, None elsewhere.  Collective: every rank must call it."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return [slot]
+    out = [torch.empty_like(slot) for _ in range(world)] if rank == 0 else None
+    dist.gather(slot, out, dst=0)
+    return out
+
+
+def unpack_slots(slots):
+    """[(stream bytes as a numpy uint8 array, records)] from gathered slots (host copies)."""
+    res = []
+    for s in slots:
+        a = s.cpu().numpy()
+        nb, nr = (int(v) for v in a[:SLOT_HEADER].view(np.int64))
+        res.append((a[SLOT_HEADER:SLOT_HEADER + nb], nr))
+    return res

@@ -248,3 +248,25 @@ def test_poll_ipfix_messages_from_flow_cache():
     g = got.copy()
     g["end_reason"] = w["end_reason"][0]
     assert ipfixdec.basic_view(g) == ipfixdec.basic_view(w)
+
+
+@pytest.mark.gpu
+def test_poll_ipfix_messages_after_partial_poll():
+    """After a partial ipxg_poll_exports the IPv6 export count no longer covers the pending
+    records: the message layer counts them itself, and the stream still decodes to them."""
+    from ipfixprobe_amd import Engine
+    arena, desc = synth.flow_stream(seed=22, n_flows=300, n_pkts=6000, v6_share=0.5).batch()
+    with Engine() as e:
+        e.submit(arena, desc)
+        e.finish()
+        n = e.pending()
+        out = np.zeros(7, dtype=FLOW_DTYPE)
+        import ctypes
+        from ipfixprobe_amd import engine as eng_mod
+        got = ctypes.c_size_t()
+        eng_mod.lib().ipxg_poll_exports(e.handle, out.ctypes.data, 7, ctypes.byref(got))
+        x = e.ipfix_exporter()
+        b, nrec, nm = e.poll_ipfix_messages(x)
+    assert got.value == 7 and nrec == n - 7
+    msgs, _, recs, _, _ = ipfixdec.decode(b)
+    assert len(recs) == n - 7

@@ -135,3 +135,91 @@ def test_rccl_gather_single_rank_aliases_device_exports():
         assert got.tobytes() == want.tobytes()
     finally:
         dist.destroy_process_group()
+
+
+def _gloo_ipfix_worker(rank, world, port, q):
+    """bench.py's N > 1 export step on CPU: each rank's flows exported as an IPFIX stream (the
+    oracle's exporter, observation domain = rank), packed into a fixed-size slot, gathered to
+    rank 0 (gather_slots), which decodes every stream."""
+    import torch
+    import torch.distributed as dist
+    import ipfixdec
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        arena, desc = _capture(seed=31)
+        own = _owners(arena, desc, world)
+        got, _ = oracle_py.run_capture(arena, np.ascontiguousarray(desc[own == rank]), 1, cache_exp=20)
+        stream, _ = oracle_py.ipfix_export(oracle_py.ipfix_exporter(odid=rank, export_time=5), got)
+        slot_bytes = shard.SLOT_HEADER + shard.ipfix_stream_bound(400)  # every rank: the same size
+        slot = torch.zeros(slot_bytes, dtype=torch.uint8)
+        shard.pack_slot(slot, torch.from_numpy(stream.copy()), len(stream), len(got))
+        out = shard.gather_slots(slot, rank, world)
+        if rank == 0:
+            parts = shard.unpack_slots(out)
+            recs, wire = [], 0
+            for r, (b, nr) in enumerate(parts):
+                msgs, _, rr, _, _ = ipfixdec.decode(b)
+                assert all(m["odid"] == r for m in msgs) and len(rr) == nr
+                recs.append(rr)
+                wire += len(b)
+            want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+            allr = np.concatenate(recs)
+            assert ipfixdec.basic_view(allr) == ipfixdec.basic_view(want)
+            q.put((wire, sum(p[1] for p in parts), len(out) * slot_bytes))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_gloo_ipfix_slots_gather_to_rank0(world):
+    """world_size 4 / 8 on CPU: the exact N > 1 export step of bench.py (IPFIX stream per rank
+    -> fixed-size slot -> gather to rank 0); the union of the decoded records is the whole
+    capture's, and rank 0 receives world slots (the volume DESIGN.md 6 budgets)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_gloo_ipfix_worker, args=(world, _free_port(), q), nprocs=world, join=True)
+    wire, nrec, moved = q.get(timeout=10)
+    assert nrec > 100 and wire < shard.ipfix_stream_bound(nrec) + world * 196
+    assert moved == world * (shard.SLOT_HEADER + shard.ipfix_stream_bound(400))
+
+
+@pytest.mark.gpu
+def test_bench_export_gather_single_rank():
+    """bench.py's N > 1 export step (ExportGather: device IPFIX stream -> slot -> dist.gather on a
+    side stream) at world size 1 over RCCL: the gathered slot decodes to the engine's flows."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    import bench
+    import ipfixdec
+    from ipfixprobe_amd import Engine
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        arena, desc = _capture(seed=25)
+        want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+        with Engine() as e:
+            g = bench.ExportGather(e, 0, 1, dev, 1000)
+            for _ in range(2):  # two steps: the second stream has no template message
+                e.submit(arena, desc)
+                e.finish()
+                g.step()
+            torch.cuda.synchronize()
+            parts = shard.unpack_slots([g.slots[1]])
+            assert g.device_ms() > 0
+        b, nr = parts[0]
+        _, t0, _, _, _ = ipfixdec.decode(shard.unpack_slots([g.slots[0]])[0][0])
+        msgs, _, recs, _, _ = ipfixdec.decode(b, t0)
+        assert nr == len(want) == len(recs) and all(s[0] != 2 for m in msgs for s in m["sets"])
+        w = want.copy()
+        w["end_reason"] = 0  # the oracle's sweep and the engine close open flows with different reasons
+        recs["end_reason"] = 0
+        assert ipfixdec.basic_view(recs) == ipfixdec.basic_view(w)
+    finally:
+        dist.destroy_process_group()

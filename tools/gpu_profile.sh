@@ -1,0 +1,32 @@
+#!/bin/bash
+# rocprofv3 evidence for one round: kernel-trace stats of bench.py per workload, then PMC
+# passes (FETCH_SIZE / WRITE_SIZE, each its own run) for the HBM traffic of every kernel.
+# Usage: TAG=r02 [WORKLOADS="udp64 imix quic"] [PMC=1] bash tools/gpu_profile.sh
+# Every GPU step has its own time limit; a fault, abort or timeout stops the script there.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/prof_${TAG:-r02}
+mkdir -p $OUT
+export TMPDIR=/tmp
+stop() { echo "STOP: $1 exited $2"; exit "$2"; }
+for W in ${WORKLOADS:-udp64 imix quic}; do
+  case $W in
+    udp64) ARGS="--steps 30 --warmup 3" ;;
+    stream) ARGS="--mode stream --steps 20 --warmup 3" ;;
+    imix) ARGS="--workload imix --steps 3 --warmup 1" ;;
+    quic) ARGS="--workload quic --steps 5 --warmup 1" ;;
+  esac
+  echo "== kernel trace $W"; date
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$W -o run -- \
+      python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/kt_$W.json 2> $OUT/kt_$W.err
+  rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/kt_$W.err; stop "kernel trace $W" $rc; }
+  if [ "${PMC:-1}" = "1" ]; then
+    for C in FETCH_SIZE WRITE_SIZE; do
+      echo "== pmc $W $C"; date
+      timeout -k 10 -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$W/$C -o run -- \
+          python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/pmc_${W}_$C.json 2> $OUT/pmc_${W}_$C.err
+      rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_${W}_$C.err; stop "pmc $W $C" $rc; }
+    done
+  fi
+done
+echo "== done"; date
