@@ -442,6 +442,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check one step's records against the oracle")
     ap.add_argument("--ingest", default="binned", choices=["binned", "atomic"])
+    ap.add_argument("--walk", default="auto", choices=["auto", "wide", "narrow"],
+                    help="k_bin's header walk (auto: chosen per batch from the previous batch's mix)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host batch) rate")
     args = ap.parse_args()
     dflt = {"udp64": (10_000_000, 1, 100_000, 20), "imix": (10_000_000, 10, 1_000_000, 5),
@@ -465,7 +467,7 @@ def main():
     from ipfixprobe_amd import Engine
     wl = make_workload(args, rank, world, device, local)
     torch.cuda.synchronize()
-    eng = Engine("s=%d;ingest=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest),
+    eng = Engine("s=%d;ingest=%s;walk=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest, args.walk),
                  device_id=local)
     cursor = [0]
     gather = ExportGather(eng, rank, world, device, wl.flows * 2) if world > 1 else None
@@ -579,6 +581,7 @@ def main():
                                             "finish")},
             "flows_exported_per_step": int(st["total_exported"] // max(st["batches"] // max(wl.per_step, 1), 1)),
             "slow_path_packets_share": round(st["slow_path_packets"] / max(st["parsed_packets"], 1), 4),
+            "walked_packets_share": round(st["walked_packets"] / max(st["parsed_packets"], 1), 4),
             "e2e_pcie": e2e,
             "spilled_packets": int(st["spilled_packets"]),
             "complex_flows": int(st["complex_flows"]),

@@ -167,6 +167,13 @@ typedef struct ipxg_config {
 #define IPXG_CFG_ATOMIC_INGEST 0x1u /* ingest=atomic: fold every packet into the table with
                                        device atomics (one kernel) instead of the binned
                                        two-phase ingest; kept for A/B measurement          */
+#define IPXG_CFG_WALK_WIDE 0x2u     /* walk=wide: k_bin loads 96 bytes per frame and parses
+                                       VLAN/QinQ, IPv6 and TCP-timestamp frames from
+                                       registers too; default walk=auto picks per batch
+                                       from the previous batch's mix                        */
+#define IPXG_CFG_WALK_NARROW 0x4u   /* walk=narrow: k_bin parses the plain Eth/IPv4/UDP|TCP
+                                       shape only (48-byte loads), the rest goes through
+                                       the slow list (k_bin_slow)                           */
 
 typedef struct ipxg_stats {
     /* parser counters, reference parser-stats.hpp:126-201 (the subset on the path) */
@@ -202,6 +209,8 @@ typedef struct ipxg_stats {
                                  device atomics (partition region or LDS table full)    */
     uint64_t slow_path_packets; /* packets k_bin left to the general parser (k_bin_slow)  */
     uint64_t aggregated_packets; /* packets folded into per-tile flow aggregates (skew)   */
+    uint64_t walked_packets;  /* packets of the wide walk's extra shapes (VLAN, IPv6, TCP
+                                 timestamp option) parsed from registers by k_bin     */
 } ipxg_stats;
 
 typedef struct ipxg_engine ipxg_engine;

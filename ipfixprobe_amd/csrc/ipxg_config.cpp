@@ -5,7 +5,8 @@
 // (CacheOptParser, cache.hpp:81-221; OptionsParser::parse, options.cpp:62-160: ';'-separated
 // tokens, "name=value" or "name" followed by its value as the next token), plus the GPU keys
 // "dev"/"device", "batch", "dlt" (EN10MB | RAW | LINUX_SLL | LINUX_SLL2 or a number) and
-// "ingest" (binned | atomic).
+// "ingest" (binned | atomic) and "walk" (auto | wide | narrow: which k_bin variant walks
+// the header chains).
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -95,6 +96,12 @@ extern "C" int ipxg_config_parse(const char* params, ipxg_config* cfg) {
             if (a == "atomic") cfg->flags |= IPXG_CFG_ATOMIC_INGEST;
             else if (a == "binned") cfg->flags &= ~IPXG_CFG_ATOMIC_INGEST;
             else return IPXG_EINVAL;
+        } else if (name == "walk") {
+            if (!arg(a)) return IPXG_EINVAL;
+            cfg->flags &= ~(IPXG_CFG_WALK_WIDE | IPXG_CFG_WALK_NARROW);
+            if (a == "wide") cfg->flags |= IPXG_CFG_WALK_WIDE;
+            else if (a == "narrow") cfg->flags |= IPXG_CFG_WALK_NARROW;
+            else if (a != "auto") return IPXG_EINVAL;
         } else if (name == "dlt") {
             if (!arg(a)) return IPXG_EINVAL;
             if (a == "EN10MB") cfg->datalink = IPXG_DLT_EN10MB;

@@ -62,7 +62,8 @@ struct ipxg_engine {
     DevBuf adefer_a, adefer_b;           // deferred tile aggregates (3 x 16 B each)
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
-    uint32_t bin_slots[2] = {0, 0};      // k_bin workgroups resident at once (its grid), [agg]
+    uint32_t bin_slots[2][2] = {};       // k_bin workgroups resident at once (its grid), [agg][wide]
+    bool wide = false;                   // the next batch's k_bin walks every header chain (WIDE)
     bool tile_agg = true;                // the next batch aggregates frequent flows per tile
     // an IPXG_BATCH_ASYNC batch whose kernels are enqueued but whose control block the host
     // has not read yet (completed by the next call on the engine)
@@ -84,7 +85,7 @@ struct ipxg_engine {
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
     // host-side counters
-    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0;
+    uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0, walked_pkts = 0;
     bool prev_valid = false;
     uint32_t prev_sec = 0, prev_usec = 0;
     // stage timing
@@ -149,6 +150,12 @@ static ExportView export_view(ipxg_engine* e) {
 // spills to atomics.  Memory is plentiful (288 GB of HBM) and only the slots written are
 // read, so the margin is generous: skewed traffic (tile aggregation leaves the configs[2] Zipf
 // mix at ~2.4x) does not spill after its first batch.
+static bool wide_walk(const ipxg_engine* e) {
+    if (e->cfg.flags & IPXG_CFG_WALK_WIDE) return true;
+    if (e->cfg.flags & IPXG_CFG_WALK_NARROW) return false;
+    return e->wide;
+}
+
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
     if (est == 0 || est > n) est = n;
@@ -158,13 +165,14 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
         bits = std::min<uint32_t>((uint32_t)std::atoi(pb), BIN_MAX_PART_BITS);
     const uint32_t P = 1u << bits;
     const uint64_t tiles = ((uint64_t)n + BIN_TILE_PKTS - 1) / BIN_TILE_PKTS;
-    const int ag = e->tile_agg ? 1 : 0;
-    if (!e->bin_slots[ag]) {
-        e->bin_slots[ag] = bin_resident_blocks(e->cfg.device_id, ag != 0);
+    const int ag = e->tile_agg ? 1 : 0, wd = wide_walk(e) ? 1 : 0;
+    uint32_t& slots = e->bin_slots[ag][wd];
+    if (!slots) {
+        slots = bin_resident_blocks(e->cfg.device_id, ag != 0, wd != 0);
         if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
-            e->bin_slots[ag] = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
+            slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
     }
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->bin_slots[ag]);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, slots);
     const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * BIN_TILE_PKTS, n);
     const double mean = (double)per_block / P;
     // aggregating batches follow a skewed one (the most loaded partition ~2.4x the mean with
@@ -212,6 +220,7 @@ static Params params(ipxg_engine* e) {
     p.prev_sec = e->prev_sec;
     p.prev_usec = e->prev_usec;
     p.tile_agg = e->tile_agg ? 1 : 0;
+    p.wide = wide_walk(e) ? 1 : 0;
     return p;
 }
 
@@ -662,9 +671,15 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         if (p.tile_agg) e->tile_agg = (uint64_t)c2.agg_packets * 50 >= n;
         else e->tile_agg = e->skew > 2.0;
         if (const char* a = std::getenv("IPXG_TILE_AGG")) e->tile_agg = std::atoi(a) != 0;  // experiments
+        // The wide walk for the next batch: switched on when >= 1/32 of the packets went to the
+        // slow list (a mix of variable-length header chains: VLAN, IPv6, TCP options, tunnels),
+        // kept while >= 1/32 are not the plain shape; plain traffic keeps the narrow 48-byte
+        // loads.  walk=wide|narrow pins it.
+        e->wide = (uint64_t)(c2.slow_count + (p.wide ? c2.walked : 0)) * 32 >= n;
     }
     e->spilled += c2.spilled;
     e->slow_pkts += c2.slow_count;
+    e->walked_pkts += c2.walked;
     e->prev_valid = true;
     e->prev_sec = c2.last_sec;
     e->prev_usec = c2.last_usec;
@@ -1191,6 +1206,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->batches = e->batches;
     out->spilled_packets = e->spilled;
     out->slow_path_packets = e->slow_pkts;
+    out->walked_packets = e->walked_pkts;
     out->aggregated_packets = e->agg_pkts;
     return IPXG_OK;
 }

@@ -105,8 +105,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t BUF_OOB = 0xFFFFFF00u;  // an offset past every buffer (arena_lim <= BUF_OOB)
 
-struct Head48 {  // bytes 0..47 of a frame
-    uint4 c0, c1, c2;
+// The first NC 16-byte chunks of a frame: 3 (bytes 0..47, parse_fast's shape) or, in the wide
+// walk, 5 (bytes 0..79, parse_medium's: up to QinQ + IPv6 + TCP, or IPv6 + TCP timestamps;
+// ~240 VGPRs, 2 waves per SIMD).
+template <int NC>
+struct Head {
+    uint4 c[NC];
 };
 
 __device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
@@ -119,14 +123,20 @@ __device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y,
 #ifndef IPXG_LOAD_AUX
 #define IPXG_LOAD_AUX 2
 #endif
-__device__ __forceinline__ Head48 load_head(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok) {
+// ok: load the frame's chunks (caplen >= 48: the first 3 always; in the wide walk the later
+// ones only below caplen -- a chunk past it reads as zeros with no memory traffic)
+template <int NC>
+__device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok) {
     const uint32_t o = ok ? d.offset : BUF_OOB;
-    Head48 h;
-    h.c0 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o, 0, IPXG_LOAD_AUX));
-    h.c1 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 16, 0, IPXG_LOAD_AUX));
-    h.c2 = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, o + 32, 0, IPXG_LOAD_AUX));
+    Head<NC> h;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const uint32_t ok_k = k < 3 || (uint32_t)(16 * k) < d.caplen;
+        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, ok_k ? o + 16 * k : BUF_OOB, 0, IPXG_LOAD_AUX));
+    }
     return h;
 }
+
 
 // descriptor i (zeros past the batch's end)
 __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, uint32_t i) {
@@ -408,9 +418,14 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 // the partition histogram, the block's segment fill counts, the tile's record stage and its
 // slow list.
 // AGG: with the per-tile flow aggregation (76 KiB of LDS, 2 workgroups per CU); without it
-// 51 KiB (3 per CU).  The host picks the variant per batch (ipxg_engine.cpp setup_bins).
-template <bool AGG>
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG ? 2 : 3)))
+// 51 KiB (3 per CU).
+// WIDE (the wide walk, for mixes of variable-length header chains): 80 bytes of each frame are
+// loaded (5 chunks, same pipeline) and parse_medium takes VLAN/QinQ, IPv6 and TCP-timestamp
+// frames from registers as well; the remaining shapes (MPLS, PPPoE, GRE, IPv6 extension
+// headers, other TCP options, ...) still go to the slow list.
+// The host picks the variants per batch (ipxg_engine.cpp: tile_agg, wide).
+template <bool AGG, bool WIDE>
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : 3)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
@@ -443,7 +458,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
     const uint64_t ts_before = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
-    uint32_t spilled = 0;
+    uint32_t spilled = 0, walked = 0;
+    constexpr int NC = WIDE ? WIDE_DW / 4 : 3;
+    auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(d); };
     bool nonmono = false;
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
@@ -473,7 +490,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
     const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
     ipxg_pkt_desc Dr[DA];
-    Head48 Hr[HA];
+    Head<NC> Hr[HA];
     // The prologue issues its loads in the order the last DA steps of a tile do, with dummy
     // stores where a tile issues heads of its own steps and its record stores: the loop's
     // first waits are shared by the first tile and all later ones, and the compiler sizes
@@ -484,7 +501,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         Dr[k] = load_desc(rs_desc, i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
-            Hr[h] = load_head(rs_arena, Dr[h], fast_ok && fast_shape(Dr[h]));
+            Hr[h] = load_head<NC>(rs_arena, Dr[h], want(Dr[h]));
         } else {
 #pragma unroll
             for (int q = 0; q < 3; ++q) g_dummy_rec[(k * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
@@ -517,15 +534,15 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t i = tile + j * IPXG_BLOCK + tid;
             // this step's packet, loaded HA (head) and DA (descriptor) steps ago
             const ipxg_pkt_desc dc = Dr[j % DA];
-            const Head48 hc = Hr[j % HA];
+            const Head<NC> hc = Hr[j % HA];
             // bytes 40-43 are not parsed: keep their register live until here, or the compiler
             // reuses it while the load is in flight and must drain every load to do so
-            asm volatile("" ::"v"(hc.c2.z));
+            asm volatile("" ::"v"(hc.c[2].z));
             // issue: the descriptor DA steps ahead, the head HA steps ahead
             const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
             Dr[j % DA] = load_desc(rs_desc, ia);
             const ipxg_pkt_desc dh = Dr[(j + HA) % DA];
-            Hr[j % HA] = load_head(rs_arena, dh, fast_ok && fast_shape(dh));
+            Hr[j % HA] = load_head<NC>(rs_arena, dh, want(dh));
             const bool act = i < b.n;
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
@@ -538,15 +555,33 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             DevPkt pk;
             bool have = false, slow = false;
 #ifdef IPXG_EXP_LOADONLY  // timing experiment only: the loads, no parse/rank
-            if (act) c.seen += hc.c0.x ^ hc.c1.y ^ hc.c2.z ^ hc.c0.w ^ hc.c1.x ^ hc.c2.y;
+            if (act) c.seen += hc.c[0].x ^ hc.c[1].y ^ hc.c[2].z ^ hc.c[0].w ^ hc.c[1].x ^ hc.c[2].y;
             if (false) {
 #else
             if (act) {
 #endif
-                if (fast_ok && fast_shape(dc) && parse_fast(hc.c0, hc.c1, hc.c2, dc.caplen, p.frag_enable, pk, c))
-                    have = true;
-                else
-                    slow = true;
+                if constexpr (WIDE) {
+                    uint32_t w[WIDE_DW];
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) {
+                        w[4 * k] = hc.c[k].x;
+                        w[4 * k + 1] = hc.c[k].y;
+                        w[4 * k + 2] = hc.c[k].z;
+                        w[4 * k + 3] = hc.c[k].w;
+                    }
+                    bool ext = false;
+                    if (fast_ok && fast_shape(dc) && parse_medium(w, dc.caplen, p.frag_enable, pk, c, ext)) {
+                        have = true;
+                        walked += ext ? 1 : 0;
+                    } else {
+                        slow = true;
+                    }
+                } else {
+                    if (fast_ok && fast_shape(dc) && parse_fast(hc.c[0], hc.c[1], hc.c[2], dc.caplen, p.frag_enable, pk, c))
+                        have = true;
+                    else
+                        slow = true;
+                }
             }
             if (slow) my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] = i;
             if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
@@ -597,6 +632,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         ctl->pending = 1;
     }
     if (AGG) add_wave_sum(&ctl->agg_packets, folded);
+    if (WIDE) add_wave_sum(&ctl->walked, walked);
 }
 
 // The frames k_bin left for the general parser (VLAN/QinQ, MPLS, PPPoE, GRE, TRILL, IPv6
@@ -683,11 +719,16 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     if (AGG) add_wave_sum(&ctl->agg_packets, folded);
 }
 
-uint32_t bin_resident_blocks(int device, bool agg) {
+typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint32_t*, uint32_t*, uint4*,
+                          unsigned long long*);
+static BinKernel bin_kernel(bool agg, bool wide) {
+    return agg ? (wide ? k_bin<true, true> : k_bin<true, false>) : (wide ? k_bin<false, true> : k_bin<false, false>);
+}
+
+uint32_t bin_resident_blocks(int device, bool agg, bool wide) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, agg ? k_bin<true> : k_bin<false>, IPXG_BLOCK, 0) !=
-            hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide), IPXG_BLOCK, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return (uint32_t)std::max(1, std::min(cus * per_cu, (int)BIN_MAX_GRID));
@@ -696,12 +737,8 @@ uint32_t bin_resident_blocks(int device, bool agg) {
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats) {
-    if (p.tile_agg)
-        hipLaunchKernelGGL(k_bin<true>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
-                           deferred_list, agg_list, stats);
-    else
-        hipLaunchKernelGGL(k_bin<false>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
-                           deferred_list, agg_list, stats);
+    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
+                       t, f, bv, ctl, slow_list, deferred_list, agg_list, stats);
 }
 
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,

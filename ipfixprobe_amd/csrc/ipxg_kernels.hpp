@@ -55,6 +55,7 @@ struct BatchCtl {
     uint32_t max_part;       // most record slots in one partition (segment sizing, k_reduce)
     uint32_t total_slots;    // record slots over all partitions (k_reduce)
     uint32_t agg_packets;    // packets folded into tile aggregates (k_bin / k_bin_slow)
+    uint32_t walked;         // wide walk: packets of its extra shapes (variant choice)
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -102,6 +103,7 @@ struct Params {
     uint32_t prev_valid;     // prev_sec/prev_usec hold the previous batch's last timestamp
     uint32_t prev_sec, prev_usec;
     uint32_t tile_agg;       // k_bin / k_bin_slow aggregate frequent flows per tile (skewed traffic)
+    uint32_t wide;           // k_bin's wide walk (96-byte loads, parse_medium)
 };
 
 struct BatchView {
@@ -164,7 +166,7 @@ struct ComplexView {
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
 // tile-aggregating variant (more LDS)
-uint32_t bin_resident_blocks(int device, bool agg);
+uint32_t bin_resident_blocks(int device, bool agg, bool wide);
 // deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
 // 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,

@@ -458,6 +458,137 @@ __device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, con
 // a frame the register parser may take: 16-byte aligned in the arena, 48 bytes captured
 __device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.offset & 15) == 0 && d.caplen >= 48; }
 
+// ---- register parser for the shapes of the variable-length mixes --------------------------
+// The wide walk (k_bin<., true>) loads a frame's first 80 bytes (WIDE_DW dwords) and parses
+// the header chains that make up most of the configs[2] / configs[4] mixes straight from those
+// registers: Ethernet with 0, 1 or 2 VLAN tags (outer 0x8100 / 0x88A8, inner 0x8100), then
+// IPv4 with IHL 5 or IPv6 whose next header is TCP or UDP, then TCP without options or with the
+// NOP,NOP,Timestamp block (doff 8, the option walk of parse_tcp_hdr succeeds on it whatever
+// the timestamp bytes; with IPv6 only untagged, as its options end at byte 78), or UDP.
+// Every header boundary of these chains sits at 2 mod 4 bytes,
+// and the tags only shift the L3 header by whole dwords, so the window is re-based by 0, 1 or
+// 2 dwords (two selects per dword) and every field is then read at a compile-time offset: no
+// dynamic register indexing, no LDS.  The fields, checks and counters are those parse_frame
+// gives such a frame (parse_eth_hdr parser.cpp:68-155, parse_ipv4_hdr :311-356,
+// parse_ipv6_hdr :423-460, parse_tcp_hdr :469-543, parse_udp_hdr :552-573); any other shape,
+// or any read the caplen checks would not cover, returns false and the frame takes the general
+// parser (k_bin_slow).  *ext: the frame is not the plain shape parse_fast takes.
+constexpr int WIDE_DW = 20;  // 80 bytes
+
+template <int O>
+__device__ __forceinline__ uint32_t wle32(const uint32_t* w) {
+    if constexpr (O % 4 == 0) return w[O / 4];
+    else return __builtin_amdgcn_alignbyte(w[O / 4 + 1], w[O / 4], O % 4);
+}
+template <int O>
+__device__ __forceinline__ uint32_t wb8(const uint32_t* w) { return (w[O / 4] >> (8 * (O % 4))) & 0xFF; }
+template <int O>
+__device__ __forceinline__ uint32_t wbe16(const uint32_t* w) { return bswap16(wle32<O>(w)); }
+
+__device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint32_t caplen, bool frag_enable,
+                                             DevPkt& p, ParseCounts& c, bool& ext) {
+    // Ethernet + tags (parse_eth_hdr): only the outermost tag's VLAN id is kept
+    uint32_t et = wbe16<12>(w), vlan = 0, S = 0;
+    if (et == ETH_P_8021AD || et == ETH_P_8021Q) {
+        vlan = wbe16<14>(w) & 0x0FFF;
+        et = wbe16<16>(w);
+        S = 1;
+        if (et == ETH_P_8021Q) {
+            et = wbe16<20>(w);
+            S = 2;
+            if (et == ETH_P_8021Q) return false;  // a third tag: the general walk
+        }
+    }
+    if (et != ETH_P_IP && et != ETH_P_IPV6) return false;
+    // the window re-based so that the L3 header starts at byte 14 of v
+    constexpr int VD = WIDE_DW - 2;
+    uint32_t v[VD];
+    // masks rather than a select the compiler could fold into a dynamic index of w (which
+    // would put w on the stack)
+    const uint32_t m0 = 0u - (S == 0), m1 = 0u - (S == 1), m2 = 0u - (S == 2);
+#pragma unroll
+    for (int k = 3; k < VD; ++k) v[k] = (w[k] & m0) | (w[k + 1] & m1) | (w[k + 2] & m2);
+    v[0] = v[1] = v[2] = 0;
+    const uint32_t o3 = 14 + 4 * S;  // the L3 offset in the frame
+    uint32_t proto, o4, frag_off = 0;
+    if (et == ETH_P_IP) {
+        if (caplen < o3 + 20) return false;
+        if (wb8<14>(v) != 0x45) return false;          // IHL 5 (options: the general walk)
+        proto = wb8<23>(v);
+        if (proto == 47) return false;                 // GRE
+        const uint32_t fo = wbe16<20>(v);
+        frag_off = fo & 0x1FFF;
+        if (frag_enable && (fo & 0x3FFF)) return false;  // the fragmentation-cache path
+        p.ip_version = 4;
+        p.ip_len = (uint16_t)wbe16<16>(v);
+        p.frag_id = wbe16<18>(v);
+        p.frag_off = (uint16_t)frag_off;
+        p.more_fragments = (fo & 0x2000) ? 1 : 0;
+        p.sip[0] = wle32<26>(v);
+        p.dip[0] = wle32<30>(v);
+        p.sip[1] = p.sip[2] = p.sip[3] = 0;
+        p.dip[1] = p.dip[2] = p.dip[3] = 0;
+        o4 = o3 + 20;
+    } else {
+        if (caplen < o3 + 40) return false;
+        proto = wb8<20>(v);
+        if (proto != 6 && proto != 17) return false;   // extension headers (or another L4)
+        p.ip_version = 6;
+        p.ip_len = (uint16_t)(wbe16<18>(v) + 40);
+        p.frag_id = 0;
+        p.frag_off = 0;
+        p.more_fragments = 0;
+        p.sip[0] = wle32<22>(v);
+        p.sip[1] = wle32<26>(v);
+        p.sip[2] = wle32<30>(v);
+        p.sip[3] = wle32<34>(v);
+        p.dip[0] = wle32<38>(v);
+        p.dip[1] = wle32<42>(v);
+        p.dip[2] = wle32<46>(v);
+        p.dip[3] = wle32<50>(v);
+        o4 = o3 + 40;
+    }
+    const bool v6 = et == ETH_P_IPV6;
+    uint32_t ports = 0, flags = 0;
+    bool tcp_opt = false;
+    if (frag_off == 0 && proto == 6) {
+        if (caplen < o4 + 20) return false;
+        const uint32_t w3 = v6 ? wle32<66>(v) : wle32<46>(v);  // L4 bytes 12..15
+        const uint32_t doff = (w3 & 0xFF) >> 4;
+        if (doff > 5) {
+            if (v6 && S != 0) return false;  // the options would end past the window
+            const uint32_t opt = v6 ? wle32<74>(w) : wle32<54>(v);  // L4 bytes 20..23
+            if (doff != 8 || opt != 0x0A080101u || caplen < o4 + 32) return false;
+            tcp_opt = true;
+        }
+        flags = (w3 >> 8) & 0xFF;
+        ports = v6 ? wle32<54>(v) : wle32<34>(v);
+    } else if (frag_off == 0 && proto == 17) {
+        if (caplen < o4 + 8) return false;
+        ports = v6 ? wle32<54>(v) : wle32<34>(v);
+    }
+    p.ip_proto = (uint8_t)proto;
+    p.tcp_flags = (uint8_t)flags;
+    p.ethertype = (uint16_t)et;
+    p.src_port = bswap16(ports);
+    p.dst_port = bswap16(ports >> 16);
+    p.vlan_id = vlan;
+    ext = S != 0 || v6 || tcp_opt;
+    c.seen++;
+    c.parsed++;
+    if (v6) {
+        c.ipv6++;
+        c.ipv6_bytes += caplen;
+    } else {
+        c.ipv4++;
+        c.ipv4_bytes += caplen;
+    }
+    if (frag_off == 0 && proto == 6) c.tcp++;
+    if (frag_off == 0 && proto == 17) c.udp++;
+    if (vlan) c.vlan++;
+    return true;
+}
+
 // ---- header staging into LDS ------------------------------------------------------------
 // Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
 // zero-masked past caplen, plus one zero chunk so straddling reads see zeros.

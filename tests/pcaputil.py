@@ -60,7 +60,7 @@ STATS_FIELDS = [
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
     "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
-    "aggregated_packets",
+    "aggregated_packets", "walked_packets",
 ]
 
 

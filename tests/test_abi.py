@@ -50,7 +50,9 @@ def test_config_defaults_and_options():
     assert (c.cache_exp, c.active_s) == (22, 5)
     c = make_config("dev=3;batch=4096;dlt=LINUX_SLL")
     assert (c.device_id, c.batch_pkts, c.datalink) == (3, 4096, 113)
-    for bad in ("s=3", "s=31", "x=1", "fe=yes", "fs=0", "a=", "batch=0"):
+    assert make_config("walk=wide").flags == 0x2 and make_config("walk=narrow").flags == 0x4
+    assert make_config("walk=wide;walk=auto").flags == 0 and make_config("ingest=atomic;walk=wide").flags == 0x3
+    for bad in ("s=3", "s=31", "x=1", "fe=yes", "fs=0", "a=", "batch=0", "walk=deep"):
         with pytest.raises(IpxgError):
             make_config(bad)
 

@@ -123,15 +123,22 @@ def _stream(case):
     return synth.flow_stream(**kw).batch()
 
 
+def _with(params, extra):
+    return ";".join(x for x in (params, extra) if x)
+
+
+@pytest.mark.parametrize("walk", ["", "walk=wide"])
 @pytest.mark.parametrize("batch", [None, 1, 37, 1000])
 @pytest.mark.parametrize("ci", range(len(STREAMS)))
-def test_stream_parity(ci, batch):
+def test_stream_parity(ci, batch, walk):
+    """walk "": the engine's choice per batch (narrow first, wide after a batch of mixed shapes);
+    walk=wide: k_bin walks every header chain in LDS from the first batch."""
     from ipfixprobe_amd import run_capture
     case = STREAMS[ci]
     arena, desc = _stream(case)
     want, wst = oracle_py.run_capture(arena, desc, 1, **oracle_kwargs(case["params"]))
     assert wst["end_no_res"] == 0
-    got, gst = run_capture(arena, desc, params=case["params"], batch=batch)
+    got, gst = run_capture(arena, desc, params=_with(case["params"], walk), batch=batch)
     d = flowcmp.diff(got, want)
     assert not d, d
     assert gst["fragmented_packets"] == wst["fragmented_packets"]
@@ -334,16 +341,19 @@ def test_partition_estimate_too_small_overflows_lds():
     assert not d, d
 
 
+@pytest.mark.parametrize("walk", ["narrow", "wide"])
 @pytest.mark.parametrize("seed", [31, 32])
-def test_flows_fuzz_corpus(seed):
-    """The parser fuzz corpus through the whole ingest (k_bin's register fast path for plain
-    Eth/IPv4/UDP|TCP frames and its general LDS path for everything else) against the
-    oracle's flow records and parser counters."""
+def test_flows_fuzz_corpus(seed, walk):
+    """The parser fuzz corpus through the whole ingest against the oracle's flow records and
+    parser counters: walk=narrow (k_bin's register fast path for plain Eth/IPv4/UDP|TCP frames,
+    k_bin_slow's LDS walk for everything else) and walk=wide (k_bin walks every chain in LDS)."""
     from ipfixprobe_amd import run_capture
     corpus = synth.fuzz_corpus(20000, seed=seed)
     arena, desc = synth.to_batch(corpus)
     want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
-    got, gst = run_capture(arena, desc)
+    got, gst = run_capture(arena, desc, params="walk=" + walk)
+    if walk == "wide":
+        assert gst["walked_packets"] > 0
     d = flowcmp.diff(got, want)
     assert not d, d
     for k in ("seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",

@@ -53,16 +53,20 @@ def _run_batches(params, batches, finish=True):
     return recs, st
 
 
+@pytest.mark.parametrize("walk", ["", ";walk=wide", ";walk=narrow"])
 @pytest.mark.parametrize("name", sorted(MIXES))
-def test_workload_parity(name):
+def test_workload_parity(name, walk):
     """2M packets of the mix over 1M flows, submitted as four device batches with flows carried
-    across them, against the oracle run over the same packets in one pass."""
+    across them, against the oracle run over the same packets in one pass; with the engine's
+    choice of header walk per batch and with each walk pinned."""
     import torch
     gen = _gen(name, 1_000_000)
     n, nb = 500_000, 4
     batches = [gen.batch(k * n, n) for k in range(nb)]
     torch.cuda.synchronize()
-    got, gst = _run_batches("s=21", batches)
+    got, gst = _run_batches("s=21" + walk, batches)
+    if walk != ";walk=narrow":
+        assert gst["walked_packets"] > 0
     want, wst = [], None
     c = oracle_py.OracleCache(cache_exp=22)
     for fr, de in batches:
