@@ -60,7 +60,7 @@ struct ipxg_engine {
     // scratch
     DevBuf defer_a, defer_b, frag_list, frag_sorted, frag_ports, sort_tmp;
     DevBuf adefer_a, adefer_b;           // deferred tile aggregates (3 x 16 B each)
-    DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 5 u32 arrays of nranks
+    DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 4 u32 arrays of nranks, then the key set
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
     uint32_t bin_slots[2][2] = {};       // k_bin workgroups resident at once (its grid), [agg][wide]
     bool wide = false;                   // the next batch's k_bin walks every header chain (WIDE)
@@ -69,6 +69,7 @@ struct ipxg_engine {
     // has not read yet (completed by the next call on the engine)
     struct {
         bool on = false;
+        bool tail = false;  // k_fin_list not launched yet (the next call picks its mode)
         BatchView bv;
         Params p;
         uint32_t n = 0;
@@ -442,11 +443,25 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
 
 // The in-flight asynchronous batch, if any: wait for its kernels and run post_batch.  Every
 // entry point that reads or changes engine state calls this first.
+// The asynchronous batch's last kernel, launched by the next call: k_fin_list, with the
+// finish folded in when that call is ipxg_finish on a table that was empty before the batch.
+static int launch_tail(ipxg_engine* e, bool finishing) {
+    if (!e->inflight.tail) return IPXG_OK;
+    e->inflight.tail = false;
+    ev_rec(e, 3);
+    launch_fin_list(e->st, e->inflight.bv, e->inflight.p, table_view(e), frag_view(e), export_view(e), e->ctl_d,
+                    (HotSlot*)e->fin_list.p, e->stats_d, e->inflight.n, finishing);
+    ev_rec(e, 4);
+    HIPCHK(e, hipGetLastError());
+    return IPXG_OK;
+}
+
 static int complete_batch(ipxg_engine* e) {
     if (!e->inflight.on) return IPXG_OK;
-    e->inflight.on = false;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     int rc;
+    if ((rc = launch_tail(e, false))) return rc;
+    e->inflight.on = false;
     if ((rc = sync_ctl(e))) return rc;
     return post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, false);
 }
@@ -509,16 +524,19 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 2);
         launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
-        ev_rec(e, 3);
-        launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n);
-        ev_rec(e, 4);
+        if (!((batch->flags & IPXG_BATCH_ASYNC) && (batch->flags & IPXG_BATCH_DEVICE))) {
+            ev_rec(e, 3);
+            launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
+            ev_rec(e, 4);
+        }
     } else {
         launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
         ev_rec(e, 1);
     }
     HIPCHK(e, hipGetLastError());
     if ((batch->flags & IPXG_BATCH_ASYNC) && (batch->flags & IPXG_BATCH_DEVICE) && binned) {
-        e->inflight.on = true;  // the next call publishes and reads the control block
+        e->inflight.on = true;  // the next call launches k_fin_list, publishes and reads the control block
+        e->inflight.tail = true;
         e->inflight.bv = bv;
         e->inflight.p = p;
         e->inflight.n = n;
@@ -617,9 +635,13 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     if (ncx) {
         ev_rec(e, 5);
         e->complex_total += ncx;
-        if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 5 * 4))) return rc;
+        const uint32_t kcap = pow2_at_least((uint64_t)ncx * 2 + 1);  // the complex flows' key set
+        if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 4 * 4 + (size_t)kcap * 12))) return rc;
         uint32_t* cr = (uint32_t*)e->cx_rank.p;
-        ComplexView cx = {nullptr, nullptr, cr, cr + ncx, cr + 2 * (size_t)ncx, cr + 3 * (size_t)ncx};
+        unsigned long long* ck = reinterpret_cast<unsigned long long*>(cr + 4 * (size_t)ncx);
+        HIPCHK(e, hipMemsetAsync(ck, 0, (size_t)kcap * 8, e->st));
+        ComplexView cx = {nullptr, nullptr, cr, cr + ncx, cr + 2 * (size_t)ncx, cr + 3 * (size_t)ncx,
+                          ck, reinterpret_cast<uint32_t*>(ck + kcap), kcap - 1};
         launch_complex_rank(e->st, table_view(e), cx, e->ctl_d, e->cap);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
@@ -718,22 +740,40 @@ int ipxg_finish(ipxg_engine* e) {
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if (e->inflight.on) {
-        // Enqueue the finish right behind the batch, guarded on the device (k_finish's guard):
-        // one host round trip for batch + finish when the batch needs nothing from the host.
-        ev_rec(e, 9);
-        launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d, e->ctl_d, e->ex_count, e->live);
-        HIPCHK(e, hipGetLastError());
-        ev_rec(e, 10);
+        // The batch's k_fin_list is still to be launched: into a table that was empty before
+        // the batch, it exports what it finalises itself (fused finish, no table scan).
+        // Otherwise the finish is enqueued right behind the batch, guarded on the device
+        // (k_finish's guard).  Either way one host round trip for batch + finish when the batch
+        // needs nothing from the host.
+        const bool fuse = e->inflight.tail && e->live == 0 && e->keys == 0;
+        if ((rc = launch_tail(e, fuse))) return rc;
+        if (!fuse) {
+            ev_rec(e, 9);
+            launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d, e->ctl_d, e->ex_count, e->live);
+            HIPCHK(e, hipGetLastError());
+            ev_rec(e, 10);
+        }
         // the batch is consumed here whatever happens next: an error below must not make the
         // next call run post_batch again on a table k_finish may already have emptied
         e->inflight.on = false;
         if ((rc = publish_ctl(e))) return rc;
         HIPCHK(e, stream_wait(e->st));
         if ((rc = check_ex(e))) return rc;
-        const bool held = e->ctl_h->hold != 0;
-        HIPCHK(e, hipMemsetAsync(&e->ctl_d->hold, 0, sizeof(uint32_t), e->st));
-        if ((rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, !held))) return rc;
-        if (!held) {
+        if (fuse) {
+            // complete unless k_fin_list could not fuse (host work) or left complex flows
+            const bool done = e->ctl_h->fused && !e->ctl_h->complex_count;
+            if ((rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, true))) return rc;
+            if (done) {
+                e->keys = e->live = 0;
+                e->prev_valid = false;
+                return IPXG_OK;
+            }
+            // the remaining flows: the finish below
+        }
+        const bool held = !fuse && e->ctl_h->hold != 0;
+        if (!fuse) HIPCHK(e, hipMemsetAsync(&e->ctl_d->hold, 0, sizeof(uint32_t), e->st));
+        if (!fuse && (rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, !held))) return rc;
+        if (!fuse && !held) {
             if (e->prof && e->prof_level == 1) {
                 e->tm.finish_ms += ev_ms(e, 9);
                 e->tm.finish_launches++;

@@ -1046,13 +1046,20 @@ void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSl
 // ---- finalisation of the flows k_reduce completed -----------------------------------------
 // One lane per listed slot: finalize_slot with the creator's headers staged in the lane's
 // LDS column (256-thread blocks keep the register budget of the general parser).
+// finishing (ipxg_finish right behind an asynchronous submit into an empty table): when
+// nothing of the batch needs the host (no fragments, deferrals or scan), every flow this
+// kernel completes is exported as FORCED and its slot emptied here -- the finish's export
+// folded into the finalise pass, so no table scan (k_finish) follows.  Flows it marks complex
+// stay; the host then runs the sequential path and a k_finish for them (ctl->fused tells it).
 __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
                                                          ExportView ex, BatchCtl* ctl, const HotSlot* fin_list,
-                                                         unsigned long long* stats) {
+                                                         unsigned long long* stats, uint32_t finishing) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     __shared__ uint32_t sc[ST_COUNT];
     __shared__ uint32_t cnt[3];  // new live, complex, exported
     const uint32_t nf = ctl->fin_count;  // final: k_reduce has completed
+    const bool fused = finishing && !(ctl->frag_count || ctl->deferred || ctl->agg_deferred || ctl->pending);
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctl->fused = fused ? 1u : 0u;
     if (blockIdx.x * IPXG_BLOCK >= nf) return;
     const uint32_t tid = threadIdx.x;
     if (tid < ST_COUNT) sc[tid] = 0;
@@ -1062,13 +1069,15 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
     uint32_t n_live = 0, n_cx = 0, n_ex = 0;
     for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {
         const uint32_t k = base + tid;
-        bool do_export = false;
+        bool do_export = false, fin_export = false;
         uint8_t reason = 0;
-        ipxg_flow_record er;
+        ipxg_flow_record er, fr_rec;
         if (k < nf) {
             const HotSlot h = fin_list[k];  // the slot's merged image, its index in pad
-            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er);
+            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er,
+                                                     fused ? &fr_rec : nullptr);
             if (fr.status == FIN_COMPLEX) n_cx++;
+            else if (fused) fin_export = true;
             else if (fr.created) n_live++;
             do_export = fr.do_export;
             reason = fr.reason;
@@ -1080,6 +1089,15 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
             n_ex++;
         }
         count_v6_exports(ex, do_export && er.ip_version == 6);
+        if (fused) {  // uniform
+            const uint32_t pf = wave_append(ex.count, fin_export);
+            if (fin_export) {
+                store_export(ex, pf, fr_rec, IPXG_FLOW_END_FORCED);
+                atomicAdd(&sc[ST_END_FORCED], 1u);
+                n_ex++;
+            }
+            count_v6_exports(ex, fin_export && fr_rec.ip_version == 6);
+        }
     }
     if (n_live) atomicAdd(&cnt[0], n_live);
     if (n_cx) atomicAdd(&cnt[1], n_cx);
@@ -1093,11 +1111,12 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
 }
 
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
-                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n) {
+                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
+                     bool finishing) {
     uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, ex, ctl, fin_list,
-                       stats);
+                       stats, finishing ? 1u : 0u);
 }
 
 }  // namespace ipxg

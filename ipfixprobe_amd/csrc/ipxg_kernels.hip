@@ -31,6 +31,15 @@ __device__ __forceinline__ bool flow_accumulate(const TableView& t, const Params
 // ---- K1: ingest ------------------------------------------------------------------------
 enum IngestMode { MODE_INGEST = 0, MODE_GATHER = 1 };
 
+// rank of the complex flow with canonical key lo, or -1
+__device__ __forceinline__ int64_t complex_rank_of(const ComplexView& cx, uint64_t lo) {
+    for (uint32_t e = (uint32_t)lo & cx.kmask;; e = (e + 1) & cx.kmask) {
+        const unsigned long long k = cx.keys[e];
+        if (k == lo) return cx.key_rank[e];
+        if (k == 0ull) return -1;
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, TableView t, FragView f,
                                                        BatchCtl* ctl, uint32_t* deferred_list,
@@ -94,9 +103,9 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, Ta
             uint64_t lo, hf;
             uint32_t cdir;
             canon(pk, p, lo, cdir, hf);
-            int64_t s = probe_find(t, lo);
-            if (s >= 0 && (t.hot[s].state & SLOT_COMPLEX)) {
-                uint32_t r = t.slot_rank[s];
+            const int64_t rr = complex_rank_of(cx, lo);
+            if (rr >= 0) {
+                const uint32_t r = (uint32_t)rr;
                 uint32_t pos = atomicAdd(&cx.cursor[r], 1u);
                 cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
             }
@@ -344,8 +353,12 @@ __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView c
         cx.seg[r] = (uint32_t)old;
         cx.len[r] = npk;
         cx.cursor[r] = 0;
+        uint32_t e = (uint32_t)h.key & cx.kmask;  // >= 2 entries per complex flow: terminates
+        while (atomicCAS(&cx.keys[e], 0ull, (unsigned long long)h.key) != 0ull) e = (e + 1) & cx.kmask;
+        cx.key_rank[e] = r;
     }
 }
+
 
 void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap) {
     hipLaunchKernelGGL(k_complex_rank, dim3(table_grid(cap)), dim3(256), 0, st, t, cx, ctl, cap);

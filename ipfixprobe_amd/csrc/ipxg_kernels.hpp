@@ -56,6 +56,7 @@ struct BatchCtl {
     uint32_t total_slots;    // record slots over all partitions (k_reduce)
     uint32_t agg_packets;    // packets folded into tile aggregates (k_bin / k_bin_slow)
     uint32_t walked;         // wide walk: packets of its extra shapes (variant choice)
+    uint32_t fused;          // k_fin_list exported and emptied the flows it finalised (finish fused)
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -161,7 +162,10 @@ struct ComplexView {
     uint32_t* slot_of;   // per rank
     uint32_t* seg;       // per rank: segment start
     uint32_t* len;       // per rank: packets
-};
+    unsigned long long* keys;  // open-addressing set of the complex flows' keys (kmask + 1
+    uint32_t* key_rank;        // entries, zeroed) -> rank: k_complex_gather finds a packet's flow
+    uint32_t kmask;            // here, not by probing the flow table (whose chains a fused
+};                             // finish may have cut: k_fin_list empties slots)
 
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
@@ -179,7 +183,8 @@ void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableV
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                    uint32_t* deferred_list, uint4* agg_list);
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
-                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n);
+                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
+                     bool finishing);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
 void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,

@@ -702,10 +702,13 @@ struct FinResult {
 // re-parses its first packet (FlowRecord::create's fields, cache.cpp:94-133).  Writes the slot
 // (and its cold record) back.
 // LDSW: stage the creator's headers in the lane's LDS column `col` (else byte loads).
+// out (a finish follows, k_fin_list's fused mode): a completed record goes to *out instead of
+// the table, and the slot is emptied.
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
-                                                   bool force_cx, uint32_t* col, ipxg_flow_record& er) {
+                                                   bool force_cx, uint32_t* col, ipxg_flow_record& er,
+                                                   ipxg_flow_record* out = nullptr) {
     FinResult res = {FIN_DONE, false, false, 0};
     const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
@@ -776,9 +779,14 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     rec.dst_tcp_flags |= (uint8_t)(h.tflags >> (8 * (sd ^ 1)));
     rec.time_last_sec = dl.ts_sec;
     rec.time_last_usec = dl.ts_usec;
+    res.created = !live;
+    if (out) {
+        *out = rec;
+        clear_slot(&t.hot[s], 0, 0);  // empty (every slot empties at the finish)
+        return res;
+    }
     t.cold[s] = rec;
     clear_slot(&t.hot[s], h.key, SLOT_LIVE);
-    res.created = !live;
     return res;
 }
 
