@@ -174,6 +174,10 @@ typedef struct ipxg_config {
 #define IPXG_CFG_WALK_NARROW 0x4u   /* walk=narrow: k_bin parses the plain Eth/IPv4/UDP|TCP
                                        shape only (48-byte loads), the rest goes through
                                        the slow list (k_bin_slow)                           */
+#define IPXG_CFG_PARSER_STATS 0x8u  /* ps=true: the parser's side statistics -- TCP/UDP port
+                                       frequencies (TopPorts) and per-VLAN counters with the
+                                       packet-size histogram (VlanStats), parser-stats.hpp
+                                       :126-201 -- kept on the device (ipxg_parser_stats) */
 
 typedef struct ipxg_stats {
     /* parser counters, reference parser-stats.hpp:126-201 (the subset on the path) */
@@ -213,6 +217,32 @@ typedef struct ipxg_stats {
                                  timestamp option) parsed from registers by k_bin     */
 } ipxg_stats;
 
+/* VlanStats (parser-stats.hpp:126-160) for one VLAN id; sizes are packet_len = caplen,
+   histogram buckets 0-64, 65-127, 128-255, 256-511, 512-1023, 1024-1517, 1518-2047,
+   2048-4095, 4096-8191, 8192+ (PacketSizeHistogram, parser-stats.hpp:42-95). */
+#define IPXG_VLAN_IDS 4096
+#define IPXG_SIZE_BUCKETS 10
+typedef struct ipxg_vlan_stats {
+    uint64_t ipv4_packets;
+    uint64_t ipv6_packets;
+    uint64_t ipv4_bytes;
+    uint64_t ipv6_bytes;
+    uint64_t tcp_packets;
+    uint64_t udp_packets;
+    uint64_t total_packets;
+    uint64_t total_bytes;
+    uint64_t hist_packets[IPXG_SIZE_BUCKETS];
+    uint64_t hist_bytes[IPXG_SIZE_BUCKETS];
+} ipxg_vlan_stats;
+
+/* One entry of TopPorts::get_top_ports (topPorts.cpp): protocol 6 (TCP) or 17 (UDP). */
+typedef struct ipxg_port_stat {
+    uint16_t port;
+    uint8_t protocol;
+    uint8_t reserved[5];
+    uint64_t frequency;
+} ipxg_port_stat;
+
 typedef struct ipxg_engine ipxg_engine;
 
 /* Fill *cfg with the reference defaults (cache.hpp:52-64, :91-102). */
@@ -249,6 +279,13 @@ int ipxg_device_exports(ipxg_engine* eng, const ipxg_flow_record** dptr, size_t*
 /* Forget the pending exports without copying them (caller consumed them on device). */
 int ipxg_clear_exports(ipxg_engine* eng);
 int ipxg_get_stats(ipxg_engine* eng, ipxg_stats* out);
+/* Parser side statistics (engine created with ps=true, else IPXG_EINVAL): TopPorts' TCP and
+ * UDP frequency arrays (65536 entries each; parser.cpp:484-485, 563-564) and VlanStats for
+ * every VLAN id (IPXG_VLAN_IDS entries; parser.cpp:798); any output may be null. */
+int ipxg_parser_stats(ipxg_engine* eng, uint64_t* tcp_ports, uint64_t* udp_ports, ipxg_vlan_stats* vlans);
+/* TopPorts::get_top_ports (topPorts.cpp): up to n most frequent ports, TCP then UDP, ties in
+ * port order, *got entries written. */
+int ipxg_top_ports(ipxg_engine* eng, size_t n, ipxg_port_stat* out, size_t* got);
 
 /* ---- stage timing (HIP events on the engine's stream) --------------------------------- */
 typedef struct ipxg_timing {

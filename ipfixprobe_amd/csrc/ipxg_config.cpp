@@ -5,8 +5,8 @@
 // (CacheOptParser, cache.hpp:81-221; OptionsParser::parse, options.cpp:62-160: ';'-separated
 // tokens, "name=value" or "name" followed by its value as the next token), plus the GPU keys
 // "dev"/"device", "batch", "dlt" (EN10MB | RAW | LINUX_SLL | LINUX_SLL2 or a number) and
-// "ingest" (binned | atomic) and "walk" (auto | wide | narrow: which k_bin variant walks
-// the header chains).
+// "ingest" (binned | atomic), "walk" (auto | wide | narrow: which k_bin variant walks
+// the header chains) and "ps"/"parser-stats" (true | false: TopPorts + VlanStats).
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -95,6 +95,11 @@ extern "C" int ipxg_config_parse(const char* params, ipxg_config* cfg) {
             if (!arg(a)) return IPXG_EINVAL;
             if (a == "atomic") cfg->flags |= IPXG_CFG_ATOMIC_INGEST;
             else if (a == "binned") cfg->flags &= ~IPXG_CFG_ATOMIC_INGEST;
+            else return IPXG_EINVAL;
+        } else if (name == "ps" || name == "parser-stats") {
+            if (!arg(a)) return IPXG_EINVAL;
+            if (a == "true") cfg->flags |= IPXG_CFG_PARSER_STATS;
+            else if (a == "false") cfg->flags &= ~IPXG_CFG_PARSER_STATS;
             else return IPXG_EINVAL;
         } else if (name == "walk") {
             if (!arg(a)) return IPXG_EINVAL;

@@ -179,6 +179,8 @@ struct DevPkt {
     uint32_t frag_id;
     uint16_t ethertype, ip_len, src_port, dst_port, frag_off;
     uint8_t ip_version, ip_proto, tcp_flags, more_fragments;
+    uint8_t l4;  // 6 / 17: parse_tcp_hdr / parse_udp_hdr read the ports (TopPorts counted them,
+                 // parser.cpp:484-485, 563-564) -- for TCP even when the packet is then dropped
     // FULL-only fields
     uint32_t mac_lo, mac_mid, mac_hi;  // dst_mac[0..5] src_mac[0..5] packed in memory order
     uint32_t mpls_top, tcp_seq, tcp_ack, tcp_mss;
@@ -412,6 +414,7 @@ __device__ __forceinline__ void parse_tcp(const S& s, uint32_t base, uint32_t da
     uint32_t w0 = s.le32(base);
     p.src_port = bswap16(w0);
     p.dst_port = bswap16(w0 >> 16);
+    p.l4 = 6;
     uint32_t w3 = s.le32(base + 12);
     p.tcp_flags = (uint8_t)(w3 >> 8);
     if (FULL) {
@@ -446,7 +449,7 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
                                             ParseCounts& c) {
     p.ip_version = 0; p.ip_proto = 0; p.tcp_flags = 0; p.more_fragments = 0;
     p.ethertype = 0; p.ip_len = 0; p.src_port = 0; p.dst_port = 0; p.frag_off = 0;
-    p.vlan_id = 0; p.frag_id = 0;
+    p.vlan_id = 0; p.frag_id = 0; p.l4 = 0;
     for (int k = 0; k < 4; ++k) p.sip[k] = p.dip[k] = 0;
     if (FULL) {
         p.mac_lo = p.mac_mid = p.mac_hi = 0;
@@ -530,6 +533,7 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
             uint32_t w0 = s.le32(off);
             p.src_port = bswap16(w0);
             p.dst_port = bswap16(w0 >> 16);
+            p.l4 = 17;
             c.udp++;
         }
     }

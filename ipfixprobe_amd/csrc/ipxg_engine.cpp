@@ -55,6 +55,7 @@ struct ipxg_engine {
     uint32_t* ctl_hd = nullptr;  // its device address
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
+    unsigned long long* pstat_d = nullptr;  // ps=true: TopPorts + VlanStats (PSTAT_WORDS)
     // staging for host batches
     DevBuf arena, desc;
     // scratch
@@ -136,7 +137,9 @@ static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
     return IPXG_OK;
 }
 
-static TableView table_view(ipxg_engine* e) { return TableView{e->hot, e->cold, e->slot_rank, e->cap - 1}; }
+static TableView table_view(ipxg_engine* e) {
+    return TableView{e->hot, e->cold, e->slot_rank, e->cap - 1, e->pstat_d};  // pstat_d starts with the ports
+}
 
 static ExportView export_view(ipxg_engine* e) {
     return ExportView{e->ex, e->ex_count_d, e->ex_cap, e->count6_on ? 1u : 0u};
@@ -286,7 +289,7 @@ static int rehash(ipxg_engine* e, uint32_t new_cap) {
     int rc = alloc_table(e, new_cap, &nh, &nc, &nr);
     if (rc) return set_err(e, rc, "table allocation failed (capacity " + std::to_string(new_cap) + ")");
     HIPCHK(e, hipMemsetAsync(e->misc_d, 0, sizeof(uint32_t), e->st));
-    TableView to{nh, nc, nr, new_cap - 1};
+    TableView to{nh, nc, nr, new_cap - 1, e->pstat_d};
     launch_rehash(e->st, table_view(e), e->cap, to, e->misc_d);
     HIPCHK(e, hipGetLastError());
     uint32_t fail = 0;
@@ -402,6 +405,10 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
         return fail(IPXG_EDEVICE);
+    if (e->cfg.flags & IPXG_CFG_PARSER_STATS) {
+        if (hipMalloc((void**)&e->pstat_d, PSTAT_WORDS * 8) != hipSuccess) return fail(IPXG_ENOMEM);
+        if (hipMemsetAsync(e->pstat_d, 0, PSTAT_WORDS * 8, e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+    }
     if (hipStreamSynchronize(e->st) != hipSuccess) return fail(IPXG_EDEVICE);
     *out = e;
     return IPXG_OK;
@@ -418,6 +425,7 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->ctl_h) hipHostFree(e->ctl_h);
     hipFree(e->misc_d);
     hipFree(e->stats_d);
+    if (e->pstat_d) hipFree(e->pstat_d);
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
     if (e->plan_h) hipHostFree(e->plan_h);
@@ -513,6 +521,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         if ((rc = setup_bins(e, n, bins))) return rc;
         if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
     }
+    if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
     ev_rec(e, 0);
     if (binned) {
         uint32_t* dl = (uint32_t*)e->defer_a.p;
@@ -810,6 +819,7 @@ int ipxg_reset(ipxg_engine* e) {
     const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
     HIPCHK(e, hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st));
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+    if (e->pstat_d) HIPCHK(e, hipMemsetAsync(e->pstat_d, 0, PSTAT_WORDS * 8, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->ex_count = e->ex_head = 0;
     e->ex6_valid = e->count6_on;
@@ -1199,6 +1209,51 @@ int ipxg_clear_exports(ipxg_engine* e) {
     e->ex_head = e->ex_count = 0;
     e->ex6_valid = e->count6_on;
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));  // ordered on the stream
+    return IPXG_OK;
+}
+
+int ipxg_parser_stats(ipxg_engine* e, uint64_t* tcp_ports, uint64_t* udp_ports, ipxg_vlan_stats* vlans) {
+    if (!e) return IPXG_EINVAL;
+    if (!e->pstat_d) return set_err(e, IPXG_EINVAL, "parser statistics are off (create the engine with ps=true)");
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    std::vector<uint64_t> h(PSTAT_WORDS);
+    HIPCHK(e, hipMemcpyAsync(h.data(), e->pstat_d, PSTAT_WORDS * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    static_assert(sizeof(ipxg_vlan_stats) == VS_N * 8, "VlanStats layout");
+    if (tcp_ports) std::memcpy(tcp_ports, h.data(), 65536 * 8);
+    if (udp_ports) std::memcpy(udp_ports, h.data() + 65536, 65536 * 8);
+    if (vlans) std::memcpy(vlans, h.data() + PSTAT_PORTS, (size_t)IPXG_VLAN_IDS * VS_N * 8);
+    return IPXG_OK;
+}
+
+// TopPorts::get_top_ports (topPorts.cpp): every TCP port, then every UDP port, in port order,
+// goes into a buffer of n entries kept in decreasing frequency, after the entries of equal
+// frequency (update_port_buffer's lower_bound on `frequency >= count`); a zero frequency never
+// enters.  That is: the ports of non-zero frequency, stably sorted by decreasing frequency,
+// the first n.
+int ipxg_top_ports(ipxg_engine* e, size_t n, ipxg_port_stat* out, size_t* got) {
+    if (!e || (!out && n) || !got) return IPXG_EINVAL;
+    std::vector<uint64_t> f(2 * 65536);
+    int rc;
+    if ((rc = ipxg_parser_stats(e, f.data(), f.data() + 65536, nullptr))) return rc;
+    std::vector<uint32_t> idx;
+    for (uint32_t k = 0; k < 2 * 65536; ++k)
+        if (f[k]) idx.push_back(k);
+    const size_t m = std::min(n, idx.size());
+    std::partial_sort(idx.begin(), idx.begin() + m, idx.end(), [&](uint32_t a, uint32_t b) {
+        return f[a] != f[b] ? f[a] > f[b] : a < b;  // a < b: TCP before UDP, then port order
+    });
+    for (size_t k = 0; k < m; ++k) {
+        std::memset(&out[k], 0, sizeof(out[k]));
+        out[k].port = (uint16_t)(idx[k] & 0xFFFF);
+        out[k].protocol = idx[k] < 65536 ? 6 : 17;
+        out[k].frequency = f[idx[k]];
+    }
+    *got = m;
     return IPXG_OK;
 }
 

@@ -926,11 +926,13 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
         // loads, no search); a segment longer than a wave loops (wave-uniform).  The segments'
         // positions are wave-uniform (scalar), read before the loads are issued, so no branch
-        // separates a load from its use.
+        // separates a load from its use.  Two register sets (A, B): the next group's loads are
+        // in flight while this group's records are folded into the LDS table.
         const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-        for (uint32_t s0 = wv; s0 < nseg; s0 += NW * RED_U) {
-            uint4 r[RED_U];
-            uint32_t sc[RED_U], sl[RED_U];
+        constexpr uint32_t STEP = NW * RED_U;
+        uint4 ra[RED_U], rb[RED_U];
+        uint32_t sca[RED_U], sla[RED_U], scb[RED_U], slb[RED_U];
+        auto issue = [&](uint32_t s0, uint4(&r)[RED_U], uint32_t(&sc)[RED_U], uint32_t(&sl)[RED_U]) {
 #pragma unroll
             for (uint32_t u = 0; u < RED_U; ++u) {
                 const uint32_t si = s0 + u * NW;
@@ -947,6 +949,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                 r[u] = segs[(size_t)sc[u] * bv.seg_cap + (lane < sl[u] ? lane : 0)];  // unconditional load
 #endif
             }
+        };
+        auto fold = [&](const uint4(&r)[RED_U], const uint32_t(&sc)[RED_U], const uint32_t(&sl)[RED_U]) {
 #pragma unroll
             for (uint32_t u = 0; u < RED_U; ++u) {
                 const uint4* sg = segs + (size_t)sc[u] * bv.seg_cap;
@@ -956,6 +960,14 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                     red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane, off + lane < sl[u]);
                 }
             }
+        };
+        issue(wv, ra, sca, sla);
+        for (uint32_t s0 = wv; s0 < nseg; s0 += 2 * STEP) {
+            issue(s0 + STEP, rb, scb, slb);
+            fold(ra, sca, sla);
+            if (s0 + STEP >= nseg) break;  // uniform
+            issue(s0 + 2 * STEP, ra, sca, sla);
+            fold(rb, scb, slb);
         }
     }
     __syncthreads();

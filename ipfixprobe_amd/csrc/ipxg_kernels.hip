@@ -219,6 +219,13 @@ __global__ __launch_bounds__(256) void k_frag_accumulate(BatchView b, Params p, 
     DevPkt pk;
     ipxg_pkt_desc d;
     if (!reparse<false>(b, p, f, idx, pk, d)) return;
+    // a non-first fragment never passed parse_tcp_hdr / parse_udp_hdr (no TopPorts count), but
+    // the ports the cache gave it put it into a flow whose count includes it: take it back out
+    if (t.port_cnt && pk.frag_off && (pk.ip_proto == 6 || pk.ip_proto == 17) && (pk.src_port || pk.dst_port)) {
+        unsigned long long* a = t.port_cnt + (pk.ip_proto == 17 ? 65536 : 0);
+        atomicAdd(a + pk.src_port, ~0ull);  // -1
+        atomicAdd(a + pk.dst_port, ~0ull);
+    }
     if (!flow_accumulate(t, p, b, pk, idx, d.ts_sec, &ctl->new_keys)) {
         uint32_t pos = atomicAdd(&ctl->deferred, 1u);
         deferred_list[pos] = idx;
@@ -425,6 +432,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
     }
     t.cold[s] = rec;
     clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+    count_flow_ports(t, rec, len);  // every packet of the walk: the flow's ports
     if (n_ex) atomicAdd(&ctl->exported, n_ex);
 }
 
@@ -698,6 +706,107 @@ __global__ __launch_bounds__(256) void k_xxh64(const uint8_t* keys, uint32_t key
 void launch_xxh64(hipStream_t st, const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
                   uint64_t* out) {
     hipLaunchKernelGGL(k_xxh64, dim3((n + 255) / 256), dim3(256), 0, st, keys, keylen, n, seed, out);
+}
+
+// ---- parser side statistics (ps=true) ----------------------------------------------------
+// Per packet of the batch, as parse_packet keeps them in ParserStats (parser-stats.hpp:126-201):
+// VlanStats for the packet's VLAN id (parser.cpp:798: every valid packet, sizes = caplen), and
+// the TopPorts increments the flow records cannot carry (count_flow_ports): a TCP segment
+// dropped after parse_tcp_hdr read its ports, and TCP/UDP packets with both ports 0.
+// Each lane sums its packets' VlanStats in registers while their VLAN id stays the same (one
+// id for untagged traffic), then adds them to the block's LDS copy of that id (64 ids,
+// direct-mapped; another id in the entry: straight to the device counters); the block adds
+// its LDS copies to the device counters at the end.
+constexpr uint32_t VS_EMPTY = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void vs_flush(uint32_t vid, const uint32_t (&acc)[VS_N], uint32_t* vkey,
+                                         uint32_t (*vacc)[VS_N], unsigned long long* vlan_st) {
+    if (vid == VS_EMPTY) return;
+    const uint32_t e = vid & 63;
+    const uint32_t k = atomicCAS(&vkey[e], VS_EMPTY, vid);
+    if (k == VS_EMPTY || k == vid) {
+#pragma unroll
+        for (uint32_t q = 0; q < VS_N; ++q)
+            if (acc[q]) atomicAdd(&vacc[e][q], acc[q]);
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < VS_N; ++q)
+            if (acc[q]) atomicAdd(&vlan_st[(size_t)vid * VS_N + q], (unsigned long long)acc[q]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pstats(BatchView b, Params p, unsigned long long* pstat) {
+    __shared__ uint32_t win[IPXG_WIN_DW * 256];
+    __shared__ uint32_t vkey[64];
+    __shared__ uint32_t vacc[64][VS_N];
+    unsigned long long* const ports = pstat;
+    unsigned long long* const vlan_st = pstat + PSTAT_PORTS;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) vkey[tid] = VS_EMPTY;
+    for (uint32_t q = tid; q < 64 * VS_N; q += 256) (&vacc[0][0])[q] = 0;
+    __syncthreads();
+    uint32_t cur = VS_EMPTY, acc[VS_N];
+#pragma unroll
+    for (uint32_t q = 0; q < VS_N; ++q) acc[q] = 0;
+    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    for (uint32_t i = blockIdx.x * 256 + tid; i < b.n; i += gridDim.x * 256) {
+        const ipxg_pkt_desc d = b.desc[i];
+        DevPkt pk;
+        ParseCounts dummy = {};
+        bool ok = false, fast = false;
+        if (eth && fast_shape(d)) {
+            const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
+            fast = ok = parse_fast(fr[0], fr[1], fr[2], d.caplen, false, pk, dummy);
+        }
+        if (!fast) {
+            stage_frame(&win[tid], b.arena, d.offset, d.caplen);
+            LdsFrame S{{&win[tid], {b.arena + d.offset, d.caplen}}};
+            ok = parse_frame<false>(S, d.caplen, p.dlt, pk, dummy);
+        }
+        if (pk.l4 && (ok ? (pk.src_port == 0 && pk.dst_port == 0) : pk.l4 == 6)) {  // rare
+            unsigned long long* a = ports + (pk.l4 == 17 ? 65536 : 0);
+            atomicAdd(a + pk.src_port, 1ull);
+            atomicAdd(a + pk.dst_port, 1ull);
+        }
+        if (!ok) continue;
+        const uint32_t vid = pk.vlan_id & 0xFFF;
+        if (vid != cur) {
+            vs_flush(cur, acc, vkey, vacc, vlan_st);
+            cur = vid;
+#pragma unroll
+            for (uint32_t q = 0; q < VS_N; ++q) acc[q] = 0;
+        }
+        const uint32_t len = d.caplen;  // packet_len = caplen (parser.cpp:771), uint16_t
+        const bool v4 = pk.ip_version == 4, v6 = pk.ip_version == 6;
+        acc[0] += v4;
+        acc[1] += v6;
+        acc[2] += v4 ? len : 0;
+        acc[3] += v6 ? len : 0;
+        acc[4] += pk.ip_proto == 6;
+        acc[5] += pk.ip_proto == 17;
+        acc[6] += 1;
+        acc[7] += len;
+        const uint32_t bk = len <= 64 ? 0 : len < 128 ? 1 : len < 256 ? 2 : len < 512 ? 3 : len < 1024 ? 4
+                          : len < 1518 ? 5 : len < 2048 ? 6 : len < 4096 ? 7 : len < 8192 ? 8 : 9;
+#pragma unroll
+        for (uint32_t q = 0; q < IPXG_SIZE_BUCKETS; ++q) {  // compile-time indices only
+            acc[8 + q] += bk == q;
+            acc[8 + IPXG_SIZE_BUCKETS + q] += bk == q ? len : 0;
+        }
+    }
+    vs_flush(cur, acc, vkey, vacc, vlan_st);
+    __syncthreads();
+    for (uint32_t q = tid; q < 64 * VS_N; q += 256) {
+        const uint32_t e = q / VS_N, f = q % VS_N;
+        const uint32_t v = (&vacc[0][0])[q];
+        if (v && vkey[e] != VS_EMPTY) atomicAdd(&vlan_st[(size_t)vkey[e] * VS_N + f], (unsigned long long)v);
+    }
+}
+
+void launch_pstats(hipStream_t st, const BatchView& b, const Params& p, unsigned long long* pstat) {
+    uint32_t g = (b.n + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_pstats, dim3(g ? g : 1), dim3(256), 0, st, b, p, pstat);
 }
 
 }  // namespace ipxg

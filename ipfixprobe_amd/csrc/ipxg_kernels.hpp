@@ -83,6 +83,7 @@ struct TableView {
     ipxg_flow_record* cold;
     uint32_t* slot_rank;
     uint32_t mask;  // capacity - 1
+    unsigned long long* port_cnt;  // ps=true: TopPorts' TCP then UDP frequencies (2 x 65536), else null
 };
 
 struct ExportView {
@@ -167,6 +168,12 @@ struct ComplexView {
     uint32_t kmask;            // here, not by probing the flow table (whose chains a fused
 };                             // finish may have cut: k_fin_list empties slots)
 
+// Parser side statistics (ps=true): TopPorts frequencies [tcp 65536][udp 65536], then
+// VlanStats per VLAN id, VS_N u64 counters each in ipxg_vlan_stats order.
+constexpr uint32_t VS_N = 8 + 2 * IPXG_SIZE_BUCKETS;
+constexpr size_t PSTAT_PORTS = 2 * 65536;
+constexpr size_t PSTAT_WORDS = PSTAT_PORTS + (size_t)IPXG_VLAN_IDS * VS_N;
+
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
 // tile-aggregating variant (more LDS)
@@ -185,6 +192,7 @@ void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSl
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
                      bool finishing);
+void launch_pstats(hipStream_t st, const BatchView& b, const Params& p, unsigned long long* pstat);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
 void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,

@@ -441,6 +441,7 @@ __device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, con
     p.more_fragments = (fo & 0x2000) ? 1 : 0;
     p.src_port = bswap16(ports);
     p.dst_port = bswap16(ports >> 16);
+    p.l4 = (frag_off == 0 && (proto == 6 || proto == 17)) ? (uint8_t)proto : 0;
     p.vlan_id = 0;
     p.sip[0] = (c1.z >> 16) | (c1.w << 16);                // bytes 26-29, memory order
     p.dip[0] = (c1.w >> 16) | (c2.x << 16);                // bytes 30-33
@@ -572,6 +573,7 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     p.ethertype = (uint16_t)et;
     p.src_port = bswap16(ports);
     p.dst_port = bswap16(ports >> 16);
+    p.l4 = (frag_off == 0 && (proto == 6 || proto == 17)) ? (uint8_t)proto : 0;
     p.vlan_id = vlan;
     ext = S != 0 || v6 || tcp_opt;
     c.seen++;
@@ -681,6 +683,22 @@ __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p,
     return true;
 }
 
+// ---- TopPorts from the flow records (ps=true) ----------------------------------------------
+// Every packet of a TCP/UDP flow passed parse_tcp_hdr / parse_udp_hdr with the flow's two
+// ports (in one order or the other), so TopPorts' per-packet increments (parser.cpp:484-485,
+// 563-564) sum to `packets` on each of the flow's ports -- two device atomics per flow and
+// batch instead of two per packet.  The packets this misses or over-counts are corrected one
+// by one where they are seen (k_pstats: TCP segments dropped after their ports were read, and
+// TCP/UDP packets with both ports 0, whose flows are skipped here because non-first fragments
+// share them; k_frag_accumulate: non-first fragments given ports by the fragmentation cache).
+__device__ __forceinline__ void count_flow_ports(const TableView& t, const ipxg_flow_record& r, uint32_t packets) {
+    if (!t.port_cnt || !packets || (r.ip_proto != 6 && r.ip_proto != 17) || (r.src_port == 0 && r.dst_port == 0))
+        return;
+    unsigned long long* a = t.port_cnt + (r.ip_proto == 17 ? 65536 : 0);
+    atomicAdd(a + r.src_port, (unsigned long long)packets);
+    atomicAdd(a + r.dst_port, (unsigned long long)packets);
+}
+
 // ---- per-slot batch finalisation ----------------------------------------------------------
 enum FinStatus : uint32_t { FIN_DONE = 1, FIN_COMPLEX = 2 };
 struct FinResult {
@@ -780,6 +798,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     rec.time_last_sec = dl.ts_sec;
     rec.time_last_usec = dl.ts_usec;
     res.created = !live;
+    count_flow_ports(t, rec, (uint32_t)(as >> 40) + (uint32_t)(ad >> 40));
     if (out) {
         *out = rec;
         clear_slot(&t.hot[s], 0, 0);  // empty (every slot empties at the finish)

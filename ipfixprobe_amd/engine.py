@@ -96,7 +96,16 @@ EXPORTED_SYMBOLS = [
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
     "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
     "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
+    "ipxg_parser_stats", "ipxg_top_ports",
 ]
+
+# ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
+VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),
+                             ("ipv6_bytes", "<u8"), ("tcp_packets", "<u8"), ("udp_packets", "<u8"),
+                             ("total_packets", "<u8"), ("total_bytes", "<u8"),
+                             ("hist_packets", "<u8", (10,)), ("hist_bytes", "<u8", (10,))])
+PORT_STAT_DTYPE = np.dtype([("port", "<u2"), ("protocol", "u1"), ("reserved", "u1", (5,)), ("frequency", "<u8")])
+VLAN_IDS = 4096
 
 _LIB = None
 
@@ -154,6 +163,8 @@ def lib():
         L.ipxg_ipfix_export.argtypes = [vp, px, vp, sz, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.ipxg_poll_ipfix_messages.argtypes = [vp, px, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz),
                                                ctypes.POINTER(sz)]
+        L.ipxg_parser_stats.argtypes = [vp, vp, vp, vp]
+        L.ipxg_top_ports.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
         L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                  ctypes.POINTER(sz), ctypes.POINTER(sz)]
         for name in EXPORTED_SYMBOLS:
@@ -302,6 +313,21 @@ class Engine:
         arr = (ctypes.c_uint64 * len(STATS_FIELDS))()
         self._check(lib().ipxg_get_stats(self._h, arr), "ipxg_get_stats")
         return dict(zip(STATS_FIELDS, list(arr)))
+
+    def parser_stats(self):
+        """(tcp port frequencies [65536], udp [65536], VlanStats [4096]) -- engine made with ps=true."""
+        tcp = np.zeros(65536, dtype=np.uint64)
+        udp = np.zeros(65536, dtype=np.uint64)
+        vl = np.zeros(VLAN_IDS, dtype=VLAN_STATS_DTYPE)
+        self._check(lib().ipxg_parser_stats(self._h, tcp.ctypes.data, udp.ctypes.data, vl.ctypes.data),
+                    "ipxg_parser_stats")
+        return tcp, udp, vl
+
+    def top_ports(self, n):
+        out = np.zeros(max(n, 1), dtype=PORT_STAT_DTYPE)
+        got = ctypes.c_size_t()
+        self._check(lib().ipxg_top_ports(self._h, n, out.ctypes.data, ctypes.byref(got)), "ipxg_top_ports")
+        return out[:got.value]
 
     def profile(self, enable=True):
         self._check(lib().ipxg_profile(self._h, int(enable)), "ipxg_profile")

@@ -126,6 +126,12 @@ typedef struct {
     uint8_t dst_mac[6];
 } eth_out;
 
+/* ParserStats' side counters (parser-stats.hpp:126-201, topPorts.hpp) */
+typedef struct {
+    uint64_t tcp[65536], udp[65536];
+    ipxg_vlan_stats vlan[IPXG_VLAN_IDS];
+} pstats;
+
 typedef struct {
     const uint8_t* d;
     uint32_t cap;
@@ -134,6 +140,7 @@ typedef struct {
     ipxg_parsed_pkt* p;
     uint16_t ip_payload_len;
     ipxg_stats* st;
+    pstats* ps; /* may be null */
 } pctx;
 
 static uint8_t B8(pctx* c, uint32_t o)
@@ -383,6 +390,10 @@ static uint16_t parse_tcp_hdr(pctx* c, uint32_t base, uint16_t data_len)
     p->tcp_ack = BE32(c, base + 8);
     p->tcp_flags = B8(c, base + 13);
     p->tcp_window = BE16(c, base + 14);
+    if (c->ps) { /* top_ports.increment_tcp_frequency, parser.cpp:484-485 (before the doff check) */
+        c->ps->tcp[p->src_port]++;
+        c->ps->tcp[p->dst_port]++;
+    }
     int hdr_len = (B8(c, base + 12) >> 4) << 2;
     int hdr_opt_len = hdr_len - 20;
     int i = 0;
@@ -411,6 +422,10 @@ static uint16_t parse_udp_hdr(pctx* c, uint32_t base, uint16_t data_len)
     if (8 > data_len) THROW(c);
     c->p->src_port = BE16(c, base);
     c->p->dst_port = BE16(c, base + 2);
+    if (c->ps) { /* parser.cpp:563-564 */
+        c->ps->udp[c->p->src_port]++;
+        c->ps->udp[c->p->dst_port]++;
+    }
     return 8;
 }
 
@@ -568,6 +583,26 @@ static int parse_packet(pctx* c, uint16_t caplen, uint32_t datalink)
         st->ipv6_bytes += caplen;
     }
     st->parsed_packets++;
+    if (c->ps) { /* vlan_stats[vlan_id].update(*pkt), parser.cpp:798 + VlanStats::update */
+        ipxg_vlan_stats* v = &c->ps->vlan[p->vlan_id & 0xFFF];
+        const uint16_t len = caplen; /* packet_len = caplen (parser.cpp:771) */
+        if (p->ip_version == 4) {
+            v->ipv4_packets++;
+            v->ipv4_bytes += len;
+        } else if (p->ip_version == 6) {
+            v->ipv6_packets++;
+            v->ipv6_bytes += len;
+        }
+        if (p->ip_proto == 6) v->tcp_packets++;
+        else if (p->ip_proto == 17) v->udp_packets++;
+        v->total_packets++;
+        v->total_bytes += len;
+        /* PacketSizeHistogram::update (parser-stats.hpp:42-80) */
+        int b = len <= 64 ? 0 : len < 128 ? 1 : len < 256 ? 2 : len < 512 ? 3 : len < 1024 ? 4
+              : len < 1518 ? 5 : len < 2048 ? 6 : len < 4096 ? 7 : len < 8192 ? 8 : 9;
+        v->hist_packets[b]++;
+        v->hist_bytes[b] += len;
+    }
     return 1;
 }
 
@@ -634,7 +669,7 @@ int oracle_parse(const uint8_t* data, uint16_t caplen, uint16_t wirelen, uint32_
     ipxg_stats st;
     memset(&st, 0, sizeof(st));
     memset(out, 0, sizeof(*out));
-    pctx c = {data, caplen, 0, 0, out, 0, &st};
+    pctx c = {data, caplen, 0, 0, out, 0, &st, NULL};
     int ok = parse_packet(&c, caplen, datalink);
     out->valid = (uint8_t)ok;
     if (ok) {
@@ -699,6 +734,7 @@ struct oracle_cache {
     size_t ex_head, ex_n, ex_cap;
     ipxg_stats st;
     uint64_t flows_in_cache;
+    pstats* ps;
 };
 
 oracle_cache* oracle_cache_new(uint32_t cache_exp, uint32_t line_exp, uint32_t active_s,
@@ -719,11 +755,12 @@ oracle_cache* oracle_cache_new(uint32_t cache_exp, uint32_t line_exp, uint32_t a
     c->frag_size = frag_size ? frag_size : 10007;
     c->frag_timeout = frag_timeout_s;
     c->recs = (orec*)calloc(c->cache_size, sizeof(orec));
+    c->ps = (pstats*)calloc(1, sizeof(pstats));
     c->tab = (uint32_t*)malloc(sizeof(uint32_t) * c->cache_size);
     c->frings = (frag_ring*)calloc(c->frag_size, sizeof(frag_ring));
     c->ex_cap = 1024;
     c->ex = (ipxg_flow_record*)malloc(sizeof(ipxg_flow_record) * c->ex_cap);
-    if (!c->recs || !c->tab || !c->frings || !c->ex) {
+    if (!c->recs || !c->tab || !c->frings || !c->ex || !c->ps) {
         oracle_cache_free(c);
         return NULL;
     }
@@ -738,6 +775,7 @@ void oracle_cache_free(oracle_cache* c)
     free(c->tab);
     free(c->frings);
     free(c->ex);
+    free(c->ps);
     free(c);
 }
 
@@ -975,7 +1013,7 @@ void oracle_cache_run(oracle_cache* c, const uint8_t* arena, const ipxg_pkt_desc
         const ipxg_pkt_desc* d = &desc[i];
         ipxg_parsed_pkt p;
         memset(&p, 0, sizeof(p));
-        pctx pc = {arena + d->offset, d->caplen, 0, 0, &p, 0, &c->st};
+        pctx pc = {arena + d->offset, d->caplen, 0, 0, &p, 0, &c->st, c->ps};
         if (!parse_packet(&pc, d->caplen, datalink)) continue;
         if (c->frag_enable) frag_process(c, &p, d->ts_sec, d->ts_usec);
         if (p.ip_version != 4 && p.ip_version != 6) c->st.keyless_packets++;
@@ -1000,6 +1038,14 @@ size_t oracle_cache_take(oracle_cache* c, ipxg_flow_record* out, size_t cap)
     c->ex_n -= k;
     if (c->ex_n == 0) c->ex_head = 0;
     return k;
+}
+
+void oracle_cache_parser_stats(const oracle_cache* c, uint64_t* tcp_ports, uint64_t* udp_ports,
+                               ipxg_vlan_stats* vlans)
+{
+    if (tcp_ports) memcpy(tcp_ports, c->ps->tcp, sizeof(c->ps->tcp));
+    if (udp_ports) memcpy(udp_ports, c->ps->udp, sizeof(c->ps->udp));
+    if (vlans) memcpy(vlans, c->ps->vlan, sizeof(c->ps->vlan));
 }
 
 void oracle_cache_stats(const oracle_cache* c, ipxg_stats* out)

@@ -60,6 +60,10 @@ size_t oracle_cache_pending(const oracle_cache* c);
 /* Move up to cap exported records into out; returns the number moved. */
 size_t oracle_cache_take(oracle_cache* c, ipxg_flow_record* out, size_t cap);
 void oracle_cache_stats(const oracle_cache* c, ipxg_stats* out);
+/* The parser's side statistics over every packet run so far (parser.cpp:484-485, 563-564,
+ * 798): TCP/UDP port frequencies (65536 each) and VlanStats per VLAN id; outputs may be null. */
+void oracle_cache_parser_stats(const oracle_cache* c, uint64_t* tcp_ports, uint64_t* udp_ports,
+                               ipxg_vlan_stats* vlans);
 
 /* IPFIXExporter::fill_basic_flow (ipfix.cpp:1470-1516) for each of n records: the basic
  * template's data records back to back into out, byte offsets into offsets[n + 1]. */

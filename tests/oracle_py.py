@@ -7,7 +7,7 @@ import os
 
 import numpy as np
 
-from pcaputil import FLOW_DTYPE, PARSED_DTYPE, STATS_FIELDS
+from pcaputil import FLOW_DTYPE, PARSED_DTYPE, STATS_FIELDS, VLAN_IDS, VLAN_STATS_DTYPE
 
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _LIB = None
@@ -40,6 +40,7 @@ def lib():
         L.oracle_cache_take.argtypes = [vp, vp, ctypes.c_size_t]
         L.oracle_ipfix_basic.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
         L.oracle_cache_stats.argtypes = [vp, vp]
+        L.oracle_cache_parser_stats.argtypes = [vp, vp, vp, vp]
         L.oracle_ipfix_export.restype = ctypes.c_size_t
         L.oracle_ipfix_export.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_bench_mt.restype = ctypes.c_double
@@ -114,6 +115,14 @@ class OracleCache:
         arr = (ctypes.c_uint64 * len(STATS_FIELDS))()
         lib().oracle_cache_stats(self._c, arr)
         return dict(zip(STATS_FIELDS, list(arr)))
+
+    def parser_stats(self):
+        """(tcp port frequencies, udp port frequencies, VlanStats per VLAN id)"""
+        tcp = np.zeros(65536, dtype=np.uint64)
+        udp = np.zeros(65536, dtype=np.uint64)
+        vl = np.zeros(VLAN_IDS, dtype=VLAN_STATS_DTYPE)
+        lib().oracle_cache_parser_stats(self._c, tcp.ctypes.data, udp.ctypes.data, vl.ctypes.data)
+        return tcp, udp, vl
 
     def close(self):
         if self._c:

@@ -52,6 +52,13 @@ PARSED_DTYPE = np.dtype([
 ])
 assert PARSED_DTYPE.itemsize == 112
 
+# include/ipxg.h ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160), test-side restatement
+VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),
+                             ("ipv6_bytes", "<u8"), ("tcp_packets", "<u8"), ("udp_packets", "<u8"),
+                             ("total_packets", "<u8"), ("total_bytes", "<u8"),
+                             ("hist_packets", "<u8", (10,)), ("hist_bytes", "<u8", (10,))])
+VLAN_IDS = 4096
+
 # ipxg_stats field order (include/ipxg.h), all uint64
 STATS_FIELDS = [
     "seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",

@@ -36,6 +36,8 @@ def test_struct_layouts_match_header_and_test_restatement():
     assert engine.PARSED_DTYPE == pcaputil.PARSED_DTYPE and engine.PARSED_DTYPE.itemsize == 112
     assert ctypes.sizeof(engine.Config) == 48
     assert engine.STATS_FIELDS == pcaputil.STATS_FIELDS
+    assert engine.VLAN_STATS_DTYPE == pcaputil.VLAN_STATS_DTYPE and engine.VLAN_STATS_DTYPE.itemsize == 224
+    assert engine.PORT_STAT_DTYPE.itemsize == 16
 
 
 def test_config_defaults_and_options():
@@ -51,8 +53,9 @@ def test_config_defaults_and_options():
     c = make_config("dev=3;batch=4096;dlt=LINUX_SLL")
     assert (c.device_id, c.batch_pkts, c.datalink) == (3, 4096, 113)
     assert make_config("walk=wide").flags == 0x2 and make_config("walk=narrow").flags == 0x4
+    assert make_config("ps=true").flags == 0x8 and make_config("parser-stats=true;ps=false").flags == 0
     assert make_config("walk=wide;walk=auto").flags == 0 and make_config("ingest=atomic;walk=wide").flags == 0x3
-    for bad in ("s=3", "s=31", "x=1", "fe=yes", "fs=0", "a=", "batch=0", "walk=deep"):
+    for bad in ("s=3", "s=31", "x=1", "fe=yes", "fs=0", "a=", "batch=0", "walk=deep", "ps=1"):
         with pytest.raises(IpxgError):
             make_config(bad)
 
