@@ -112,7 +112,11 @@ typedef struct ipxg_flow_record {
     uint16_t vlan_id;
     uint8_t end_reason;       /* IPXG_FLOW_END_*                                        */
     uint8_t reserved0;
-    uint8_t reserved[24];
+    uint8_t reserved[8];      /* zero on export                                          */
+    uint64_t ext;             /* the process plugins' per-flow handle (Flow::m_exts,
+                                 see ipxg_plugin): zero on a record the engine creates,
+                                 kept while the flow lives, exported with the record   */
+    uint8_t reserved2[8];
 } ipxg_flow_record;
 
 /* ---- per-packet parse result (debug / parity entry point) ----------------------------
@@ -145,6 +149,9 @@ typedef struct ipxg_parsed_pkt {
     uint32_t tcp_ack;
     uint64_t hash_fwd;        /* XXH64(key), 0 when the packet has no flow key          */
     uint64_t hash_inv;        /* XXH64(inverse key)                                     */
+    uint16_t payload_off;     /* Packet::payload - packet (data_offset, parser.cpp:797)  */
+    uint16_t payload_len;     /* Packet::payload_len (parser.cpp:780-796: padding trim)  */
+    uint32_t reserved2;
 } ipxg_parsed_pkt;
 
 /* ---- engine ------------------------------------------------------------------------ */
@@ -286,6 +293,55 @@ int ipxg_parser_stats(ipxg_engine* eng, uint64_t* tcp_ports, uint64_t* udp_ports
 /* TopPorts::get_top_ports (topPorts.cpp): up to n most frequent ports, TCP then UDP, ties in
  * port order, *got entries written. */
 int ipxg_top_ports(ipxg_engine* eng, size_t n, ipxg_port_stat* out, size_t* got);
+
+/* ---- process-plugin bridge (processPlugin.hpp:42-119; call sites cache.cpp:290-491) ---- */
+#define IPXG_FLOW_FLUSH 0x1               /* FLOW_FLUSH (processPlugin.hpp:27)                 */
+#define IPXG_FLOW_FLUSH_WITH_REINSERT 0x3 /* FLOW_FLUSH_WITH_REINSERT (processPlugin.hpp:36)   */
+#define IPXG_PLUGIN_MAX_PORTS 16
+#define IPXG_PLUGIN_MAX_PREFIXES 8
+#define IPXG_PLUGIN_PREFIX_LEN 16
+
+/* What a hook sees of ipxp::Packet (packet.hpp:46-147): the parsed fields (payload_off /
+ * payload_len locate Packet::payload in data), the captured bytes, the timestamp and
+ * source_pkt (set before post_create / pre_update / post_update, cache.cpp:428). */
+typedef struct ipxg_packet_view {
+    const ipxg_parsed_pkt* pkt;
+    const uint8_t* data;
+    uint32_t caplen;
+    uint32_t wirelen;
+    uint32_t ts_sec;
+    uint32_t ts_usec;
+    uint32_t index;           /* position of the packet in its batch                   */
+    uint8_t source_pkt;
+    uint8_t reserved[3];
+} ipxg_packet_view;
+
+/* A process plugin: the device pre-classifier rule (a packet is the plugin's when it is
+ * TCP/UDP -- proto_mask bit 0 TCP, bit 1 UDP -- with its source or destination port in
+ * ports[], or its payload starts with one of prefixes[]), and the hooks.  Contract: on the
+ * packets outside the rule every hook returns 0 and changes nothing (so flows with none of the
+ * plugin's packets in a batch stay on the device).  A flow with one of them has all its packets
+ * of the batch replayed in order on the host, through these hooks at put_pkt_recursive's call
+ * sites.  The record's ext field (ipxg_flow_record.reserved[8..15], a 64-bit handle) is the
+ * plugins' per-flow state -- RecordExt: zero on a new record, cleared by erase/reuse, carried by
+ * the exported record.  Hooks return 0 or IPXG_FLOW_FLUSH / IPXG_FLOW_FLUSH_WITH_REINSERT. */
+typedef struct ipxg_plugin {
+    void* ctx;
+    uint32_t proto_mask;
+    uint32_t n_ports;
+    uint16_t ports[IPXG_PLUGIN_MAX_PORTS];
+    uint32_t n_prefixes;
+    uint8_t prefix_len[IPXG_PLUGIN_MAX_PREFIXES];
+    uint8_t prefix[IPXG_PLUGIN_MAX_PREFIXES][IPXG_PLUGIN_PREFIX_LEN];
+    int (*pre_create)(void* ctx, ipxg_packet_view* pkt);
+    int (*post_create)(void* ctx, ipxg_flow_record* flow, const ipxg_packet_view* pkt);
+    int (*pre_update)(void* ctx, ipxg_flow_record* flow, ipxg_packet_view* pkt);
+    int (*post_update)(void* ctx, ipxg_flow_record* flow, const ipxg_packet_view* pkt);
+    void (*pre_export)(void* ctx, ipxg_flow_record* flow);
+} ipxg_plugin;
+
+/* Register a plugin (the order of registration is the order of the hook calls). */
+int ipxg_add_plugin(ipxg_engine* eng, const ipxg_plugin* plugin);
 
 /* ---- stage timing (HIP events on the engine's stream) --------------------------------- */
 typedef struct ipxg_timing {

@@ -1,0 +1,159 @@
+// ipxg_bridge.hip -- device side of the process-plugin bridge.
+//
+// The reference calls its process plugins' hooks from NHTFlowCache::put_pkt_recursive for
+// every packet (processPlugin.hpp:59-108; call sites cache.cpp:330-491), and a hook may end the
+// flow there (FLOW_FLUSH / FLOW_FLUSH_WITH_REINSERT, cache.cpp:290-320).  Plugins look at
+// particular packets only (DNS: port 53, HTTP: request/response lines, ...), so:
+//   k_classify      pre-classifies every packet of the batch against the registered plugins'
+//                   rules (TCP/UDP ports, payload prefixes) and marks the flows of the matching
+//                   packets SLOT_PLUGIN in the flow table, before the ingest;
+//   (ingest)        such a flow is aggregated as usual, then finalize_slot turns it complex,
+//                   and the complex path gathers and sorts its packets of the batch;
+//   k_plugin_pack   lists the plugin flows among the complex ones with their slot images;
+//   k_plugin_pkts   parses their packets (every field a hook reads, payload included) and
+//   k_plugin_bytes  copies the frames out -- the host replays put_pkt_recursive for these
+//                   flows through the hooks, in packet order (ipxg_engine.cpp, plugin_walk);
+//   k_plugin_apply  writes the flows' final slot and record back.
+// Flows with none of the plugins' packets in a batch never leave the device (the plugin
+// contract: hooks are no-ops on the packets outside the rule).
+#include "ipxg_table.hpp"
+
+namespace ipxg {
+
+// Does the parsed packet match rule r?  Its frame is staged in S (LDS window + global).
+template <class S>
+__device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, const S& s) {
+    const bool tcp = pk.l4 == 6, udp = pk.l4 == 17;
+    if (!((tcp && (r.proto_mask & 1)) || (udp && (r.proto_mask & 2)))) return false;
+    for (uint32_t k = 0; k < r.n_ports; ++k)
+        if (pk.src_port == r.ports[k] || pk.dst_port == r.ports[k]) return true;
+    for (uint32_t q = 0; q < r.n_prefixes; ++q) {
+        const uint32_t n = r.prefix_len[q];
+        if (n == 0 || n > pk.payload_len) continue;
+        bool eq = true;
+        for (uint32_t k = 0; k < n && eq; ++k) eq = s.b(pk.payload_off + k) == r.prefix[q][k];
+        if (eq) return true;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(IPXG_BLOCK) void k_classify(BatchView b, Params p, TableView t, const DevRule* rules,
+                                                         uint32_t nrules, BatchCtl* ctl) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    uint32_t* col = &win[threadIdx.x];
+    uint32_t claimed_n = 0;
+    for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
+        const ipxg_pkt_desc d = b.desc[i];
+        stage_frame(col, b.arena, d.offset, d.caplen);
+        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        DevPkt pk;
+        ParseCounts dummy = {};
+        if (!parse_frame<true>(S, d.caplen, p.dlt, pk, dummy)) continue;
+        if (pk.ip_version != 4 && pk.ip_version != 6) continue;
+        if (pk.frag_off) continue;  // no L4 header (its ports come from the fragmentation cache)
+        bool hit = false;
+        for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, S);
+        if (!hit) continue;
+        uint64_t lo, hf;
+        uint32_t cdir;
+        canon(pk, p, lo, cdir, hf);
+        uint4 head;
+        bool claimed;
+        HotSlot* h = probe_insert(t, lo, head, claimed);
+        if (!h) {
+            atomicOr(&ctl->plugin_fail, 1u);  // table too full to mark the flow (host: error)
+            continue;
+        }
+        if (claimed) claimed_n++;
+        atomicOr(&h->state, SLOT_PLUGIN);
+    }
+    if (claimed_n) atomicAdd(&ctl->new_keys, claimed_n);
+}
+
+void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
+                     uint32_t nrules, BatchCtl* ctl) {
+    uint32_t g = (b.n + IPXG_BLOCK - 1) / IPXG_BLOCK;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_classify, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, rules, nrules, ctl);
+}
+
+// The plugin flows among the ncx complex ones (rank order is arbitrary; the host sorts).
+__global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out,
+                                                     uint32_t* count) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= ncx) return;
+    const uint32_t s = cx.slot_of[r];
+    const HotSlot h = t.hot[s];
+    if (!(h.state & SLOT_PLUGIN)) return;
+    const uint32_t pos = atomicAdd(count, 1u);
+    PluginFlow f;
+    f.slot = s;
+    f.seg = cx.seg[r];
+    f.len = cx.len[r];
+    f.state = h.state;
+    f.key = h.key;
+    f.rec = t.cold[s];
+    out[pos] = f;
+}
+
+void launch_plugin_pack(hipStream_t st, TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out,
+                        uint32_t* count) {
+    hipLaunchKernelGGL(k_plugin_pack, dim3((ncx + 255) / 256), dim3(256), 0, st, t, cx, ncx, out, count);
+}
+
+// Packet idx[k] (k < m): every field a hook reads (ipxg_parsed_pkt, FULL parse) and its descriptor.
+__global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_pkts(BatchView b, Params p, FragView f, const uint32_t* idx,
+                                                            uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    const uint32_t k = blockIdx.x * IPXG_BLOCK + threadIdx.x;
+    if (k >= m) return;
+    const uint32_t i = idx[k];
+    const ipxg_pkt_desc d = b.desc[i];
+    uint32_t* col = &win[threadIdx.x];
+    stage_frame(col, b.arena, d.offset, d.caplen);
+    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    DevPkt pk;
+    ParseCounts c = {};
+    const bool ok = parse_frame<true>(S, d.caplen, p.dlt, pk, c);
+    if (ok) apply_frag_ports(p, f, i, pk);  // a fragment's ports from the fragmentation cache
+    out[k] = to_parsed(pk, ok);
+    dout[k] = d;
+}
+
+void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
+                        uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout) {
+    hipLaunchKernelGGL(k_plugin_pkts, dim3((m + IPXG_BLOCK - 1) / IPXG_BLOCK), dim3(IPXG_BLOCK), 0, st, b, p, f, idx,
+                       m, out, dout);
+}
+
+// Frame bytes of packet idx[k] to out + off[k] (one workgroup per packet, byte copies).
+__global__ __launch_bounds__(256) void k_plugin_bytes(BatchView b, const uint32_t* idx, const uint64_t* off,
+                                                      uint32_t m, uint8_t* out) {
+    for (uint32_t k = blockIdx.x; k < m; k += gridDim.x) {
+        const ipxg_pkt_desc d = b.desc[idx[k]];
+        const uint8_t* src = b.arena + d.offset;
+        uint8_t* dst = out + off[k];
+        for (uint32_t j = threadIdx.x; j < d.caplen; j += 256) dst[j] = src[j];
+    }
+}
+
+void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
+                         uint8_t* out) {
+    const uint32_t g = m < 4096 ? m : 4096;
+    hipLaunchKernelGGL(k_plugin_bytes, dim3(g ? g : 1), dim3(256), 0, st, b, idx, off, m, out);
+}
+
+// The host walk's result for flow k: its slot (state LIVE with the record, or empty of records).
+__global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginFlow* in, uint32_t n) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    const PluginFlow f = in[k];
+    if (f.state & SLOT_LIVE) t.cold[f.slot] = f.rec;
+    clear_slot(&t.hot[f.slot], f.key, f.state & SLOT_LIVE);
+}
+
+void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n) {
+    hipLaunchKernelGGL(k_plugin_apply, dim3((n + 255) / 256), dim3(256), 0, st, t, in, n);
+}
+
+}  // namespace ipxg

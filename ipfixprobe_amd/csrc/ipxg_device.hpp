@@ -187,6 +187,8 @@ struct DevPkt {
     uint64_t tcp_options;
     uint16_t tcp_window;
     uint8_t ip_ttl, ip_tos, ip_flags;
+    uint16_t ip_payload_len;            // Packet::ip_payload_len (parser.cpp:332, 412, 436)
+    uint16_t payload_off, payload_len;  // Packet::payload / payload_len (parser.cpp:780-797)
 };
 
 // parser counters kept per lane and reduced per block (parser-stats.hpp:126-201)
@@ -243,8 +245,8 @@ __device__ __forceinline__ void ipv4_fields(const S& s, uint32_t base, uint32_t 
         p.ip_tos = (uint8_t)rd8(s, base + 1);
         p.ip_ttl = (uint8_t)rd8(s, base + 8);
         p.ip_flags = (uint8_t)((fo & 0xE000) >> 13);
+        p.ip_payload_len = (uint16_t)(p.ip_len - ihl);
     }
-    (void)ihl;
 }
 
 // IPv6 header + extension-header walk (parse_ipv6_hdr :423-460, skip_ipv6_ext_hdrs :365-414).
@@ -266,6 +268,7 @@ __device__ __forceinline__ uint32_t parse_ipv6(const S& s, uint32_t base, uint32
         p.ip_tos = (uint8_t)((rd32(s, base) & 0x0ff00000) >> 20);
         p.ip_ttl = (uint8_t)rd8(s, base + 7);
         p.ip_flags = 0;
+        p.ip_payload_len = (uint16_t)plen;
     }
     uint32_t hdr_len = 40;
     if (proto != 6 && proto != 17) {
@@ -304,6 +307,7 @@ __device__ __forceinline__ uint32_t parse_ipv6(const S& s, uint32_t base, uint32
         }
         if (hdrs_len > 65535u) { err = true; return 0; }
         hdr_len = (hdr_len + hdrs_len) & 0xFFFF;
+        if (FULL) p.ip_payload_len = (uint16_t)(p.ip_payload_len - hdrs_len);
     }
     return hdr_len;
 }
@@ -406,11 +410,11 @@ __device__ __forceinline__ uint32_t parse_l3(const S& s, uint32_t kind, uint32_t
     return 0;
 }
 
-// parse_tcp_hdr :469-543.  Returns hdr_len (unused by the caller), err on throw.
+// parse_tcp_hdr :469-543.  Returns hdr_len, err on throw.
 template <bool FULL, class S>
-__device__ __forceinline__ void parse_tcp(const S& s, uint32_t base, uint32_t data_len, DevPkt& p,
-                                          bool& err) {
-    if (20 > data_len) { err = true; return; }
+__device__ __forceinline__ uint32_t parse_tcp(const S& s, uint32_t base, uint32_t data_len, DevPkt& p,
+                                              bool& err) {
+    if (20 > data_len) { err = true; return 0; }
     uint32_t w0 = s.le32(base);
     p.src_port = bswap16(w0);
     p.dst_port = bswap16(w0 >> 16);
@@ -424,23 +428,24 @@ __device__ __forceinline__ void parse_tcp(const S& s, uint32_t base, uint32_t da
     }
     int hdr_len = (int)((w3 & 0xFF) >> 4) << 2;
     int hdr_opt_len = hdr_len - 20;
-    if (hdr_len > (int)data_len) { err = true; return; }
+    if (hdr_len > (int)data_len) { err = true; return 0; }
     int i = 0;
     while (i < hdr_opt_len) {
         uint32_t opt = base + 20 + (uint32_t)i;
         uint32_t kind = rd8(s, opt);
         if (i + 1 >= hdr_opt_len) {
-            if (kind <= 1) return;
+            if (kind <= 1) return (uint32_t)hdr_len;
             err = true;
-            return;
+            return 0;
         }
         uint32_t opt_len = kind <= 1 ? 1 : rd8(s, opt + 1);
         if (FULL) p.tcp_options |= 1ULL << (((kind & 0xF8) + (7 - (kind & 7))) & 63);
         if (kind == 0) break;
         if (FULL && kind == 2) p.tcp_mss = rd32(s, opt + 2);
-        if (opt_len == 0) { err = true; return; }
+        if (opt_len == 0) { err = true; return 0; }
         i += (int)opt_len;
     }
+    return (uint32_t)hdr_len;
 }
 
 // parse_packet :673-805 with parse_all = false.  Returns valid (pblock->cnt++).
@@ -457,6 +462,7 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
         p.tcp_options = 0;
         p.tcp_window = 0;
         p.ip_ttl = p.ip_tos = p.ip_flags = 0;
+        p.ip_payload_len = p.payload_off = p.payload_len = 0;
     }
     c.seen++;
     bool err = false;
@@ -509,6 +515,7 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
         off = (off + r) & 0xFFFF;
     }
     p.ethertype = (uint16_t)et;
+    const uint32_t l3_off = off;
     uint32_t kind;
     if (et == ETH_P_IP) kind = L3_IPV4;
     else if (et == ETH_P_IPV6) kind = L3_IPV6;
@@ -523,10 +530,12 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
     if (kind == L3_MPLS) c.mpls++;
     if (kind == L3_PPPOE) c.pppoe++;
     off = (off + r) & 0xFFFF;
+    const uint32_t l4_off = off;
     if (p.frag_off == 0) {
         if (p.ip_proto == 6) {
-            parse_tcp<FULL>(s, off, (caplen - off) & 0xFFFF, p, err);
+            const uint32_t h = parse_tcp<FULL>(s, off, (caplen - off) & 0xFFFF, p, err);
             if (err) return false;
+            off = (off + h) & 0xFFFF;
             c.tcp++;
         } else if (p.ip_proto == 17) {  // parse_udp_hdr :552-573
             if (8 > ((caplen - off) & 0xFFFF)) return false;
@@ -534,8 +543,22 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
             p.src_port = bswap16(w0);
             p.dst_port = bswap16(w0 >> 16);
             p.l4 = 17;
+            off = (off + 8) & 0xFFFF;
             c.udp++;
         }
+    }
+    if (FULL) {  // payload, parser.cpp:780-797 (uint16_t arithmetic as there)
+        uint32_t pkt_len = caplen, wire;
+        if (l4_off != l3_off) {
+            if (l4_off + p.ip_payload_len < 64) pkt_len = (l4_off + p.ip_payload_len) & 0xFFFF;
+            wire = (p.ip_payload_len - (off - l4_off)) & 0xFFFF;
+        } else {
+            wire = (pkt_len - off) & 0xFFFF;
+        }
+        uint32_t plen = wire;
+        if (plen + off > pkt_len) plen = (pkt_len - off) & 0xFFFF;
+        p.payload_off = (uint16_t)off;
+        p.payload_len = (uint16_t)plen;
     }
     if (p.vlan_id) c.vlan++;
     if (et == ETH_P_IP) {

@@ -56,6 +56,12 @@ struct ipxg_engine {
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
     unsigned long long* pstat_d = nullptr;  // ps=true: TopPorts + VlanStats (PSTAT_WORDS)
+    // process-plugin bridge: the registered plugins, their rules on the device, and what the
+    // host walks add to the device-side counters (exports by reason, TopPorts)
+    std::vector<ipxg_plugin> plugins;
+    DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
+    uint64_t host_end[5] = {0, 0, 0, 0, 0};
+    std::vector<uint64_t> host_ports;  // 2 x 65536 when ps=true and plugins walk flows
     // staging for host batches
     DevBuf arena, desc;
     // scratch
@@ -432,7 +438,8 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->plan_ev) (void)hipEventDestroy(e->plan_ev);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (DevBuf* b : {&e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
+    for (DevBuf* b : {&e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_parsed, &e->pf_desc, &e->pf_off, &e->pf_bytes,
+                      &e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
                       &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
@@ -522,6 +529,9 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
     }
     if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
+    if (!e->plugins.empty() && binned)  // the process plugins' flows: SLOT_PLUGIN, before the ingest
+        launch_classify(e->st, bv, p, table_view(e), (const DevRule*)e->rules_d.p, (uint32_t)e->plugins.size(),
+                        e->ctl_d);
     ev_rec(e, 0);
     if (binned) {
         uint32_t* dl = (uint32_t*)e->defer_a.p;
@@ -558,6 +568,307 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 // Everything after the batch's main kernels, from the control block in e->ctl_h: timing,
 // the fragment, deferral, table-scan and complex paths when the batch needs them, then the
 // host's accounting.  `finishing`: a finish follows at once (no table growth needed).
+// ---- process-plugin bridge: the host walk ----------------------------------------------------
+// put_pkt_recursive (cache.cpp:330-491) for the plugin flows of a batch, one flow at a time,
+// with every registered plugin's hooks at their call sites and flush() (cache.cpp:290-320);
+// the same per-packet rules as the device's sequential walk (k_complex_walk) and the oracle.
+// Not emulated here, as nowhere in the engine: the per-packet expiry sweep (only end reasons
+// differ) and the 16-way line (no NO_RES evictions).
+namespace {
+
+struct WalkOut {
+    std::vector<ipxg_flow_record> ex;  // exported records, in order
+    uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
+};
+
+struct FlowWalk {
+    const std::vector<ipxg_plugin>& pl;
+    const Params& p;
+    WalkOut& out;
+    ipxg_flow_record rec;
+    bool live;
+
+    int pre_create(ipxg_packet_view* v) {
+        int r = 0;
+        for (const ipxg_plugin& q : pl)
+            if (q.pre_create) r |= q.pre_create(q.ctx, v);
+        return r;
+    }
+    int post_create(const ipxg_packet_view* v) {
+        int r = 0;
+        for (const ipxg_plugin& q : pl)
+            if (q.post_create) r |= q.post_create(q.ctx, &rec, v);
+        return r;
+    }
+    int pre_update(ipxg_packet_view* v) {
+        int r = 0;
+        for (const ipxg_plugin& q : pl)
+            if (q.pre_update) r |= q.pre_update(q.ctx, &rec, v);
+        return r;
+    }
+    int post_update(const ipxg_packet_view* v) {
+        int r = 0;
+        for (const ipxg_plugin& q : pl)
+            if (q.post_update) r |= q.post_update(q.ctx, &rec, v);
+        return r;
+    }
+    void pre_export() {
+        for (const ipxg_plugin& q : pl)
+            if (q.pre_export) q.pre_export(q.ctx, &rec);
+    }
+    // export_flow (cache.cpp:262-274): the record with its end reason, counted; slot erased
+    void export_flow(uint8_t reason, bool counted = true) {
+        ipxg_flow_record o = rec;
+        o.end_reason = reason;
+        o.reserved0 = 0;
+        std::memset(o.reserved, 0, sizeof(o.reserved));
+        out.ex.push_back(o);
+        if (counted && reason >= 1 && reason <= 5) out.end[reason - 1]++;
+    }
+    // FlowRecord::create (cache.cpp:94-132), the engine's record layout (rec_create)
+    void create(const ipxg_parsed_pkt& k, const ipxg_packet_view& v) {
+        std::memset(&rec, 0, sizeof(rec));
+        rec.flow_hash = k.hash_fwd;
+        rec.time_first_sec = rec.time_last_sec = v.ts_sec;
+        rec.time_first_usec = rec.time_last_usec = v.ts_usec;
+        rec.ip_version = k.ip_version;
+        rec.ip_proto = k.ip_proto;
+        std::memcpy(rec.src_ip, k.src_ip, 16);
+        std::memcpy(rec.dst_ip, k.dst_ip, 16);
+        std::memcpy(rec.src_mac, k.src_mac, 6);
+        std::memcpy(rec.dst_mac, k.dst_mac, 6);
+        if (k.ip_proto == 6 || k.ip_proto == 17 || k.ip_proto == 1 || k.ip_proto == 58) {
+            rec.src_port = k.src_port;
+            rec.dst_port = k.dst_port;
+        }
+        rec.vlan_id = (uint16_t)k.vlan_id;
+        rec.reserved[0] = (p.split_biflow || k.hash_fwd <= k.hash_inv) ? 0 : 1;  // creator's canonical dir
+        rec.src_packets = 1;
+        rec.src_bytes = k.ip_len;
+        if (k.ip_proto == 6) rec.src_tcp_flags = k.tcp_flags;
+        live = true;
+    }
+    // FlowRecord::update (cache.cpp:134-152)
+    void update(const ipxg_parsed_pkt& k, const ipxg_packet_view& v, bool src) {
+        rec.time_last_sec = v.ts_sec;
+        rec.time_last_usec = v.ts_usec;
+        if (src) {
+            rec.src_packets++;
+            rec.src_bytes += k.ip_len;
+            if (k.ip_proto == 6) rec.src_tcp_flags |= k.tcp_flags;
+        } else {
+            rec.dst_packets++;
+            rec.dst_bytes += k.ip_len;
+            if (k.ip_proto == 6) rec.dst_tcp_flags |= k.tcp_flags;
+        }
+    }
+    // flush (cache.cpp:290-320)
+    void flush(int ret, const ipxg_parsed_pkt& k, ipxg_packet_view* v, bool src) {
+        if (ret == IPXG_FLOW_FLUSH_WITH_REINSERT) {
+            export_flow(IPXG_FLOW_END_FORCED, false);  // ipx_ring_push only: not counted
+            rec.ext = 0;                                // remove_extensions
+            rec.time_first_sec = rec.time_last_sec;     // reuse (cache.cpp:73-83)
+            rec.time_first_usec = rec.time_last_usec;
+            rec.src_packets = rec.dst_packets = 0;
+            rec.src_bytes = rec.dst_bytes = 0;
+            rec.src_tcp_flags = rec.dst_tcp_flags = 0;
+            update(k, *v, src);
+            const int r2 = post_create(v);
+            if (r2 & IPXG_FLOW_FLUSH) flush(r2, k, v, src);
+        } else {
+            export_flow(IPXG_FLOW_END_FORCED);
+            live = false;
+        }
+    }
+    void put(const ipxg_parsed_pkt& k, ipxg_packet_view* v) {
+        for (;;) {  // the recursion of put_pkt_recursive after an export
+            pre_create(v);  // its return is not used (cache.cpp:332)
+            const bool src = !live || p.split_biflow || k.hash_fwd == rec.flow_hash;
+            v->source_pkt = src ? 1 : 0;  // cache.cpp:428
+            if (live) {
+                const uint8_t flw = src ? rec.src_tcp_flags : rec.dst_tcp_flags;
+                if ((k.tcp_flags & 0x02) && (flw & 0x05)) {  // :431-438
+                    export_flow(IPXG_FLOW_END_EOF);
+                    live = false;
+                    continue;
+                }
+                if ((int64_t)v->ts_sec - (int64_t)rec.time_last_sec >= (int64_t)p.inactive_s) {  // :453
+                    const uint8_t reason = ((rec.src_tcp_flags | rec.dst_tcp_flags) & 0x05) ? IPXG_FLOW_END_EOF
+                                                                                            : IPXG_FLOW_END_INACTIVE;
+                    rec.end_reason = reason;
+                    pre_export();
+                    export_flow(reason);
+                    live = false;
+                    continue;
+                }
+                if ((int64_t)v->ts_sec - (int64_t)rec.time_first_sec >= (int64_t)p.active_s) {  // :464
+                    rec.end_reason = IPXG_FLOW_END_ACTIVE;
+                    pre_export();
+                    export_flow(IPXG_FLOW_END_ACTIVE);
+                    live = false;
+                    continue;
+                }
+                int ret = pre_update(v);  // :474-486
+                if (ret & IPXG_FLOW_FLUSH) {
+                    flush(ret, k, v, src);
+                    return;
+                }
+                update(k, *v, src);
+                ret = post_update(v);
+                if (ret & IPXG_FLOW_FLUSH) flush(ret, k, v, src);
+                return;
+            }
+            create(k, *v);  // :441-449
+            if (post_create(v) & IPXG_FLOW_FLUSH) {
+                export_flow(rec.end_reason);  // end reason as the record holds it
+                live = false;
+            }
+            return;
+        }
+    }
+};
+
+}  // namespace
+
+// After the batch's complex path (its packets gathered and sorted, the device walk done): walk
+// the plugin flows on the host and write them back.  *live_delta: records created - closed.
+static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, const ComplexView& cx, uint32_t ncx,
+                       uint32_t npk, int64_t* live_delta) {
+    int rc;
+    *live_delta = 0;
+    if ((rc = ensure(e, e->pf_d, (size_t)ncx * sizeof(PluginFlow) + 16))) return rc;
+    uint32_t* cnt_d = (uint32_t*)((char*)e->pf_d.p + (size_t)ncx * sizeof(PluginFlow));
+    HIPCHK(e, hipMemsetAsync(cnt_d, 0, sizeof(uint32_t), e->st));
+    launch_plugin_pack(e->st, table_view(e), cx, ncx, (PluginFlow*)e->pf_d.p, cnt_d);
+    HIPCHK(e, hipGetLastError());
+    uint32_t nf = 0;
+    HIPCHK(e, hipMemcpyAsync(&nf, cnt_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    if (!nf) return IPXG_OK;
+    std::vector<PluginFlow> flows(nf);
+    std::vector<uint64_t> sorted(npk);
+    HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(sorted.data(), cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    // the flows' packets, each flow's in arrival order (the sorted list: rank << 24 | index)
+    std::vector<uint32_t> idx, first(nf + 1);
+    for (uint32_t f = 0; f < nf; ++f) {
+        first[f] = (uint32_t)idx.size();
+        for (uint32_t k = 0; k < flows[f].len; ++k) idx.push_back((uint32_t)(sorted[flows[f].seg + k] & 0xFFFFFF));
+    }
+    first[nf] = (uint32_t)idx.size();
+    const uint32_t m = (uint32_t)idx.size();
+    if ((rc = ensure(e, e->pf_idx, (size_t)m * 4 + 4))) return rc;
+    if ((rc = ensure(e, e->pf_parsed, (size_t)m * sizeof(ipxg_parsed_pkt) + 8))) return rc;
+    if ((rc = ensure(e, e->pf_desc, (size_t)m * sizeof(ipxg_pkt_desc) + 16))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->pf_idx.p, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice, e->st));
+    launch_plugin_pkts(e->st, bv, p, frag_view(e), (const uint32_t*)e->pf_idx.p, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
+                       (ipxg_pkt_desc*)e->pf_desc.p);
+    HIPCHK(e, hipGetLastError());
+    std::vector<ipxg_parsed_pkt> pk(m);
+    std::vector<ipxg_pkt_desc> de(m);
+    HIPCHK(e, hipMemcpyAsync(pk.data(), e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost,
+                             e->st));
+    HIPCHK(e, hipMemcpyAsync(de.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    std::vector<uint64_t> off(m + 1, 0);
+    for (uint32_t k = 0; k < m; ++k) off[k + 1] = off[k] + de[k].caplen;
+    if ((rc = ensure(e, e->pf_off, (size_t)(m + 1) * 8))) return rc;
+    if ((rc = ensure(e, e->pf_bytes, off[m] + 16))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->pf_off.p, off.data(), (size_t)(m + 1) * 8, hipMemcpyHostToDevice, e->st));
+    launch_plugin_bytes(e->st, bv, (const uint32_t*)e->pf_idx.p, (const uint64_t*)e->pf_off.p, m,
+                        (uint8_t*)e->pf_bytes.p);
+    HIPCHK(e, hipGetLastError());
+    std::vector<uint8_t> bytes(off[m] + 1);
+    HIPCHK(e, hipMemcpyAsync(bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    // the walks, flows in order of their first packet (export order is arbitrary otherwise)
+    std::vector<uint32_t> order(nf);
+    for (uint32_t f = 0; f < nf; ++f) order[f] = f;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return idx[first[a]] < idx[first[b]]; });
+    WalkOut wo;
+    const bool ports = e->pstat_d != nullptr;
+    if (ports && e->host_ports.empty()) e->host_ports.assign(2 * 65536, 0);
+    for (uint32_t f : order) {
+        PluginFlow& F = flows[f];
+        FlowWalk w{e->plugins, p, wo, F.rec, (F.state & SLOT_LIVE) != 0};
+        const bool was_live = w.live;
+        for (uint32_t k = first[f]; k < first[f + 1]; ++k) {
+            ipxg_packet_view v;
+            std::memset(&v, 0, sizeof(v));
+            v.pkt = &pk[k];
+            v.data = bytes.data() + off[k];
+            v.caplen = de[k].caplen;
+            v.wirelen = de[k].wirelen;
+            v.ts_sec = de[k].ts_sec;
+            v.ts_usec = de[k].ts_usec;
+            v.index = idx[k];
+            w.put(pk[k], &v);
+        }
+        F.state = w.live ? SLOT_LIVE : 0;
+        F.rec = w.rec;
+        *live_delta += (w.live ? 1 : 0) - (was_live ? 1 : 0);
+        // TopPorts from the flow's packets (count_flow_ports: every packet counts both ports)
+        const ipxg_flow_record& r = w.rec;
+        if (ports && (r.ip_proto == 6 || r.ip_proto == 17) && (r.src_port || r.dst_port)) {
+            uint64_t* a = e->host_ports.data() + (r.ip_proto == 17 ? 65536 : 0);
+            a[r.src_port] += F.len;
+            a[r.dst_port] += F.len;
+        }
+    }
+    // back to the device: the slots, then the exports after the batch's own
+    HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows.data(), (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
+    launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf);
+    HIPCHK(e, hipGetLastError());
+    const size_t nx = wo.ex.size();
+    if (nx) {
+        if ((rc = ensure_export(e, nx))) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->ex + e->ex_count, wo.ex.data(), nx * sizeof(ipxg_flow_record),
+                                 hipMemcpyHostToDevice, e->st));
+        uint32_t c3[3] = {e->ex_count + (uint32_t)nx, 0, e->ex_count6};
+        for (const ipxg_flow_record& r : wo.ex) c3[2] += r.ip_version == 6 ? 1 : 0;
+        HIPCHK(e, hipMemcpyAsync(e->ex_count_d, c3, sizeof(c3), hipMemcpyHostToDevice, e->st));
+        e->ex_count = c3[0];
+        e->ex_count6 = c3[2];
+    }
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
+    return IPXG_OK;
+}
+
+int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
+    if (!e || !pl) return IPXG_EINVAL;
+    if (pl->n_ports > IPXG_PLUGIN_MAX_PORTS || pl->n_prefixes > IPXG_PLUGIN_MAX_PREFIXES)
+        return set_err(e, IPXG_EINVAL, "plugin rule: too many ports or prefixes");
+    for (uint32_t q = 0; q < pl->n_prefixes; ++q)
+        if (pl->prefix_len[q] > IPXG_PLUGIN_PREFIX_LEN) return set_err(e, IPXG_EINVAL, "plugin rule: prefix too long");
+    if (e->cfg.flags & IPXG_CFG_ATOMIC_INGEST)
+        return set_err(e, IPXG_EINVAL, "process plugins need the binned ingest");
+    {
+        const int rc0 = complete_batch(e);
+        if (rc0) return rc0;
+    }
+    e->plugins.push_back(*pl);
+    std::vector<DevRule> rules(e->plugins.size());
+    for (size_t k = 0; k < rules.size(); ++k) {
+        const ipxg_plugin& q = e->plugins[k];
+        DevRule& r = rules[k];
+        std::memset(&r, 0, sizeof(r));
+        r.proto_mask = q.proto_mask;
+        r.n_ports = q.n_ports;
+        std::memcpy(r.ports, q.ports, sizeof(r.ports));
+        r.n_prefixes = q.n_prefixes;
+        std::memcpy(r.prefix_len, q.prefix_len, sizeof(r.prefix_len));
+        std::memcpy(r.prefix, q.prefix, sizeof(r.prefix));
+    }
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if ((rc = ensure(e, e->rules_d, rules.size() * sizeof(DevRule)))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->rules_d.p, rules.data(), rules.size() * sizeof(DevRule), hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return IPXG_OK;
+}
+
 static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool binned, bool finishing) {
     int rc;
     FragView fv = frag_view(e);
@@ -640,6 +951,8 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
             e->tm.finalize_launches++;
         }
     }
+    if (c1.plugin_fail) return set_err(e, IPXG_EDEVICE, "flow table too full to mark a process plugin's flow");
+    int64_t plugin_live = 0;
     const uint32_t ncx = e->ctl_h->complex_count;
     if (ncx) {
         ev_rec(e, 5);
@@ -675,6 +988,11 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ev_rec(e, 6);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
+        if (!e->plugins.empty()) {  // the process plugins' flows: walked on the host
+            int64_t dl = 0;
+            if ((rc = plugin_walk(e, bv, p, cx, ncx, npk, &dl))) return rc;
+            plugin_live += dl;
+        }
         if (e->prof && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
@@ -689,6 +1007,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         e->live += c2.new_live;
     }
     e->live += c2.cx_new_live;
+    e->live = (uint32_t)((int64_t)e->live + plugin_live);
     e->last_touched = c2.touched;
     if (binned && c2.total_slots) {  // the next batch's segment sizing
         const uint32_t P = 1u << e->part_bits_last;
@@ -1224,6 +1543,8 @@ int ipxg_parser_stats(ipxg_engine* e, uint64_t* tcp_ports, uint64_t* udp_ports, 
     HIPCHK(e, hipMemcpyAsync(h.data(), e->pstat_d, PSTAT_WORDS * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     static_assert(sizeof(ipxg_vlan_stats) == VS_N * 8, "VlanStats layout");
+    if (!e->host_ports.empty())
+        for (size_t k = 0; k < 2 * 65536; ++k) h[k] += e->host_ports[k];  // the plugin walks' flows
     if (tcp_ports) std::memcpy(tcp_ports, h.data(), 65536 * 8);
     if (udp_ports) std::memcpy(udp_ports, h.data() + 65536, 65536 * 8);
     if (vlans) std::memcpy(vlans, h.data() + PSTAT_PORTS, (size_t)IPXG_VLAN_IDS * VS_N * 8);
@@ -1284,6 +1605,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->vlan_packets = s[ST_VLAN];
     out->ipv4_bytes = s[ST_IPV4_BYTES];
     out->ipv6_bytes = s[ST_IPV6_BYTES];
+    for (int k = 0; k < 5; ++k) s[ST_END_INACTIVE + k] += e->host_end[k];  // the plugin walks' exports
     out->end_inactive = s[ST_END_INACTIVE];
     out->end_active = s[ST_END_ACTIVE];
     out->end_eof = s[ST_END_EOF];

@@ -378,6 +378,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
     if (r >= nranks) return;
     const uint32_t s = cx.slot_of[r];
     const HotSlot h = t.hot[s];
+    if (h.state & SLOT_PLUGIN) return;  // a process plugin's flow: the host walks it (plugin_walk)
     bool live = h.state & SLOT_LIVE;
     if (!live) atomicAdd(&ctl->cx_new_live, 1u);  // the slot ends the walk live
     ipxg_flow_record rec;
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_ca
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < from_cap; s += gridDim.x * blockDim.x) {
         const HotSlot h = from.hot[s];
         if (h.key == 0) continue;
-        if (!(h.state & (SLOT_LIVE | SLOT_COMPLEX)) && h.last1 == 0) continue;  // dead slot
+        if (!(h.state & (SLOT_LIVE | SLOT_COMPLEX | SLOT_PLUGIN)) && h.last1 == 0) continue;  // dead slot
         uint32_t ns = (uint32_t)h.key & to.mask;
         bool ok = false;
         for (uint32_t probe = 0; probe <= to.mask; ++probe) {
@@ -632,47 +633,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_parse_batch(BatchView b, uint32_
     LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
     DevPkt pk;
     ParseCounts c = {};
-    ipxg_parsed_pkt o;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-    for (int k = 0; k < (int)(sizeof(o) / 4); ++k) ow[k] = 0;
     const bool ok = parse_frame<true>(S, d.caplen, dlt, pk, c);
-    o.valid = ok;
-    o.ip_version = pk.ip_version;
-    o.ip_proto = pk.ip_proto;
-    o.tcp_flags = pk.tcp_flags;
-    o.ethertype = pk.ethertype;
-    o.ip_len = pk.ip_len;
-    o.src_port = pk.src_port;
-    o.dst_port = pk.dst_port;
-    o.frag_off = pk.frag_off;
-    o.more_fragments = pk.more_fragments;
-    o.ip_ttl = pk.ip_ttl;
-    o.vlan_id = pk.vlan_id;
-    o.frag_id = pk.frag_id;
-    o.mpls_top = pk.mpls_top;
-    o.tcp_mss = pk.tcp_mss;
-    o.tcp_options = pk.tcp_options;
-    for (int k = 0; k < 4; ++k)
-        for (int q = 0; q < 4; ++q) {
-            o.src_ip[4 * k + q] = (uint8_t)(pk.sip[k] >> (8 * q));
-            o.dst_ip[4 * k + q] = (uint8_t)(pk.dip[k] >> (8 * q));
-        }
-    const uint32_t m[3] = {pk.mac_lo, pk.mac_mid, pk.mac_hi};
-    for (int q = 0; q < 6; ++q) {
-        o.dst_mac[q] = (uint8_t)(m[q >> 2] >> (8 * (q & 3)));
-        o.src_mac[q] = (uint8_t)(m[(q + 6) >> 2] >> (8 * ((q + 6) & 3)));
-    }
-    o.ip_tos = pk.ip_tos;
-    o.ip_flags = pk.ip_flags;
-    o.tcp_window = pk.tcp_window;
-    o.tcp_seq = pk.tcp_seq;
-    o.tcp_ack = pk.tcp_ack;
-    if (ok && (pk.ip_version == 4 || pk.ip_version == 6)) {
-        FlowKey kf, ki;
-        build_keys(pk, kf, ki);
-        o.hash_fwd = key_hash(kf);
-        o.hash_inv = key_hash(ki);
-    }
+    ipxg_parsed_pkt o = to_parsed(pk, ok);
     out[i] = o;
 }
 

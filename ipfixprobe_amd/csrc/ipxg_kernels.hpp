@@ -27,6 +27,7 @@ struct alignas(64) HotSlot {
 static_assert(sizeof(HotSlot) == 64, "hot slot must be one 64-byte line");
 
 constexpr uint32_t SLOT_LIVE = 1u, SLOT_COMPLEX = 2u;
+constexpr uint32_t SLOT_PLUGIN = 4u;  // a process plugin's packet in this batch: replayed on the host
 constexpr uint64_t ACC_BYTES_MASK = (1ull << 40) - 1;
 constexpr uint32_t MAX_PROBE = 64;
 
@@ -57,6 +58,7 @@ struct BatchCtl {
     uint32_t agg_packets;    // packets folded into tile aggregates (k_bin / k_bin_slow)
     uint32_t walked;         // wide walk: packets of its extra shapes (variant choice)
     uint32_t fused;          // k_fin_list exported and emptied the flows it finalised (finish fused)
+    uint32_t plugin_fail;    // k_classify found no slot for a plugin flow (table too full)
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -174,6 +176,25 @@ constexpr uint32_t VS_N = 8 + 2 * IPXG_SIZE_BUCKETS;
 constexpr size_t PSTAT_PORTS = 2 * 65536;
 constexpr size_t PSTAT_WORDS = PSTAT_PORTS + (size_t)IPXG_VLAN_IDS * VS_N;
 
+// A registered plugin's pre-classifier rule (ipxg_plugin's rule fields), on the device.
+struct DevRule {
+    uint32_t proto_mask, n_ports;
+    uint16_t ports[IPXG_PLUGIN_MAX_PORTS];
+    uint32_t n_prefixes;
+    uint8_t prefix_len[IPXG_PLUGIN_MAX_PREFIXES];
+    uint8_t prefix[IPXG_PLUGIN_MAX_PREFIXES][IPXG_PLUGIN_PREFIX_LEN];
+};
+
+// A plugin flow between the device and the host walk: its slot, packets (segment of the complex
+// path's sorted list), slot state and key, and its record (k_plugin_pack -> host -> k_plugin_apply).
+struct PluginFlow {
+    uint32_t slot, seg, len, state;
+    uint64_t key;
+    uint64_t pad;
+    ipxg_flow_record rec;
+};
+static_assert(sizeof(PluginFlow) == 160, "plugin flow image");
+
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
 // tile-aggregating variant (more LDS)
@@ -192,6 +213,14 @@ void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSl
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
                      bool finishing);
+void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
+                     uint32_t nrules, BatchCtl* ctl);
+void launch_plugin_pack(hipStream_t st, TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out, uint32_t* count);
+void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
+                        uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout);
+void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
+                         uint8_t* out);
+void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n);
 void launch_pstats(hipStream_t st, const BatchView& b, const Params& p, unsigned long long* pstat);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);

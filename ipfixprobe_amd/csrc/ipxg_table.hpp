@@ -379,7 +379,7 @@ __device__ __forceinline__ void store_export(ExportView ex, uint32_t pos, const 
     ipxg_flow_record o = r;
     o.end_reason = reason;
     o.reserved0 = 0;
-    for (int k = 0; k < 24; ++k) o.reserved[k] = 0;
+    for (int k = 0; k < 8; ++k) o.reserved[k] = 0;  // (ext: exported with the record)
     ex.buf[pos] = o;
 }
 
@@ -591,6 +591,55 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     return true;
 }
 
+// DevPkt (FULL parse) -> the C-ABI's ipxg_parsed_pkt, flow-key hashes included
+__device__ __forceinline__ ipxg_parsed_pkt to_parsed(const DevPkt& pk, bool ok) {
+    ipxg_parsed_pkt o;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+    for (int k = 0; k < (int)(sizeof(o) / 4); ++k) ow[k] = 0;
+    o.valid = ok;
+    o.ip_version = pk.ip_version;
+    o.ip_proto = pk.ip_proto;
+    o.tcp_flags = pk.tcp_flags;
+    o.ethertype = pk.ethertype;
+    o.ip_len = pk.ip_len;
+    o.src_port = pk.src_port;
+    o.dst_port = pk.dst_port;
+    o.frag_off = pk.frag_off;
+    o.more_fragments = pk.more_fragments;
+    o.ip_ttl = pk.ip_ttl;
+    o.vlan_id = pk.vlan_id;
+    o.frag_id = pk.frag_id;
+    o.mpls_top = pk.mpls_top;
+    o.tcp_mss = pk.tcp_mss;
+    o.tcp_options = pk.tcp_options;
+    for (int k = 0; k < 4; ++k)
+        for (int q = 0; q < 4; ++q) {
+            o.src_ip[4 * k + q] = (uint8_t)(pk.sip[k] >> (8 * q));
+            o.dst_ip[4 * k + q] = (uint8_t)(pk.dip[k] >> (8 * q));
+        }
+    const uint32_t m[3] = {pk.mac_lo, pk.mac_mid, pk.mac_hi};
+    for (int q = 0; q < 6; ++q) {
+        o.dst_mac[q] = (uint8_t)(m[q >> 2] >> (8 * (q & 3)));
+        o.src_mac[q] = (uint8_t)(m[(q + 6) >> 2] >> (8 * ((q + 6) & 3)));
+    }
+    o.ip_tos = pk.ip_tos;
+    o.ip_flags = pk.ip_flags;
+    o.tcp_window = pk.tcp_window;
+    o.tcp_seq = pk.tcp_seq;
+    o.tcp_ack = pk.tcp_ack;
+    if (ok && (pk.ip_version == 4 || pk.ip_version == 6)) {
+        FlowKey kf, ki;
+        build_keys(pk, kf, ki);
+        o.hash_fwd = key_hash(kf);
+        o.hash_inv = key_hash(ki);
+    }
+    if (ok) {
+        o.payload_off = pk.payload_off;
+        o.payload_len = pk.payload_len;
+    }
+    return o;
+}
+
 // ---- header staging into LDS ------------------------------------------------------------
 // Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
 // zero-masked past caplen, plus one zero chunk so straddling reads see zeros.
@@ -746,7 +795,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         else if ((int64_t)df.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
     }
     const bool cont = live && !bsplit;
-    bool cx = force_cx;
+    bool cx = force_cx || (h.state & SLOT_PLUGIN);  // a process plugin's flow: the host walks it
     const uint32_t tb = h.tbits;
     if (tb >> 31) cx = true;
     else if (tb) {

@@ -31,7 +31,8 @@ FLOW_DTYPE = np.dtype([
     ("src_port", "<u2"), ("dst_port", "<u2"),
     ("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,)),
     ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)),
-    ("vlan_id", "<u2"), ("end_reason", "u1"), ("reserved0", "u1"), ("reserved", "u1", (24,)),
+    ("vlan_id", "<u2"), ("end_reason", "u1"), ("reserved0", "u1"), ("reserved", "u1", (8,)),
+    ("ext", "<u8"), ("reserved2", "u1", (8,)),
 ])
 PARSED_DTYPE = np.dtype([
     ("valid", "u1"), ("ip_version", "u1"), ("ip_proto", "u1"), ("tcp_flags", "u1"),
@@ -44,6 +45,7 @@ PARSED_DTYPE = np.dtype([
     ("ip_tos", "u1"), ("ip_flags", "u1"), ("tcp_window", "<u2"),
     ("tcp_seq", "<u4"), ("tcp_ack", "<u4"),
     ("hash_fwd", "<u8"), ("hash_inv", "<u8"),
+    ("payload_off", "<u2"), ("payload_len", "<u2"), ("reserved2", "<u4"),
 ])
 STATS_FIELDS = [
     "seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",
@@ -96,8 +98,32 @@ EXPORTED_SYMBOLS = [
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
     "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
     "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
-    "ipxg_parser_stats", "ipxg_top_ports",
+    "ipxg_parser_stats", "ipxg_top_ports", "ipxg_add_plugin",
 ]
+
+FLOW_FLUSH = 0x1
+FLOW_FLUSH_WITH_REINSERT = 0x3
+
+
+class PacketView(ctypes.Structure):
+    """include/ipxg.h ipxg_packet_view: what a process-plugin hook sees of the packet."""
+    _fields_ = [("pkt", ctypes.c_void_p), ("data", ctypes.POINTER(ctypes.c_uint8)), ("caplen", ctypes.c_uint32),
+                ("wirelen", ctypes.c_uint32), ("ts_sec", ctypes.c_uint32), ("ts_usec", ctypes.c_uint32),
+                ("index", ctypes.c_uint32), ("source_pkt", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
+PRE_CREATE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(PacketView))
+FLOW_HOOK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(PacketView))
+PRE_EXPORT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+
+
+class Plugin(ctypes.Structure):
+    """include/ipxg.h ipxg_plugin: a process plugin's pre-classifier rule and hooks."""
+    _fields_ = [("ctx", ctypes.c_void_p), ("proto_mask", ctypes.c_uint32), ("n_ports", ctypes.c_uint32),
+                ("ports", ctypes.c_uint16 * 16), ("n_prefixes", ctypes.c_uint32),
+                ("prefix_len", ctypes.c_uint8 * 8), ("prefix", (ctypes.c_uint8 * 16) * 8),
+                ("pre_create", PRE_CREATE_FN), ("post_create", FLOW_HOOK_FN), ("pre_update", FLOW_HOOK_FN),
+                ("post_update", FLOW_HOOK_FN), ("pre_export", PRE_EXPORT_FN)]
 
 # ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),
@@ -164,6 +190,7 @@ def lib():
         L.ipxg_poll_ipfix_messages.argtypes = [vp, px, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz),
                                                ctypes.POINTER(sz)]
         L.ipxg_parser_stats.argtypes = [vp, vp, vp, vp]
+        L.ipxg_add_plugin.argtypes = [vp, ctypes.POINTER(Plugin)]
         L.ipxg_top_ports.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
         L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                  ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -314,6 +341,10 @@ class Engine:
         self._check(lib().ipxg_get_stats(self._h, arr), "ipxg_get_stats")
         return dict(zip(STATS_FIELDS, list(arr)))
 
+    def add_plugin(self, plugin):
+        """Register a Plugin (ctypes struct); the caller keeps it (and its callbacks) alive."""
+        self._check(lib().ipxg_add_plugin(self._h, ctypes.byref(plugin)), "ipxg_add_plugin")
+
     def parser_stats(self):
         """(tcp port frequencies [65536], udp [65536], VlanStats [4096]) -- engine made with ps=true."""
         tcp = np.zeros(65536, dtype=np.uint64)
@@ -431,9 +462,11 @@ class Engine:
         self.close()
 
 
-def run_capture(arena, desc, datalink=DLT_EN10MB, params="", batch=None, finish=True, **kw):
+def run_capture(arena, desc, datalink=DLT_EN10MB, params="", batch=None, finish=True, plugins=(), **kw):
     """Whole capture through the engine, returns (records, stats)."""
     with Engine(params, datalink=datalink, **kw) as e:
+        for pl in plugins:
+            e.add_plugin(pl)
         e.submit_all(arena, desc, batch)
         if finish:
             e.finish()

@@ -511,6 +511,7 @@ static int parse_packet(pctx* c, uint16_t caplen, uint32_t datalink)
     ipxg_parsed_pkt* p = c->p;
     ipxg_stats* st = c->st;
     uint16_t data_offset = 0;
+    uint32_t l3_hdr_offset, l4_hdr_offset;
     eth_out e;
     st->seen_packets++;
     if (datalink == 0 || datalink == IPXG_DLT_EN10MB) {
@@ -541,6 +542,7 @@ static int parse_packet(pctx* c, uint16_t caplen, uint32_t datalink)
         data_offset = (uint16_t)(data_offset + r);
     }
     uint16_t r;
+    l3_hdr_offset = data_offset;
     if (p->ethertype == ETH_P_IP) {
         r = parse_ipv4_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
         if (c->err) return 0;
@@ -563,16 +565,32 @@ static int parse_packet(pctx* c, uint16_t caplen, uint32_t datalink)
         st->unknown_packets++;
         return 0;
     }
+    l4_hdr_offset = data_offset;
     if (p->frag_off == 0) {
         if (p->ip_proto == 6) {
-            parse_tcp_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
+            r = parse_tcp_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
             if (c->err) return 0;
+            data_offset = (uint16_t)(data_offset + r);
             st->tcp_packets++;
         } else if (p->ip_proto == 17) {
-            parse_udp_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
+            r = parse_udp_hdr(c, data_offset, (uint16_t)(caplen - data_offset));
             if (c->err) return 0;
+            data_offset = (uint16_t)(data_offset + r);
             st->udp_packets++;
         }
+    }
+    { /* payload, parser.cpp:780-797 */
+        uint16_t pkt_len = caplen, wire;
+        if (l4_hdr_offset != l3_hdr_offset) {
+            if (l4_hdr_offset + c->ip_payload_len < 64) pkt_len = (uint16_t)(l4_hdr_offset + c->ip_payload_len);
+            wire = (uint16_t)(c->ip_payload_len - (data_offset - l4_hdr_offset));
+        } else {
+            wire = (uint16_t)(pkt_len - data_offset);
+        }
+        uint16_t plen = wire;
+        if (plen + data_offset > pkt_len) plen = (uint16_t)(pkt_len - data_offset);
+        p->payload_off = data_offset;
+        p->payload_len = plen;
     }
     if (p->vlan_id) st->vlan_packets++;
     if (p->ethertype == ETH_P_IP) {
@@ -735,7 +753,51 @@ struct oracle_cache {
     ipxg_stats st;
     uint64_t flows_in_cache;
     pstats* ps;
+    ipxg_plugin plugins[8];
+    int n_plugins;
 };
+
+void oracle_cache_add_plugin(oracle_cache* c, const ipxg_plugin* p)
+{
+    if (c->n_plugins < 8) c->plugins[c->n_plugins++] = *p;
+}
+
+/* plugins_* (cache.cpp:596-655 / storagePlugin.hpp:97-158): every plugin's hook, OR of the
+ * returns */
+static int hook_pre_create(oracle_cache* c, ipxg_packet_view* v)
+{
+    int r = 0;
+    for (int k = 0; k < c->n_plugins; ++k)
+        if (c->plugins[k].pre_create) r |= c->plugins[k].pre_create(c->plugins[k].ctx, v);
+    return r;
+}
+static int hook_post_create(oracle_cache* c, ipxg_flow_record* f, const ipxg_packet_view* v)
+{
+    int r = 0;
+    for (int k = 0; k < c->n_plugins; ++k)
+        if (c->plugins[k].post_create) r |= c->plugins[k].post_create(c->plugins[k].ctx, f, v);
+    return r;
+}
+static int hook_pre_update(oracle_cache* c, ipxg_flow_record* f, ipxg_packet_view* v)
+{
+    int r = 0;
+    for (int k = 0; k < c->n_plugins; ++k)
+        if (c->plugins[k].pre_update) r |= c->plugins[k].pre_update(c->plugins[k].ctx, f, v);
+    return r;
+}
+static int hook_post_update(oracle_cache* c, ipxg_flow_record* f, const ipxg_packet_view* v)
+{
+    int r = 0;
+    for (int k = 0; k < c->n_plugins; ++k)
+        if (c->plugins[k].post_update) r |= c->plugins[k].post_update(c->plugins[k].ctx, f, v);
+    return r;
+}
+static void hook_pre_export(oracle_cache* c, ipxg_flow_record* f)
+{
+    for (int k = 0; k < c->n_plugins; ++k)
+        if (c->plugins[k].pre_export) c->plugins[k].pre_export(c->plugins[k].ctx, f);
+}
+static void ext_clear(ipxg_flow_record* f) { memset(f->reserved + 8, 0, 8); } /* remove_extensions */
 
 oracle_cache* oracle_cache_new(uint32_t cache_exp, uint32_t line_exp, uint32_t active_s,
                                uint32_t inactive_s, int split_biflow, int frag_enable,
@@ -884,15 +946,54 @@ void oracle_cache_export_expired(oracle_cache* c, int64_t ts)
 {
     for (uint32_t i = c->timeout_idx; i < c->timeout_idx + c->line_new_idx; ++i) {
         orec* r = &c->recs[c->tab[i]];
-        if (r->hash != 0 && ts - (int64_t)r->f.time_last_sec >= (int64_t)c->inactive)
-            export_flow(c, i, export_reason(&r->f));
+        if (r->hash != 0 && ts - (int64_t)r->f.time_last_sec >= (int64_t)c->inactive) {
+            r->f.end_reason = export_reason(&r->f);
+            hook_pre_export(c, &r->f);
+            export_flow(c, i, r->f.end_reason);
+        }
     }
     c->timeout_idx = (c->timeout_idx + c->line_new_idx) & (c->cache_size - 1);
 }
 
-/* put_pkt_recursive cache.cpp:330-491 (no process plugins: every hook returns 0) */
-static void put_pkt_recursive(oracle_cache* c, const ipxg_parsed_pkt* p, uint32_t sec, uint32_t usec)
+/* flush cache.cpp:290-320.  FLOW_FLUSH_WITH_REINSERT: the record goes to the export ring as
+ * it is (FORCED; ipx_ring_push only -- no export statistics), and the slot continues with a
+ * copy of it: extensions removed, reuse() (time_first = time_last, counters zero), update()
+ * with the packet, then post_create (whose flush recurses).  FLOW_FLUSH: export_flow, FORCED. */
+static void flush(oracle_cache* c, uint32_t fi, int ret, ipxg_packet_view* v, const ipxg_parsed_pkt* p, uint32_t sec,
+                  uint32_t usec, int source_flow)
 {
+    orec* r = &c->recs[c->tab[fi]];
+    if (ret == IPXG_FLOW_FLUSH_WITH_REINSERT) {
+        r->f.end_reason = IPXG_FLOW_END_FORCED;
+        if (c->ex_head + c->ex_n == c->ex_cap) {
+            if (c->ex_head > 0) {
+                memmove(c->ex, c->ex + c->ex_head, c->ex_n * sizeof(*c->ex));
+                c->ex_head = 0;
+            } else {
+                c->ex_cap *= 2;
+                c->ex = (ipxg_flow_record*)realloc(c->ex, c->ex_cap * sizeof(*c->ex));
+            }
+        }
+        c->ex[c->ex_head + c->ex_n++] = r->f;
+        ext_clear(&r->f);
+        r->f.time_first_sec = r->f.time_last_sec; /* FlowRecord::reuse cache.cpp:73-83 */
+        r->f.time_first_usec = r->f.time_last_usec;
+        r->f.src_packets = r->f.dst_packets = 0;
+        r->f.src_bytes = r->f.dst_bytes = 0;
+        r->f.src_tcp_flags = r->f.dst_tcp_flags = 0;
+        rec_update(r, p, sec, usec, source_flow);
+        ret = hook_post_create(c, &r->f, v);
+        if (ret & IPXG_FLOW_FLUSH) flush(c, fi, ret, v, p, sec, usec, source_flow);
+    } else {
+        export_flow(c, fi, IPXG_FLOW_END_FORCED);
+    }
+}
+
+/* put_pkt_recursive cache.cpp:330-491, with the process-plugin hooks at their call sites */
+static void put_pkt_recursive(oracle_cache* c, const ipxg_parsed_pkt* p, uint32_t sec, uint32_t usec,
+                              ipxg_packet_view* v)
+{
+    if (c->n_plugins) hook_pre_create(c, v); /* its return is not used (:332) */
     uint8_t key[40], inv[40];
     int keylen = build_keys(p, key, inv);
     if (!keylen) return;
@@ -931,6 +1032,7 @@ static void put_pkt_recursive(oracle_cache* c, const ipxg_parsed_pkt* p, uint32_
             }
         if (!found) { /* line full: evict the last slot, insert at the middle, :400-419 */
             fi = next_line - 1;
+            hook_pre_export(c, &c->recs[c->tab[fi]].f);
             export_flow(c, fi, IPXG_FLOW_END_NO_RES);
             uint32_t new_idx = line_index + c->line_new_idx;
             uint32_t flow = c->tab[fi];
@@ -939,28 +1041,49 @@ static void put_pkt_recursive(oracle_cache* c, const ipxg_parsed_pkt* p, uint32_
             c->tab[new_idx] = flow;
         }
     }
+    if (v) v->source_pkt = (uint8_t)source_flow; /* :428 */
     orec* r = &c->recs[c->tab[fi]];
     uint8_t flw_flags = source_flow ? r->f.src_tcp_flags : r->f.dst_tcp_flags;
     if ((p->tcp_flags & 0x02) && (flw_flags & (0x01 | 0x04))) { /* :431-438 */
         export_flow(c, fi, IPXG_FLOW_END_EOF);
-        put_pkt_recursive(c, p, sec, usec);
+        put_pkt_recursive(c, p, sec, usec, v);
         return;
     }
     if (r->hash == 0) {
         c->flows_in_cache++;
         rec_create(r, p, sec, usec, hashval);
+        if (c->n_plugins && (hook_post_create(c, &r->f, v) & IPXG_FLOW_FLUSH)) /* :443-449 */
+            export_flow(c, fi, r->f.end_reason);  /* end_reason as the record holds it */
     } else {
         if ((int64_t)sec - (int64_t)r->f.time_last_sec >= (int64_t)c->inactive) { /* :453 */
-            export_flow(c, fi, export_reason(&r->f));
-            put_pkt_recursive(c, p, sec, usec);
+            r->f.end_reason = export_reason(&r->f);
+            hook_pre_export(c, &r->f);
+            export_flow(c, fi, r->f.end_reason);
+            put_pkt_recursive(c, p, sec, usec, v);
             return;
         }
         if ((int64_t)sec - (int64_t)r->f.time_first_sec >= (int64_t)c->active) { /* :464 */
+            r->f.end_reason = IPXG_FLOW_END_ACTIVE;
+            hook_pre_export(c, &r->f);
             export_flow(c, fi, IPXG_FLOW_END_ACTIVE);
-            put_pkt_recursive(c, p, sec, usec);
+            put_pkt_recursive(c, p, sec, usec, v);
             return;
         }
-        rec_update(r, p, sec, usec, source_flow);
+        if (c->n_plugins) {
+            int ret = hook_pre_update(c, &r->f, v); /* :474-486 */
+            if (ret & IPXG_FLOW_FLUSH) {
+                flush(c, fi, ret, v, p, sec, usec, source_flow);
+                return;
+            }
+            rec_update(r, p, sec, usec, source_flow);
+            ret = hook_post_update(c, &r->f, v);
+            if (ret & IPXG_FLOW_FLUSH) {
+                flush(c, fi, ret, v, p, sec, usec, source_flow);
+                return;
+            }
+        } else {
+            rec_update(r, p, sec, usec, source_flow);
+        }
     }
     oracle_cache_export_expired(c, (int64_t)sec); /* :489 */
 }
@@ -1017,7 +1140,8 @@ void oracle_cache_run(oracle_cache* c, const uint8_t* arena, const ipxg_pkt_desc
         if (!parse_packet(&pc, d->caplen, datalink)) continue;
         if (c->frag_enable) frag_process(c, &p, d->ts_sec, d->ts_usec);
         if (p.ip_version != 4 && p.ip_version != 6) c->st.keyless_packets++;
-        put_pkt_recursive(c, &p, d->ts_sec, d->ts_usec);
+        ipxg_packet_view v = {&p, arena + d->offset, d->caplen, d->wirelen, d->ts_sec, d->ts_usec, (uint32_t)i, 0, {0}};
+        put_pkt_recursive(c, &p, d->ts_sec, d->ts_usec, &v);
     }
 }
 
@@ -1025,7 +1149,10 @@ void oracle_cache_run(oracle_cache* c, const uint8_t* arena, const ipxg_pkt_desc
 void oracle_cache_finish(oracle_cache* c)
 {
     for (uint32_t i = 0; i < c->cache_size; ++i)
-        if (c->recs[c->tab[i]].hash != 0) export_flow(c, i, IPXG_FLOW_END_FORCED);
+        if (c->recs[c->tab[i]].hash != 0) {
+            hook_pre_export(c, &c->recs[c->tab[i]].f);
+            export_flow(c, i, IPXG_FLOW_END_FORCED);
+        }
 }
 
 size_t oracle_cache_pending(const oracle_cache* c) { return c->ex_n; }

@@ -51,6 +51,9 @@ oracle_cache* oracle_cache_new(uint32_t cache_exp, uint32_t line_exp, uint32_t a
                                uint32_t inactive_s, int split_biflow, int frag_enable,
                                uint32_t frag_size, uint32_t frag_timeout_s);
 void oracle_cache_free(oracle_cache* c);
+/* Process-plugin hooks at the reference's call sites (cache.cpp:290-491; the same
+ * ipxg_plugin callbacks the engine's bridge calls); up to 8, called in order. */
+void oracle_cache_add_plugin(oracle_cache* c, const ipxg_plugin* p);
 /* parse_packet + NHTFlowCache::put_pkt for each packet of a batch, in order. */
 void oracle_cache_run(oracle_cache* c, const uint8_t* arena, const ipxg_pkt_desc* desc,
                       size_t n, uint32_t datalink);

@@ -41,6 +41,7 @@ def lib():
         L.oracle_ipfix_basic.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
         L.oracle_cache_stats.argtypes = [vp, vp]
         L.oracle_cache_parser_stats.argtypes = [vp, vp, vp, vp]
+        L.oracle_cache_add_plugin.argtypes = [vp, vp]
         L.oracle_ipfix_export.restype = ctypes.c_size_t
         L.oracle_ipfix_export.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_bench_mt.restype = ctypes.c_double
@@ -116,6 +117,10 @@ class OracleCache:
         lib().oracle_cache_stats(self._c, arr)
         return dict(zip(STATS_FIELDS, list(arr)))
 
+    def add_plugin(self, plugin):
+        """The same ipxg_plugin callbacks the engine's bridge calls (ctypes Plugin struct)."""
+        lib().oracle_cache_add_plugin(self._c, ctypes.addressof(plugin))
+
     def parser_stats(self):
         """(tcp port frequencies, udp port frequencies, VlanStats per VLAN id)"""
         tcp = np.zeros(65536, dtype=np.uint64)
@@ -170,8 +175,10 @@ def ipfix_export(x, recs):
     return out[:n], nm.value
 
 
-def run_capture(arena, desc, datalink=1, finish=True, **kw):
+def run_capture(arena, desc, datalink=1, finish=True, plugins=(), **kw):
     c = OracleCache(**kw)
+    for pl in plugins:
+        c.add_plugin(pl)
     c.run(arena, desc, datalink)
     if finish:
         c.finish()

@@ -34,7 +34,8 @@ FLOW_DTYPE = np.dtype([
     ("src_port", "<u2"), ("dst_port", "<u2"),
     ("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,)),
     ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)),
-    ("vlan_id", "<u2"), ("end_reason", "u1"), ("reserved0", "u1"), ("reserved", "u1", (24,)),
+    ("vlan_id", "<u2"), ("end_reason", "u1"), ("reserved0", "u1"), ("reserved", "u1", (8,)),
+    ("ext", "<u8"), ("reserved2", "u1", (8,)),
 ])
 assert FLOW_DTYPE.itemsize == 128
 
@@ -49,8 +50,9 @@ PARSED_DTYPE = np.dtype([
     ("ip_tos", "u1"), ("ip_flags", "u1"), ("tcp_window", "<u2"),
     ("tcp_seq", "<u4"), ("tcp_ack", "<u4"),
     ("hash_fwd", "<u8"), ("hash_inv", "<u8"),
+    ("payload_off", "<u2"), ("payload_len", "<u2"), ("reserved2", "<u4"),
 ])
-assert PARSED_DTYPE.itemsize == 112
+assert PARSED_DTYPE.itemsize == 120
 
 # include/ipxg.h ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160), test-side restatement
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),

@@ -33,7 +33,7 @@ def test_struct_layouts_match_header_and_test_restatement():
     from ipfixprobe_amd import engine
     assert engine.DESC_DTYPE == pcaputil.DESC_DTYPE and engine.DESC_DTYPE.itemsize == 16
     assert engine.FLOW_DTYPE == pcaputil.FLOW_DTYPE and engine.FLOW_DTYPE.itemsize == 128
-    assert engine.PARSED_DTYPE == pcaputil.PARSED_DTYPE and engine.PARSED_DTYPE.itemsize == 112
+    assert engine.PARSED_DTYPE == pcaputil.PARSED_DTYPE and engine.PARSED_DTYPE.itemsize == 120
     assert ctypes.sizeof(engine.Config) == 48
     assert engine.STATS_FIELDS == pcaputil.STATS_FIELDS
     assert engine.VLAN_STATS_DTYPE == pcaputil.VLAN_STATS_DTYPE and engine.VLAN_STATS_DTYPE.itemsize == 224

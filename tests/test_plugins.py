@@ -1,0 +1,160 @@
+"""Process-plugin bridge: hooks at put_pkt_recursive's call sites
+(processPlugin.hpp:59-108, cache.cpp:290-491), FLOW_FLUSH and FLOW_FLUSH_WITH_REINSERT.
+
+Pinned by the reference's own goldens: with the DNS stand-in (tests/plugins_py.py, restating
+dns.cpp's flush decision) the basic columns of tests/functional/outputs/dns -- which the
+plain cache does not reproduce, every DNS message being flushed into a record of its own --
+and with the HTTP stand-in those of outputs/http.  The oracle (the same hooks at the same call
+sites) is checked against those goldens on the CPU; the engine's bridge (device pre-classifier,
+host walk of the plugin flows) against the goldens and the oracle on the GPU, including
+synthetic flows whose HTTP requests trigger FLOW_FLUSH_WITH_REINSERT and DNS flows spread over
+several batches."""
+import os
+from collections import Counter
+
+import numpy as np
+import pytest
+
+import flowcmp
+import oracle_py
+import pcaputil
+import plugins_py
+import synth
+
+REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference")
+
+
+def _capture(name):
+    dl, pk = pcaputil.read_capture(os.path.join(REF, name + ".pcap"))
+    arena, desc = pcaputil.to_batch(pk)
+    return dl, arena, desc
+
+
+def _gold(name):
+    return Counter(pcaputil.read_golden(os.path.join(REF, "outputs", name)))
+
+
+def test_plain_cache_does_not_reproduce_dns_golden():
+    dl, arena, desc = _capture("dns")
+    recs, _ = oracle_py.run_capture(arena, desc, dl)
+    assert Counter(pcaputil.format_records(recs)) != _gold("dns")
+
+
+@pytest.mark.parametrize("name,plugin", [("dns", plugins_py.DnsFlush), ("http", plugins_py.HttpReinsert)])
+def test_oracle_with_plugin_reproduces_reference_golden(name, plugin):
+    dl, arena, desc = _capture(name)
+    pl = plugin()
+    recs, st = oracle_py.run_capture(arena, desc, dl, plugins=[pl.struct])
+    assert Counter(pcaputil.format_records(recs)) == _gold(name)
+    assert pl.calls["pre_create"] >= st["parsed_packets"] - st["keyless_packets"]
+
+
+def test_dns_stand_in_decisions():
+    q = bytes.fromhex("abcd01000001000000000000") + b"\x07example\x03com\x00" + b"\x00\x01\x00\x01"
+    assert plugins_py.dns_valid(q, False)
+    assert not plugins_py.dns_valid(q[:11], False)                        # < 12 bytes
+    assert plugins_py.dns_valid(q[:-2], False)                            # overflow: returns success
+    assert not plugins_py.dns_valid(q[:12] + b"\x40" + b"a" * 64 + b"\x00" + q[-4:], False)  # label > 63
+    assert plugins_py.dns_valid(len(q).to_bytes(2, "big") + q, True)
+    assert not plugins_py.dns_valid((len(q) + 1).to_bytes(2, "big") + q, True)  # TCP length mismatch
+
+
+def _http_stream():
+    """TCP flows on port 80, three with two requests and two responses each (REINSERT), three
+    plain; DNS flows (queries and responses flushed one by one, a non-DNS datagram on port 53
+    staying in its flow); other UDP.  The flows are interleaved round-robin, each keeping its
+    own packet order."""
+    cli, srv = synth.ip4(10), synth.ip4(200)
+    get = b"GET /a HTTP/1.1\r\nHost: x\r\n\r\n"
+    resp = b"HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n"
+    e = lambda ip: synth.pad(synth.eth(synth.mac(1), synth.mac(2), 0x0800) + ip)  # noqa: E731
+    flows = []
+    for f in range(6):
+        sp = 40000 + f
+        seq = [(0x02, b"", 0), (0x12, b"", 1), (0x10, b"", 0), (0x18, get, 0), (0x18, resp, 1), (0x10, b"", 0)]
+        if f % 2 == 0:
+            seq += [(0x18, get, 0), (0x18, resp, 1), (0x18, get, 0), (0x10, b"", 1)]
+        seq += [(0x11, b"", 0), (0x11, b"", 1)]
+        fl = []
+        for flags, pay, rev in seq:
+            a, b_, s1, s2 = (srv, cli, 80, sp) if rev else (cli, srv, sp, 80)
+            fl.append(e(synth.ipv4(a, b_, 6, synth.tcp(s1, s2, flags, payload=pay))))
+        flows.append(fl)
+    q = bytes.fromhex("abcd01000001000000000000") + b"\x07example\x03com\x00" + b"\x00\x01\x00\x01"
+    r = bytes.fromhex("abcd81800001000100000000") + b"\x07example\x03com\x00" + b"\x00\x01\x00\x01" + \
+        b"\xc0\x0c\x00\x01\x00\x01\x00\x00\x00\x3c\x00\x04\x01\x02\x03\x04"
+    for k in range(7):
+        sp = 50000 + k
+        fl = []
+        for _ in range(6):
+            fl.append(e(synth.ipv4(cli, srv, 17, synth.udp(sp, 53, q))))
+            fl.append(e(synth.ipv4(srv, cli, 17, synth.udp(53, sp, r))))
+            fl.append(e(synth.ipv4(cli, srv, 17, synth.udp(sp, 53, b"\x00\x01"))))  # not DNS
+        flows.append(fl)
+    for k in range(3):
+        flows.append([e(synth.ipv4(cli, srv, 17, synth.udp(7000 + k, 9000, b"x" * 20))) for _ in range(12)])
+    frames = []
+    for rnd in range(max(len(fl) for fl in flows)):
+        for fl in flows:
+            if rnd < len(fl):
+                frames.append(fl[rnd])
+    return synth.to_batch([(f, len(f), len(f)) for f in frames])
+
+
+def test_oracle_reinsert_splits_http_flows():
+    arena, desc = _http_stream()
+    plain, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=16)
+    pl = plugins_py.HttpReinsert()
+    got, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=16, plugins=[pl.struct])
+    assert len(got) > len(plain)  # REINSERT exported the flows holding a request already
+    # from pre_update the packet goes into the reinserted record only: no packet counted twice
+    assert int(got["src_packets"].sum() + got["dst_packets"].sum()) == int(plain["src_packets"].sum() +
+                                                                            plain["dst_packets"].sum())
+    assert pl.calls["pre_export"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,plugin", [("dns", plugins_py.DnsFlush), ("http", plugins_py.HttpReinsert)])
+@pytest.mark.parametrize("batch", [None, 7])
+def test_bridge_reproduces_reference_golden(name, plugin, batch):
+    from ipfixprobe_amd import run_capture
+    dl, arena, desc = _capture(name)
+    pl = plugin()
+    got, st = run_capture(arena, desc, datalink=dl, params="s=16", batch=batch, plugins=[pl.struct])
+    assert Counter(pcaputil.format_records(got)) == _gold(name)
+    ref_pl = plugin()
+    want, _ = oracle_py.run_capture(arena, desc, dl, cache_exp=16, plugins=[ref_pl.struct])
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [None, 50, 333])
+def test_bridge_reinsert_and_flush_match_oracle(batch):
+    from ipfixprobe_amd import run_capture
+    arena, desc = _http_stream()
+    pls = [plugins_py.HttpReinsert(), plugins_py.DnsFlush()]
+    got, st = run_capture(arena, desc, params="s=16", batch=batch, plugins=[p.struct for p in pls])
+    ref = [plugins_py.HttpReinsert(), plugins_py.DnsFlush()]
+    want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=16, plugins=[p.struct for p in ref])
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+    assert st["complex_flows"] > 0
+    # the hooks saw the plugin flows' packets only (other flows stayed on the device)
+    assert 0 < pls[0].calls["pre_create"] < len(desc)
+
+
+@pytest.mark.gpu
+def test_bridge_leaves_other_flows_on_device():
+    """A stream without any plugin packet: no hook is called, records equal the plain run."""
+    from ipfixprobe_amd import run_capture
+    arena, desc = synth.flow_stream(seed=61, n_flows=100, n_pkts=3000, frag=False).batch()
+    pl = plugins_py.HttpReinsert()
+    pl.struct.n_prefixes = 0
+    pl.struct.n_ports = 1
+    pl.struct.ports[0] = 1  # no packet of the stream uses port 1
+    got, _ = run_capture(arena, desc, params="s=16", plugins=[pl.struct])
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=16)
+    d = flowcmp.diff(got, want)
+    assert not d, d
+    assert sum(pl.calls.values()) == 0
