@@ -298,7 +298,7 @@ int ipxg_top_ports(ipxg_engine* eng, size_t n, ipxg_port_stat* out, size_t* got)
 #define IPXG_FLOW_FLUSH 0x1               /* FLOW_FLUSH (processPlugin.hpp:27)                 */
 #define IPXG_FLOW_FLUSH_WITH_REINSERT 0x3 /* FLOW_FLUSH_WITH_REINSERT (processPlugin.hpp:36)   */
 #define IPXG_PLUGIN_MAX_PORTS 16
-#define IPXG_PLUGIN_MAX_PREFIXES 8
+#define IPXG_PLUGIN_MAX_PREFIXES 16
 #define IPXG_PLUGIN_PREFIX_LEN 16
 
 /* What a hook sees of ipxp::Packet (packet.hpp:46-147): the parsed fields (payload_off /

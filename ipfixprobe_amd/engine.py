@@ -121,7 +121,7 @@ class Plugin(ctypes.Structure):
     """include/ipxg.h ipxg_plugin: a process plugin's pre-classifier rule and hooks."""
     _fields_ = [("ctx", ctypes.c_void_p), ("proto_mask", ctypes.c_uint32), ("n_ports", ctypes.c_uint32),
                 ("ports", ctypes.c_uint16 * 16), ("n_prefixes", ctypes.c_uint32),
-                ("prefix_len", ctypes.c_uint8 * 8), ("prefix", (ctypes.c_uint8 * 16) * 8),
+                ("prefix_len", ctypes.c_uint8 * 16), ("prefix", (ctypes.c_uint8 * 16) * 16),
                 ("pre_create", PRE_CREATE_FN), ("post_create", FLOW_HOOK_FN), ("pre_update", FLOW_HOOK_FN),
                 ("post_update", FLOW_HOOK_FN), ("pre_export", PRE_EXPORT_FN)]
 

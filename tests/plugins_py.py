@@ -209,7 +209,7 @@ class DnsFlush(PyPlugin):
 
 
 # ---- HTTP -----------------------------------------------------------------------------------
-METHODS = (b"GET ", b"POST", b"PUT ", b"HEAD", b"DELE", b"OPTI", b"PATC")  # 7 + "HTTP": the rule's 8 prefixes
+METHODS = (b"GET ", b"POST", b"PUT ", b"HEAD", b"DELE", b"TRAC", b"OPTI", b"CONN", b"PATC")
 
 
 def _request_line(data):
@@ -270,3 +270,65 @@ class HttpReinsert(PyPlugin):
         if ok:
             rec["ext"] = ext | bit
         return 0
+
+
+# ---- NTP ------------------------------------------------------------------------------------
+class NtpFlush(PyPlugin):
+    """ntp.cpp:80-90: post_create on a port-123 packet always returns FLOW_FLUSH."""
+    ports = (123,)
+
+    def post_create(self, rec, p, data):
+        if 123 in (int(p["src_port"]), int(p["dst_port"])):
+            rec["ext"] = 1
+            return FLOW_FLUSH
+        return 0
+
+
+# ---- SIP ------------------------------------------------------------------------------------
+def _le32(s):
+    return int.from_bytes(s, "little")
+
+
+SIP_T1 = {_le32(b"REGI"): 5, _le32(b"INVI"): 1, _le32(b"OPTI"): 6, _le32(b"NOTI"): 8, _le32(b"CANC"): 3,
+          _le32(b"INFO"): 9}
+SIP_T2 = {_le32(b"SIP/"): 99, _le32(b"ACK "): 2, _le32(b"BYE "): 4, _le32(b"SUBS"): 10, _le32(b"PUBL"): 7}
+
+
+def _sip_filter(first, test):
+    """sip.cpp:125-135 on amd64: uint32 check against the 64-bit MAGIC_BITS (sip.hpp:293-296)."""
+    check = (first ^ test) & 0xFFFFFFFF
+    t = ((check + 0x7efefefe7efefeff) & 0xFFFFFFFFFFFFFFFF) ^ (~check & 0xFFFFFFFF)
+    return (t & 0x8101010181010100) != 0
+
+
+def sip_msg_type(d):
+    """SIPPlugin::parse_msg_type (sip.cpp:107-185): 0 = SIP_MSG_TYPE_INVALID."""
+    if len(d) < 64:  # payload_len == 0 or < SIP_MIN_MSG_LEN
+        return 0
+    first = _le32(d[0:4])
+    if _sip_filter(first, _le32(b"IATI")):
+        t = SIP_T1.get(first)
+        if t == 6:
+            return 6 if d[4:8] == b"ONS " and d[8:12] == b"sip:" else 0
+        if t == 8:
+            return 0 if d[4:8] == b"FY *" and d[8:12] == b" HTT" else 8
+        if t:
+            return t
+    if _sip_filter(first, _le32(b"SIB ")):
+        t = SIP_T2.get(first)
+        if t:
+            return t
+    return 0
+
+
+class SipReinsert(PyPlugin):
+    """sip.cpp:66-95: pre_update on a SIP message returns FLOW_FLUSH_WITH_REINSERT."""
+    prefixes = (b"REGI", b"INVI", b"OPTI", b"NOTI", b"CANC", b"INFO", b"SIP/", b"ACK ", b"BYE ", b"SUBS", b"PUBL")
+
+    def post_create(self, rec, p, data):
+        if sip_msg_type(data):
+            rec["ext"] = 1
+        return 0
+
+    def pre_update(self, rec, p, data):
+        return FLOW_FLUSH_WITH_REINSERT if sip_msg_type(data) else 0
