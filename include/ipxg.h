@@ -71,11 +71,13 @@ typedef struct ipxg_pkt_desc {
 } ipxg_pkt_desc;
 
 #define IPXG_BATCH_DEVICE 0x1u /* arena and desc are device pointers (already in HBM)   */
-#define IPXG_BATCH_ASYNC 0x2u  /* with IPXG_BATCH_DEVICE: ipxg_submit may return before the
-                                * batch is applied (its kernels enqueued); the batch's
-                                * buffers must stay unchanged until the next call on the
-                                * engine, which completes it (ipxg_finish right behind it
-                                * then costs one host round trip instead of two)            */
+#define IPXG_BATCH_ASYNC 0x2u  /* ipxg_submit may return before the batch is applied (its
+                                * kernels enqueued); the batch's buffers must stay unchanged
+                                * until the next call on the engine, which completes it
+                                * (ipxg_finish right behind it then costs one host round
+                                * trip instead of two).  Host batches: copied into one of two
+                                * device staging slots on a copy stream while the previous
+                                * batch is in the kernels (pinned host memory for overlap) */
 
 typedef struct ipxg_batch {
     const uint8_t* arena;       /* frame bytes                                          */
@@ -222,6 +224,14 @@ typedef struct ipxg_stats {
     uint64_t aggregated_packets; /* packets folded into per-tile flow aggregates (skew)   */
     uint64_t walked_packets;  /* packets of the wide walk's extra shapes (VLAN, IPv6, TCP
                                  timestamp option) parsed from registers by k_bin     */
+    /* FlowRecordStats (cache.cpp:601-616, counted in export_flow :262-267): exported records
+       by src_packets + dst_packets = 1, 2-5, 6-10, 11-20, 21-50, anything else (51+) */
+    uint64_t flows_1_packet;
+    uint64_t flows_2_5_packets;
+    uint64_t flows_6_10_packets;
+    uint64_t flows_11_20_packets;
+    uint64_t flows_21_50_packets;
+    uint64_t flows_51_plus_packets;
 } ipxg_stats;
 
 /* VlanStats (parser-stats.hpp:126-160) for one VLAN id; sizes are packet_len = caplen,

@@ -61,6 +61,7 @@ struct ipxg_engine {
     std::vector<ipxg_plugin> plugins;
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
+    uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint64_t> host_ports;  // 2 x 65536 when ps=true and plugins walk flows
     // staging for host batches
     DevBuf arena, desc;
@@ -82,6 +83,12 @@ struct ipxg_engine {
         uint32_t n = 0;
     } inflight;
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
+    // asynchronous host batches: two staging slots, filled on a copy stream while the other
+    // slot's batch is in the kernels (the double-buffered ingest ring)
+    DevBuf stage_arena[2], stage_desc[2];
+    hipStream_t cst = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr};
+    int stage_next = 0;
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     DevBuf ipf_msg, ipf_plan;                   // IPFIX messages: output, plan (sets + messages)
     uint8_t* plan_h = nullptr;                  // pinned staging of the plan (asynchronous upload)
@@ -195,7 +202,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     if ((rc = ensure(e, e->bin_count, (size_t)P * cols * sizeof(uint32_t)))) return rc;
     // each k_bin workgroup's slow list holds every packet of its tiles
     const uint64_t slow_stride = (tiles + grid - 1) / grid * BIN_TILE_PKTS;
-    if ((rc = ensure(e, e->slow_list, (size_t)grid * slow_stride * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(e, e->slow_list, (size_t)grid * slow_stride * sizeof(uint4)))) return rc;
     if ((rc = ensure(e, e->slow_cnt, (size_t)grid * sizeof(uint32_t)))) return rc;
     bv.slow_stride = (uint32_t)slow_stride;
     bv.slow_cnt = (uint32_t*)e->slow_cnt.p;  // written by every k_bin workgroup
@@ -431,6 +438,9 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->ctl_h) hipHostFree(e->ctl_h);
     hipFree(e->misc_d);
     hipFree(e->stats_d);
+    if (e->cst) (void)hipStreamDestroy(e->cst);
+    for (hipEvent_t ev : e->copied)
+        if (ev) (void)hipEventDestroy(ev);
     if (e->pstat_d) hipFree(e->pstat_d);
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
@@ -438,7 +448,7 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->plan_ev) (void)hipEventDestroy(e->plan_ev);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (DevBuf* b : {&e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_parsed, &e->pf_desc, &e->pf_off, &e->pf_bytes,
+    for (DevBuf* b : {&e->stage_arena[0], &e->stage_arena[1], &e->stage_desc[0], &e->stage_desc[1], &e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_parsed, &e->pf_desc, &e->pf_off, &e->pf_bytes,
                       &e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
                       &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
@@ -489,14 +499,42 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     if (batch->arena_len > (1ull << 32)) return set_err(e, IPXG_ETOOBIG, "arena larger than 4 GiB");
     if (!batch->arena || !batch->desc) return set_err(e, IPXG_EINVAL, "null arena/desc");
     int rc;
-    if ((rc = complete_batch(e))) return rc;
+    const bool binned = !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST);
+    const bool dev_batch = (batch->flags & IPXG_BATCH_DEVICE) != 0;
+    const bool async = (batch->flags & IPXG_BATCH_ASYNC) && binned;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     BatchView bv;
     bv.n = n;
     bv.arena_lim = (uint32_t)std::min<uint64_t>(batch->arena_len, 0xFFFFFF00ull);
-    if (batch->flags & IPXG_BATCH_DEVICE) {
+    int slot = -1;
+    if (!dev_batch && async) {
+        // Host batch, asynchronous: its H2D copy goes into the staging slot the batch in
+        // flight does not use, on the copy stream, before that batch is completed -- the copy
+        // overlaps the kernels of the previous batch (slot reuse is safe: the batch that used
+        // this slot was completed by the previous call).
+        slot = e->stage_next;
+        e->stage_next ^= 1;
+        if (!e->cst) {
+            HIPCHK(e, hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
+            HIPCHK(e, hipEventCreateWithFlags(&e->copied[0], hipEventDisableTiming));
+            HIPCHK(e, hipEventCreateWithFlags(&e->copied[1], hipEventDisableTiming));
+        }
+        if ((rc = ensure(e, e->stage_arena[slot], batch->arena_len + 64))) return rc;
+        if ((rc = ensure(e, e->stage_desc[slot], (size_t)n * sizeof(ipxg_pkt_desc)))) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->stage_arena[slot].p, batch->arena, batch->arena_len, hipMemcpyHostToDevice,
+                                 e->cst));
+        HIPCHK(e, hipMemcpyAsync(e->stage_desc[slot].p, batch->desc, (size_t)n * sizeof(ipxg_pkt_desc),
+                                 hipMemcpyHostToDevice, e->cst));
+        HIPCHK(e, hipEventRecord(e->copied[slot], e->cst));
+    }
+    if ((rc = complete_batch(e))) return rc;
+    if (dev_batch) {
         bv.arena = batch->arena;
         bv.desc = batch->desc;
+    } else if (slot >= 0) {
+        HIPCHK(e, hipStreamWaitEvent(e->st, e->copied[slot], 0));
+        bv.arena = (const uint8_t*)e->stage_arena[slot].p;
+        bv.desc = (const ipxg_pkt_desc*)e->stage_desc[slot].p;
     } else {
         if ((rc = ensure(e, e->arena, batch->arena_len + 64))) return rc;
         if ((rc = ensure(e, e->desc, (size_t)n * sizeof(ipxg_pkt_desc)))) return rc;
@@ -522,7 +560,6 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 
     Params p = params(e);
     FragView fv = frag_view(e);
-    const bool binned = !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST);
     BinView bins = {};
     if (binned) {
         if ((rc = setup_bins(e, n, bins))) return rc;
@@ -535,7 +572,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     ev_rec(e, 0);
     if (binned) {
         uint32_t* dl = (uint32_t*)e->defer_a.p;
-        uint32_t* sl = (uint32_t*)e->slow_list.p;
+        uint4* sl = (uint4*)e->slow_list.p;
         HotSlot* fl = (HotSlot*)e->fin_list.p;
         uint4* al = (uint4*)e->adefer_a.p;
         launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
@@ -543,7 +580,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 2);
         launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
-        if (!((batch->flags & IPXG_BATCH_ASYNC) && (batch->flags & IPXG_BATCH_DEVICE))) {
+        if (!async) {
             ev_rec(e, 3);
             launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
             ev_rec(e, 4);
@@ -553,7 +590,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         ev_rec(e, 1);
     }
     HIPCHK(e, hipGetLastError());
-    if ((batch->flags & IPXG_BATCH_ASYNC) && (batch->flags & IPXG_BATCH_DEVICE) && binned) {
+    if (async) {
         e->inflight.on = true;  // the next call launches k_fin_list, publishes and reads the control block
         e->inflight.tail = true;
         e->inflight.bv = bv;
@@ -579,6 +616,7 @@ namespace {
 struct WalkOut {
     std::vector<ipxg_flow_record> ex;  // exported records, in order
     uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
+    uint64_t pkts[6] = {0, 0, 0, 0, 0, 0};  // FlowRecordStats buckets
 };
 
 struct FlowWalk {
@@ -623,7 +661,10 @@ struct FlowWalk {
         o.reserved0 = 0;
         std::memset(o.reserved, 0, sizeof(o.reserved));
         out.ex.push_back(o);
-        if (counted && reason >= 1 && reason <= 5) out.end[reason - 1]++;
+        if (counted && reason >= 1 && reason <= 5) {
+            out.end[reason - 1]++;
+            out.pkts[pkts_bucket((uint64_t)o.src_packets + o.dst_packets)]++;
+        }
     }
     // FlowRecord::create (cache.cpp:94-132), the engine's record layout (rec_create)
     void create(const ipxg_parsed_pkt& k, const ipxg_packet_view& v) {
@@ -833,6 +874,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     }
     HIPCHK(e, hipStreamSynchronize(e->st));
     for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
+    for (int k = 0; k < 6; ++k) e->host_pkts[k] += wo.pkts[k];
     return IPXG_OK;
 }
 
@@ -1273,7 +1315,7 @@ struct IpfixPlan {
     uint32_t seq_end = 0;
 };
 
-IpfixPlan ipfix_plan(uint64_t n4, uint64_t n6, const ipxg_ipfix_exporter& x) {
+static IpfixPlan ipfix_plan(uint64_t n4, uint64_t n6, const ipxg_ipfix_exporter& x) {
     IpfixPlan P;
     const uint32_t mtu = x.mtu;
     uint64_t b[2] = {0, 0}, emitted[2] = {0, 0};
@@ -1625,6 +1667,13 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->slow_path_packets = e->slow_pkts;
     out->walked_packets = e->walked_pkts;
     out->aggregated_packets = e->agg_pkts;
+    for (int k = 0; k < 6; ++k) s[ST_PKTS_1 + k] += e->host_pkts[k];
+    out->flows_1_packet = s[ST_PKTS_1];
+    out->flows_2_5_packets = s[ST_PKTS_2_5];
+    out->flows_6_10_packets = s[ST_PKTS_6_10];
+    out->flows_11_20_packets = s[ST_PKTS_11_20];
+    out->flows_21_50_packets = s[ST_PKTS_21_50];
+    out->flows_51_plus_packets = s[ST_PKTS_51];
     return IPXG_OK;
 }
 

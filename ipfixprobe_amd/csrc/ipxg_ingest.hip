@@ -426,7 +426,7 @@ __device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& 
 // The host picks the variants per batch (ipxg_engine.cpp: tile_agg, wide).
 template <bool AGG, bool WIDE>
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : 3)))
-void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint32_t* slow_list,
+void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
     __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: slots in the block's segments
@@ -448,7 +448,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // the block's slow list: every packet of its tiles fits, so a slow packet is stored at
     // its rank without any device atomic (a returning one inside the pipelined loop made the
     // compiler drain every load in flight)
-    uint32_t* const my_slow = slow_list + (size_t)blockIdx.x * bv.slow_stride;
+    uint4* const my_slow = slow_list + (size_t)blockIdx.x * bv.slow_stride;
     uint32_t slow_fill = 0, par = 0;
     if (b.n == 0) return;
     const uint32_t last = b.n - 1;
@@ -583,7 +583,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         slow = true;
                 }
             }
-            if (slow) my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] = i;
+            if (slow)
+                my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] =
+                    make_uint4(i, dc.offset, (uint32_t)dc.caplen | ((uint32_t)dc.wirelen << 16), dc.ts_sec);
             if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
         }
         PROBE_T(t2);
@@ -635,15 +637,94 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     if (WIDE) add_wave_sum(&ctl->walked, walked);
 }
 
+// A slow-list entry (k_bin -> k_bin_slow): {packet index, offset, caplen | wirelen << 16,
+// ts_sec} -- the descriptor fields the slow pass reads, so one 16-byte load replaces the
+// index load and the dependent descriptor load.
+__device__ __forceinline__ ipxg_pkt_desc slow_desc(const uint4 e) {
+    ipxg_pkt_desc d;
+    d.offset = e.y;
+    d.caplen = (uint16_t)e.z;
+    d.wirelen = (uint16_t)(e.z >> 16);
+    d.ts_sec = e.w;
+    d.ts_usec = 0;  // not read by the slow pass
+    return d;
+}
+
+// The first IPXG_WIN bytes of an aligned frame as 16-byte buffer loads (a chunk at or past
+// caplen, and every chunk of an unaligned frame, reads as zeros with no memory traffic).
+constexpr int SLOW_NCH = IPXG_WIN / 16;
+struct SlowWin {
+    uint4 c[SLOW_NCH];
+};
+
+__device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t arena, const uint4 e) {
+    const uint32_t cap = e.z & 0xFFFFu;
+    const uint32_t o = (e.y & 15) ? BUF_OOB : e.y;
+    SlowWin w;
+#pragma unroll
+    for (int k = 0; k < SLOW_NCH; ++k)
+        w.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, (uint32_t)(16 * k) < cap ? o + 16 * k : BUF_OOB, 0,
+                                                          IPXG_LOAD_AUX));
+    return w;
+}
+
+// The window into the lane's LDS column, zero-masked past caplen, plus one zero chunk so
+// straddling reads see zeros (stage_frame's layout); unaligned frames: stage_frame's byte loads.
+__device__ __forceinline__ void put_window(uint32_t* col, const uint8_t* arena, const uint4 e, const SlowWin& w) {
+    const uint32_t cap = e.z & 0xFFFFu;
+    if (e.y & 15) {
+        stage_frame(col, arena, e.y, cap);
+        return;
+    }
+    const uint32_t nch = ((cap < IPXG_WIN ? cap : IPXG_WIN) + 15) >> 4;
+#pragma unroll
+    for (int ch = 0; ch < SLOW_NCH; ++ch) {
+        if ((uint32_t)ch > nch) break;
+        const uint32_t v[4] = {w.c[ch].x, w.c[ch].y, w.c[ch].z, w.c[ch].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int valid = (int)cap - (16 * ch + 4 * k);
+            const uint32_t m = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+            col[(4 * ch + k) * IPXG_BLOCK] = v[k] & m;
+        }
+    }
+}
+
+// One slow packet: staged, parsed by parse_frame, then keyless / fragment / record slot j.
+template <bool AGG>
+__device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b, const FragView& f, BatchCtl* ctl,
+                                            uint32_t* col, const uint4 e, const SlowWin& w, int j, ParseCounts& c,
+                                            uint32_t& keyless, uint32_t& frags, uint32_t (&r0)[BIN_K],
+                                            uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
+                                            uint32_t (&ix)[BIN_K]) {
+    const ipxg_pkt_desc d = slow_desc(e);
+    const uint32_t i = e.x;
+    put_window(col, b.arena, e, w);
+    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    DevPkt pk;
+    if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) return;
+    if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
+        keyless++;
+        return;
+    }
+    if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
+        frags++;
+        divert_fragment(pk, p, f, ctl, i);
+        return;
+    }
+    tile_rank<true>(p, b, pk, d, i, j, r0, r1, r2, rk, ix);
+}
+
 // The frames k_bin left for the general parser (VLAN/QinQ, MPLS, PPPoE, GRE, TRILL, IPv6
 // and its extension headers, IPv4 options, TCP options, SLL/SLL2/raw link types, truncated
 // or unaligned frames): staged in the lane's LDS column, parsed by parse_frame, ranked and
 // emitted exactly like k_bin's records.  The list length is read on the device.
-// 168 VGPRs (3 waves/SIMD = the LDS limit of 3 workgroups per CU)
+// Up to 256 VGPRs (2 waves/SIMD): the packet pairs' windows take 64; two pairs in flight per
+// SIMD hide more latency than three single packets did.
 template <bool AGG>
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG ? 2 : 3)))
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
-                const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
+                const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     // the header columns (parse), the tile hash and the tile's slots (emit) are never live
     // together: one 32 KiB area; 76 KiB in all with aggregation (2 workgroups per CU), 48 KiB
     // without (3 per CU)
@@ -661,7 +742,9 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     uint32_t* win = reinterpret_cast<uint32_t*>(stage);
     // k_bin workgroup b's slow packets, into segment column bin_grid + b
     const uint32_t ns = bv.slow_cnt[blockIdx.x];  // final: k_bin has completed
-    const uint32_t* const list = slow_list + (size_t)blockIdx.x * bv.slow_stride;
+    const uint4* const list = slow_list + (size_t)blockIdx.x * bv.slow_stride;
+    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
     if (ns == 0) return;  // no work: k_reduce does not read the column
     for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
@@ -680,26 +763,22 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
+        // two packets per lane and step: both list entries, then both frames' windows, are in
+        // flight together, so one pair of memory round trips serves two packets
+        static_assert(BIN_K % 2 == 0, "the slow pass takes its packets in pairs");
 #pragma unroll 1
-        for (int j = 0; j < BIN_K; ++j) {
-            const uint32_t k = tile + (uint32_t)j * IPXG_BLOCK + tid;
-            if (k >= ns) continue;
-            const uint32_t i = list[k];
-            const ipxg_pkt_desc d = b.desc[i];
-            stage_frame(col, b.arena, d.offset, d.caplen);
-            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-            DevPkt pk;
-            if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
-            if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
-                keyless++;
-                continue;
+        for (int j = 0; j < BIN_K; j += 2) {
+            const uint32_t k0 = tile + (uint32_t)j * IPXG_BLOCK + tid, k1 = k0 + IPXG_BLOCK;
+            if (k0 >= ns) break;
+            const uint4 e0 = list[k0];
+            const uint4 e1 = k1 < ns ? list[k1] : make_uint4(0, BUF_OOB, 0, 0);
+            SlowWin w1;
+            {
+                const SlowWin w0 = load_win(rs_arena, e0);
+                w1 = load_win(rs_arena, e1);
+                slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix);
             }
-            if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
-                frags++;
-                divert_fragment(pk, p, f, ctl, i);
-                continue;
-            }
-            tile_rank<true>(p, b, pk, d, i, j, r0, r1, r2, rk, ix);
+            if (k1 < ns) slow_packet<AGG>(p, b, f, ctl, col, e1, w1, j + 1, c, keyless, frags, r0, r1, r2, rk, ix);
         }
         if (AGG) tile_aggregate<true>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
         else tile_rank_all(hist, pmask, r1, rk);
@@ -719,7 +798,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     if (AGG) add_wave_sum(&ctl->agg_packets, folded);
 }
 
-typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint32_t*, uint32_t*, uint4*,
+typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint4*, uint32_t*, uint4*,
                           unsigned long long*);
 static BinKernel bin_kernel(bool agg, bool wide) {
     return agg ? (wide ? k_bin<true, true> : k_bin<true, false>) : (wide ? k_bin<false, true> : k_bin<false, false>);
@@ -735,14 +814,14 @@ uint32_t bin_resident_blocks(int device, bool agg, bool wide) {
 }
 
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                BatchCtl* ctl, uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats) {
     hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
                        t, f, bv, ctl, slow_list, deferred_list, agg_list, stats);
 }
 
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                     BatchCtl* ctl, const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                      unsigned long long* stats) {
     if (p.tile_agg)
         hipLaunchKernelGGL(k_bin_slow<true>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
@@ -1097,7 +1176,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
         const uint32_t pos = wave_append(ex.count, do_export);
         if (do_export) {
             store_export(ex, pos, er, reason);
-            atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
+            count_export(sc, er, reason);
             n_ex++;
         }
         count_v6_exports(ex, do_export && er.ip_version == 6);
@@ -1105,7 +1184,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
             const uint32_t pf = wave_append(ex.count, fin_export);
             if (fin_export) {
                 store_export(ex, pf, fr_rec, IPXG_FLOW_END_FORCED);
-                atomicAdd(&sc[ST_END_FORCED], 1u);
+                count_export(sc, fr_rec, IPXG_FLOW_END_FORCED);
                 n_ex++;
             }
             count_v6_exports(ex, fin_export && fr_rec.ip_version == 6);

@@ -275,10 +275,6 @@ void launch_deferred_agg(hipStream_t st, TableView t, const uint4* in_list, uint
     hipLaunchKernelGGL(k_deferred_agg, dim3((n_in + 255) / 256), dim3(256), 0, st, t, in_list, n_in, ctl, out_list);
 }
 
-__device__ __forceinline__ void reason_count(uint32_t* sc, uint8_t reason) {
-    atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
-}
-
 // ---- K3: finalize (full-table scan; the fast path finalises inside k_reduce) -------------
 __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableView t, FragView f,
                                                   ExportView ex, BatchCtl* ctl, unsigned long long* stats,
@@ -316,7 +312,7 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
         uint32_t pos = wave_append(ex.count, do_export);
         if (do_export) {
             store_export(ex, pos, er, reason);
-            reason_count(sc, reason);
+            count_export(sc, er, reason);
             ex_n++;
         }
         count_v6_exports(ex, do_export && er.ip_version == 6);
@@ -407,6 +403,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
                 store_export(ex, pos, rec, reason);
                 if (ex.count6 && rec.ip_version == 6) atomicAdd(ex.count + 2, 1u);
                 atomicAdd(&stats[ST_END_INACTIVE + reason - 1], 1ull);
+                atomicAdd(&stats[ST_PKTS_1 + pkts_bucket((uint64_t)rec.src_packets + rec.dst_packets)], 1ull);
                 n_ex++;
                 live = false;
             }
@@ -491,7 +488,7 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
             rec = t.cold[base + j * 256 + threadIdx.x];
             const uint8_t reason = export_reason(rec);
             store_export(ex, pos++, rec, reason);
-            reason_count(sc, reason);
+            count_export(sc, rec, reason);
         }
         count_v6_exports(ex, mine && rec.ip_version == 6);
     }
@@ -516,6 +513,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
                                                 uint32_t live_before) {
     __shared__ uint32_t scratch[8];
     __shared__ uint32_t bbase;
+    __shared__ uint32_t pb[6];  // FlowRecordStats buckets of the block's exports
     if (guard) {
         const bool hold = guard->frag_count || guard->deferred || guard->agg_deferred || guard->pending ||
                           guard->complex_count ||
@@ -540,6 +538,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     uint32_t total;
     const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
     if (threadIdx.x == 0) bbase = total ? atomicAdd(ex.count, total) : 0;
+    if (threadIdx.x < 6) pb[threadIdx.x] = 0;
     __syncthreads();
     uint32_t pos = bbase + off;
 #pragma unroll
@@ -549,11 +548,14 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         if (mine) {
             rec = t.cold[base + j * 256 + threadIdx.x];
             store_export(ex, pos++, rec, IPXG_FLOW_END_FORCED);
+            atomicAdd(&pb[pkts_bucket((uint64_t)rec.src_packets + rec.dst_packets)], 1u);
         }
         count_v6_exports(ex, mine && rec.ip_version == 6);
     }
-    if (threadIdx.x == 0 && total)
-        atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + ST_END_FORCED], (unsigned long long)total);
+    __syncthreads();
+    unsigned long long* const sh = &stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT];
+    if (threadIdx.x == 0 && total) atomicAdd(&sh[ST_END_FORCED], (unsigned long long)total);
+    if (threadIdx.x < 6 && pb[threadIdx.x]) atomicAdd(&sh[ST_PKTS_1 + threadIdx.x], (unsigned long long)pb[threadIdx.x]);
 }
 
 // Copy the control block (+ export counter) into host-mapped memory: the host reads it after

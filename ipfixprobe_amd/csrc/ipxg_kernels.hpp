@@ -76,8 +76,16 @@ constexpr int STAT_SHARDS = 16;
 enum StatIdx {
     ST_SEEN, ST_PARSED, ST_UNKNOWN, ST_IPV4, ST_IPV6, ST_TCP, ST_UDP, ST_MPLS, ST_PPPOE, ST_TRILL,
     ST_VLAN, ST_IPV4_BYTES, ST_IPV6_BYTES, ST_KEYLESS, ST_FRAGMENTED, ST_FRAG_FILLED,
-    ST_END_INACTIVE, ST_END_ACTIVE, ST_END_EOF, ST_END_FORCED, ST_END_NO_RES, ST_COUNT
+    ST_END_INACTIVE, ST_END_ACTIVE, ST_END_EOF, ST_END_FORCED, ST_END_NO_RES,
+    ST_PKTS_1, ST_PKTS_2_5, ST_PKTS_6_10, ST_PKTS_11_20, ST_PKTS_21_50, ST_PKTS_51, ST_COUNT
 };
+
+// FlowRecordStats bucket of a record of n = src_packets + dst_packets packets
+// (update_flow_record_stats, cache.cpp:601-616: 0 falls to the last bucket, as there)
+__host__ __device__ inline uint32_t pkts_bucket(uint64_t n) {
+    return n == 1 ? 0 : (n >= 2 && n <= 5) ? 1 : (n >= 6 && n <= 10) ? 2 : (n >= 11 && n <= 20) ? 3
+         : (n >= 21 && n <= 50) ? 4 : 5;
+}
 
 // Everything a kernel needs about the engine, passed by value.
 struct TableView {
@@ -139,7 +147,7 @@ struct BinView {
     uint32_t cols;       // 2 * bin_grid: k_bin's columns, then k_bin_slow's
     uint32_t bin_grid;   // workgroups of k_bin (and of k_bin_slow)
     uint32_t part_bits;  // parts = 1 << part_bits
-    uint32_t slow_stride;  // k_bin workgroup b lists its slow packets at slow_list[b * slow_stride ...]
+    uint32_t slow_stride;  // k_bin workgroup b lists its slow packets (16-B entries) at slow_list[b * slow_stride ...]
     uint32_t* slow_cnt;    // bin_grid: slow packets listed by each k_bin workgroup
 };
 #ifndef IPXG_BIN_K
@@ -202,10 +210,10 @@ uint32_t bin_resident_blocks(int device, bool agg, bool wide);
 // deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
 // 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                BatchCtl* ctl, uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                BatchCtl* ctl, uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats);
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
-                     BatchCtl* ctl, const uint32_t* slow_list, uint32_t* deferred_list, uint4* agg_list,
+                     BatchCtl* ctl, const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                      unsigned long long* stats);
 // fin_list: the merged images of the slots k_reduce completed (HotSlot::pad = slot index)
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,

@@ -383,6 +383,13 @@ __device__ __forceinline__ void store_export(ExportView ex, uint32_t pos, const 
     ex.buf[pos] = o;
 }
 
+// export_flow's statistics (cache.cpp:264-267) into a block's counters: end reason and
+// FlowRecordStats bucket
+__device__ __forceinline__ void count_export(uint32_t* sc, const ipxg_flow_record& r, uint8_t reason) {
+    atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
+    atomicAdd(&sc[ST_PKTS_1 + pkts_bucket((uint64_t)r.src_packets + r.dst_packets)], 1u);
+}
+
 // ex.count[2] counts the exported records that take the IPv6 basic template (the IPFIX message
 // layout needs the split, ipxg_engine.cpp ipfix_plan).  Convergent: every lane of the wave.
 __device__ __forceinline__ void count_v6_exports(ExportView ex, bool v6) {

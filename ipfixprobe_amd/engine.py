@@ -54,7 +54,8 @@ STATS_FIELDS = [
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
     "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
-    "aggregated_packets", "walked_packets",
+    "aggregated_packets", "walked_packets", "flows_1_packet", "flows_2_5_packets", "flows_6_10_packets",
+    "flows_11_20_packets", "flows_21_50_packets", "flows_51_plus_packets",
 ]
 
 
@@ -268,7 +269,7 @@ class Engine:
             b.arena_len = arena.numel() * arena.element_size()
             b.desc = desc.data_ptr()
             b.n = desc.numel() * desc.element_size() // 16
-            b.flags = (BATCH_DEVICE | (BATCH_ASYNC if asynchronous else 0)) if device else 0
+            b.flags = (BATCH_DEVICE if device else 0) | (BATCH_ASYNC if asynchronous else 0)
             b._keep = (arena, desc)
         else:
             arena = np.ascontiguousarray(arena, dtype=np.uint8)
@@ -277,13 +278,14 @@ class Engine:
             b.arena_len = arena.nbytes
             b.desc = desc.ctypes.data
             b.n = len(desc)
-            b.flags = 0
+            b.flags = BATCH_ASYNC if asynchronous else 0
             b._keep = (arena, desc)
         return b
 
     def submit(self, arena, desc, device=False, asynchronous=False, wait_producer=True):
-        """asynchronous (device batches): may return before the batch is applied; keep the
-        tensors alive and unchanged until the next call on the engine.  wait_producer (device
+        """asynchronous: may return before the batch is applied; keep the arrays / tensors alive
+        and unchanged until the next call on the engine (host batches: pinned memory lets the
+        copy overlap the previous batch's kernels).  wait_producer (device
         torch tensors): the engine's stream first waits for the work queued so far on torch's
         current stream (the kernels that wrote the batch) -- the engine's stream is a
         non-blocking stream, unordered with respect to torch's; pass False when the caller has
@@ -295,7 +297,7 @@ class Engine:
                 self._ext_stream = torch.cuda.ExternalStream(self.stream(), device=dev)
             self._ext_stream.wait_stream(torch.cuda.current_stream(dev))
         b = self._batch(arena, desc, device, asynchronous)
-        self._keep_async = b._keep if (device and asynchronous) else None
+        self._keep_async = b._keep if asynchronous else None
         self._check(lib().ipxg_submit(self._h, ctypes.byref(b)), "ipxg_submit")
 
     def submit_all(self, arena, desc, batch=None):

@@ -920,6 +920,13 @@ static void export_flow(oracle_cache* c, uint32_t index, uint8_t reason)
     case IPXG_FLOW_END_NO_RES: c->st.end_no_res++; break;
     }
     c->st.total_exported++;
+    { /* update_flow_record_stats cache.cpp:601-616 (0 packets: the final else) */
+        const uint64_t n = (uint64_t)r->f.src_packets + r->f.dst_packets;
+        uint64_t* b = n == 1 ? &c->st.flows_1_packet : (n >= 2 && n <= 5) ? &c->st.flows_2_5_packets
+                    : (n >= 6 && n <= 10) ? &c->st.flows_6_10_packets : (n >= 11 && n <= 20) ? &c->st.flows_11_20_packets
+                    : (n >= 21 && n <= 50) ? &c->st.flows_21_50_packets : &c->st.flows_51_plus_packets;
+        (*b)++;
+    }
     c->flows_in_cache--;
     if (c->ex_head + c->ex_n == c->ex_cap) {
         if (c->ex_head > 0) {

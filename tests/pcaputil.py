@@ -69,7 +69,8 @@ STATS_FIELDS = [
     "end_forced", "end_no_res", "flows_in_cache", "total_exported", "keyless_packets",
     "fragmented_packets", "fragments_filled", "complex_flows", "table_capacity",
     "table_rehashes", "batches", "spilled_packets", "slow_path_packets",
-    "aggregated_packets", "walked_packets",
+    "aggregated_packets", "walked_packets", "flows_1_packet", "flows_2_5_packets", "flows_6_10_packets",
+    "flows_11_20_packets", "flows_21_50_packets", "flows_51_plus_packets",
 ]
 
 

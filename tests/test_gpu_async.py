@@ -114,3 +114,31 @@ def test_async_then_expire_stats_and_sync_submit():
         got = e.poll()
     d = flowcmp.diff(got, want)
     assert not d, d
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_async_host_batches_double_buffered(ci, pinned):
+    """Host batches with IPXG_BATCH_ASYNC: each copied into one of two device staging slots on
+    the copy stream while the previous batch is in the kernels.  Every batch is a separate
+    host array (kept alive until the next call, as the contract asks)."""
+    import torch
+    from ipfixprobe_amd import Engine
+    arena, desc = synth.flow_stream(**CASES[ci]).batch()
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    step = 600
+    keep = []
+    with Engine() as e:
+        for s in range(0, len(desc), step):
+            d = np.ascontiguousarray(desc[s:s + step])
+            if pinned:
+                a_h = torch.from_numpy(np.ascontiguousarray(arena)).pin_memory()
+                d_h = torch.from_numpy(d.view(np.uint8).reshape(-1)).pin_memory()
+            else:
+                a_h, d_h = np.ascontiguousarray(arena), d
+            keep.append((a_h, d_h))
+            e.submit(a_h, d_h, asynchronous=True)
+        e.finish()
+        got = e.poll()
+    d = flowcmp.diff(got, want)
+    assert not d, d

@@ -9,6 +9,7 @@ import flowcmp
 import oracle_py
 import pcaputil
 import synth
+from test_oracle_synth import PKT_BUCKETS
 
 pytestmark = pytest.mark.gpu
 
@@ -143,6 +144,9 @@ def test_stream_parity(ci, batch, walk):
     assert not d, d
     assert gst["fragmented_packets"] == wst["fragmented_packets"]
     assert gst["fragments_filled"] == wst["fragments_filled"]
+    # FlowRecordStats (cache.cpp:601-616): the records are equal, so are their packet buckets
+    assert [gst[k] for k in PKT_BUCKETS] == [wst[k] for k in PKT_BUCKETS]
+    assert sum(gst[k] for k in PKT_BUCKETS) == gst["total_exported"] == len(got)
 
 
 def test_stream_reasons_and_counts():

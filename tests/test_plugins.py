@@ -20,6 +20,7 @@ import oracle_py
 import pcaputil
 import plugins_py
 import synth
+from test_oracle_synth import PKT_BUCKETS
 
 REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference")
 
@@ -154,6 +155,10 @@ def test_bridge_reinsert_and_flush_match_oracle(batch):
     d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
     assert not d, d
     assert st["complex_flows"] > 0
+    # FlowRecordStats / end reasons count export_flow only (a REINSERT push is not counted)
+    for k in PKT_BUCKETS + ["total_exported"]:
+        assert st[k] == wst[k], k
+    assert st["total_exported"] < len(got)
     # the hooks saw the plugin flows' packets only (other flows stayed on the device)
     assert 0 < pls[0].calls["pre_create"] < len(desc)
 
