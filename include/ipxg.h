@@ -159,7 +159,7 @@ typedef struct ipxg_parsed_pkt {
 /* ---- engine ------------------------------------------------------------------------ */
 typedef struct ipxg_config {
     uint32_t cache_exp;       /* s=  initial table capacity 2^s slots (4..30)          */
-    uint32_t line_exp;        /* l=  accepted for option compatibility                 */
+    uint32_t line_exp;        /* l=  line size 2^l (strict=true; otherwise accepted)    */
     uint32_t active_s;        /* a=  active timeout, seconds (default 300)             */
     uint32_t inactive_s;      /* i=  inactive timeout, seconds (default 30)            */
     uint32_t split_biflow;    /* S   1 = uniflows                                      */
@@ -187,6 +187,14 @@ typedef struct ipxg_config {
                                        frequencies (TopPorts) and per-VLAN counters with the
                                        packet-size histogram (VlanStats), parser-stats.hpp
                                        :126-201 -- kept on the device (ipxg_parser_stats) */
+#define IPXG_CFG_STRICT 0x10u       /* strict=true: the reference's table exactly -- 2^s records
+                                       in lines of 2^l (l <= 4, at most 32768 lines), move to
+                                       front, FLOW_END_NO_RES eviction with insertion at the
+                                       middle, the per-packet sweep (cache.cpp:322-523) --
+                                       replayed on the device in packet order per line
+                                       (ipxg_strict.hip); ipxg_expire is then one
+                                       export_expired(now) step.  Not with ingest=atomic, ps=true
+                                       or process plugins. */
 
 typedef struct ipxg_stats {
     /* parser counters, reference parser-stats.hpp:126-201 (the subset on the path) */

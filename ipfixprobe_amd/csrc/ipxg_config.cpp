@@ -6,7 +6,8 @@
 // tokens, "name=value" or "name" followed by its value as the next token), plus the GPU keys
 // "dev"/"device", "batch", "dlt" (EN10MB | RAW | LINUX_SLL | LINUX_SLL2 or a number) and
 // "ingest" (binned | atomic), "walk" (auto | wide | narrow: which k_bin variant walks
-// the header chains) and "ps"/"parser-stats" (true | false: TopPorts + VlanStats).
+// the header chains), "ps"/"parser-stats" (true | false: TopPorts + VlanStats) and "strict"
+// (true | false: the reference's line table replayed exactly, ipxg_strict.hip).
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -95,6 +96,11 @@ extern "C" int ipxg_config_parse(const char* params, ipxg_config* cfg) {
             if (!arg(a)) return IPXG_EINVAL;
             if (a == "atomic") cfg->flags |= IPXG_CFG_ATOMIC_INGEST;
             else if (a == "binned") cfg->flags &= ~IPXG_CFG_ATOMIC_INGEST;
+            else return IPXG_EINVAL;
+        } else if (name == "strict") {
+            if (!arg(a)) return IPXG_EINVAL;
+            if (a == "true") cfg->flags |= IPXG_CFG_STRICT;
+            else if (a == "false") cfg->flags &= ~IPXG_CFG_STRICT;
             else return IPXG_EINVAL;
         } else if (name == "ps" || name == "parser-stats") {
             if (!arg(a)) return IPXG_EINVAL;

@@ -99,6 +99,11 @@ struct ipxg_engine {
     uint32_t part_bits_last = 0;         // partitions of the last binned batch (log2)
     FragEntry* frag_ent = nullptr;
     uint32_t* frag_cnt = nullptr;
+    // strict mode (strict=true): the reference's line table, replayed in packet order
+    bool strict = false;
+    StrictView sv = {};
+    uint64_t strict_q = 0;  // sweep steps taken (keyed packets + expire calls): the cursor
+    DevBuf st_pkt, st_crec, st_keyed, st_qx, st_keys, st_vals, st_keys2, st_vals2, st_start, st_evpos;
     // host-side counters
     uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0, walked_pkts = 0;
     bool prev_valid = false;
@@ -418,6 +423,21 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
         return fail(IPXG_EDEVICE);
+    if (e->cfg.flags & IPXG_CFG_STRICT) {
+        if (cfg->line_exp > 4 || cfg->line_exp > cfg->cache_exp || cfg->cache_exp - cfg->line_exp > 15 ||
+            (cfg->flags & (IPXG_CFG_ATOMIC_INGEST | IPXG_CFG_PARSER_STATS)))
+            return fail(IPXG_EINVAL);
+        e->strict = true;
+        const uint32_t S = 1u << cfg->cache_exp;
+        e->sv.line_bits = cfg->line_exp;
+        e->sv.lines = S >> cfg->line_exp;
+        e->sv.slot_mask = S - 1;
+        if (hipMalloc((void**)&e->sv.rec, (size_t)S * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
+        if (hipMalloc((void**)&e->sv.hash, (size_t)S * 8) != hipSuccess) return fail(IPXG_ENOMEM);
+        if (hipMalloc((void**)&e->sv.perm, (size_t)e->sv.lines * 8) != hipSuccess) return fail(IPXG_ENOMEM);
+        launch_strict_clear(e->st, e->sv);
+        if (hipGetLastError() != hipSuccess) return fail(IPXG_EDEVICE);
+    }
     if (e->cfg.flags & IPXG_CFG_PARSER_STATS) {
         if (hipMalloc((void**)&e->pstat_d, PSTAT_WORDS * 8) != hipSuccess) return fail(IPXG_ENOMEM);
         if (hipMemsetAsync(e->pstat_d, 0, PSTAT_WORDS * 8, e->st) != hipSuccess) return fail(IPXG_EDEVICE);
@@ -442,6 +462,9 @@ int ipxg_destroy(ipxg_engine* e) {
     for (hipEvent_t ev : e->copied)
         if (ev) (void)hipEventDestroy(ev);
     if (e->pstat_d) hipFree(e->pstat_d);
+    hipFree(e->sv.rec);
+    hipFree(e->sv.hash);
+    hipFree(e->sv.perm);
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
     if (e->plan_h) hipHostFree(e->plan_h);
@@ -453,7 +476,8 @@ int ipxg_destroy(ipxg_engine* e) {
                       &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
-                      &e->ipf_tot, &e->ipf_off, &e->ipf_msg, &e->ipf_plan})
+                      &e->ipf_tot, &e->ipf_off, &e->ipf_msg, &e->ipf_plan, &e->st_pkt, &e->st_crec, &e->st_keyed,
+                      &e->st_qx, &e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2, &e->st_start, &e->st_evpos})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -491,6 +515,93 @@ static int complete_batch(ipxg_engine* e) {
     return post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, false);
 }
 
+// The fragmentation cache over the batch's nf listed fragments (fragmentationCache.cpp):
+// ordered by (bucket, arrival), each bucket's ring replayed; the ports land in frag_ports.
+static int frag_replay(ipxg_engine* e, const BatchView& bv, const Params& p, uint32_t nf) {
+    int rc;
+    if ((rc = ensure(e, e->frag_sorted, (size_t)nf * 8))) return rc;
+    size_t tb = 0;
+    HIPCHK(e, sort_keys_u64(nullptr, tb, nullptr, nullptr, nf, 64, e->st));
+    if ((rc = ensure(e, e->sort_tmp, tb))) return rc;
+    FragView fv = frag_view(e);
+    tb = e->sort_tmp.bytes;
+    HIPCHK(e, sort_keys_u64(e->sort_tmp.p, tb, fv.list, fv.sorted, nf, 64, e->st));
+    launch_frag_walk(e->st, bv, p, fv, nf, e->stats_d);
+    HIPCHK(e, hipGetLastError());
+    return IPXG_OK;
+}
+
+// Strict mode: one batch through the reference's line table (ipxg_strict.hip), synchronously.
+static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
+    int rc;
+    const Params p = params(e);
+    const uint64_t m = 3ull * n;  // events: forward, inverse and sweep line per packet
+    if (e->cfg.frag_enable) {
+        if ((rc = ensure(e, e->frag_list, (size_t)n * 8))) return rc;
+        if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
+    }
+    if ((rc = ensure(e, e->st_pkt, (size_t)n * sizeof(StrictPkt)))) return rc;
+    if ((rc = ensure(e, e->st_crec, (size_t)n * sizeof(ipxg_flow_record)))) return rc;
+    if ((rc = ensure(e, e->st_keyed, (size_t)n * 4))) return rc;
+    if ((rc = ensure(e, e->st_qx, (size_t)n * 4))) return rc;
+    for (DevBuf* b : {&e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2})
+        if ((rc = ensure(e, *b, m * 4))) return rc;
+    if ((rc = ensure(e, e->st_start, (size_t)e->sv.lines * 4))) return rc;
+    if ((rc = ensure(e, e->st_evpos, (size_t)n * 16))) return rc;
+    // every record alive now plus every record this batch creates may leave during it
+    if ((rc = ensure_export(e, (size_t)e->sv.slot_mask + 1 + n))) return rc;
+    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+    ev_rec(e, 0);
+    launch_strict_prep1(e->st, bv, p, frag_view(e), e->ctl_d, e->stats_d);
+    HIPCHK(e, hipGetLastError());
+    if (e->cfg.frag_enable) {
+        if ((rc = sync_ctl(e))) return rc;
+        const uint32_t nf = e->ctl_h->frag_count;
+        if (nf && (rc = frag_replay(e, bv, p, nf))) return rc;
+    }
+    StrictPkt* sp = (StrictPkt*)e->st_pkt.p;
+    ipxg_flow_record* crec = (ipxg_flow_record*)e->st_crec.p;
+    uint32_t* keyed = (uint32_t*)e->st_keyed.p;
+    uint32_t* qx = (uint32_t*)e->st_qx.p;
+    launch_strict_prep2(e->st, bv, p, frag_view(e), sp, crec, keyed);
+    HIPCHK(e, hipGetLastError());
+    size_t tb = 0, tb2 = 0;
+    int bits = 1;
+    while ((1ull << bits) <= e->sv.lines) bits++;  // line numbers and the no-event key (lines)
+    HIPCHK(e, exclusive_scan_u32(nullptr, tb, keyed, qx, n, e->st));
+    HIPCHK(e, sort_pairs_u32(nullptr, tb2, nullptr, nullptr, nullptr, nullptr, (uint32_t)m, bits, e->st));
+    if ((rc = ensure(e, e->sort_tmp, std::max(tb, tb2)))) return rc;
+    tb = e->sort_tmp.bytes;
+    HIPCHK(e, exclusive_scan_u32(e->sort_tmp.p, tb, keyed, qx, n, e->st));
+    uint32_t *ks = (uint32_t*)e->st_keys.p, *vs = (uint32_t*)e->st_vals.p;
+    uint32_t *ks2 = (uint32_t*)e->st_keys2.p, *vs2 = (uint32_t*)e->st_vals2.p;
+    launch_strict_events(e->st, e->sv, sp, keyed, qx, n, e->strict_q, p.split_biflow, ks, vs);
+    HIPCHK(e, hipGetLastError());
+    tb = e->sort_tmp.bytes;
+    HIPCHK(e, sort_pairs_u32(e->sort_tmp.p, tb, ks, ks2, vs, vs2, (uint32_t)m, bits, e->st));
+    uint32_t* evpos = (uint32_t*)e->st_evpos.p;
+    launch_strict_positions(e->st, ks2, vs2, (uint32_t)m, e->sv.lines, (uint32_t*)e->st_start.p, evpos);
+    launch_strict_walk(e->st, e->sv, p, sp, crec, keyed, qx, evpos, n, e->strict_q, export_view(e), e->ctl_d,
+                       e->stats_d);
+    HIPCHK(e, hipGetLastError());
+    ev_rec(e, 1);
+    uint32_t tail[2] = {0, 0};  // the last packet's keyed rank and mark: keyed packets in the batch
+    HIPCHK(e, hipMemcpyAsync(&tail[0], qx + n - 1, 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(&tail[1], keyed + n - 1, 4, hipMemcpyDeviceToHost, e->st));
+    if ((rc = sync_ctl(e))) return rc;
+    if (e->ctl_h->strict_fail) return set_err(e, IPXG_EDEVICE, "strict replay stalled (engine bug)");
+    if (e->prof) {
+        e->tm.ingest_ms += ev_ms(e, 0);
+        e->tm.ingest_launches++;
+        e->tm.ingest_packets += n;
+    }
+    e->strict_q += (uint64_t)tail[0] + tail[1];
+    e->live = (uint32_t)((int64_t)e->live + e->ctl_h->strict_live);
+    e->keys = e->live;
+    e->batches++;
+    return IPXG_OK;
+}
+
 int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     if (!e || !batch) return IPXG_EINVAL;
     const uint32_t n = batch->n;
@@ -501,7 +612,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     int rc;
     const bool binned = !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST);
     const bool dev_batch = (batch->flags & IPXG_BATCH_DEVICE) != 0;
-    const bool async = (batch->flags & IPXG_BATCH_ASYNC) && binned;
+    const bool async = (batch->flags & IPXG_BATCH_ASYNC) && binned && !e->strict;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     BatchView bv;
     bv.n = n;
@@ -545,6 +656,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         bv.desc = (const ipxg_pkt_desc*)e->desc.p;
     }
     bv.base_sec = BASE_FROM_DESC0;  // kernels read desc[0] themselves (no host round trip)
+    if (e->strict) return strict_submit(e, bv, n);
     // per-batch scratch sized for the worst case (every packet deferred / a fragment)
     if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
     if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
@@ -884,7 +996,7 @@ int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
         return set_err(e, IPXG_EINVAL, "plugin rule: too many ports or prefixes");
     for (uint32_t q = 0; q < pl->n_prefixes; ++q)
         if (pl->prefix_len[q] > IPXG_PLUGIN_PREFIX_LEN) return set_err(e, IPXG_EINVAL, "plugin rule: prefix too long");
-    if (e->cfg.flags & IPXG_CFG_ATOMIC_INGEST)
+    if (e->cfg.flags & (IPXG_CFG_ATOMIC_INGEST | IPXG_CFG_STRICT))
         return set_err(e, IPXG_EINVAL, "process plugins need the binned ingest");
     {
         const int rc0 = complete_batch(e);
@@ -935,15 +1047,8 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         if (!slow) ev_rec(e, 5);
         slow = true;
         const uint32_t nf = c1.frag_count;
-        if ((rc = ensure(e, e->frag_sorted, (size_t)nf * 8))) return rc;
-        size_t tb = 0;
-        HIPCHK(e, sort_keys_u64(nullptr, tb, nullptr, nullptr, nf, 64, e->st));
-        if ((rc = ensure(e, e->sort_tmp, tb))) return rc;
+        if ((rc = frag_replay(e, bv, p, nf))) return rc;
         fv = frag_view(e);
-        tb = e->sort_tmp.bytes;
-        HIPCHK(e, sort_keys_u64(e->sort_tmp.p, tb, fv.list, fv.sorted, nf, 64, e->st));
-        launch_frag_walk(e->st, bv, p, fv, nf, e->stats_d);
-        HIPCHK(e, hipGetLastError());
         launch_frag_accumulate(e->st, bv, p, table_view(e), fv, nf, e->ctl_d, (uint32_t*)e->defer_a.p);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
@@ -1094,6 +1199,18 @@ int ipxg_expire(ipxg_engine* e, int64_t now_sec) {
     }
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (e->strict) {  // the reference's export_expired(now): one sweep step (cache.cpp:508-523)
+        if ((rc = ensure_export(e, 16))) return rc;
+        HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+        if (e->sv.line_bits) launch_strict_expire(e->st, e->sv, params(e), e->strict_q, now_sec, export_view(e), e->ctl_d,
+                                                  e->stats_d);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        e->strict_q++;
+        e->live = (uint32_t)((int64_t)e->live + e->ctl_h->strict_live);
+        e->keys = e->live;
+        return IPXG_OK;
+    }
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
     launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d);
     HIPCHK(e, hipGetLastError());
@@ -1109,6 +1226,17 @@ int ipxg_finish(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (e->strict) {  // finish (cache.cpp:276-288): every record FORCED
+        if ((rc = ensure_export(e, e->live))) return rc;
+        HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+        launch_strict_finish(e->st, e->sv, export_view(e), e->ctl_d, e->stats_d);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        e->live = (uint32_t)((int64_t)e->live + e->ctl_h->strict_live);
+        if (e->live) return set_err(e, IPXG_EDEVICE, "strict finish left records (engine bug)");
+        e->keys = 0;
+        return IPXG_OK;
+    }
     if (e->inflight.on) {
         // The batch's k_fin_list is still to be launched: into a table that was empty before
         // the batch, it exports what it finalises itself (fused finish, no table scan).
@@ -1177,6 +1305,11 @@ int ipxg_reset(ipxg_engine* e) {
     }
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
+    if (e->strict) {
+        launch_strict_clear(e->st, e->sv);
+        HIPCHK(e, hipGetLastError());
+        e->strict_q = 0;
+    }
     const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
     HIPCHK(e, hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st));
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
@@ -1660,7 +1793,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->fragmented_packets = s[ST_FRAGMENTED];
     out->fragments_filled = s[ST_FRAG_FILLED];
     out->complex_flows = e->complex_total;
-    out->table_capacity = e->cap;
+    out->table_capacity = e->strict ? (uint64_t)e->sv.slot_mask + 1 : e->cap;
     out->table_rehashes = e->rehashes;
     out->batches = e->batches;
     out->spilled_packets = e->spilled;

@@ -405,13 +405,6 @@ __device__ __forceinline__ void tile_aggregate(const BinLds& L, uint32_t pmask, 
     for (uint32_t a = tid; a < na; a += IPXG_BLOCK) L.agg[a].rank = atomicAdd(&L.hist[L.agg[a].part], 3u);
 }
 
-__device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& p, const FragView& f, BatchCtl* ctl,
-                                                uint32_t i) {
-    const uint32_t bucket = (uint32_t)(frag_key_hash(pk) % (uint64_t)p.frag_size);
-    const uint32_t pos = atomicAdd(&ctl->frag_count, 1u);
-    f.list[pos] = ((uint64_t)bucket << 24) | i;
-}
-
 // Every packet of the batch, in tiles of BIN_K x 256, parsed in registers by parse_fast
 // from buffer loads software-pipelined across the tiles (below).  Frames the register parser
 // does not take go to the slow list for k_bin_slow.  No LDS header staging here: LDS holds

@@ -59,6 +59,8 @@ struct BatchCtl {
     uint32_t walked;         // wide walk: packets of its extra shapes (variant choice)
     uint32_t fused;          // k_fin_list exported and emptied the flows it finalised (finish fused)
     uint32_t plugin_fail;    // k_classify found no slot for a plugin flow (table too full)
+    int32_t strict_live;     // strict mode: records created - records exported
+    uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
     uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -117,6 +119,28 @@ struct Params {
     uint32_t tile_agg;       // k_bin / k_bin_slow aggregate frequent flows per tile (skewed traffic)
     uint32_t wide;           // k_bin's wide walk (96-byte loads, parse_medium)
 };
+
+// ---- strict mode (ipxg_strict.hip): the reference's line table -------------------------------
+struct StrictView {
+    ipxg_flow_record* rec;  // 2^s records, [line << line_bits | slot]
+    uint64_t* hash;         // their FlowRecord::m_hash (0 = empty)
+    uint64_t* perm;         // per line: position j -> record slot, bits 4j..4j+3
+    uint32_t line_bits;     // l= (line size 2^l, at most 16)
+    uint32_t lines;         // 2^s >> l
+    uint32_t slot_mask;     // 2^s - 1
+};
+struct StrictPkt {          // what put_pkt_recursive reads of a keyed packet (h_fwd 0: not keyed)
+    uint64_t h_fwd, h_inv;
+    uint32_t ts_sec, ts_usec;
+    uint16_t ip_len;
+    uint8_t tcp_flags, ip_proto;
+    uint32_t pad;
+};
+static_assert(sizeof(StrictPkt) == 32, "");
+constexpr uint32_t STRICT_LANES = 1024;          // the replay's one workgroup
+constexpr uint32_t STRICT_MAX_LINES = 32768;     // per-line counters in its LDS (128 KiB)
+constexpr uint32_t STRICT_NONE = 0xFFFFFFFFu;
+constexpr uint32_t STRICT_SPIN_MAX = 1u << 24;   // rounds a lane may wait before giving up
 
 struct BatchView {
     const uint8_t* arena;
@@ -278,6 +302,27 @@ void launch_xxh64(hipStream_t st, const uint8_t* keys, uint32_t keylen, uint32_t
                   uint64_t* out);
 
 // rocPRIM radix sort of 64-bit keys (slow paths only).  temp may be null to query size.
+hipError_t sort_pairs_u32(void* temp, size_t& temp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                          uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
+hipError_t exclusive_scan_u32(void* temp, size_t& temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
+                              hipStream_t st);
+void launch_strict_prep1(hipStream_t st, const BatchView& b, const Params& p, FragView f, BatchCtl* ctl,
+                         unsigned long long* stats);
+void launch_strict_prep2(hipStream_t st, const BatchView& b, const Params& p, FragView f, StrictPkt* sp,
+                         ipxg_flow_record* crec, uint32_t* keyed);
+void launch_strict_events(hipStream_t st, StrictView v, const StrictPkt* sp, const uint32_t* keyed,
+                          const uint32_t* qx, uint32_t n, uint64_t q_base, uint32_t split, uint32_t* keys,
+                          uint32_t* vals);
+void launch_strict_positions(hipStream_t st, const uint32_t* keys, const uint32_t* vals, uint32_t m, uint32_t lines,
+                             uint32_t* start, uint32_t* evpos);
+void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const StrictPkt* sp,
+                        const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx,
+                        const uint32_t* evpos, uint32_t n, uint64_t q_base, ExportView ex, BatchCtl* ctl,
+                        unsigned long long* stats);
+void launch_strict_expire(hipStream_t st, StrictView v, const Params& p, uint64_t q, int64_t now, ExportView ex,
+                          BatchCtl* ctl, unsigned long long* stats);
+void launch_strict_finish(hipStream_t st, StrictView v, ExportView ex, BatchCtl* ctl, unsigned long long* stats);
+void launch_strict_clear(hipStream_t st, StrictView v);
 hipError_t sort_keys_u64(void* temp, size_t& temp_bytes, const uint64_t* in, uint64_t* out,
                          uint32_t n, int end_bit, hipStream_t st);
 

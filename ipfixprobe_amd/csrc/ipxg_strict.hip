@@ -1,0 +1,462 @@
+// ipxg_strict.hip -- strict mode (strict=true): the reference's own flow table, bit for bit.
+//
+// NHTFlowCache (cache.cpp:322-523) keeps 2^s records in lines of L = 2^l (default 16): a packet
+// looks for its flow in the line of XXH64(key), then in the line of XXH64(inverse key); a hit
+// moves to the line's front; a miss takes the line's first empty position or, in a full line,
+// evicts the last one (FLOW_END_NO_RES) and inserts at position L/2; after every keyed packet
+// a sweep cursor exports the idle records of the next L/2 positions of the table.  The result
+// depends on the order of every packet that touches a line, which is why the default engine
+// (order-independent batch reductions into a growing table) is exact only while no line
+// overflows.  This mode replays those rules exactly, on the device:
+//
+//   k_strict_prep1   parse (statistics), fragments listed for the fragmentation cache (the
+//                    engine then replays it: k_frag_walk) and the keyed packets marked;
+//   (scan)           keyed prefix -> each keyed packet's sweep step q (cursor = q * L/2);
+//   k_strict_prep2   re-parse with the fragment ports: both hashes, the update fields and the
+//                    record the packet would create (FlowRecord::create, cache.cpp:94-132);
+//   k_strict_events  a keyed packet is an event on up to three lines: its forward line, its
+//                    inverse line and the line its sweep visits;
+//   (sort)           events by line, stably: each event's position in its line's sequence;
+//   k_strict_walk    the replay.  Packets are taken in index order by the 1024 lanes of ONE
+//                    workgroup; a lane processes its packet once every line it touches has
+//                    processed all earlier events (per-line counters in LDS), so every line sees
+//                    exactly the reference's sequence of operations while packets touching
+//                    disjoint lines proceed in parallel.  One workgroup: its lanes share one L1
+//                    and LDS, so the hand-off between two packets of a line needs only
+//                    workgroup-scope ordering (no cross-CU release/acquire).
+// The state: records [line * L + slot], their hashes (FlowRecord::m_hash, 0 = empty) and per
+// line the position -> slot permutation (4 bits per position) standing in for the
+// reference's pointer array m_flow_table: moves and evictions rewrite one 64-bit word.
+#include "ipxg_table.hpp"
+
+namespace ipxg {
+
+// ---- parse, statistics, fragments, keyed marks -------------------------------------------------
+__global__ __launch_bounds__(IPXG_BLOCK) void k_strict_prep1(BatchView b, Params p, FragView f, BatchCtl* ctl,
+                                                             unsigned long long* stats) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    __shared__ uint32_t sc[ST_COUNT];
+    const uint32_t tid = threadIdx.x;
+    if (tid < ST_COUNT) sc[tid] = 0;
+    __syncthreads();
+    ParseCounts c = {};
+    uint32_t keyless = 0, frags = 0;
+    uint32_t* col = &win[tid];
+    for (uint32_t i = blockIdx.x * IPXG_BLOCK + tid; i < b.n; i += gridDim.x * IPXG_BLOCK) {
+        const ipxg_pkt_desc d = b.desc[i];
+        stage_frame(col, b.arena, d.offset, d.caplen);
+        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        DevPkt pk;
+        if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
+        if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
+            keyless++;
+            continue;
+        }
+        if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
+            frags++;
+            divert_fragment(pk, p, f, ctl, i);
+        }
+    }
+    flush_counts(c, keyless, frags, sc);
+    flush_block_stats(sc, stats);
+}
+
+// every keyed packet's update fields, the record it would create, and its keyed mark
+__global__ __launch_bounds__(IPXG_BLOCK) void k_strict_prep2(BatchView b, Params p, FragView f, StrictPkt* sp,
+                                                             ipxg_flow_record* crec, uint32_t* keyed) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    uint32_t* col = &win[threadIdx.x];
+    for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
+        DevPkt pk;
+        ipxg_pkt_desc d;
+        StrictPkt s = {};
+        const bool ok = reparse_lds<false>(b, p, f, i, col, pk, d) && (pk.ip_version == 4 || pk.ip_version == 6);
+        if (ok) {
+            FlowKey kf, ki;
+            build_keys(pk, kf, ki);
+            s.h_fwd = key_hash(kf);
+            s.h_inv = key_hash(ki);
+            s.ts_sec = d.ts_sec;
+            s.ts_usec = d.ts_usec;
+            s.ip_len = pk.ip_len;
+            s.tcp_flags = pk.tcp_flags;
+            s.ip_proto = pk.ip_proto;
+            ipxg_flow_record r;
+            rec_create(r, pk, d, s.h_fwd, 0);
+            r.src_packets = 1;  // FlowRecord::create, cache.cpp:96-126
+            r.src_bytes = pk.ip_len;
+            if (pk.ip_proto == 6) r.src_tcp_flags = pk.tcp_flags;
+            crec[i] = r;
+        }
+        sp[i] = s;
+        keyed[i] = ok ? 1u : 0u;
+    }
+}
+
+// Lines of packet i's events: forward, inverse (not split, not the forward line), and the line
+// its sweep visits (not one of those); NONE = no event.  Sweep step q = q_base + its rank
+// among the keyed packets (qx).
+__device__ __forceinline__ void strict_lines(const StrictView& v, const StrictPkt& s, uint64_t q, uint32_t split,
+                                             uint32_t (&ln)[3]) {
+    const uint32_t mask = v.slot_mask & ~((1u << v.line_bits) - 1u);
+    ln[0] = (uint32_t)(s.h_fwd & mask) >> v.line_bits;
+    ln[1] = split ? STRICT_NONE : (uint32_t)(s.h_inv & mask) >> v.line_bits;
+    if (ln[1] == ln[0]) ln[1] = STRICT_NONE;
+    const uint32_t half = (1u << v.line_bits) >> 1;
+    ln[2] = half ? (uint32_t)((q * half) & v.slot_mask) >> v.line_bits : STRICT_NONE;
+    if (ln[2] == ln[0] || ln[2] == ln[1]) ln[2] = STRICT_NONE;
+}
+
+__global__ __launch_bounds__(256) void k_strict_events(StrictView v, const StrictPkt* sp, const uint32_t* keyed,
+                                                       const uint32_t* qx, uint32_t n, uint64_t q_base,
+                                                       uint32_t split, uint32_t* keys, uint32_t* vals) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t ln[3] = {STRICT_NONE, STRICT_NONE, STRICT_NONE};
+    if (keyed[i]) strict_lines(v, sp[i], q_base + qx[i], split, ln);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        keys[3 * i + j] = ln[j] == STRICT_NONE ? v.lines : ln[j];  // v.lines sorts after every line
+        vals[3 * i + j] = 4 * i + j;
+    }
+}
+
+// position of each event in its line's (index-ordered) sequence
+__global__ __launch_bounds__(256) void k_strict_starts(const uint32_t* keys, uint32_t m, uint32_t lines,
+                                                       uint32_t* start) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t k = keys[i];
+    if (k < lines && (i == 0 || keys[i - 1] != k)) start[k] = i;
+}
+
+__global__ __launch_bounds__(256) void k_strict_pos(const uint32_t* keys, const uint32_t* vals, uint32_t m,
+                                                    uint32_t lines, const uint32_t* start, uint32_t* evpos) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t k = keys[i];
+    if (k < lines) evpos[vals[i]] = i - start[k];
+}
+
+// ---- the line permutation ---------------------------------------------------------------------
+__device__ __forceinline__ uint32_t nib(uint64_t perm, uint32_t j) { return (uint32_t)(perm >> (4 * j)) & 15u; }
+__device__ __forceinline__ uint64_t below(uint32_t j) { return j >= 16 ? ~0ull : ((1ull << (4 * j)) - 1ull); }
+// the record at position a moves to position b <= a; positions b..a-1 move up by one
+__device__ __forceinline__ uint64_t perm_move(uint64_t perm, uint32_t a, uint32_t b) {
+    const uint64_t r = nib(perm, a);
+    const uint64_t keep = perm & ~(below(a + 1) & ~below(b));
+    const uint64_t seg = perm & below(a) & ~below(b);
+    return keep | (seg << 4) | (r << (4 * b));
+}
+
+struct LineImg {
+    uint64_t perm;
+    uint64_t h[16];  // by record slot
+};
+
+__device__ __forceinline__ void load_line(const StrictView& v, uint32_t line, LineImg& li) {
+    const uint32_t L = 1u << v.line_bits;
+    li.perm = v.perm[line];
+    const uint64_t* hp = v.hash + (size_t)line * L;
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) li.h[r] = r < L ? hp[r] : 0;
+}
+
+// positions whose record has hash h (bit j = position j)
+__device__ __forceinline__ uint32_t match_pos(const LineImg& li, uint32_t L, uint64_t h) {
+    uint32_t rm = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r)
+        if (r < L && li.h[r] == h) rm |= 1u << r;
+    uint32_t pm = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)
+        if (j < L && ((rm >> nib(li.perm, j)) & 1u)) pm |= 1u << j;
+    return pm;
+}
+
+// ---- the replay --------------------------------------------------------------------------------
+struct WalkCtx {
+    StrictView v;
+    ExportView ex;
+    uint32_t* sc;        // block counters (LDS)
+    int32_t live;        // records created - exported (this lane)
+    uint32_t inactive, active;
+};
+
+// export_flow (cache.cpp:262-274): the record leaves with its reason, its slot becomes empty
+__device__ __forceinline__ void strict_export(WalkCtx& w, uint32_t slot, const ipxg_flow_record& r, uint8_t reason) {
+    const uint32_t pos = atomicAdd(w.ex.count, 1u);
+    store_export(w.ex, pos, r, reason);
+    if (w.ex.count6 && r.ip_version == 6) atomicAdd(w.ex.count + 2, 1u);
+    count_export(w.sc, r, reason);
+    w.v.hash[slot] = 0;
+    w.live--;
+}
+
+// export_expired (cache.cpp:508-523) at sweep step q: positions [q * L/2, +L/2) of the table
+__device__ void strict_sweep(WalkCtx& w, uint64_t q, int64_t ts) {
+    const StrictView& v = w.v;
+    const uint32_t L = 1u << v.line_bits, half = L >> 1;
+    const uint32_t at = (uint32_t)((q * half) & v.slot_mask);
+    const uint32_t line = at >> v.line_bits, off = at & (L - 1u);
+    const uint64_t perm = v.perm[line];
+    for (uint32_t j = off; j < off + half; ++j) {
+        const uint32_t slot = line * L + nib(perm, j);
+        if (v.hash[slot] == 0) continue;
+        const ipxg_flow_record r = v.rec[slot];
+        if (ts - (int64_t)r.time_last_sec >= (int64_t)w.inactive) strict_export(w, slot, r, export_reason(r));
+    }
+}
+
+// put_pkt_recursive (cache.cpp:330-491) for one keyed packet, its sweep included
+__device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_record* crec_i, uint64_t q,
+                              uint32_t split) {
+    const StrictView& v = w.v;
+    const uint32_t L = 1u << v.line_bits, half = L >> 1;
+    uint32_t ln[3];
+    strict_lines(v, s, q, split, ln);
+    const uint32_t lf = ln[0];
+    const uint32_t li_line = split ? lf : (uint32_t)(s.h_inv & (v.slot_mask & ~(L - 1u))) >> v.line_bits;
+    for (int depth = 0; depth < 8; ++depth) {  // the recursion after an export (at most twice)
+        LineImg F;
+        load_line(v, lf, F);
+        uint32_t line = lf, pos = 0;
+        bool found = false, src = true;
+        uint64_t perm = F.perm;
+        uint32_t pm = match_pos(F, L, s.h_fwd);
+        if (pm) {
+            found = true;
+            pos = __builtin_ctz(pm);
+        } else if (!split) {
+            LineImg I;
+            load_line(v, li_line, I);
+            pm = match_pos(I, L, s.h_inv);
+            if (pm) {
+                found = true;
+                src = false;
+                line = li_line;
+                pos = __builtin_ctz(pm);
+                perm = I.perm;
+            }
+        }
+        if (found) {  // move to the line's front (:375-391)
+            perm = perm_move(perm, pos, 0);
+            v.perm[line] = perm;
+            pos = 0;
+        } else {
+            const uint32_t em = match_pos(F, L, 0);
+            if (em) {
+                pos = __builtin_ctz(em);
+            } else {  // line full: the last position leaves (NO_RES), its slot re-enters at L/2 (:400-419)
+                const uint32_t slot = lf * L + nib(perm, L - 1);
+                const ipxg_flow_record ev = v.rec[slot];
+                strict_export(w, slot, ev, IPXG_FLOW_END_NO_RES);
+                perm = perm_move(perm, L - 1, half);
+                v.perm[lf] = perm;
+                pos = half;
+            }
+        }
+        const uint32_t slot = line * L + nib(perm, pos);
+        if (!found) {  // FlowRecord::create (:440-443)
+            ipxg_flow_record r = *crec_i;
+            v.rec[slot] = r;
+            v.hash[slot] = s.h_fwd;
+            w.live++;
+            break;
+        }
+        ipxg_flow_record r = v.rec[slot];
+        const uint8_t flw = src ? r.src_tcp_flags : r.dst_tcp_flags;
+        if ((s.tcp_flags & 0x02) && (flw & 0x05)) {  // SYN after FIN/RST (:431-438)
+            strict_export(w, slot, r, IPXG_FLOW_END_EOF);
+            continue;
+        }
+        if ((int64_t)s.ts_sec - (int64_t)r.time_last_sec >= (int64_t)w.inactive) {  // :453-461
+            strict_export(w, slot, r, export_reason(r));
+            continue;
+        }
+        if ((int64_t)s.ts_sec - (int64_t)r.time_first_sec >= (int64_t)w.active) {  // :464-472
+            strict_export(w, slot, r, IPXG_FLOW_END_ACTIVE);
+            continue;
+        }
+        r.time_last_sec = s.ts_sec;  // FlowRecord::update (:134-152)
+        r.time_last_usec = s.ts_usec;
+        if (src) {
+            r.src_packets++;
+            r.src_bytes += s.ip_len;
+            if (s.ip_proto == 6) r.src_tcp_flags |= s.tcp_flags;
+        } else {
+            r.dst_packets++;
+            r.dst_bytes += s.ip_len;
+            if (s.ip_proto == 6) r.dst_tcp_flags |= s.tcp_flags;
+        }
+        v.rec[slot] = r;
+        break;
+    }
+    // export_expired (:508-523): positions [q * L/2, +L/2) of the table, idle against this packet
+    if (half) strict_sweep(w, q, (int64_t)s.ts_sec);
+}
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// One workgroup: lane t takes packets t, t + 1024, ...; see the file comment.  A lane whose
+// lines are not ready spins (bounded: a lane that waits STRICT_SPIN_MAX rounds in a row gives up
+// and flags ctl->strict_fail -- the replay cannot deadlock, the bound guards engine bugs).
+__global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Params p, const StrictPkt* sp,
+                                                              const ipxg_flow_record* crec, const uint32_t* keyed,
+                                                              const uint32_t* qx, const uint32_t* evpos, uint32_t n,
+                                                              uint64_t q_base, ExportView ex, BatchCtl* ctl,
+                                                              unsigned long long* stats) {
+    __shared__ uint32_t ctr[STRICT_MAX_LINES];
+    __shared__ uint32_t sc[ST_COUNT];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t l = tid; l < v.lines; l += STRICT_LANES) ctr[l] = 0;
+    if (tid < ST_COUNT) sc[tid] = 0;
+    __syncthreads();
+    WalkCtx w{v, ex, sc, 0, p.inactive_s, p.active_s};
+    uint32_t spins = 0;
+    bool failed = false;
+    // this lane's next keyed packet: its fields, sweep step, lines and event positions
+    uint32_t k = tid;
+    StrictPkt s = {};
+    uint64_t q = 0;
+    uint32_t ln[3] = {STRICT_NONE, STRICT_NONE, STRICT_NONE}, want[3] = {0, 0, 0};
+    auto advance = [&](uint32_t from) {
+        while (from < n && !keyed[from]) from += STRICT_LANES;
+        k = from;
+        if (k >= n) return;
+        s = sp[k];
+        q = q_base + qx[k];
+        strict_lines(v, s, q, p.split_biflow, ln);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) want[j] = ln[j] == STRICT_NONE ? 0 : evpos[4 * k + j];
+    };
+    advance(tid);
+    while (__any(k < n)) {
+        bool progressed = false;
+        if (k < n) {
+            bool ready = true;
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                if (ln[j] != STRICT_NONE && lds_ld(&ctr[ln[j]]) != want[j]) ready = false;
+            if (ready) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                strict_packet(w, s, crec + k, q, p.split_biflow);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's table stores are done
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    if (ln[j] != STRICT_NONE)
+                        __hip_atomic_store(&ctr[ln[j]], want[j] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                advance(k + STRICT_LANES);
+                progressed = true;
+                spins = 0;
+            } else if (++spins > STRICT_SPIN_MAX) {
+                failed = true;
+                k = n;  // give up (engine bug): the host reports it
+            }
+        }
+        if (!__any(progressed)) __builtin_amdgcn_s_sleep(2);
+    }
+    if (failed) atomicOr(&ctl->strict_fail, 1u);
+    if (w.live) atomicAdd(&ctl->strict_live, w.live);
+    flush_block_stats(sc, stats);
+}
+
+// ipxg_expire in strict mode: one export_expired call (cache.cpp:508-523) at `now`, sweep step q
+__global__ void k_strict_expire(StrictView v, Params p, uint64_t q, int64_t now, ExportView ex, BatchCtl* ctl,
+                                unsigned long long* stats) {
+    __shared__ uint32_t sc[ST_COUNT];
+    if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        WalkCtx w{v, ex, sc, 0, p.inactive_s, p.active_s};
+        strict_sweep(w, q, now);
+        if (w.live) atomicAdd(&ctl->strict_live, w.live);
+    }
+    flush_block_stats(sc, stats);
+}
+
+// finish (cache.cpp:276-288): every record FORCED, the table emptied
+__global__ __launch_bounds__(256) void k_strict_finish(StrictView v, ExportView ex, BatchCtl* ctl,
+                                                       unsigned long long* stats) {
+    __shared__ uint32_t sc[ST_COUNT];
+    if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    __syncthreads();
+    WalkCtx w{v, ex, sc, 0, 0, 0};
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s <= v.slot_mask; s += gridDim.x * 256) {
+        if (v.hash[s] == 0) continue;
+        const ipxg_flow_record r = v.rec[s];
+        strict_export(w, s, r, IPXG_FLOW_END_FORCED);
+    }
+    if (w.live) atomicAdd(&ctl->strict_live, w.live);
+    flush_block_stats(sc, stats);
+}
+
+// the identity permutation of every line, every record empty
+__global__ __launch_bounds__(256) void k_strict_clear(StrictView v) {
+    const uint32_t L = 1u << v.line_bits;
+    uint64_t id = 0;
+    for (uint32_t j = 0; j < L; ++j) id |= (uint64_t)j << (4 * j);
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s <= v.slot_mask; s += gridDim.x * 256) {
+        v.hash[s] = 0;
+        if (s < v.lines) v.perm[s] = id;
+    }
+}
+
+// ---- launchers -----------------------------------------------------------------------------------
+static uint32_t grid_for(uint32_t n, uint32_t block, uint32_t cap) {
+    uint32_t g = (n + block - 1) / block;
+    return g < 1 ? 1 : (g > cap ? cap : g);
+}
+
+void launch_strict_prep1(hipStream_t st, const BatchView& b, const Params& p, FragView f, BatchCtl* ctl,
+                         unsigned long long* stats) {
+    hipLaunchKernelGGL(k_strict_prep1, dim3(grid_for(b.n, IPXG_BLOCK, 2048)), dim3(IPXG_BLOCK), 0, st, b, p, f, ctl,
+                       stats);
+}
+
+void launch_strict_prep2(hipStream_t st, const BatchView& b, const Params& p, FragView f, StrictPkt* sp,
+                         ipxg_flow_record* crec, uint32_t* keyed) {
+    hipLaunchKernelGGL(k_strict_prep2, dim3(grid_for(b.n, IPXG_BLOCK, 2048)), dim3(IPXG_BLOCK), 0, st, b, p, f, sp,
+                       crec, keyed);
+}
+
+void launch_strict_events(hipStream_t st, StrictView v, const StrictPkt* sp, const uint32_t* keyed,
+                          const uint32_t* qx, uint32_t n, uint64_t q_base, uint32_t split, uint32_t* keys,
+                          uint32_t* vals) {
+    hipLaunchKernelGGL(k_strict_events, dim3((n + 255) / 256), dim3(256), 0, st, v, sp, keyed, qx, n, q_base, split,
+                       keys, vals);
+}
+
+void launch_strict_positions(hipStream_t st, const uint32_t* keys, const uint32_t* vals, uint32_t m, uint32_t lines,
+                             uint32_t* start, uint32_t* evpos) {
+    hipLaunchKernelGGL(k_strict_starts, dim3((m + 255) / 256), dim3(256), 0, st, keys, m, lines, start);
+    hipLaunchKernelGGL(k_strict_pos, dim3((m + 255) / 256), dim3(256), 0, st, keys, vals, m, lines, start, evpos);
+}
+
+void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const StrictPkt* sp,
+                        const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx,
+                        const uint32_t* evpos, uint32_t n, uint64_t q_base, ExportView ex, BatchCtl* ctl,
+                        unsigned long long* stats) {
+    hipLaunchKernelGGL(k_strict_walk, dim3(1), dim3(STRICT_LANES), 0, st, v, p, sp, crec, keyed, qx, evpos, n, q_base,
+                       ex, ctl, stats);
+}
+
+void launch_strict_expire(hipStream_t st, StrictView v, const Params& p, uint64_t q, int64_t now, ExportView ex,
+                          BatchCtl* ctl, unsigned long long* stats) {
+    hipLaunchKernelGGL(k_strict_expire, dim3(1), dim3(64), 0, st, v, p, q, now, ex, ctl, stats);
+}
+
+void launch_strict_finish(hipStream_t st, StrictView v, ExportView ex, BatchCtl* ctl, unsigned long long* stats) {
+    hipLaunchKernelGGL(k_strict_finish, dim3(grid_for(v.slot_mask + 1, 256, 1024)), dim3(256), 0, st, v, ex, ctl,
+                       stats);
+}
+
+void launch_strict_clear(hipStream_t st, StrictView v) {
+    hipLaunchKernelGGL(k_strict_clear, dim3(grid_for(v.slot_mask + 1, 256, 1024)), dim3(256), 0, st, v);
+}
+
+}  // namespace ipxg

@@ -414,6 +414,14 @@ __device__ __forceinline__ void apply_frag_ports(const Params& p, const FragView
     }
 }
 
+// a fragment for the fragmentation-cache path: (bucket << 24) | packet index
+__device__ __forceinline__ void divert_fragment(const DevPkt& pk, const Params& p, const FragView& f, BatchCtl* ctl,
+                                                uint32_t i) {
+    const uint32_t bucket = (uint32_t)(frag_key_hash(pk) % (uint64_t)p.frag_size);
+    const uint32_t pos = atomicAdd(&ctl->frag_count, 1u);
+    f.list[pos] = ((uint64_t)bucket << 24) | i;
+}
+
 // ---- register parser for the common frame shape -------------------------------------------
 // The common frame shape -- Ethernet (no VLAN tag), IPv4 with IHL 5, UDP or TCP without
 // options -- read straight from its first 48 bytes in registers: exactly the fields, checks

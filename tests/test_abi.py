@@ -55,7 +55,8 @@ def test_config_defaults_and_options():
     assert make_config("walk=wide").flags == 0x2 and make_config("walk=narrow").flags == 0x4
     assert make_config("ps=true").flags == 0x8 and make_config("parser-stats=true;ps=false").flags == 0
     assert make_config("walk=wide;walk=auto").flags == 0 and make_config("ingest=atomic;walk=wide").flags == 0x3
-    for bad in ("s=3", "s=31", "x=1", "fe=yes", "fs=0", "a=", "batch=0", "walk=deep", "ps=1"):
+    assert make_config("strict=true").flags == 0x10 and make_config("strict=true;strict=false").flags == 0
+    for bad in ("s=3", "s=31", "x=1", "fe=yes", "fs=0", "a=", "batch=0", "walk=deep", "ps=1", "strict=1"):
         with pytest.raises(IpxgError):
             make_config(bad)
 
