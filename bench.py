@@ -476,6 +476,9 @@ def main():
     ap.add_argument("--walk", default="auto", choices=["auto", "wide", "narrow"],
                     help="k_bin's header walk (auto: chosen per batch from the previous batch's mix)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host batch) rate")
+    ap.add_argument("--strict", type=int, default=None, metavar="S",
+                    help="strict mode with the reference's table of 2^S records (S=17: its default): "
+                         "its evictions and sweep replayed exactly (ipxg_strict.hip)")
     args = ap.parse_args()
     dflt = {"udp64": (10_000_000, 1, 100_000, 20), "imix": (10_000_000, 10, 1_000_000, 5),
             "quic": (5_000_000, 4, 1_000_000, 10)}[args.workload]
@@ -498,8 +501,12 @@ def main():
     from ipfixprobe_amd import Engine
     wl = make_workload(args, rank, world, device, local)
     torch.cuda.synchronize()
-    eng = Engine("s=%d;ingest=%s;walk=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest, args.walk),
-                 device_id=local)
+    if args.strict is not None:
+        wl.description += "; strict mode: the reference's table of 2^%d records in 16-way lines" % args.strict
+        eng = Engine("strict=true;s=%d" % args.strict, device_id=local)
+    else:
+        eng = Engine("s=%d;ingest=%s;walk=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest,
+                                                args.walk), device_id=local)
     cursor = [0]
     gather = ExportGather(eng, rank, world, device, wl.flows * 2) if world > 1 else None
 
@@ -524,7 +531,7 @@ def main():
         step()
     verify = None
     if args.verify and rank == 0 and wl.finish:
-        verify = verify_step(eng, wl)
+        verify = verify_step(eng, wl, args.strict)
     # timed region: HIP events around the ingest kernels only (k_bin, k_bin_slow); the
     # every-stage events cost ~35 us of host time per step, so the stage breakdown comes from a
     # separate pass below
@@ -563,7 +570,9 @@ def main():
     slow_ms = tm_in["ingest_slow_ms"] / launches
     alg_launch = alg_step / (wl.per_step if wl.finish else 1)
     kname = "k_bin" if args.ingest == "binned" else "k_ingest"
-    if args.ingest == "binned" and slow_ms > bin_ms:
+    if args.strict is not None:
+        kname = "strict (prep + sort + k_strict_walk)"
+    elif args.ingest == "binned" and slow_ms > bin_ms:
         kname, kms = "k_bin_slow", slow_ms
     else:
         kms = bin_ms
@@ -573,7 +582,8 @@ def main():
     step_gbs = alg_step * world / (step_ms / 1e3) / 1e9
     pmc = pmc_traffic(kname, wl.name if wl.name != "udp64-stream" else "stream")
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "udp64" and args.mode == "cold":
+    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "udp64" and args.mode == "cold" and \
+            args.strict is None:
         e2e = end_to_end(eng, wl.batches[0][0], wl.batches[0][1], wl.packets[0])
         e2e["pipelined"] = end_to_end_pipelined(eng, wl.batches[0][0], wl.batches[0][1], wl.packets[0])
     cpu = None
@@ -624,6 +634,8 @@ def main():
                        "stream_bytes_per_step": round(gather.bytes / max(gather.k, 1))} if gather is not None else None,
             "verify": verify,
             "cpu_baseline": cpu,
+            "strict": {"cache_exp": args.strict, "end_no_res_per_step": int(st["end_no_res"] // max(st["batches"], 1))}
+            if args.strict is not None else None,
         }
         print(json.dumps(line))
     eng.close()
@@ -631,7 +643,7 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def verify_step(eng, wl):
+def verify_step(eng, wl, strict=None):
     """One step of the workload against the oracle (the first batch only for multi-batch steps,
     in its own engine state): bit-exact flow records or the first differences."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -642,8 +654,9 @@ def verify_step(eng, wl):
     eng.finish()
     got = eng.poll()
     d = de.cpu().numpy().view(DESC_NP)
-    want, _ = oracle_py.run_capture(fr.cpu().numpy(), d, 1, cache_exp=min(30, int(math.ceil(math.log2(2 * wl.flows))) + 2))
-    diff = flowcmp.diff(got, want)
+    s = strict if strict is not None else min(30, int(math.ceil(math.log2(2 * wl.flows))) + 2)
+    want, _ = oracle_py.run_capture(fr.cpu().numpy(), d, 1, cache_exp=s)
+    diff = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + (["end_reason"] if strict is not None else []))
     return "%d records, %s" % (len(got), "bit-exact vs oracle" if not diff else diff[:500])
 
 
