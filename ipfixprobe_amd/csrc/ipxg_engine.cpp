@@ -62,6 +62,7 @@ struct ipxg_engine {
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t host_unreasoned = 0;  // counted exports without an end reason (total_exported only)
     std::vector<uint64_t> host_ports;  // 2 x 65536 when ps=true and plugins walk flows
     // staging for host batches
     DevBuf arena, desc;
@@ -729,6 +730,7 @@ struct WalkOut {
     std::vector<ipxg_flow_record> ex;  // exported records, in order
     uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
     uint64_t pkts[6] = {0, 0, 0, 0, 0, 0};  // FlowRecordStats buckets
+    uint64_t unreasoned = 0;  // export_flow with end_reason 0 (post_create FLUSH of a new record)
 };
 
 struct FlowWalk {
@@ -773,10 +775,12 @@ struct FlowWalk {
         o.reserved0 = 0;
         std::memset(o.reserved, 0, sizeof(o.reserved));
         out.ex.push_back(o);
-        if (counted && reason >= 1 && reason <= 5) {
-            out.end[reason - 1]++;
-            out.pkts[pkts_bucket((uint64_t)o.src_packets + o.dst_packets)]++;
-        }
+        // m_total_exported and update_flow_record_stats count every export_flow;
+        // update_flow_end_reason_stats ignores a reason outside 1..5 (cache.cpp:264-267,618-638)
+        if (!counted) return;
+        if (reason >= 1 && reason <= 5) out.end[reason - 1]++;
+        else out.unreasoned++;
+        out.pkts[pkts_bucket((uint64_t)o.src_packets + o.dst_packets)]++;
     }
     // FlowRecord::create (cache.cpp:94-132), the engine's record layout (rec_create)
     void create(const ipxg_parsed_pkt& k, const ipxg_packet_view& v) {
@@ -987,6 +991,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipStreamSynchronize(e->st));
     for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
     for (int k = 0; k < 6; ++k) e->host_pkts[k] += wo.pkts[k];
+    e->host_unreasoned += wo.unreasoned;
     return IPXG_OK;
 }
 
@@ -1788,7 +1793,7 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
     out->end_no_res = s[ST_END_NO_RES];
     out->flows_in_cache = e->live;
     out->total_exported = s[ST_END_INACTIVE] + s[ST_END_ACTIVE] + s[ST_END_EOF] + s[ST_END_FORCED] +
-                          s[ST_END_NO_RES];
+                          s[ST_END_NO_RES] + e->host_unreasoned;
     out->keyless_packets = s[ST_KEYLESS];
     out->fragmented_packets = s[ST_FRAGMENTED];
     out->fragments_filled = s[ST_FRAG_FILLED];

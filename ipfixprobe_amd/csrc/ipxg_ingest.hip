@@ -1140,18 +1140,20 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
                                                          unsigned long long* stats, uint32_t finishing) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     __shared__ uint32_t sc[ST_COUNT];
-    __shared__ uint32_t cnt[3];  // new live, complex, exported
+    __shared__ uint32_t cnt[4];  // new live, complex, exported, IPv6 exports
+    __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
+    __shared__ uint32_t ex_base;
     const uint32_t nf = ctl->fin_count;  // final: k_reduce has completed
     const bool fused = finishing && !(ctl->frag_count || ctl->deferred || ctl->agg_deferred || ctl->pending);
     if (blockIdx.x == 0 && threadIdx.x == 0) ctl->fused = fused ? 1u : 0u;
     if (blockIdx.x * IPXG_BLOCK >= nf) return;
     const uint32_t tid = threadIdx.x;
     if (tid < ST_COUNT) sc[tid] = 0;
-    if (tid < 3) cnt[tid] = 0;
+    if (tid < 4) cnt[tid] = 0;
     __syncthreads();
     const bool force_cx = p.force_complex || ctl->nonmono;
-    uint32_t n_live = 0, n_cx = 0, n_ex = 0;
-    for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {
+    uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0;
+    for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
         const uint32_t k = base + tid;
         bool do_export = false, fin_export = false;
         uint8_t reason = 0;
@@ -1166,28 +1168,37 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
             do_export = fr.do_export;
             reason = fr.reason;
         }
-        const uint32_t pos = wave_append(ex.count, do_export);
+        // one reservation in the export buffer per workgroup and pass (a returning atomic per
+        // wave on the one counter serialised ~1600 waves at ~12 ns each: MI355X_MICROARCH.md
+        // "fanin" / "dequeue")
+        const uint32_t mine = (do_export ? 1u : 0u) + (fin_export ? 1u : 0u);
+        uint32_t btot;
+        uint32_t pos = block_exclusive_scan<IPXG_BLOCK>(mine, scan_s, &btot);
+        if (btot == 0) continue;  // uniform
+        if (tid == 0) ex_base = atomicAdd(ex.count, btot);
+        __syncthreads();
+        pos += ex_base;
         if (do_export) {
-            store_export(ex, pos, er, reason);
+            store_export(ex, pos++, er, reason);
             count_export(sc, er, reason);
             n_ex++;
+            n_v6 += er.ip_version == 6 ? 1 : 0;
         }
-        count_v6_exports(ex, do_export && er.ip_version == 6);
-        if (fused) {  // uniform
-            const uint32_t pf = wave_append(ex.count, fin_export);
-            if (fin_export) {
-                store_export(ex, pf, fr_rec, IPXG_FLOW_END_FORCED);
-                count_export(sc, fr_rec, IPXG_FLOW_END_FORCED);
-                n_ex++;
-            }
-            count_v6_exports(ex, fin_export && fr_rec.ip_version == 6);
+        if (fin_export) {
+            store_export(ex, pos, fr_rec, IPXG_FLOW_END_FORCED);
+            count_export(sc, fr_rec, IPXG_FLOW_END_FORCED);
+            n_ex++;
+            n_v6 += fr_rec.ip_version == 6 ? 1 : 0;
         }
+        __syncthreads();  // ex_base is rewritten by the next pass
     }
     if (n_live) atomicAdd(&cnt[0], n_live);
     if (n_cx) atomicAdd(&cnt[1], n_cx);
     if (n_ex) atomicAdd(&cnt[2], n_ex);
+    if (n_v6) atomicAdd(&cnt[3], n_v6);
     flush_block_stats(sc, stats);
     if (tid == 0) {
+        if (cnt[3] && ex.count6) atomicAdd(ex.count + 2, cnt[3]);  // count_v6_exports' counter
         if (cnt[0]) atomicAdd(&ctl->new_live, cnt[0]);
         if (cnt[1]) atomicAdd(&ctl->complex_count, cnt[1]);
         if (cnt[2]) atomicAdd(&ctl->exported, cnt[2]);

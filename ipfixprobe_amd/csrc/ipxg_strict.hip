@@ -70,7 +70,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_strict_prep2(BatchView b, Params
         DevPkt pk;
         ipxg_pkt_desc d;
         StrictPkt s = {};
-        const bool ok = reparse_lds<false>(b, p, f, i, col, pk, d) && (pk.ip_version == 4 || pk.ip_version == 6);
+        const bool ok = reparse_lds<true>(b, p, f, i, col, pk, d) && (pk.ip_version == 4 || pk.ip_version == 6);
         if (ok) {
             FlowKey kf, ki;
             build_keys(pk, kf, ki);

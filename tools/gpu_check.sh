@@ -15,7 +15,7 @@ stop_on_fault() {  # $1 = exit status, $2 = step name
     esac
 }
 echo "== pytest -m gpu"; date
-timeout -k 10 1200 python -u -m pytest tests -m gpu -q ${PYTEST_X:--x} -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 1200 python -u -m pytest tests -m gpu -q ${PYTEST_X--x} -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
 rc=$?; tail -5 $OUT/pytest_gpu_$TAG.log; stop_on_fault $rc pytest
 echo "== smoke"; date
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1

@@ -21,6 +21,7 @@ def summarise(pmc_dir):
         for (k, c), v in vals.items():
             steady = v[1:] if len(v) > 1 else v
             out[k][c] = sum(steady) / len(steady)
+            out[k]["calls"] = max(out[k].get("calls", 0), len(v))
     return dict(out)
 
 
