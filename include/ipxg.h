@@ -378,8 +378,8 @@ typedef struct ipxg_timing {
     uint64_t ingest_packets;   /* packets covered by the timed ingest launches             */
 } ipxg_timing;
 
-/* Per-phase shader-clock sums of the last batch's k_bin (8 values; all zero unless the
- * library was built with -DIPXG_PROBE -- a tuning aid). */
+/* Per-phase shader-clock sums of the last batch's k_bin, k_reduce and k_bin_slow (16 values;
+ * all zero unless the library was built with -DIPXG_PROBE -- a tuning aid). */
 int ipxg_probe_counters(ipxg_engine* eng, uint64_t* out);
 /* Event timing: 1 = every stage, 2 = the ingest kernel only (two events per batch, the
  * least host overhead), 3 = k_bin and k_bin_slow (three events), 0 = off; enabling also

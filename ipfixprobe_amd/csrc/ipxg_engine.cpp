@@ -1821,7 +1821,7 @@ int ipxg_probe_counters(ipxg_engine* e, uint64_t* out) {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
-    for (int k = 0; k < 8; ++k) out[k] = e->ctl_h->probe[k];
+    for (int k = 0; k < 16; ++k) out[k] = e->ctl_h->probe[k];
     return IPXG_OK;
 }
 

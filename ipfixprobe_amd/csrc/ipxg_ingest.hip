@@ -37,8 +37,10 @@ namespace ipxg {
 #ifndef IPXG_RED_U
 #define IPXG_RED_U 4
 #endif
-// IPXG_PROBE builds accumulate per-phase shader clocks of k_bin into ctl->probe (read with
-// ipxg_probe_counters): [0] tile start, [1] packet loop, [2] emit, [3] slow-list flush.
+// IPXG_PROBE builds accumulate per-phase shader clocks into ctl->probe (read with
+// ipxg_probe_counters): k_bin [0] tile start, [1] packet loop, [2] emit, [3] slow-list flush;
+// k_reduce [4] prefix + zero, [5] aggregate, [6] merge + list; k_bin_slow [8] entry + window
+// loads (issue to arrival), [9] stage + parse + rank, [10] aggregate + emit, [11] packets.
 #ifdef IPXG_PROBE
 #define PROBE_T(v) const uint64_t v = __builtin_readcyclecounter()
 #define PROBE_ADD(k, a, b) probe_acc[k] += (b) - (a)
@@ -300,7 +302,7 @@ template <bool LISTED>
 __device__ __forceinline__ void tile_rank(const Params& p, const BatchView& b, const DevPkt& pk,
                                           const ipxg_pkt_desc& d, uint32_t i, int j, uint32_t (&r0)[BIN_K],
                                           uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
-                                          uint32_t (&ix)[BIN_K]) {
+                                          uint32_t (&ix)[BIN_K], uint32_t& tb_or) {
     uint64_t lo, hf;
     uint32_t cdir;
 #ifdef IPXG_EXP_NOHASH  // timing experiment only: one cheap mixer instead of 2x XXH64
@@ -312,6 +314,7 @@ __device__ __forceinline__ void tile_rank(const Params& p, const BatchView& b, c
     canon(pk, p, lo, cdir, hf);
 #endif
     const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
+    tb_or |= misc_tb(m);
 #pragma unroll
     for (int q = 0; q < BIN_K; ++q) {  // registers indexed by compile-time q only
         if (q == j) {
@@ -405,6 +408,35 @@ __device__ __forceinline__ void tile_aggregate(const BinLds& L, uint32_t pmask, 
     for (uint32_t a = tid; a < na; a += IPXG_BLOCK) L.agg[a].rank = atomicAdd(&L.hist[L.agg[a].part], 3u);
 }
 
+// ---- shape classes of the slow list ------------------------------------------------------
+// k_bin_slow's general parser is a state machine (Ethernet -> VLAN -> MPLS / PPPoE / IPv4 ->
+// GRE -> ... -> L4): a wave whose lanes walk different header chains executes every state's
+// code on every step.  So k_bin tags each slow entry with the shape class of its first 48 bytes
+// (a guess from fixed offsets -- it only orders the work, the parser decides everything) and
+// k_bin_slow parses each tile's packets grouped by class.
+constexpr uint32_t SLOW_NCLS = 16;
+constexpr uint32_t SLOW_IDX_MASK = 0xFFFFFFu;  // entry.x: packet index (< 2^24) | class << 24
+__device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xFF) << 8) | ((w >> 8) & 0xFF); }
+__device__ __forceinline__ uint32_t slow_class(const uint4 c0, const uint4 c1, const uint4 c2) {
+    const uint32_t et0 = be16_lo(c0.w);                        // bytes 12-13
+    const bool t1 = et0 == 0x8100 || et0 == 0x88A8;
+    const uint32_t et1 = be16_lo(c1.x);                        // bytes 16-17
+    const bool t2 = t1 && (et1 == 0x8100 || et1 == 0x88A8);
+    const uint32_t et = t2 ? be16_lo(c1.y) : (t1 ? et1 : et0);  // bytes 20-21
+    // the L3 header at 14, 18 or 22: IPv4 protocol (+9), IPv6 next header (+6)
+    const uint32_t v4p = t2 ? (c1.w >> 24) : (t1 ? (c1.z >> 24) : (c1.y >> 24));
+    const uint32_t v6n = t2 ? (c1.w & 0xFF) : (t1 ? (c1.z & 0xFF) : (c1.y & 0xFF));
+    uint32_t cls = 15;  // other link layers / ethertypes
+    if (et == 0x0800) cls = v4p == 47 ? 1 : (v4p == 6 ? 2 : 0);
+    else if (et == 0x86DD) cls = (v6n == 6 || v6n == 17) ? 3 : (v6n == 44 ? 4 : 5);
+    else if (et == 0x8847 || et == 0x8848) {  // labels from byte 14 (untagged): bottom-of-stack bits
+        const uint32_t n = (c1.x & 1) ? 1 : ((c1.y & 1) ? 2 : 3);  // S bit: byte 2 of a label
+        cls = 5 + n;
+    } else if (et == 0x8864) cls = 9;
+    else if (et == 0x22F3) cls = 10;  // TRILL
+    return cls;
+}
+
 // Every packet of the batch, in tiles of BIN_K x 256, parsed in registers by parse_fast
 // from buffer loads software-pipelined across the tiles (below).  Frames the register parser
 // does not take go to the slow list for k_bin_slow.  No LDS header staging here: LDS holds
@@ -451,7 +483,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
     const uint64_t ts_before = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
-    uint32_t spilled = 0, walked = 0;
+    uint32_t spilled = 0, walked = 0, tb_or = 0;
     constexpr int NC = WIDE ? WIDE_DW / 4 : 3;
     auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(d); };
     bool nonmono = false;
@@ -578,8 +610,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             }
             if (slow)
                 my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] =
-                    make_uint4(i, dc.offset, (uint32_t)dc.caplen | ((uint32_t)dc.wirelen << 16), dc.ts_sec);
-            if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix);
+                    make_uint4(i | (slow_class(hc.c[0], hc.c[1], hc.c[2]) << 24), dc.offset,
+                               (uint32_t)dc.caplen | ((uint32_t)dc.wirelen << 16), dc.ts_sec);
+            if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix, tb_or);
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
@@ -628,6 +661,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     }
     if (AGG) add_wave_sum(&ctl->agg_packets, folded);
     if (WIDE) add_wave_sum(&ctl->walked, walked);
+    if (tb_or) atomicOr(&ctl->tb_any, tb_or);  // no atomic while one bucket holds the batch
 }
 
 // A slow-list entry (k_bin -> k_bin_slow): {packet index, offset, caplen | wirelen << 16,
@@ -689,9 +723,9 @@ __device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b,
                                             uint32_t* col, const uint4 e, const SlowWin& w, int j, ParseCounts& c,
                                             uint32_t& keyless, uint32_t& frags, uint32_t (&r0)[BIN_K],
                                             uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
-                                            uint32_t (&ix)[BIN_K]) {
+                                            uint32_t (&ix)[BIN_K], uint32_t& tb_or) {
     const ipxg_pkt_desc d = slow_desc(e);
-    const uint32_t i = e.x;
+    const uint32_t i = e.x & SLOW_IDX_MASK;
     put_window(col, b.arena, e, w);
     LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
     DevPkt pk;
@@ -705,7 +739,7 @@ __device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b,
         divert_fragment(pk, p, f, ctl, i);
         return;
     }
-    tile_rank<true>(p, b, pk, d, i, j, r0, r1, r2, rk, ix);
+    tile_rank<true>(p, b, pk, d, i, j, r0, r1, r2, rk, ix, tb_or);
 }
 
 // The frames k_bin left for the general parser (VLAN/QinQ, MPLS, PPPoE, GRE, TRILL, IPv6
@@ -745,10 +779,42 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
     ParseCounts c = {};
-    uint32_t keyless = 0, frags = 0, spilled = 0;
+    uint32_t keyless = 0, frags = 0, spilled = 0, tb_or = 0;
     uint32_t* col = &win[tid];
+#ifdef IPXG_PROBE
+    uint64_t probe_acc[4] = {0, 0, 0, 0};  // [0] loads, [1] parse + rank, [2] emit, [3] packets (lane 0)
+#endif
+    __shared__ uint32_t ccnt[SLOW_NCLS];  // the tile's packets per shape class, then the class's start
+    uint16_t* const ord = reinterpret_cast<uint16_t*>(hist);  // sorted position -> entry (hist is free until the ranking)
+    static_assert(sizeof(hist) >= BIN_TILE * sizeof(uint16_t), "tile order in the histogram area");
     for (uint32_t tile = 0; tile < ns; tile += BIN_TILE) {
-        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
+        // group the tile's entries by shape class: counting sort of their positions into ord
+        const uint32_t nt = min(ns - tile, BIN_TILE);
+        if (tid < SLOW_NCLS) ccnt[tid] = 0;
+        __syncthreads();
+        uint32_t crk[BIN_K];  // class << 16 | rank in class
+#pragma unroll
+        for (int j = 0; j < BIN_K; ++j) {
+            const uint32_t k = (uint32_t)j * IPXG_BLOCK + tid;
+            crk[j] = 0xFFFFFFFFu;
+            if (k < nt) {
+                const uint32_t c = list[tile + k].x >> 24;
+                crk[j] = (c << 16) | atomicAdd(&ccnt[c], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t run = 0;
+            for (uint32_t c = 0; c < SLOW_NCLS; ++c) {
+                const uint32_t v = ccnt[c];
+                ccnt[c] = run;
+                run += v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < BIN_K; ++j)
+            if (crk[j] != 0xFFFFFFFFu) ord[ccnt[crk[j] >> 16] + (crk[j] & 0xFFFF)] = (uint16_t)(j * IPXG_BLOCK + tid);
         __syncthreads();
         uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
 #pragma unroll
@@ -763,21 +829,49 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         for (int j = 0; j < BIN_K; j += 2) {
             const uint32_t k0 = tile + (uint32_t)j * IPXG_BLOCK + tid, k1 = k0 + IPXG_BLOCK;
             if (k0 >= ns) break;
-            const uint4 e0 = list[k0];
-            const uint4 e1 = k1 < ns ? list[k1] : make_uint4(0, BUF_OOB, 0, 0);
+            PROBE_T(s0);
+#ifdef IPXG_PROBE
+            uint64_t s1;
+#endif
+            const uint4 e0 = list[tile + ord[k0 - tile]];
+            const uint4 e1 = k1 < ns ? list[tile + ord[k1 - tile]] : make_uint4(0, BUF_OOB, 0, 0);
             SlowWin w1;
             {
                 const SlowWin w0 = load_win(rs_arena, e0);
                 w1 = load_win(rs_arena, e1);
-                slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix);
+#ifdef IPXG_PROBE
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                s1 = __builtin_readcyclecounter();
+                PROBE_ADD(0, s0, s1);
+                probe_acc[3] += 1 + (k1 < ns ? 1 : 0);
+#endif
+                slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix, tb_or);
             }
-            if (k1 < ns) slow_packet<AGG>(p, b, f, ctl, col, e1, w1, j + 1, c, keyless, frags, r0, r1, r2, rk, ix);
+            if (k1 < ns) slow_packet<AGG>(p, b, f, ctl, col, e1, w1, j + 1, c, keyless, frags, r0, r1, r2, rk, ix, tb_or);
+#ifdef IPXG_PROBE
+            PROBE_T(s2);
+            PROBE_ADD(1, s1, s2);
+#endif
         }
+        PROBE_T(s3);
+        __syncthreads();  // ord (in hist) is read by the loop above
+        for (uint32_t q = tid; q < P; q += IPXG_BLOCK) hist[q] = 0;
+        if (!AGG) __syncthreads();  // (tile_aggregate starts with a barrier)
         if (AGG) tile_aggregate<true>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
         else tile_rank_all(hist, pmask, r1, rk);
         tile_emit<true, AGG>(L, P, pmask, bv, bcol, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile,
                              spilled);
+        PROBE_T(s4);
+        PROBE_ADD(2, s3, s4);
     }
+#ifdef IPXG_PROBE
+    if (lane_id() == 0) {
+        atomicAdd((unsigned long long*)&ctl->probe[8], (unsigned long long)probe_acc[0]);
+        atomicAdd((unsigned long long*)&ctl->probe[9], (unsigned long long)probe_acc[1]);
+        atomicAdd((unsigned long long*)&ctl->probe[10], (unsigned long long)probe_acc[2]);
+        atomicAdd((unsigned long long*)&ctl->probe[11], (unsigned long long)probe_acc[3]);
+    }
+#endif
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, bcol);
     if (tid < ST_COUNT) hist[tid] = 0;
@@ -789,6 +883,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         ctl->pending = 1;
     }
     if (AGG) add_wave_sum(&ctl->agg_packets, folded);
+    if (tb_or) atomicOr(&ctl->tb_any, tb_or);
 }
 
 typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint4*, uint32_t*, uint4*,
@@ -841,12 +936,14 @@ __device__ __forceinline__ int lds_slot(FlowAgg* ht, uint64_t lo, bool insert) {
     return -1;
 }
 
-__device__ __forceinline__ void lds_fold(FlowAgg& a, uint32_t idx, uint32_t m) {
+// one_tb: every record of the batch is in time bucket 0 (ctl->tb_any == 0), so the occupancy
+// map of every flow is bit 0 -- set once per flow after the fold, not once per record
+__device__ __forceinline__ void lds_fold(FlowAgg& a, uint32_t idx, uint32_t m, bool one_tb) {
     const uint32_t cdir = misc_dir(m);
     atomicAdd(&a.acc[cdir], (1ull << 40) | (unsigned long long)misc_len(m));
     atomicMax(&a.last1, idx + 1);
     atomicMax(&a.first_n, first_key(idx, m));
-    atomicOr(&a.tbits, 1u << misc_tb(m));
+    if (!one_tb) atomicOr(&a.tbits, 1u << misc_tb(m));
     const uint32_t fl = misc_flags(m);
     if (misc_tcp(m) && fl) {
         atomicOr(&a.tflags, fl << (8 * cdir));
@@ -893,7 +990,8 @@ __device__ __forceinline__ void lds_fold_agg(FlowAgg& e, const FlowAgg& a) {
 // ok: the slot exists (tested here, not by overwriting the loaded value: a write into the
 // load's destination made the compiler wait for each load as soon as it was issued)
 __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
-                                           uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp, bool ok) {
+                                           uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp, bool ok,
+                                           bool one_tb) {
     if (!ok || r.z == NO_REC) return;
     if (rec_is_agg(r)) {
         if (rec_agg_slot(r) != 0) return;
@@ -909,9 +1007,17 @@ __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, Batc
         return;
     }
     const uint64_t lo = ((uint64_t)r.y << 32) | r.x;
+#ifdef IPXG_EXP_RED_NOFOLD  // timing experiment only: the record loads, no LDS table
+    if ((lo ^ r.z ^ r.w) == 0x1234567ull) atomicAdd(&cnt[C_SPILL], 1u);
+    return;
+#endif
     const int e = lds_slot(ht, lo, true);
+#ifdef IPXG_EXP_RED_NOATOM  // timing experiment only: the LDS table lookups, no fold atomics
+    if (e >= 0 && r.w == 0x1234567u) atomicAdd(&cnt[C_SPILL], 1u);
+    if (e >= 0) return;
+#endif
     if (e >= 0) {
-        lds_fold(ht[e], r.z, r.w);
+        lds_fold(ht[e], r.z, r.w, one_tb);
     } else {
         atomicAdd(&cnt[C_SPILL], 1u);
         if (!merge_packet_atomic(t, lo, r.z, r.w, &ctl->new_keys)) defer_packet(ctl, deferred_list, r.z, false);
@@ -974,6 +1080,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __syncthreads();
     PROBE_T(q1t);
     const uint4* segs = bv.rec + (size_t)part * bv.cols * bv.seg_cap;
+    const bool one_tb = ctl->tb_any == 0;  // final: k_bin and k_bin_slow have completed
     const uint32_t lane = tid & 63, wave = tid >> 6;
     constexpr uint32_t NW = RED_THREADS / 64;
     if (total < nseg * 16) {
@@ -992,7 +1099,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
             }
 #pragma unroll
             for (uint32_t u = 0; u < RED_U; ++u)
-                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], rp[u], k0 + u * RED_THREADS + tid < total);
+                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], rp[u], k0 + u * RED_THREADS + tid < total, one_tb);
         }
     } else {
         // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
@@ -1026,21 +1133,42 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
             for (uint32_t u = 0; u < RED_U; ++u) {
                 const uint4* sg = segs + (size_t)sc[u] * bv.seg_cap;
-                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], sg + lane, lane < sl[u]);
+                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], sg + lane, lane < sl[u], one_tb);
                 for (uint32_t off = 64; off < sl[u]; off += 64) {  // long segment (uniform over the wave)
                     const uint4 x = sg[off + lane < sl[u] ? off + lane : 0];
-                    red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane, off + lane < sl[u]);
+                    red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane, off + lane < sl[u], one_tb);
                 }
             }
         };
+#ifdef IPXG_PROBE  // [12] waits for a group's records (the next group's loads in flight), [13] folds
+        uint64_t pw = 0, pf = 0;
+#define RED_PROBE_FOLD(R, SC, SL)                                                              \
+    do {                                                                                        \
+        const uint64_t a_ = __builtin_readcyclecounter();                                      \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RED_U) : "memory");                           \
+        const uint64_t b_ = __builtin_readcyclecounter();                                      \
+        fold(R, SC, SL);                                                                        \
+        pw += b_ - a_;                                                                          \
+        pf += __builtin_readcyclecounter() - b_;                                                \
+    } while (0)
+#else
+#define RED_PROBE_FOLD(R, SC, SL) fold(R, SC, SL)
+#endif
         issue(wv, ra, sca, sla);
         for (uint32_t s0 = wv; s0 < nseg; s0 += 2 * STEP) {
             issue(s0 + STEP, rb, scb, slb);
-            fold(ra, sca, sla);
+            RED_PROBE_FOLD(ra, sca, sla);
             if (s0 + STEP >= nseg) break;  // uniform
             issue(s0 + 2 * STEP, ra, sca, sla);
-            fold(rb, scb, slb);
+            RED_PROBE_FOLD(rb, scb, slb);
         }
+#undef RED_PROBE_FOLD
+#ifdef IPXG_PROBE
+        if (lane == 0) {
+            atomicAdd((unsigned long long*)&ctl->probe[12], (unsigned long long)pw);
+            atomicAdd((unsigned long long*)&ctl->probe[13], (unsigned long long)pf);
+        }
+#endif
     }
     __syncthreads();
     PROBE_T(q2t);
@@ -1056,7 +1184,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q) {
         const uint32_t e = tid + q * RED_THREADS;
-        const FlowAgg a = ht[e];
+        FlowAgg a = ht[e];
+        if (one_tb) a.tbits |= 1u;  // bucket 0 (lds_fold skipped the per-record OR)
         listed[q] = false;
         if (a.key) {
             n_touch++;

@@ -61,7 +61,8 @@ struct BatchCtl {
     uint32_t plugin_fail;    // k_classify found no slot for a plugin flow (table too full)
     int32_t strict_live;     // strict mode: records created - records exported
     uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
-    uint64_t probe[8];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
+    uint32_t tb_any;         // OR of the time buckets of k_bin / k_bin_slow's records (0: all in bucket 0)
+    uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
 // Fragmentation-cache ring entry (fragmentationKeyData.hpp:49-112), 4 per bucket.

@@ -371,7 +371,7 @@ class Engine:
         return {f: getattr(t, f) for f, _ in Timing._fields_}
 
     def probe_counters(self):
-        out = np.zeros(8, dtype=np.uint64)
+        out = np.zeros(16, dtype=np.uint64)
         self._check(lib().ipxg_probe_counters(self._h, out.ctypes.data), "ipxg_probe_counters")
         return out
 

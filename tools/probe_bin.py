@@ -33,6 +33,9 @@ def main():
     for k, nme in ((4, "red: prefix+zero"), (5, "red: aggregate"), (6, "red: merge+list")):
         print("%-18s %10.0f cycles/workgroup" % (nme, int(pc[k]) / blocks))
     print("k_reduce avg %.4f ms" % (tm["reduce_ms"] / max(tm["reduce_launches"], 1)))
+    waves = blocks * 16
+    print("red aggregate: wait for records %10.0f cycles/wave, fold %10.0f cycles/wave"
+          % (int(pc[12]) / waves, int(pc[13]) / waves))
 
 
 if __name__ == "__main__":
