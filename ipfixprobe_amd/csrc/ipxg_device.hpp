@@ -527,8 +527,8 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
     }
     uint32_t r = parse_l3<FULL>(s, kind, off, (caplen - off) & 0xFFFF, caplen, p, err);
     if (err) return false;
-    if (kind == L3_MPLS) c.mpls++;
-    if (kind == L3_PPPOE) c.pppoe++;
+    c.mpls += kind == L3_MPLS ? 1u : 0u;
+    c.pppoe += kind == L3_PPPOE ? 1u : 0u;
     off = (off + r) & 0xFFFF;
     const uint32_t l4_off = off;
     if (p.frag_off == 0) {
@@ -536,7 +536,6 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
             const uint32_t h = parse_tcp<FULL>(s, off, (caplen - off) & 0xFFFF, p, err);
             if (err) return false;
             off = (off + h) & 0xFFFF;
-            c.tcp++;
         } else if (p.ip_proto == 17) {  // parse_udp_hdr :552-573
             if (8 > ((caplen - off) & 0xFFFF)) return false;
             uint32_t w0 = s.le32(off);
@@ -544,9 +543,10 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
             p.dst_port = bswap16(w0 >> 16);
             p.l4 = 17;
             off = (off + 8) & 0xFFFF;
-            c.udp++;
         }
     }
+    c.tcp += p.l4 == 6 ? 1u : 0u;  // (branch-free: see the counters below)
+    c.udp += p.l4 == 17 ? 1u : 0u;
     if (FULL) {  // payload, parser.cpp:780-797 (uint16_t arithmetic as there)
         uint32_t pkt_len = caplen, wire;
         if (l4_off != l3_off) {
@@ -560,14 +560,14 @@ __device__ __forceinline__ bool parse_frame(const S& s, uint32_t caplen, uint32_
         p.payload_off = (uint16_t)off;
         p.payload_len = (uint16_t)plen;
     }
-    if (p.vlan_id) c.vlan++;
-    if (et == ETH_P_IP) {
-        c.ipv4++;
-        c.ipv4_bytes += caplen;
-    } else if (et == ETH_P_IPV6) {
-        c.ipv6++;
-        c.ipv6_bytes += caplen;
-    }
+    // branch-free counter updates: with if/else the compiler merged them into one update at a
+    // selected field offset, which put the whole ParseCounts in scratch memory
+    const uint32_t is4 = et == ETH_P_IP ? 1u : 0u, is6 = et == ETH_P_IPV6 ? 1u : 0u;
+    c.vlan += p.vlan_id ? 1u : 0u;
+    c.ipv4 += is4;
+    c.ipv4_bytes += is4 ? caplen : 0u;
+    c.ipv6 += is6;
+    c.ipv6_bytes += is6 ? caplen : 0u;
     c.parsed++;
     return true;
 }

@@ -1284,40 +1284,30 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
     uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0;
     for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
         const uint32_t k = base + tid;
-        bool do_export = false, fin_export = false;
+        bool do_export = false;  // er is exported with `reason` (a boundary split, or the fused finish)
         uint8_t reason = 0;
-        ipxg_flow_record er, fr_rec;
+        ipxg_flow_record er;
         if (k < nf) {
             const HotSlot h = fin_list[k];  // the slot's merged image, its index in pad
-            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er,
-                                                     fused ? &fr_rec : nullptr);
+            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused);
             if (fr.status == FIN_COMPLEX) n_cx++;
-            else if (fused) fin_export = true;
-            else if (fr.created) n_live++;
-            do_export = fr.do_export;
-            reason = fr.reason;
+            else if (!fused && fr.created) n_live++;
+            do_export = fr.do_export || fr.fin_export;
+            reason = fr.fin_export ? (uint8_t)IPXG_FLOW_END_FORCED : fr.reason;
         }
         // one reservation in the export buffer per workgroup and pass (a returning atomic per
         // wave on the one counter serialised ~1600 waves at ~12 ns each: MI355X_MICROARCH.md
         // "fanin" / "dequeue")
-        const uint32_t mine = (do_export ? 1u : 0u) + (fin_export ? 1u : 0u);
         uint32_t btot;
-        uint32_t pos = block_exclusive_scan<IPXG_BLOCK>(mine, scan_s, &btot);
+        const uint32_t pos = block_exclusive_scan<IPXG_BLOCK>(do_export ? 1u : 0u, scan_s, &btot);
         if (btot == 0) continue;  // uniform
         if (tid == 0) ex_base = atomicAdd(ex.count, btot);
         __syncthreads();
-        pos += ex_base;
         if (do_export) {
-            store_export(ex, pos++, er, reason);
+            store_export(ex, ex_base + pos, er, reason);
             count_export(sc, er, reason);
             n_ex++;
             n_v6 += er.ip_version == 6 ? 1 : 0;
-        }
-        if (fin_export) {
-            store_export(ex, pos, fr_rec, IPXG_FLOW_END_FORCED);
-            count_export(sc, fr_rec, IPXG_FLOW_END_FORCED);
-            n_ex++;
-            n_v6 += fr_rec.ip_version == 6 ? 1 : 0;
         }
         __syncthreads();  // ex_base is rewritten by the next pass
     }

@@ -593,16 +593,13 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     ext = S != 0 || v6 || tcp_opt;
     c.seen++;
     c.parsed++;
-    if (v6) {
-        c.ipv6++;
-        c.ipv6_bytes += caplen;
-    } else {
-        c.ipv4++;
-        c.ipv4_bytes += caplen;
-    }
-    if (frag_off == 0 && proto == 6) c.tcp++;
-    if (frag_off == 0 && proto == 17) c.udp++;
-    if (vlan) c.vlan++;
+    c.ipv6 += v6 ? 1u : 0u;  // branch-free (see parse_frame)
+    c.ipv6_bytes += v6 ? caplen : 0u;
+    c.ipv4 += v6 ? 0u : 1u;
+    c.ipv4_bytes += v6 ? 0u : caplen;
+    c.tcp += (frag_off == 0 && proto == 6) ? 1u : 0u;
+    c.udp += (frag_off == 0 && proto == 17) ? 1u : 0u;
+    c.vlan += vlan ? 1u : 0u;
     return true;
 }
 
@@ -768,7 +765,8 @@ enum FinStatus : uint32_t { FIN_DONE = 1, FIN_COMPLEX = 2 };
 struct FinResult {
     uint32_t status;   // FIN_DONE / FIN_COMPLEX
     bool created;      // the slot held no live record before (a record was created)
-    bool do_export;    // the open record was closed at the batch boundary
+    bool do_export;    // the open record was closed at the batch boundary (er, reason)
+    bool fin_export;   // fuse: the completed record (er) is exported FORCED and the slot emptied
     uint8_t reason;
 };
 
@@ -784,14 +782,16 @@ struct FinResult {
 // re-parses its first packet (FlowRecord::create's fields, cache.cpp:94-133).  Writes the slot
 // (and its cold record) back.
 // LDSW: stage the creator's headers in the lane's LDS column `col` (else byte loads).
-// out (a finish follows, k_fin_list's fused mode): a completed record goes to *out instead of
-// the table, and the slot is emptied.
+// fuse (a finish follows, k_fin_list's fused mode; only on a table that held no live record
+// before the batch, so no boundary export can coincide): the completed record goes to er
+// (fin_export) instead of the table, and the slot is emptied.  One record out per slot either
+// way, so the caller holds one record, not two (two were kept in scratch).
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
                                                    bool force_cx, uint32_t* col, ipxg_flow_record& er,
-                                                   ipxg_flow_record* out = nullptr) {
-    FinResult res = {FIN_DONE, false, false, 0};
+                                                   bool fuse = false) {
+    FinResult res = {FIN_DONE, false, false, false, 0};
     const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
     ipxg_flow_record rec;
@@ -863,8 +863,9 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     rec.time_last_usec = dl.ts_usec;
     res.created = !live;
     count_flow_ports(t, rec, (uint32_t)(as >> 40) + (uint32_t)(ad >> 40));
-    if (out) {
-        *out = rec;
+    if (fuse && !res.do_export) {
+        er = rec;
+        res.fin_export = true;
         clear_slot(&t.hot[s], 0, 0);  // empty (every slot empties at the finish)
         return res;
     }
