@@ -586,6 +586,18 @@ def main():
     step_ms = dt / args.steps * 1e3
     step_gbs = alg_step * world / (step_ms / 1e3) / 1e9
     pmc = pmc_traffic(kname, wl.name if wl.name != "udp64-stream" else "stream")
+    # the slow pass (frames the register walks do not take) on its own: its packets per launch
+    # from the engine's counter, their algorithmic bytes at the workload's mean per packet
+    slow_share = st["slow_path_packets"] / max(st["parsed_packets"], 1)
+    slow_pk = slow_share * alg_launch / max(alg_step / pk_step, 1e-9)
+    slow_line = None
+    if slow_share > 0.001 and slow_ms > 0:
+        sgbs = slow_pk * (alg_step / pk_step) / (slow_ms / 1e3) / 1e9
+        slow_line = {"kernel": "k_bin_slow", "packets_per_launch": round(slow_pk), "avg_launch_ms": round(slow_ms, 4),
+                     "Mpkts_per_s": round(slow_pk / (slow_ms / 1e3) / 1e6, 1), "achieved": round(sgbs, 1),
+                     "frac": round(sgbs / HBM_PEAK_GBS, 4),
+                     "what": "slow-list packets (the workload's mean algorithmic bytes per packet) / k_bin_slow's "
+                             "average launch"}
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and args.workload == "udp64" and args.mode == "cold" and \
             args.strict is None:
@@ -622,7 +634,8 @@ def main():
                          "step": {"what": "algorithmic bytes of the step / the whole step (every kernel, host "
                                           "round trips, finish)",
                                   "achieved": round(step_gbs, 1), "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
-                         "step_frac": round(step_gbs / HBM_PEAK_GBS, 4)},
+                         "step_frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                         "slow": slow_line},
             "stage_ms_per_step": {k: round(tm[k + "_ms"] / stage_steps, 4)
                                   for k in ("ingest", "ingest_slow", "reduce", "fin", "finalize", "slow",
                                             "finish")},

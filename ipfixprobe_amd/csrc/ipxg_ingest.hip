@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
         const uint32_t k = base + tid;
         bool do_export = false;  // er is exported with `reason` (a boundary split, or the fused finish)
         uint8_t reason = 0;
-        ipxg_flow_record er;
+        RecW er;
         if (k < nf) {
             const HotSlot h = fin_list[k];  // the slot's merged image, its index in pad
             const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused);
@@ -1304,10 +1304,10 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
         if (tid == 0) ex_base = atomicAdd(ex.count, btot);
         __syncthreads();
         if (do_export) {
-            store_export(ex, ex_base + pos, er, reason);
-            count_export(sc, er, reason);
+            store_export_w(ex, ex_base + pos, er, reason);
+            count_export_w(sc, er, reason);
             n_ex++;
-            n_v6 += er.ip_version == 6 ? 1 : 0;
+            n_v6 += rw_ipver(er) == 6 ? 1 : 0;
         }
         __syncthreads();  // ex_base is rewritten by the next pass
     }

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
         const HotSlot h = t.hot[s];
         bool do_export = false;
         uint8_t reason = 0;
-        ipxg_flow_record er;
+        RecW er;
         if (h.key != 0) {
             keys++;
             const bool was_live = h.state & SLOT_LIVE;
@@ -311,11 +311,11 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
         }
         uint32_t pos = wave_append(ex.count, do_export);
         if (do_export) {
-            store_export(ex, pos, er, reason);
-            count_export(sc, er, reason);
+            store_export_w(ex, pos, er, reason);
+            count_export_w(sc, er, reason);
             ex_n++;
         }
-        count_v6_exports(ex, do_export && er.ip_version == 6);
+        count_v6_exports(ex, do_export && rw_ipver(er) == 6);
     }
     atomicAdd(&cnt[0], keys);
     atomicAdd(&cnt[1], live_n);
@@ -483,14 +483,14 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
 #pragma unroll
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const bool mine = mask >> j & 1;
-        ipxg_flow_record rec;
+        RecW rec;
         if (mine) {
-            rec = t.cold[base + j * 256 + threadIdx.x];
-            const uint8_t reason = export_reason(rec);
-            store_export(ex, pos++, rec, reason);
-            count_export(sc, rec, reason);
+            rec = rec_load_w(&t.cold[base + j * 256 + threadIdx.x]);
+            const uint8_t reason = export_reason_w(rec);
+            store_export_w(ex, pos++, rec, reason);
+            count_export_w(sc, rec, reason);
         }
-        count_v6_exports(ex, mine && rec.ip_version == 6);
+        count_v6_exports(ex, mine && rw_ipver(rec) == 6);
     }
     flush_block_stats(sc, stats);
 }
@@ -544,13 +544,13 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
 #pragma unroll
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const bool mine = mask >> j & 1;
-        ipxg_flow_record rec;
+        RecW rec;
         if (mine) {
-            rec = t.cold[base + j * 256 + threadIdx.x];
-            store_export(ex, pos++, rec, IPXG_FLOW_END_FORCED);
-            atomicAdd(&pb[pkts_bucket((uint64_t)rec.src_packets + rec.dst_packets)], 1u);
+            rec = rec_load_w(&t.cold[base + j * 256 + threadIdx.x]);
+            store_export_w(ex, pos++, rec, IPXG_FLOW_END_FORCED);
+            atomicAdd(&pb[pkts_bucket((uint64_t)rec.w[RW_SPK] + rec.w[RW_DPK])], 1u);
         }
-        count_v6_exports(ex, mine && rec.ip_version == 6);
+        count_v6_exports(ex, mine && rw_ipver(rec) == 6);
     }
     __syncthreads();
     unsigned long long* const sh = &stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT];

@@ -390,6 +390,102 @@ __device__ __forceinline__ void count_export(uint32_t* sc, const ipxg_flow_recor
     atomicAdd(&sc[ST_PKTS_1 + pkts_bucket((uint64_t)r.src_packets + r.dst_packets)], 1u);
 }
 
+// ---- the flow record as 32 words in registers -----------------------------------------------
+// Built or updated through ipxg_flow_record's byte fields, a record stayed in scratch memory
+// (128 B per lane in k_fin_list, 84 B in k_finish); the per-flow finalise and export paths
+// handle it as 32 words at compile-time indices instead (ipxg.h layout, little-endian).
+struct RecW {
+    uint32_t w[32];
+};
+enum RecWord : int {
+    RW_HASH = 0, RW_TFS = 2, RW_TFU = 3, RW_TLS = 4, RW_TLU = 5, RW_SBYTES = 6, RW_DBYTES = 8, RW_SPK = 10,
+    RW_DPK = 11,
+    RW_FLAGS = 12,  // src_tcp_flags | dst_tcp_flags << 8 | ip_version << 16 | ip_proto << 24
+    RW_PORTS = 13,  // src_port | dst_port << 16
+    RW_SIP = 14, RW_DIP = 18,
+    RW_MAC = 22,    // src_mac[6], dst_mac[6] over words 22..24
+    RW_VLAN = 25,   // vlan_id | end_reason << 16 | reserved0 << 24
+    RW_RSV = 26,    // reserved[8]: byte 0 = the creator's canonical direction while the flow lives
+    RW_EXT = 28, RW_RSV2 = 30
+};
+static_assert(offsetof(ipxg_flow_record, time_first_sec) == 4 * RW_TFS && offsetof(ipxg_flow_record, src_bytes) == 4 * RW_SBYTES &&
+              offsetof(ipxg_flow_record, src_packets) == 4 * RW_SPK && offsetof(ipxg_flow_record, src_tcp_flags) == 4 * RW_FLAGS &&
+              offsetof(ipxg_flow_record, src_port) == 4 * RW_PORTS && offsetof(ipxg_flow_record, src_ip) == 4 * RW_SIP &&
+              offsetof(ipxg_flow_record, dst_ip) == 4 * RW_DIP && offsetof(ipxg_flow_record, src_mac) == 4 * RW_MAC &&
+              offsetof(ipxg_flow_record, vlan_id) == 4 * RW_VLAN && offsetof(ipxg_flow_record, reserved) == 4 * RW_RSV &&
+              offsetof(ipxg_flow_record, ext) == 4 * RW_EXT && sizeof(ipxg_flow_record) == 128,
+              "RecW word map");
+__device__ __forceinline__ uint64_t rw64(const RecW& r, int k) { return ((uint64_t)r.w[k + 1] << 32) | r.w[k]; }
+__device__ __forceinline__ void rw64_set(RecW& r, int k, uint64_t v) {
+    r.w[k] = (uint32_t)v;
+    r.w[k + 1] = (uint32_t)(v >> 32);
+}
+__device__ __forceinline__ uint32_t rw_sflags(const RecW& r) { return r.w[RW_FLAGS] & 0xFF; }
+__device__ __forceinline__ uint32_t rw_dflags(const RecW& r) { return (r.w[RW_FLAGS] >> 8) & 0xFF; }
+__device__ __forceinline__ uint32_t rw_ipver(const RecW& r) { return (r.w[RW_FLAGS] >> 16) & 0xFF; }
+__device__ __forceinline__ uint32_t rw_proto(const RecW& r) { return r.w[RW_FLAGS] >> 24; }
+__device__ __forceinline__ uint32_t rw_creator(const RecW& r) { return r.w[RW_RSV] & 0xFF; }
+__device__ __forceinline__ RecW rec_load_w(const ipxg_flow_record* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    RecW r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 v = q[i];
+        r.w[4 * i] = v.x;
+        r.w[4 * i + 1] = v.y;
+        r.w[4 * i + 2] = v.z;
+        r.w[4 * i + 3] = v.w;
+    }
+    return r;
+}
+__device__ __forceinline__ void rec_store_w(ipxg_flow_record* p, const RecW& r) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = make_uint4(r.w[4 * i], r.w[4 * i + 1], r.w[4 * i + 2], r.w[4 * i + 3]);
+}
+__device__ __forceinline__ uint8_t export_reason_w(const RecW& r) {
+    return ((rw_sflags(r) | rw_dflags(r)) & 0x05) ? IPXG_FLOW_END_EOF : IPXG_FLOW_END_INACTIVE;
+}
+// store_export / count_export on the word form
+__device__ __forceinline__ void store_export_w(ExportView ex, uint32_t pos, const RecW& r, uint8_t reason) {
+    if (pos >= ex.cap) {
+        atomicOr(ex.count + 1, 1u);
+        return;
+    }
+    RecW o = r;
+    o.w[RW_VLAN] = (r.w[RW_VLAN] & 0xFFFF) | ((uint32_t)reason << 16);  // end_reason; reserved0 = 0
+    o.w[RW_RSV] = o.w[RW_RSV + 1] = 0;                                  // reserved zero on export
+    rec_store_w(&ex.buf[pos], o);
+}
+__device__ __forceinline__ void count_export_w(uint32_t* sc, const RecW& r, uint8_t reason) {
+    atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
+    atomicAdd(&sc[ST_PKTS_1 + pkts_bucket((uint64_t)r.w[RW_SPK] + r.w[RW_DPK])], 1u);
+}
+
+// FlowRecord::create's fields (rec_create) into the word form
+__device__ __forceinline__ void rec_create_w(RecW& r, const DevPkt& pk, const ipxg_pkt_desc& d, uint64_t hf,
+                                             uint32_t cdir) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) r.w[k] = 0;
+    rw64_set(r, RW_HASH, hf);
+    r.w[RW_TFS] = r.w[RW_TLS] = d.ts_sec;
+    r.w[RW_TFU] = r.w[RW_TLU] = d.ts_usec;
+    r.w[RW_FLAGS] = ((uint32_t)pk.ip_version << 16) | ((uint32_t)pk.ip_proto << 24);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        r.w[RW_SIP + k] = pk.sip[k];
+        r.w[RW_DIP + k] = pk.dip[k];
+    }
+    // frame bytes 0-5 = dst_mac, 6-11 = src_mac (mac_lo/mid/hi = bytes 0-11, little-endian)
+    r.w[RW_MAC] = (pk.mac_mid >> 16) | (pk.mac_hi << 16);     // src_mac[0..3]
+    r.w[RW_MAC + 1] = (pk.mac_hi >> 16) | (pk.mac_lo << 16);  // src_mac[4..5], dst_mac[0..1]
+    r.w[RW_MAC + 2] = (pk.mac_lo >> 16) | (pk.mac_mid << 16); // dst_mac[2..5]
+    const uint8_t pr = pk.ip_proto;
+    if (pr == 6 || pr == 17 || pr == 1 || pr == 58) r.w[RW_PORTS] = (uint32_t)pk.src_port | ((uint32_t)pk.dst_port << 16);
+    r.w[RW_VLAN] = (uint32_t)pk.vlan_id & 0xFFFF;
+    r.w[RW_RSV] = cdir & 0xFF;  // creator's canonical direction (not exported)
+}
+
 // ex.count[2] counts the exported records that take the IPv6 basic template (the IPFIX message
 // layout needs the split, ipxg_engine.cpp ipfix_plan).  Convergent: every lane of the wave.
 __device__ __forceinline__ void count_v6_exports(ExportView ex, bool v6) {
@@ -760,6 +856,14 @@ __device__ __forceinline__ void count_flow_ports(const TableView& t, const ipxg_
     atomicAdd(a + r.dst_port, (unsigned long long)packets);
 }
 
+__device__ __forceinline__ void count_flow_ports_w(const TableView& t, const RecW& r, uint32_t packets) {
+    const uint32_t pr = rw_proto(r), sp = r.w[RW_PORTS] & 0xFFFF, dp = r.w[RW_PORTS] >> 16;
+    if (!t.port_cnt || !packets || (pr != 6 && pr != 17) || (sp == 0 && dp == 0)) return;
+    unsigned long long* a = t.port_cnt + (pr == 17 ? 65536 : 0);
+    atomicAdd(a + sp, (unsigned long long)packets);
+    atomicAdd(a + dp, (unsigned long long)packets);
+}
+
 // ---- per-slot batch finalisation ----------------------------------------------------------
 enum FinStatus : uint32_t { FIN_DONE = 1, FIN_COMPLEX = 2 };
 struct FinResult {
@@ -789,25 +893,24 @@ struct FinResult {
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
-                                                   bool force_cx, uint32_t* col, ipxg_flow_record& er,
-                                                   bool fuse = false) {
+                                                   bool force_cx, uint32_t* col, RecW& er, bool fuse = false) {
     FinResult res = {FIN_DONE, false, false, false, 0};
     const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
-    ipxg_flow_record rec;
-    if (live) rec = t.cold[s];
+    RecW rec;
+    if (live) rec = rec_load_w(&t.cold[s]);
     const ipxg_pkt_desc df = b.desc[first];
     const ipxg_pkt_desc dl = b.desc[last];
     const uint32_t cdf = p.split_biflow ? 0u : first_dir(h.first_n);
     const uint32_t I = p.inactive_s, A = p.active_s;
     uint8_t bsplit = 0;
     if (live) {
-        const uint32_t creator = rec.reserved[0];
+        const uint32_t creator = rw_creator(rec);
         const bool dsrc = p.split_biflow || cdf == creator;
-        const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
+        const uint32_t flw = dsrc ? rw_sflags(rec) : rw_dflags(rec);
         if (first_syn(h.first_n) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
-        else if ((int64_t)df.ts_sec - (int64_t)rec.time_last_sec >= (int64_t)I) bsplit = export_reason(rec);
-        else if ((int64_t)df.ts_sec - (int64_t)rec.time_first_sec >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
+        else if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TLS] >= (int64_t)I) bsplit = export_reason_w(rec);
+        else if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TFS] >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
     }
     const bool cont = live && !bsplit;
     bool cx = force_cx || (h.state & SLOT_PLUGIN);  // a process plugin's flow: the host walks it
@@ -817,13 +920,13 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         uint32_t x = tb >> __builtin_ctz(tb);
         if (x & (x + 1)) cx = true;  // an empty bucket between two busy ones
     }
-    const uint32_t tfirst = cont ? rec.time_first_sec : df.ts_sec;
+    const uint32_t tfirst = cont ? rec.w[RW_TFS] : df.ts_sec;
     if ((int64_t)dl.ts_sec - (int64_t)tfirst >= (int64_t)A) cx = true;
     for (int dd = 0; dd < 2; ++dd) {
         if (!h.syn1[dd]) continue;
         const uint32_t sidx = h.syn1[dd] - 1;
         if (cont) {
-            const uint8_t cf = (uint32_t)dd == rec.reserved[0] ? rec.src_tcp_flags : rec.dst_tcp_flags;
+            const uint32_t cf = (uint32_t)dd == rw_creator(rec) ? rw_sflags(rec) : rw_dflags(rec);
             if (cf & 0x05) cx = true;
         }
         if (h.fin_n[dd] && sidx > ~h.fin_n[dd]) cx = true;
@@ -849,27 +952,26 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         uint64_t lo, hf;
         uint32_t c2;
         canon(fp, p, lo, c2, hf);
-        rec_create(rec, fp, df, hf, cdf);
+        rec_create_w(rec, fp, df, hf, cdf);
     }
-    const uint32_t sd = rec.reserved[0];
-    const uint64_t as = h.acc[sd], ad = h.acc[sd ^ 1];
-    rec.src_packets += (uint32_t)(as >> 40);
-    rec.src_bytes += as & ACC_BYTES_MASK;
-    rec.dst_packets += (uint32_t)(ad >> 40);
-    rec.dst_bytes += ad & ACC_BYTES_MASK;
-    rec.src_tcp_flags |= (uint8_t)(h.tflags >> (8 * sd));
-    rec.dst_tcp_flags |= (uint8_t)(h.tflags >> (8 * (sd ^ 1)));
-    rec.time_last_sec = dl.ts_sec;
-    rec.time_last_usec = dl.ts_usec;
+    const uint32_t sd = rw_creator(rec);
+    const uint64_t as = sd ? h.acc[1] : h.acc[0], ad = sd ? h.acc[0] : h.acc[1];  // (selects: no indexed copy)
+    rec.w[RW_SPK] += (uint32_t)(as >> 40);
+    rw64_set(rec, RW_SBYTES, rw64(rec, RW_SBYTES) + (as & ACC_BYTES_MASK));
+    rec.w[RW_DPK] += (uint32_t)(ad >> 40);
+    rw64_set(rec, RW_DBYTES, rw64(rec, RW_DBYTES) + (ad & ACC_BYTES_MASK));
+    rec.w[RW_FLAGS] |= ((h.tflags >> (8 * sd)) & 0xFF) | (((h.tflags >> (8 * (sd ^ 1))) & 0xFF) << 8);
+    rec.w[RW_TLS] = dl.ts_sec;
+    rec.w[RW_TLU] = dl.ts_usec;
     res.created = !live;
-    count_flow_ports(t, rec, (uint32_t)(as >> 40) + (uint32_t)(ad >> 40));
+    count_flow_ports_w(t, rec, (uint32_t)(as >> 40) + (uint32_t)(ad >> 40));
     if (fuse && !res.do_export) {
         er = rec;
         res.fin_export = true;
         clear_slot(&t.hot[s], 0, 0);  // empty (every slot empties at the finish)
         return res;
     }
-    t.cold[s] = rec;
+    rec_store_w(&t.cold[s], rec);
     clear_slot(&t.hot[s], h.key, SLOT_LIVE);
     return res;
 }
