@@ -47,6 +47,14 @@ struct GlobalSrc {
     }
 };
 
+// Bytes past the staged window (deep header chains only): out of line, so the ~60 read sites of
+// the parser do not each carry an inlined copy of the byte loads (code size: the slow pass's
+// kernel outgrew the instruction cache).
+__device__ __noinline__ uint32_t far_le32(const uint8_t* p, uint32_t cap, uint32_t o) {
+    const GlobalSrc g{p, cap};
+    return g.le32(o);
+}
+
 // Per-lane view of the LDS-staged window.  win points at dword 0 of this lane's column;
 // dword d lives at win[d * IPXG_BLOCK].
 struct LdsWin {
@@ -61,11 +69,11 @@ struct LdsWin {
             uint32_t hi = (d + 1 < IPXG_WIN_DW) ? dw(d + 1) : 0u;
             return __builtin_amdgcn_alignbyte(hi, lo, sh);
         }
-        return g.le32(o);
+        return far_le32(g.p, g.cap, o);
     }
     __device__ __forceinline__ uint32_t b(uint32_t o) const {
         if (o < IPXG_WIN) return (dw(o >> 2) >> ((o & 3) * 8)) & 0xFF;
-        return g.b(o);
+        return far_le32(g.p, g.cap, o) & 0xFF;
     }
 };
 

@@ -822,36 +822,37 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
-        // two packets per lane and step: both list entries, then both frames' windows, are in
-        // flight together, so one pair of memory round trips serves two packets
-        static_assert(BIN_K % 2 == 0, "the slow pass takes its packets in pairs");
+        // One packet per step with a rolling prefetch -- the entry two steps ahead and the window
+        // one step ahead are in flight while this step's packet is parsed -- and ONE call site of
+        // the general parser: two inlined copies (a pair per step) made the kernel's hot code
+        // larger than the instruction cache.
+        auto entry = [&](int j) {
+            const uint32_t k = tile + (uint32_t)j * IPXG_BLOCK + tid;
+            return j < BIN_K && k < ns ? list[tile + ord[k - tile]] : make_uint4(0, BUF_OOB, 0, 0);
+        };
+        uint4 e0 = entry(0), e1 = entry(1);
+        SlowWin w0 = load_win(rs_arena, e0);
 #pragma unroll 1
-        for (int j = 0; j < BIN_K; j += 2) {
-            const uint32_t k0 = tile + (uint32_t)j * IPXG_BLOCK + tid, k1 = k0 + IPXG_BLOCK;
+        for (int j = 0; j < BIN_K; ++j) {
+            const uint32_t k0 = tile + (uint32_t)j * IPXG_BLOCK + tid;
             if (k0 >= ns) break;
             PROBE_T(s0);
+            const uint4 e2 = entry(j + 2);
+            const SlowWin w1 = load_win(rs_arena, e1);
 #ifdef IPXG_PROBE
-            uint64_t s1;
+            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // w0 (the entry and window ahead stay in flight)
+            const uint64_t s1 = __builtin_readcyclecounter();
+            PROBE_ADD(0, s0, s1);
+            probe_acc[3] += 1;
 #endif
-            const uint4 e0 = list[tile + ord[k0 - tile]];
-            const uint4 e1 = k1 < ns ? list[tile + ord[k1 - tile]] : make_uint4(0, BUF_OOB, 0, 0);
-            SlowWin w1;
-            {
-                const SlowWin w0 = load_win(rs_arena, e0);
-                w1 = load_win(rs_arena, e1);
-#ifdef IPXG_PROBE
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                s1 = __builtin_readcyclecounter();
-                PROBE_ADD(0, s0, s1);
-                probe_acc[3] += 1 + (k1 < ns ? 1 : 0);
-#endif
-                slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix, tb_or);
-            }
-            if (k1 < ns) slow_packet<AGG>(p, b, f, ctl, col, e1, w1, j + 1, c, keyless, frags, r0, r1, r2, rk, ix, tb_or);
+            slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix, tb_or);
 #ifdef IPXG_PROBE
             PROBE_T(s2);
             PROBE_ADD(1, s1, s2);
 #endif
+            e0 = e1;
+            e1 = e2;
+            w0 = w1;
         }
         PROBE_T(s3);
         __syncthreads();  // ord (in hist) is read by the loop above
@@ -989,39 +990,40 @@ __device__ __forceinline__ void lds_fold_agg(FlowAgg& e, const FlowAgg& a) {
 // payload slots after it; the payload slots themselves are skipped).
 // ok: the slot exists (tested here, not by overwriting the loaded value: a write into the
 // load's destination made the compiler wait for each load as soon as it was issued)
+// The rare cases of red_record out of line -- an aggregate (3 slots), a record whose flow found
+// no LDS entry -- so the RED_U-unrolled fold loop inlines only the common path (probe + fold):
+// with every case inlined in every unrolled copy k_reduce's code was 117 KB.
+__device__ __noinline__ void red_agg(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint4* agg_list, uint32_t* cnt,
+                                     const uint4 r, const uint4* rp) {
+    if (rec_agg_slot(r) != 0) return;
+    const uint4 s1 = rp[1], s2 = rp[2];
+    const FlowAgg a = agg_decode(r, s1, s2);
+    const int e = lds_slot(ht, a.key, true);
+    if (e >= 0) {
+        lds_fold_agg(ht[e], a);
+    } else {
+        atomicAdd(&cnt[C_SPILL], 1u);
+        if (!merge_agg_probe(t, a, &ctl->new_keys)) defer_agg(&ctl->agg_deferred, agg_list, r, s1, s2);
+    }
+}
+__device__ __noinline__ void red_spill(const TableView& t, BatchCtl* ctl, uint32_t* deferred_list, uint32_t* cnt,
+                                       const uint4 r) {
+    atomicAdd(&cnt[C_SPILL], 1u);
+    if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
+        defer_packet(ctl, deferred_list, r.z, false);
+}
+
 __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
                                            uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp, bool ok,
                                            bool one_tb) {
     if (!ok || r.z == NO_REC) return;
     if (rec_is_agg(r)) {
-        if (rec_agg_slot(r) != 0) return;
-        const uint4 s1 = rp[1], s2 = rp[2];
-        const FlowAgg a = agg_decode(r, s1, s2);
-        const int e = lds_slot(ht, a.key, true);
-        if (e >= 0) {
-            lds_fold_agg(ht[e], a);
-        } else {
-            atomicAdd(&cnt[C_SPILL], 1u);
-            if (!merge_agg_probe(t, a, &ctl->new_keys)) defer_agg(&ctl->agg_deferred, agg_list, r, s1, s2);
-        }
+        red_agg(ht, t, ctl, agg_list, cnt, r, rp);
         return;
     }
-    const uint64_t lo = ((uint64_t)r.y << 32) | r.x;
-#ifdef IPXG_EXP_RED_NOFOLD  // timing experiment only: the record loads, no LDS table
-    if ((lo ^ r.z ^ r.w) == 0x1234567ull) atomicAdd(&cnt[C_SPILL], 1u);
-    return;
-#endif
-    const int e = lds_slot(ht, lo, true);
-#ifdef IPXG_EXP_RED_NOATOM  // timing experiment only: the LDS table lookups, no fold atomics
-    if (e >= 0 && r.w == 0x1234567u) atomicAdd(&cnt[C_SPILL], 1u);
-    if (e >= 0) return;
-#endif
-    if (e >= 0) {
-        lds_fold(ht[e], r.z, r.w, one_tb);
-    } else {
-        atomicAdd(&cnt[C_SPILL], 1u);
-        if (!merge_packet_atomic(t, lo, r.z, r.w, &ctl->new_keys)) defer_packet(ctl, deferred_list, r.z, false);
-    }
+    const int e = lds_slot(ht, ((uint64_t)r.y << 32) | r.x, true);
+    if (e >= 0) lds_fold(ht[e], r.z, r.w, one_tb);
+    else red_spill(t, ctl, deferred_list, cnt, r);
 }
 
 // One workgroup per partition: the partition's records sit in one segment per k_bin /
