@@ -554,20 +554,27 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             r0[q] = r1[q] = r2[q] = ix[q] = 0;
             rk[q] = NO_REC;
         }
+        // The wide walk's steps are unrolled DA at a time (the register rings' period), not all
+        // BIN_K: eight inlined copies of parse_medium made the kernel larger than the
+        // instruction cache.  (Record slot j is then a runtime index: tile_rank selects.)
+        constexpr int SU = WIDE ? DA : BIN_K;
+#pragma unroll 1
+        for (int g = 0; g < BIN_K; g += SU) {
 #pragma unroll
-        for (int j = 0; j < BIN_K; ++j) {
+        for (int jj = 0; jj < SU; ++jj) {
+            const int j = g + jj;
             const uint32_t i = tile + j * IPXG_BLOCK + tid;
             // this step's packet, loaded HA (head) and DA (descriptor) steps ago
-            const ipxg_pkt_desc dc = Dr[j % DA];
-            const Head<NC> hc = Hr[j % HA];
+            const ipxg_pkt_desc dc = Dr[jj % DA];
+            const Head<NC> hc = Hr[jj % HA];
             // bytes 40-43 are not parsed: keep their register live until here, or the compiler
             // reuses it while the load is in flight and must drain every load to do so
             asm volatile("" ::"v"(hc.c[2].z));
             // issue: the descriptor DA steps ahead, the head HA steps ahead
             const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
-            Dr[j % DA] = load_desc(rs_desc, ia);
-            const ipxg_pkt_desc dh = Dr[(j + HA) % DA];
-            Hr[j % HA] = load_head<NC>(rs_arena, dh, want(dh));
+            Dr[jj % DA] = load_desc(rs_desc, ia);
+            const ipxg_pkt_desc dh = Dr[(jj + HA) % DA];
+            Hr[jj % HA] = load_head<NC>(rs_arena, dh, want(dh));
             const bool act = i < b.n;
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
@@ -613,6 +620,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                     make_uint4(i | (slow_class(hc.c[0], hc.c[1], hc.c[2]) << 24), dc.offset,
                                (uint32_t)dc.caplen | ((uint32_t)dc.wirelen << 16), dc.ts_sec);
             if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix, tb_or);
+        }
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
