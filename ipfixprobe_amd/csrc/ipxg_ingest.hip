@@ -1191,6 +1191,23 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     HotSlot img[EPT];
     bool listed[EPT];
     bool failed = false;
+    // The thread's entries' home slots are read, and the empty ones claimed, together (one
+    // memory round trip for all of them, not one chain per entry); a home slot held by another
+    // key continues with the general probe.
+    uint64_t hkey[EPT];
+    unsigned long long old[EPT];
+#pragma unroll
+    for (uint32_t q = 0; q < EPT; ++q) {
+        hkey[q] = ht[tid + q * RED_THREADS].key;
+        if (hkey[q]) img[q] = t.hot[(uint32_t)hkey[q] & t.mask];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < EPT; ++q) {
+        old[q] = ~0ull;
+        if (hkey[q] && img[q].key == 0)
+            old[q] = atomicCAS((unsigned long long*)&t.hot[(uint32_t)hkey[q] & t.mask].key, 0ull,
+                               (unsigned long long)hkey[q]);
+    }
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q) {
         const uint32_t e = tid + q * RED_THREADS;
@@ -1199,9 +1216,20 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         listed[q] = false;
         if (a.key) {
             n_touch++;
-            bool claimed;
-            HotSlot* hp = probe_insert_full(t, a.key, img[q], claimed);  // this workgroup is the
-            if (claimed) n_keys++;                                       // slot's only writer here
+            bool claimed = false;
+            HotSlot* hp = &t.hot[(uint32_t)a.key & t.mask];  // this workgroup is the slot's only writer here
+            if (img[q].key == a.key) {
+                // found at home
+            } else if (img[q].key == 0 && old[q] == 0) {
+                img[q] = HotSlot{};
+                img[q].key = a.key;
+                claimed = true;
+            } else if (img[q].key == 0 && old[q] == a.key) {
+                img[q] = *hp;  // inserted meanwhile by another path
+            } else {
+                hp = probe_insert_full(t, a.key, img[q], claimed);
+            }
+            if (claimed) n_keys++;
             if (!hp) {
                 ht[e].tflags = a.tflags | RED_FAILED;
                 failed = true;

@@ -38,6 +38,10 @@ def main():
     names = ["tile start", "packet loop", "emit", "slow flush"]
     for k, nme in enumerate(names):
         print("k_bin %-12s %14.0f cycles summed over waves" % (nme, int(pc[k])))
+    for k, nme in ((4, "prefix+zero"), (5, "aggregate"), (6, "merge+list")):
+        print("k_reduce %-12s %14.0f cycles summed over workgroups" % (nme, int(pc[k])))
+    print("k_reduce avg %.4f ms, k_fin_list avg %.4f ms" % (tm["reduce_ms"] / max(tm["reduce_launches"], 1),
+                                                        tm["fin_ms"] / max(tm["reduce_launches"], 1)))
 
 
 if __name__ == "__main__":
