@@ -104,7 +104,7 @@ struct ipxg_engine {
     bool strict = false;
     StrictView sv = {};
     uint64_t strict_q = 0;  // sweep steps taken (keyed packets + expire calls): the cursor
-    DevBuf st_pkt, st_crec, st_keyed, st_qx, st_keys, st_vals, st_keys2, st_vals2, st_start, st_evpos;
+    DevBuf st_pkt, st_crec, st_keyed, st_qx, st_keys, st_vals, st_keys2, st_vals2, st_succ, st_pred, st_indeg, st_queue;
     // host-side counters
     uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0, walked_pkts = 0;
     bool prev_valid = false;
@@ -425,7 +425,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
         return fail(IPXG_EDEVICE);
     if (e->cfg.flags & IPXG_CFG_STRICT) {
-        if (cfg->line_exp > 4 || cfg->line_exp > cfg->cache_exp || cfg->cache_exp - cfg->line_exp > 15 ||
+        if (cfg->line_exp > 4 || cfg->line_exp > cfg->cache_exp || cfg->cache_exp - cfg->line_exp > 24 ||
             (cfg->flags & (IPXG_CFG_ATOMIC_INGEST | IPXG_CFG_PARSER_STATS)))
             return fail(IPXG_EINVAL);
         e->strict = true;
@@ -436,6 +436,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
         if (hipMalloc((void**)&e->sv.rec, (size_t)S * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
         if (hipMalloc((void**)&e->sv.hash, (size_t)S * 8) != hipSuccess) return fail(IPXG_ENOMEM);
         if (hipMalloc((void**)&e->sv.perm, (size_t)e->sv.lines * 8) != hipSuccess) return fail(IPXG_ENOMEM);
+        if (hipMalloc((void**)&e->sv.tlast, (size_t)S * 4) != hipSuccess) return fail(IPXG_ENOMEM);
         launch_strict_clear(e->st, e->sv);
         if (hipGetLastError() != hipSuccess) return fail(IPXG_EDEVICE);
     }
@@ -466,6 +467,7 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->sv.rec);
     hipFree(e->sv.hash);
     hipFree(e->sv.perm);
+    hipFree(e->sv.tlast);
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
     if (e->plan_h) hipHostFree(e->plan_h);
@@ -478,7 +480,8 @@ int ipxg_destroy(ipxg_engine* e) {
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
                       &e->ipf_tot, &e->ipf_off, &e->ipf_msg, &e->ipf_plan, &e->st_pkt, &e->st_crec, &e->st_keyed,
-                      &e->st_qx, &e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2, &e->st_start, &e->st_evpos})
+                      &e->st_qx, &e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2, &e->st_succ, &e->st_pred, &e->st_indeg,
+                      &e->st_queue})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -547,8 +550,10 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     if ((rc = ensure(e, e->st_qx, (size_t)n * 4))) return rc;
     for (DevBuf* b : {&e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2})
         if ((rc = ensure(e, *b, m * 4))) return rc;
-    if ((rc = ensure(e, e->st_start, (size_t)e->sv.lines * 4))) return rc;
-    if ((rc = ensure(e, e->st_evpos, (size_t)n * 16))) return rc;
+    if ((rc = ensure(e, e->st_succ, (size_t)n * 16))) return rc;   // per event slot: the line's next packet
+    if ((rc = ensure(e, e->st_pred, (size_t)n * 4))) return rc;    // per event slot: has a predecessor
+    if ((rc = ensure(e, e->st_indeg, (size_t)n * 4))) return rc;
+    if ((rc = ensure(e, e->st_queue, (size_t)n * 4 + 16))) return rc;  // ready queue + its initial count
     // every record alive now plus every record this batch creates may leave during it
     if ((rc = ensure_export(e, (size_t)e->sv.slot_mask + 1 + n))) return rc;
     HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
@@ -580,10 +585,14 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     HIPCHK(e, hipGetLastError());
     tb = e->sort_tmp.bytes;
     HIPCHK(e, sort_pairs_u32(e->sort_tmp.p, tb, ks, ks2, vs, vs2, (uint32_t)m, bits, e->st));
-    uint32_t* evpos = (uint32_t*)e->st_evpos.p;
-    launch_strict_positions(e->st, ks2, vs2, (uint32_t)m, e->sv.lines, (uint32_t*)e->st_start.p, evpos);
-    launch_strict_walk(e->st, e->sv, p, sp, crec, keyed, qx, evpos, n, e->strict_q, export_view(e), e->ctl_d,
-                       e->stats_d);
+    uint32_t* queue = (uint32_t*)e->st_queue.p;
+    uint32_t* q_count = queue + n;
+    HIPCHK(e, hipMemsetAsync(queue, 0xFF, (size_t)n * 4, e->st));  // STRICT_NONE: not filled yet
+    HIPCHK(e, hipMemsetAsync(q_count, 0, 4, e->st));
+    launch_strict_dag(e->st, ks2, vs2, (uint32_t)m, ks, keyed, n, e->sv.lines, (uint32_t*)e->st_succ.p,
+                      (uint8_t*)e->st_pred.p, (uint32_t*)e->st_indeg.p, queue, q_count);
+    launch_strict_walk(e->st, e->sv, p, sp, crec, keyed, qx, (const uint32_t*)e->st_succ.p, (uint32_t*)e->st_indeg.p,
+                       queue, q_count, n, e->strict_q, export_view(e), e->ctl_d, e->stats_d);
     HIPCHK(e, hipGetLastError());
     ev_rec(e, 1);
     uint32_t tail[2] = {0, 0};  // the last packet's keyed rank and mark: keyed packets in the batch

@@ -126,6 +126,7 @@ struct StrictView {
     ipxg_flow_record* rec;  // 2^s records, [line << line_bits | slot]
     uint64_t* hash;         // their FlowRecord::m_hash (0 = empty)
     uint64_t* perm;         // per line: position j -> record slot, bits 4j..4j+3
+    uint32_t* tlast;        // per slot: the record's time_last_sec, 0xFFFFFFFF while empty (the sweep's test)
     uint32_t line_bits;     // l= (line size 2^l, at most 16)
     uint32_t lines;         // 2^s >> l
     uint32_t slot_mask;     // 2^s - 1
@@ -138,10 +139,9 @@ struct StrictPkt {          // what put_pkt_recursive reads of a keyed packet (h
     uint32_t pad;
 };
 static_assert(sizeof(StrictPkt) == 32, "");
-constexpr uint32_t STRICT_LANES = 1024;          // the replay's one workgroup
-constexpr uint32_t STRICT_MAX_LINES = 32768;     // per-line counters in its LDS (128 KiB)
+constexpr uint32_t STRICT_LANES = 768;           // the replay's one workgroup (3 waves per SIMD; the DAG is ~260 packets wide at the reference default)
 constexpr uint32_t STRICT_NONE = 0xFFFFFFFFu;
-constexpr uint32_t STRICT_SPIN_MAX = 1u << 24;   // rounds a lane may wait before giving up
+constexpr uint32_t STRICT_SPIN_MAX = 1u << 24;   // rounds a lane may wait for one queue entry before giving up
 
 struct BatchView {
     const uint8_t* arena;
@@ -314,12 +314,13 @@ void launch_strict_prep2(hipStream_t st, const BatchView& b, const Params& p, Fr
 void launch_strict_events(hipStream_t st, StrictView v, const StrictPkt* sp, const uint32_t* keyed,
                           const uint32_t* qx, uint32_t n, uint64_t q_base, uint32_t split, uint32_t* keys,
                           uint32_t* vals);
-void launch_strict_positions(hipStream_t st, const uint32_t* keys, const uint32_t* vals, uint32_t m, uint32_t lines,
-                             uint32_t* start, uint32_t* evpos);
+void launch_strict_dag(hipStream_t st, const uint32_t* keys_sorted, const uint32_t* vals_sorted, uint32_t m,
+                       const uint32_t* keys, const uint32_t* keyed, uint32_t n, uint32_t lines, uint32_t* succ,
+                       uint8_t* pred, uint32_t* indeg, uint32_t* queue, uint32_t* q_count);
 void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const StrictPkt* sp,
-                        const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx,
-                        const uint32_t* evpos, uint32_t n, uint64_t q_base, ExportView ex, BatchCtl* ctl,
-                        unsigned long long* stats);
+                        const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx, const uint32_t* succ,
+                        uint32_t* indeg, uint32_t* queue, const uint32_t* q_count, uint32_t n, uint64_t q_base,
+                        ExportView ex, BatchCtl* ctl, unsigned long long* stats);
 void launch_strict_expire(hipStream_t st, StrictView v, const Params& p, uint64_t q, int64_t now, ExportView ex,
                           BatchCtl* ctl, unsigned long long* stats);
 void launch_strict_finish(hipStream_t st, StrictView v, ExportView ex, BatchCtl* ctl, unsigned long long* stats);

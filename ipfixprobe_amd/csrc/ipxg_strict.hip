@@ -16,14 +16,20 @@
 //                    record the packet would create (FlowRecord::create, cache.cpp:94-132);
 //   k_strict_events  a keyed packet is an event on up to three lines: its forward line, its
 //                    inverse line and the line its sweep visits;
-//   (sort)           events by line, stably: each event's position in its line's sequence;
-//   k_strict_walk    the replay.  Packets are taken in index order by the 1024 lanes of ONE
-//                    workgroup; a lane processes its packet once every line it touches has
-//                    processed all earlier events (per-line counters in LDS), so every line sees
-//                    exactly the reference's sequence of operations while packets touching
-//                    disjoint lines proceed in parallel.  One workgroup: its lanes share one L1
-//                    and LDS, so the hand-off between two packets of a line needs only
-//                    workgroup-scope ordering (no cross-CU release/acquire).
+//   (sort)           events by line, stably: each line's sequence of packets;
+//   k_strict_dag     each event's successor on its line and whether it has a predecessor: the
+//                    per-line orders form a DAG over the packets (edges from lower to higher
+//                    index, at most three per packet);
+//   k_strict_ready   each packet's in-degree; the packets with none start the ready queue;
+//   k_strict_walk    the replay: the 1024 lanes of ONE workgroup take queue tickets in order; a
+//                    lane runs its ticket's packet once the entry is filled, then decrements its
+//                    successors' in-degrees and queues those that reach zero.  Every line sees
+//                    exactly the reference's sequence of operations (a topological order of the
+//                    DAG), packets touching disjoint lines proceed in parallel, and every lane
+//                    works on whatever is ready (round-robin packet ownership left most lanes of
+//                    a wave waiting on their one packet: 4 Mpkt/s).  One workgroup: its lanes
+//                    share one L1 and LDS, so the hand-off between two packets of a line needs
+//                    only workgroup-scope ordering (no cross-CU release/acquire).
 // The state: records [line * L + slot], their hashes (FlowRecord::m_hash, 0 = empty) and per
 // line the position -> slot permutation (4 bits per position) standing in for the
 // reference's pointer array m_flow_table: moves and evictions rewrite one 64-bit word.
@@ -121,21 +127,34 @@ __global__ __launch_bounds__(256) void k_strict_events(StrictView v, const Stric
     }
 }
 
-// position of each event in its line's (index-ordered) sequence
-__global__ __launch_bounds__(256) void k_strict_starts(const uint32_t* keys, uint32_t m, uint32_t lines,
-                                                       uint32_t* start) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t k = keys[i];
-    if (k < lines && (i == 0 || keys[i - 1] != k)) start[k] = i;
+// each event's successor on its line (STRICT_NONE: the line's last) and predecessor flag
+__global__ __launch_bounds__(256) void k_strict_dag(const uint32_t* keys, const uint32_t* vals, uint32_t m,
+                                                    uint32_t lines, uint32_t* succ, uint8_t* pred) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= m) return;
+    const uint32_t L = keys[e];
+    if (L >= lines) return;
+    const uint32_t v = vals[e];  // 4 * packet + event slot
+    succ[v] = e + 1 < m && keys[e + 1] == L ? vals[e + 1] >> 2 : STRICT_NONE;
+    pred[v] = e > 0 && keys[e - 1] == L ? 1 : 0;
 }
 
-__global__ __launch_bounds__(256) void k_strict_pos(const uint32_t* keys, const uint32_t* vals, uint32_t m,
-                                                    uint32_t lines, const uint32_t* start, uint32_t* evpos) {
+// in-degrees (events with a predecessor); the keyed packets with none go to the ready queue
+__global__ __launch_bounds__(256) void k_strict_ready(const uint32_t* keys, const uint8_t* pred, const uint32_t* keyed,
+                                                      uint32_t n, uint32_t lines, uint32_t* indeg, uint32_t* queue,
+                                                      uint32_t* q_count) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t k = keys[i];
-    if (k < lines) evpos[vals[i]] = i - start[k];
+    uint32_t d = 0;
+    bool ready = false;
+    if (i < n) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (keys[3 * i + j] < lines && pred[4 * i + j]) d++;
+        indeg[i] = d;
+        ready = keyed[i] && d == 0;
+    }
+    const uint32_t pos = wave_append(q_count, ready);
+    if (ready) queue[pos] = i;
 }
 
 // ---- the line permutation ---------------------------------------------------------------------
@@ -185,27 +204,57 @@ struct WalkCtx {
 };
 
 // export_flow (cache.cpp:262-274): the record leaves with its reason, its slot becomes empty
-__device__ __forceinline__ void strict_export(WalkCtx& w, uint32_t slot, const ipxg_flow_record& r, uint8_t reason) {
+// (the record as 32 words in registers, RecW: through ipxg_flow_record's byte fields it lived
+// in scratch memory)
+__device__ __forceinline__ void strict_export(WalkCtx& w, uint32_t slot, const RecW& r, uint8_t reason) {
     const uint32_t pos = atomicAdd(w.ex.count, 1u);
-    store_export(w.ex, pos, r, reason);
-    if (w.ex.count6 && r.ip_version == 6) atomicAdd(w.ex.count + 2, 1u);
-    count_export(w.sc, r, reason);
+    store_export_w(w.ex, pos, r, reason);
+    if (w.ex.count6 && rw_ipver(r) == 6) atomicAdd(w.ex.count + 2, 1u);
+    count_export_w(w.sc, r, reason);
     w.v.hash[slot] = 0;
+    w.v.tlast[slot] = 0xFFFFFFFFu;
     w.live--;
 }
 
-// export_expired (cache.cpp:508-523) at sweep step q: positions [q * L/2, +L/2) of the table
-__device__ void strict_sweep(WalkCtx& w, uint64_t q, int64_t ts) {
+// the sweep line's position -> slot map and its slots' time_last (prefetched with the packet's
+// own lines when the sweep visits a third line)
+struct SweepImg {
+    uint64_t perm;
+    uint32_t tl[16];
+};
+__device__ __forceinline__ void load_sweep(const StrictView& v, uint32_t line, SweepImg& si) {
+    const uint32_t L = 1u << v.line_bits;
+    si.perm = v.perm[line];
+    const uint32_t* tp = v.tlast + (size_t)line * L;
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) si.tl[r] = r < L ? tp[r] : 0xFFFFFFFFu;
+}
+
+// export_expired (cache.cpp:508-523) at sweep step q: positions [q * L/2, +L/2) of the table.
+// An empty slot's time_last is 0xFFFFFFFF, so it never tests idle; only the records that
+// leave are read.  pre: the line's map and time_last as loaded before this packet's own update
+// (valid when the sweep line is none of the packet's lookup lines).
+__device__ void strict_sweep(WalkCtx& w, uint64_t q, int64_t ts, const SweepImg* pre = nullptr) {
     const StrictView& v = w.v;
     const uint32_t L = 1u << v.line_bits, half = L >> 1;
     const uint32_t at = (uint32_t)((q * half) & v.slot_mask);
     const uint32_t line = at >> v.line_bits, off = at & (L - 1u);
-    const uint64_t perm = v.perm[line];
-    for (uint32_t j = off; j < off + half; ++j) {
-        const uint32_t slot = line * L + nib(perm, j);
-        if (v.hash[slot] == 0) continue;
-        const ipxg_flow_record r = v.rec[slot];
-        if (ts - (int64_t)r.time_last_sec >= (int64_t)w.inactive) strict_export(w, slot, r, export_reason(r));
+    SweepImg si;
+    if (pre) si = *pre;
+    else load_sweep(v, line, si);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t j = off + k;
+        if (k >= half) break;
+        const uint32_t r = nib(si.perm, j);
+        uint32_t tl = si.tl[0];
+#pragma unroll
+        for (uint32_t x = 1; x < 16; ++x) tl = r == x ? si.tl[x] : tl;  // (selects: no indexed copy)
+        if (ts - (int64_t)tl >= (int64_t)w.inactive) {
+            const uint32_t slot = line * L + r;
+            const RecW rec = rec_load_w(&v.rec[slot]);
+            strict_export(w, slot, rec, export_reason_w(rec));
+        }
     }
 }
 
@@ -218,9 +267,21 @@ __device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_re
     strict_lines(v, s, q, split, ln);
     const uint32_t lf = ln[0];
     const uint32_t li_line = split ? lf : (uint32_t)(s.h_inv & (v.slot_mask & ~(L - 1u))) >> v.line_bits;
+    // The packet's lines are loaded together up front: the forward line, the inverse line (read
+    // only when the forward search misses, about every other packet) and the line its sweep
+    // visits -- no other packet touches them until this one is done (the DAG), so the images
+    // stay valid until this packet changes them itself.
+    LineImg F, I;
+    SweepImg S;
+    const bool pre_sweep = half && ln[2] != STRICT_NONE;
+    load_line(v, lf, F);
+    if (!split) load_line(v, li_line, I);
+    if (pre_sweep) load_sweep(v, ln[2], S);
     for (int depth = 0; depth < 8; ++depth) {  // the recursion after an export (at most twice)
-        LineImg F;
-        load_line(v, lf, F);
+        if (depth) {  // an export changed the table: read the lines again
+            load_line(v, lf, F);
+            if (!split) load_line(v, li_line, I);
+        }
         uint32_t line = lf, pos = 0;
         bool found = false, src = true;
         uint64_t perm = F.perm;
@@ -229,8 +290,6 @@ __device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_re
             found = true;
             pos = __builtin_ctz(pm);
         } else if (!split) {
-            LineImg I;
-            load_line(v, li_line, I);
             pm = match_pos(I, L, s.h_inv);
             if (pm) {
                 found = true;
@@ -250,7 +309,7 @@ __device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_re
                 pos = __builtin_ctz(em);
             } else {  // line full: the last position leaves (NO_RES), its slot re-enters at L/2 (:400-419)
                 const uint32_t slot = lf * L + nib(perm, L - 1);
-                const ipxg_flow_record ev = v.rec[slot];
+                const RecW ev = rec_load_w(&v.rec[slot]);
                 strict_export(w, slot, ev, IPXG_FLOW_END_NO_RES);
                 perm = perm_move(perm, L - 1, half);
                 v.perm[lf] = perm;
@@ -259,103 +318,109 @@ __device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_re
         }
         const uint32_t slot = line * L + nib(perm, pos);
         if (!found) {  // FlowRecord::create (:440-443)
-            ipxg_flow_record r = *crec_i;
-            v.rec[slot] = r;
+            const RecW r = rec_load_w(crec_i);
+            rec_store_w(&v.rec[slot], r);
             v.hash[slot] = s.h_fwd;
+            v.tlast[slot] = r.w[RW_TLS];
             w.live++;
             break;
         }
-        ipxg_flow_record r = v.rec[slot];
-        const uint8_t flw = src ? r.src_tcp_flags : r.dst_tcp_flags;
+        RecW r = rec_load_w(&v.rec[slot]);
+        const uint32_t flw = src ? rw_sflags(r) : rw_dflags(r);
         if ((s.tcp_flags & 0x02) && (flw & 0x05)) {  // SYN after FIN/RST (:431-438)
             strict_export(w, slot, r, IPXG_FLOW_END_EOF);
             continue;
         }
-        if ((int64_t)s.ts_sec - (int64_t)r.time_last_sec >= (int64_t)w.inactive) {  // :453-461
-            strict_export(w, slot, r, export_reason(r));
+        if ((int64_t)s.ts_sec - (int64_t)r.w[RW_TLS] >= (int64_t)w.inactive) {  // :453-461
+            strict_export(w, slot, r, export_reason_w(r));
             continue;
         }
-        if ((int64_t)s.ts_sec - (int64_t)r.time_first_sec >= (int64_t)w.active) {  // :464-472
+        if ((int64_t)s.ts_sec - (int64_t)r.w[RW_TFS] >= (int64_t)w.active) {  // :464-472
             strict_export(w, slot, r, IPXG_FLOW_END_ACTIVE);
             continue;
         }
-        r.time_last_sec = s.ts_sec;  // FlowRecord::update (:134-152)
-        r.time_last_usec = s.ts_usec;
+        r.w[RW_TLS] = s.ts_sec;  // FlowRecord::update (:134-152)
+        r.w[RW_TLU] = s.ts_usec;
+        const uint32_t fl = s.ip_proto == 6 ? s.tcp_flags : 0u;
         if (src) {
-            r.src_packets++;
-            r.src_bytes += s.ip_len;
-            if (s.ip_proto == 6) r.src_tcp_flags |= s.tcp_flags;
+            r.w[RW_SPK]++;
+            rw64_set(r, RW_SBYTES, rw64(r, RW_SBYTES) + s.ip_len);
+            r.w[RW_FLAGS] |= fl;
         } else {
-            r.dst_packets++;
-            r.dst_bytes += s.ip_len;
-            if (s.ip_proto == 6) r.dst_tcp_flags |= s.tcp_flags;
+            r.w[RW_DPK]++;
+            rw64_set(r, RW_DBYTES, rw64(r, RW_DBYTES) + s.ip_len);
+            r.w[RW_FLAGS] |= fl << 8;
         }
-        v.rec[slot] = r;
+        rec_store_w(&v.rec[slot], r);
+        v.tlast[slot] = s.ts_sec;
         break;
     }
     // export_expired (:508-523): positions [q * L/2, +L/2) of the table, idle against this packet
-    if (half) strict_sweep(w, q, (int64_t)s.ts_sec);
+    if (half) strict_sweep(w, q, (int64_t)s.ts_sec, pre_sweep ? &S : nullptr);
 }
 
-__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// One workgroup: lane t takes packets t, t + 1024, ...; see the file comment.  A lane whose
-// lines are not ready spins (bounded: a lane that waits STRICT_SPIN_MAX rounds in a row gives up
-// and flags ctl->strict_fail -- the replay cannot deadlock, the bound guards engine bugs).
+// One workgroup: the DAG scheduler of the file comment.  A lane holds one ticket (a queue
+// position) at a time and runs the ticket's packet once a predecessor (or k_strict_ready) has
+// filled it; the ticket count is the batch's keyed packets, so every lane ends.  A lane that
+// waits STRICT_SPIN_MAX rounds for one entry gives up and stops the workgroup (ctl->strict_fail;
+// the scheduler cannot deadlock -- the lowest unfinished packet is always queued -- the bound
+// guards engine bugs).
 __global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Params p, const StrictPkt* sp,
                                                               const ipxg_flow_record* crec, const uint32_t* keyed,
-                                                              const uint32_t* qx, const uint32_t* evpos, uint32_t n,
-                                                              uint64_t q_base, ExportView ex, BatchCtl* ctl,
+                                                              const uint32_t* qx, const uint32_t* succ,
+                                                              uint32_t* indeg, uint32_t* queue,
+                                                              const uint32_t* q_count, uint32_t n, uint64_t q_base,
+                                                              ExportView ex, BatchCtl* ctl,
                                                               unsigned long long* stats) {
-    __shared__ uint32_t ctr[STRICT_MAX_LINES];
+    __shared__ uint32_t head, tail, stop;
     __shared__ uint32_t sc[ST_COUNT];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t l = tid; l < v.lines; l += STRICT_LANES) ctr[l] = 0;
+    if (tid == 0) {
+        head = 0;
+        tail = *q_count;
+        stop = 0;
+    }
     if (tid < ST_COUNT) sc[tid] = 0;
     __syncthreads();
+    const uint32_t K = n ? qx[n - 1] + keyed[n - 1] : 0;  // keyed packets = tickets
     WalkCtx w{v, ex, sc, 0, p.inactive_s, p.active_s};
-    uint32_t spins = 0;
+    uint32_t t = atomicAdd(&head, 1u), spins = 0;
     bool failed = false;
-    // this lane's next keyed packet: its fields, sweep step, lines and event positions
-    uint32_t k = tid;
-    StrictPkt s = {};
-    uint64_t q = 0;
-    uint32_t ln[3] = {STRICT_NONE, STRICT_NONE, STRICT_NONE}, want[3] = {0, 0, 0};
-    auto advance = [&](uint32_t from) {
-        while (from < n && !keyed[from]) from += STRICT_LANES;
-        k = from;
-        if (k >= n) return;
-        s = sp[k];
-        q = q_base + qx[k];
-        strict_lines(v, s, q, p.split_biflow, ln);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) want[j] = ln[j] == STRICT_NONE ? 0 : evpos[4 * k + j];
-    };
-    advance(tid);
-    while (__any(k < n)) {
+    while (__any(t < K)) {
         bool progressed = false;
-        if (k < n) {
-            bool ready = true;
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-                if (ln[j] != STRICT_NONE && lds_ld(&ctr[ln[j]]) != want[j]) ready = false;
-            if (ready) {
+        if (t < K) {
+            // poll the queue's LDS tail; the global entry is read only once it is due (1024 lanes
+            // polling global memory queued the working lanes' loads behind theirs)
+            const bool due = t < __hip_atomic_load(&tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t pk = due ? __hip_atomic_load(&queue[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                    : STRICT_NONE;
+            if (pk != STRICT_NONE) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                strict_packet(w, s, crec + k, q, p.split_biflow);
+                const StrictPkt s = sp[pk];
+                const uint64_t q = q_base + qx[pk];
+                strict_packet(w, s, crec + pk, q, p.split_biflow);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's table stores are done
+                uint32_t ln[3];
+                strict_lines(v, s, q, p.split_biflow, ln);
 #pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    if (ln[j] != STRICT_NONE)
-                        __hip_atomic_store(&ctr[ln[j]], want[j] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                advance(k + STRICT_LANES);
+                for (int j = 0; j < 3; ++j) {
+                    const uint32_t nx = ln[j] == STRICT_NONE ? STRICT_NONE : succ[4 * pk + j];
+                    if (nx == STRICT_NONE) continue;
+                    if (__hip_atomic_fetch_add(&indeg[nx], 0xFFFFFFFFu, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u) {
+                        const uint32_t at = atomicAdd(&tail, 1u);
+                        __hip_atomic_store(&queue[at], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                t = atomicAdd(&head, 1u);
                 progressed = true;
                 spins = 0;
-            } else if (++spins > STRICT_SPIN_MAX) {
-                failed = true;
-                k = n;  // give up (engine bug): the host reports it
+            } else if (++spins > STRICT_SPIN_MAX || __hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                if (spins > STRICT_SPIN_MAX) {
+                    failed = true;
+                    atomicOr(&stop, 1u);
+                }
+                t = K;  // give up (engine bug): the host reports it
             }
         }
         if (!__any(progressed)) __builtin_amdgcn_s_sleep(2);
@@ -388,8 +453,7 @@ __global__ __launch_bounds__(256) void k_strict_finish(StrictView v, ExportView 
     WalkCtx w{v, ex, sc, 0, 0, 0};
     for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s <= v.slot_mask; s += gridDim.x * 256) {
         if (v.hash[s] == 0) continue;
-        const ipxg_flow_record r = v.rec[s];
-        strict_export(w, s, r, IPXG_FLOW_END_FORCED);
+        strict_export(w, s, rec_load_w(&v.rec[s]), IPXG_FLOW_END_FORCED);
     }
     if (w.live) atomicAdd(&ctl->strict_live, w.live);
     flush_block_stats(sc, stats);
@@ -402,6 +466,7 @@ __global__ __launch_bounds__(256) void k_strict_clear(StrictView v) {
     for (uint32_t j = 0; j < L; ++j) id |= (uint64_t)j << (4 * j);
     for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s <= v.slot_mask; s += gridDim.x * 256) {
         v.hash[s] = 0;
+        v.tlast[s] = 0xFFFFFFFFu;
         if (s < v.lines) v.perm[s] = id;
     }
 }
@@ -431,18 +496,21 @@ void launch_strict_events(hipStream_t st, StrictView v, const StrictPkt* sp, con
                        keys, vals);
 }
 
-void launch_strict_positions(hipStream_t st, const uint32_t* keys, const uint32_t* vals, uint32_t m, uint32_t lines,
-                             uint32_t* start, uint32_t* evpos) {
-    hipLaunchKernelGGL(k_strict_starts, dim3((m + 255) / 256), dim3(256), 0, st, keys, m, lines, start);
-    hipLaunchKernelGGL(k_strict_pos, dim3((m + 255) / 256), dim3(256), 0, st, keys, vals, m, lines, start, evpos);
+void launch_strict_dag(hipStream_t st, const uint32_t* keys_sorted, const uint32_t* vals_sorted, uint32_t m,
+                       const uint32_t* keys, const uint32_t* keyed, uint32_t n, uint32_t lines, uint32_t* succ,
+                       uint8_t* pred, uint32_t* indeg, uint32_t* queue, uint32_t* q_count) {
+    hipLaunchKernelGGL(k_strict_dag, dim3((m + 255) / 256), dim3(256), 0, st, keys_sorted, vals_sorted, m, lines, succ,
+                       pred);
+    hipLaunchKernelGGL(k_strict_ready, dim3((n + 255) / 256), dim3(256), 0, st, keys, pred, keyed, n, lines, indeg,
+                       queue, q_count);
 }
 
 void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const StrictPkt* sp,
-                        const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx,
-                        const uint32_t* evpos, uint32_t n, uint64_t q_base, ExportView ex, BatchCtl* ctl,
-                        unsigned long long* stats) {
-    hipLaunchKernelGGL(k_strict_walk, dim3(1), dim3(STRICT_LANES), 0, st, v, p, sp, crec, keyed, qx, evpos, n, q_base,
-                       ex, ctl, stats);
+                        const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx, const uint32_t* succ,
+                        uint32_t* indeg, uint32_t* queue, const uint32_t* q_count, uint32_t n, uint64_t q_base,
+                        ExportView ex, BatchCtl* ctl, unsigned long long* stats) {
+    hipLaunchKernelGGL(k_strict_walk, dim3(1), dim3(STRICT_LANES), 0, st, v, p, sp, crec, keyed, qx, succ, indeg, queue,
+                       q_count, n, q_base, ex, ctl, stats);
 }
 
 void launch_strict_expire(hipStream_t st, StrictView v, const Params& p, uint64_t q, int64_t now, ExportView ex,

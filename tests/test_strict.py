@@ -98,6 +98,14 @@ def test_strict_fuzz_corpus():
 
 
 @pytest.mark.gpu
+def test_strict_large_table():
+    """2^16 lines (past the per-line LDS counters of the first replay; the DAG scheduler has no
+    line limit): a stream whose flows spread over the table, every record still bit-exact."""
+    arena, desc = synth.flow_stream(seed=35, n_flows=4000, n_pkts=30000, v6_share=0.2).batch()
+    _check(arena, desc, "s=20", batch=7000)
+
+
+@pytest.mark.gpu
 def test_strict_one_hot_line():
     """Every packet of one flow (a chain of dependent events on one line) plus a few others."""
     arena, desc = synth.flow_stream(seed=34, n_flows=3, n_pkts=20000, frag=False).batch()
@@ -122,7 +130,7 @@ def test_strict_reproduces_reference_golden(name):
 @pytest.mark.gpu
 def test_strict_rejects_what_it_does_not_replay():
     from ipfixprobe_amd import Engine, IpxgError
-    for bad in ("strict=true;l=5", "strict=true;s=20;l=4", "strict=true;ingest=atomic", "strict=true;ps=true"):
+    for bad in ("strict=true;l=5", "strict=true;s=29;l=4", "strict=true;ingest=atomic", "strict=true;ps=true"):
         with pytest.raises(IpxgError):
             Engine(bad)
     import plugins_py
