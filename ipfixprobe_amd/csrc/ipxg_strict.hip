@@ -359,12 +359,11 @@ __device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_re
     if (half) strict_sweep(w, q, (int64_t)s.ts_sec, pre_sweep ? &S : nullptr);
 }
 
-// One workgroup: the DAG scheduler of the file comment.  A lane holds one ticket (a queue
-// position) at a time and runs the ticket's packet once a predecessor (or k_strict_ready) has
-// filled it; the ticket count is the batch's keyed packets, so every lane ends.  A lane that
-// waits STRICT_SPIN_MAX rounds for one entry gives up and stops the workgroup (ctl->strict_fail;
-// the scheduler cannot deadlock -- the lowest unfinished packet is always queued -- the bound
-// guards engine bugs).
+// One workgroup: the DAG scheduler of the file comment.  An idle lane holds one ticket (a queue
+// position) and runs the ticket's packet once a predecessor (or k_strict_ready) has filled it.
+// A lane that waits STRICT_SPIN_MAX rounds gives up and stops the workgroup (ctl->strict_fail;
+// the scheduler cannot deadlock -- the lowest unfinished packet is always running or queued at
+// a position some lane's ticket reaches -- the bound guards engine bugs).
 __global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Params p, const StrictPkt* sp,
                                                               const ipxg_flow_record* crec, const uint32_t* keyed,
                                                               const uint32_t* qx, const uint32_t* succ,
@@ -372,56 +371,76 @@ __global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Para
                                                               const uint32_t* q_count, uint32_t n, uint64_t q_base,
                                                               ExportView ex, BatchCtl* ctl,
                                                               unsigned long long* stats) {
-    __shared__ uint32_t head, tail, stop;
+    __shared__ uint32_t head, tail, stop, done;
     __shared__ uint32_t sc[ST_COUNT];
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
         head = 0;
         tail = *q_count;
         stop = 0;
+        done = 0;
     }
     if (tid < ST_COUNT) sc[tid] = 0;
     __syncthreads();
     const uint32_t K = n ? qx[n - 1] + keyed[n - 1] : 0;  // keyed packets = tickets
     WalkCtx w{v, ex, sc, 0, p.inactive_s, p.active_s};
-    uint32_t t = atomicAdd(&head, 1u), spins = 0;
-    bool failed = false;
-    while (__any(t < K)) {
+    // A lane that makes a successor ready runs it next itself (the chain's hand-off costs no queue
+    // round trip and no wait for another wave's poll); further ready successors are queued.  An
+    // idle lane holds one ticket; every lane stops when all K keyed packets are done.
+    constexpr uint32_t NO_TICKET = 0xFFFFFFFFu;
+    uint32_t t = NO_TICKET, cur = STRICT_NONE, spins = 0;
+    bool failed = false, fin = K == 0;
+    while (__any(!fin)) {
         bool progressed = false;
-        if (t < K) {
-            // poll the queue's LDS tail; the global entry is read only once it is due (1024 lanes
+        if (!fin && cur == STRICT_NONE) {
+            if (t == NO_TICKET) t = atomicAdd(&head, 1u);
+            // poll the queue's LDS tail; the global entry is read only once it is due (lanes
             // polling global memory queued the working lanes' loads behind theirs)
             const bool due = t < __hip_atomic_load(&tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const uint32_t pk = due ? __hip_atomic_load(&queue[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
                                     : STRICT_NONE;
             if (pk != STRICT_NONE) {
+                cur = pk;
+                t = NO_TICKET;
+                spins = 0;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const StrictPkt s = sp[pk];
-                const uint64_t q = q_base + qx[pk];
-                strict_packet(w, s, crec + pk, q, p.split_biflow);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's table stores are done
-                uint32_t ln[3];
-                strict_lines(v, s, q, p.split_biflow, ln);
+            } else if (__hip_atomic_load(&done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= K ||
+                       __hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                fin = true;  // every packet done (this ticket is never filled), or a lane gave up
+            } else if (++spins > STRICT_SPIN_MAX) {
+                failed = true;  // engine bug: the host reports it
+                atomicOr(&stop, 1u);
+                fin = true;
+            }
+        }
+        if (!fin && cur != STRICT_NONE) {
+            const uint32_t pk = cur;
+            const StrictPkt s = sp[pk];
+            const uint64_t q = q_base + qx[pk];
+            uint32_t nxt[3];  // the packet's successors, read with its fields (not after its update)
 #pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const uint32_t nx = ln[j] == STRICT_NONE ? STRICT_NONE : succ[4 * pk + j];
-                    if (nx == STRICT_NONE) continue;
-                    if (__hip_atomic_fetch_add(&indeg[nx], 0xFFFFFFFFu, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u) {
+            for (int j = 0; j < 3; ++j) nxt[j] = succ[4 * pk + j];
+            strict_packet(w, s, crec + pk, q, p.split_biflow);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's table stores are done
+            uint32_t ln[3];
+            strict_lines(v, s, q, p.split_biflow, ln);
+            cur = STRICT_NONE;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint32_t nx = ln[j] == STRICT_NONE ? STRICT_NONE : nxt[j];
+                if (nx == STRICT_NONE) continue;
+                if (__hip_atomic_fetch_add(&indeg[nx], 0xFFFFFFFFu, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u) {
+                    if (cur == STRICT_NONE) {
+                        cur = nx;  // run it next, on this lane
+                    } else {
                         const uint32_t at = atomicAdd(&tail, 1u);
                         __hip_atomic_store(&queue[at], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
-                t = atomicAdd(&head, 1u);
-                progressed = true;
-                spins = 0;
-            } else if (++spins > STRICT_SPIN_MAX || __hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                if (spins > STRICT_SPIN_MAX) {
-                    failed = true;
-                    atomicOr(&stop, 1u);
-                }
-                t = K;  // give up (engine bug): the host reports it
             }
+            atomicAdd(&done, 1u);
+            progressed = true;
         }
         if (!__any(progressed)) __builtin_amdgcn_s_sleep(2);
     }
