@@ -45,6 +45,9 @@ struct ipxg_engine {
     ipxg_flow_record* ex = nullptr;
     uint32_t ex_cap = 0;
     uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag, [2] IPv6 records (ctl block)
+    // ipxg_clear_exports' zeroing of ex_count_d, deferred to the next device work on exports (the
+    // next submit folds it into its control-block memset: one fill command per step, not two)
+    bool ex_zero_pending = false;
     uint32_t ex_count = 0, ex_head = 0;
     uint32_t ex_count6 = 0;          // [2] at the last readback
     bool ex6_valid = false;          // [2] counts exactly the records [0, ex_count) (ex_head == 0)
@@ -161,6 +164,10 @@ static TableView table_view(ipxg_engine* e) {
 }
 
 static ExportView export_view(ipxg_engine* e) {
+    if (e->ex_zero_pending) {  // every kernel that appends exports gets its view here
+        e->ex_zero_pending = false;
+        (void)hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st);
+    }
     return ExportView{e->ex, e->ex_count_d, e->ex_cap, e->count6_on ? 1u : 0u};
 }
 
@@ -279,6 +286,7 @@ static hipError_t stream_wait(hipStream_t st) {
 }
 
 static int check_ex(ipxg_engine* e) {
+    if (e->ex_zero_pending) return IPXG_OK;  // the device counters are stale until zeroed; the host's are 0
     e->ex_count = ex_host(e)[0];
     e->ex_count6 = ex_host(e)[2];
     if (ex_host(e)[1]) return set_err(e, IPXG_EDEVICE, "export buffer overflow (engine bug: capacity under-sized)");
@@ -666,7 +674,13 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         bv.desc = (const ipxg_pkt_desc*)e->desc.p;
     }
     bv.base_sec = BASE_FROM_DESC0;  // kernels read desc[0] themselves (no host round trip)
-    if (e->strict) return strict_submit(e, bv, n);
+    if (e->strict) {
+        if (e->ex_zero_pending) {
+            e->ex_zero_pending = false;
+            HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+        }
+        return strict_submit(e, bv, n);
+    }
     // per-batch scratch sized for the worst case (every packet deferred / a fragment)
     if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
     if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
@@ -678,7 +692,10 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
     }
     if ((rc = ensure_export(e, n))) return rc;
-    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+    // the control block, and the export counters when a clear is pending (they follow it)
+    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, e->ex_zero_pending ? CTL_EX_OFF + 3 * sizeof(uint32_t) : sizeof(BatchCtl),
+                             e->st));
+    e->ex_zero_pending = false;
 
     Params p = params(e);
     FragView fv = frag_view(e);
@@ -994,6 +1011,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         uint32_t c3[3] = {e->ex_count + (uint32_t)nx, 0, e->ex_count6};
         for (const ipxg_flow_record& r : wo.ex) c3[2] += r.ip_version == 6 ? 1 : 0;
         HIPCHK(e, hipMemcpyAsync(e->ex_count_d, c3, sizeof(c3), hipMemcpyHostToDevice, e->st));
+        e->ex_zero_pending = false;  // all three counters written
         e->ex_count = c3[0];
         e->ex_count6 = c3[2];
     }
@@ -1327,6 +1345,7 @@ int ipxg_reset(ipxg_engine* e) {
     const uint32_t fs = e->cfg.frag_size ? e->cfg.frag_size : 10007;
     HIPCHK(e, hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st));
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+    e->ex_zero_pending = false;
     if (e->pstat_d) HIPCHK(e, hipMemsetAsync(e->pstat_d, 0, PSTAT_WORDS * 8, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->ex_count = e->ex_head = 0;
@@ -1366,6 +1385,7 @@ int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t*
         e->ex_head = e->ex_count = 0;
         e->ex6_valid = e->count6_on;
         HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+        e->ex_zero_pending = false;
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     *n = k;
@@ -1434,6 +1454,7 @@ int ipxg_poll_ipfix(ipxg_engine* e, uint32_t dir_bit_field, uint8_t* out, size_t
         e->ex_head = e->ex_count = 0;
         e->ex6_valid = e->count6_on;
         HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+        e->ex_zero_pending = false;
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     *n = k;
@@ -1665,6 +1686,7 @@ int ipxg_device_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const uin
     e->ex_head = e->ex_count = 0;  // consumed
     e->ex6_valid = e->count6_on;
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+    e->ex_zero_pending = false;
     return IPXG_OK;
 }
 
@@ -1689,6 +1711,7 @@ int ipxg_poll_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, uint8_t* ou
     e->ex_head = e->ex_count = 0;
     e->ex6_valid = e->count6_on;
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
+    e->ex_zero_pending = false;
     HIPCHK(e, hipStreamSynchronize(e->st));
     *x = y;
     *n_records = pend;
@@ -1716,7 +1739,7 @@ int ipxg_clear_exports(ipxg_engine* e) {
     }
     e->ex_head = e->ex_count = 0;
     e->ex6_valid = e->count6_on;
-    HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));  // ordered on the stream
+    e->ex_zero_pending = true;  // zeroed on the stream before the next export append (export_view / submit)
     return IPXG_OK;
 }
 
