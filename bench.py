@@ -484,12 +484,13 @@ def main():
                     help="strict mode with the reference's table of 2^S records (S=17: its default): "
                          "its evictions and sweep replayed exactly (ipxg_strict.hip)")
     args = ap.parse_args()
-    dflt = {"udp64": (10_000_000, 1, 100_000, 20), "imix": (10_000_000, 10, 1_000_000, 5),
+    dflt = {"udp64": (10_000_000, 1, 100_000, 3000), "imix": (10_000_000, 10, 1_000_000, 5),
             "quic": (5_000_000, 4, 1_000_000, 10)}[args.workload]
     args.packets = args.packets or dflt[0]
     args.batches = args.batches or dflt[1]
     args.flows = args.flows or dflt[2]
-    args.steps = args.steps or dflt[3]
+    # (stream mode keeps one descriptor array per step: 160 MB each at 10M packets)
+    args.steps = args.steps or (50 if args.workload == "udp64" and args.mode == "stream" else dflt[3])
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
