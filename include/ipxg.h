@@ -465,6 +465,22 @@ typedef struct ipxg_capture {
 int ipxg_capture_load(const char* path, ipxg_capture** out);
 void ipxg_capture_free(ipxg_capture* cap);
 
+/* ---- multi-GPU host demux (SURVEY 8(e) "input distribution", 8(f) row 3) ---------------
+ * The host side of the end-to-end multi-GPU path: which engine (one per GPU, each with its
+ * own table) takes each packet of a host batch -- the analogue of the NIC's symmetric RSS
+ * into per-queue rings (dpdkDevice.cpp:230-262; one pipeline per queue, ipfixprobe.cpp:381-464).
+ * shard = a symmetric hash of the outermost IP address pair, found through Ethernet, VLAN/QinQ
+ * tags, MPLS labels and PPPoE (the link types of ipxg_batch; SLL/SLL2/RAW too), so both
+ * directions of a biflow and every fragment of a datagram go to the same engine; frames
+ * without an IP header go to shard 0.  Reads at most the first 64 header bytes per frame.
+ * shard_of[i] (n entries) receives packet i's shard; counts[k] (n_shards) the shard sizes.
+ * ipxg_demux_split then gathers shard k's frames into its own batch (arena at 16-byte aligned
+ * offsets, descriptors in arrival order): arena_out must hold ipxg_demux_arena_bytes(...). */
+int ipxg_demux(const ipxg_batch* in, uint32_t datalink, uint32_t n_shards, uint32_t* shard_of, uint32_t* counts);
+uint64_t ipxg_demux_arena_bytes(const ipxg_batch* in, const uint32_t* shard_of, uint32_t shard);
+int ipxg_demux_split(const ipxg_batch* in, const uint32_t* shard_of, uint32_t shard, uint8_t* arena_out,
+                     ipxg_pkt_desc* desc_out, uint32_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,6 +100,7 @@ EXPORTED_SYMBOLS = [
     "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
     "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
     "ipxg_parser_stats", "ipxg_top_ports", "ipxg_add_plugin",
+    "ipxg_demux", "ipxg_demux_arena_bytes", "ipxg_demux_split",
 ]
 
 FLOW_FLUSH = 0x1
@@ -195,8 +196,12 @@ def lib():
         L.ipxg_top_ports.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
         L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                  ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.ipxg_demux.argtypes = [ctypes.POINTER(Batch), u32, u32, vp, vp]
+        L.ipxg_demux_arena_bytes.argtypes = [ctypes.POINTER(Batch), vp, u32]
+        L.ipxg_demux_arena_bytes.restype = ctypes.c_uint64
+        L.ipxg_demux_split.argtypes = [ctypes.POINTER(Batch), vp, u32, vp, vp, ctypes.POINTER(u32)]
         for name in EXPORTED_SYMBOLS:
-            if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default",
+            if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default", "ipxg_demux_arena_bytes",
                             "ipxg_capture_free", "ipxg_ipfix_exporter_init", "ipxg_ipfix_bound"):
                 getattr(L, name).restype = ctypes.c_int
         _LIB = L
@@ -235,6 +240,31 @@ def load_capture(path):
         return arena, desc, int(c.datalink)
     finally:
         lib().ipxg_capture_free(p)
+
+
+def demux(arena, desc, n_shards, datalink=DLT_EN10MB):
+    """Host symmetric demux (ipxg_demux / ipxg_demux_split): one (arena, desc) batch per shard,
+    packets in arrival order, each shard's frames copied into its own arena -- the per-GPU rings
+    of the end-to-end multi-GPU path.  Returns (batches, shard_of)."""
+    b = Engine._batch(arena, desc)
+    n = int(b.n)
+    shard_of = np.zeros(n, dtype=np.uint32)
+    counts = np.zeros(n_shards, dtype=np.uint32)
+    rc = lib().ipxg_demux(ctypes.byref(b), datalink, n_shards, shard_of.ctypes.data, counts.ctypes.data)
+    if rc:
+        raise IpxgError("ipxg_demux failed: %d" % rc)
+    out = []
+    for k in range(n_shards):
+        nb = int(lib().ipxg_demux_arena_bytes(ctypes.byref(b), shard_of.ctypes.data, k))
+        a = np.zeros(max(nb, 16), dtype=np.uint8)
+        d = np.zeros(int(counts[k]), dtype=DESC_DTYPE)
+        got = ctypes.c_uint32(0)
+        rc = lib().ipxg_demux_split(ctypes.byref(b), shard_of.ctypes.data, k, a.ctypes.data, d.ctypes.data,
+                                    ctypes.byref(got))
+        if rc or got.value != counts[k]:
+            raise IpxgError("ipxg_demux_split failed: %d" % rc)
+        out.append((a, d))
+    return out, shard_of
 
 
 class Engine:
