@@ -611,19 +611,41 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
             if (et == ETH_P_8021Q) return false;  // a third tag: the general walk
         }
     }
-    if (et != ETH_P_IP && et != ETH_P_IPV6) return false;
+    // untagged MPLS (1-3 labels) and PPPoE sessions (process_mpls_stack :581-602 + process_mpls
+    // :611-634, process_pppoe :643-671) shift the IP header by whole dwords too; the counters keep
+    // the Ethernet ethertype (parse_packet counts IPv4/IPv6 by it, :798-805)
+    uint32_t l3 = et;
+    bool mpls = false, pppoe = false;
+    if ((et == ETH_P_MPLS_UC || et == ETH_P_MPLS_MC) && S == 0) {
+        // bottom of stack: bit 0 of a label's byte 2 (frame bytes 16, 20, 24)
+        const uint32_t n = (wb8<16>(w) & 1) ? 1u : ((wb8<20>(w) & 1) ? 2u : ((wb8<24>(w) & 1) ? 3u : 0u));
+        if (n == 0 || caplen < 14 + 4 * n + 1) return false;  // deeper stacks / past caplen: the general walk
+        const uint32_t nib = (n == 1 ? wb8<18>(w) : (n == 2 ? wb8<22>(w) : wb8<26>(w))) >> 4;
+        l3 = nib == 4 ? ETH_P_IP : (nib == 6 ? ETH_P_IPV6 : 0u);  // 0 (EoMPLS) or other: the general walk
+        S = n;
+        mpls = true;
+    } else if (et == ETH_P_PPP_SES && S == 0) {
+        if (caplen < 22 || wb8<15>(w) != 0) return false;  // code != 0 ends the reference's parse
+        const uint32_t nh = wbe16<20>(w);
+        l3 = nh == 0x0021 ? ETH_P_IP : (nh == 0x0057 ? ETH_P_IPV6 : 0u);
+        S = 2;
+        pppoe = true;
+    }
+    if (l3 != ETH_P_IP && l3 != ETH_P_IPV6) return false;
+    if (S == 3 && l3 == ETH_P_IPV6) return false;  // its L4 header would end past the window
     // the window re-based so that the L3 header starts at byte 14 of v
     constexpr int VD = WIDE_DW - 2;
     uint32_t v[VD];
     // masks rather than a select the compiler could fold into a dynamic index of w (which
     // would put w on the stack)
-    const uint32_t m0 = 0u - (S == 0), m1 = 0u - (S == 1), m2 = 0u - (S == 2);
+    const uint32_t m0 = 0u - (S == 0), m1 = 0u - (S == 1), m2 = 0u - (S == 2), m3 = 0u - (S == 3);
 #pragma unroll
-    for (int k = 3; k < VD; ++k) v[k] = (w[k] & m0) | (w[k + 1] & m1) | (w[k + 2] & m2);
+    for (int k = 3; k < VD; ++k)
+        v[k] = (w[k] & m0) | (w[k + 1] & m1) | (w[k + 2] & m2) | (k + 3 < WIDE_DW ? w[k + 3] & m3 : 0u);
     v[0] = v[1] = v[2] = 0;
     const uint32_t o3 = 14 + 4 * S;  // the L3 offset in the frame
     uint32_t proto, o4, frag_off = 0;
-    if (et == ETH_P_IP) {
+    if (l3 == ETH_P_IP) {
         if (caplen < o3 + 20) return false;
         if (wb8<14>(v) != 0x45) return false;          // IHL 5 (options: the general walk)
         proto = wb8<23>(v);
@@ -660,7 +682,7 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
         p.dip[3] = wle32<50>(v);
         o4 = o3 + 40;
     }
-    const bool v6 = et == ETH_P_IPV6;
+    const bool v6 = l3 == ETH_P_IPV6;
     uint32_t ports = 0, flags = 0;
     bool tcp_opt = false;
     if (frag_off == 0 && proto == 6) {
@@ -689,10 +711,13 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     ext = S != 0 || v6 || tcp_opt;
     c.seen++;
     c.parsed++;
-    c.ipv6 += v6 ? 1u : 0u;  // branch-free (see parse_frame)
-    c.ipv6_bytes += v6 ? caplen : 0u;
-    c.ipv4 += v6 ? 0u : 1u;
-    c.ipv4_bytes += v6 ? 0u : caplen;
+    const uint32_t e4 = et == ETH_P_IP ? 1u : 0u, e6 = et == ETH_P_IPV6 ? 1u : 0u;  // branch-free (see parse_frame)
+    c.ipv6 += e6;
+    c.ipv6_bytes += e6 ? caplen : 0u;
+    c.ipv4 += e4;
+    c.ipv4_bytes += e4 ? caplen : 0u;
+    c.mpls += mpls ? 1u : 0u;
+    c.pppoe += pppoe ? 1u : 0u;
     c.tcp += (frag_off == 0 && proto == 6) ? 1u : 0u;
     c.udp += (frag_off == 0 && proto == 17) ? 1u : 0u;
     c.vlan += vlan ? 1u : 0u;
