@@ -576,7 +576,10 @@ __device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.o
 // registers: Ethernet with 0, 1 or 2 VLAN tags (outer 0x8100 / 0x88A8, inner 0x8100), then
 // IPv4 with IHL 5 or IPv6 whose next header is TCP or UDP, then TCP without options or with the
 // NOP,NOP,Timestamp block (doff 8, the option walk of parse_tcp_hdr succeeds on it whatever
-// the timestamp bytes; with IPv6 only untagged, as its options end at byte 78), or UDP.
+// the timestamp bytes; with IPv6 only untagged, as its options end at byte 78), or UDP;
+// untagged IPv6 may carry one or two 8-byte extension headers (two: UDP only), and untagged
+// IPv4 may carry GRE with an inner IPv4 + UDP, or + option-less TCP (GRE with at most one
+// optional field).
 // Every header boundary of these chains sits at 2 mod 4 bytes,
 // and the tags only shift the L3 header by whole dwords, so the window is re-based by 0, 1 or
 // 2 dwords (two selects per dword) and every field is then read at a compile-time offset: no
@@ -643,13 +646,29 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     for (int k = 3; k < VD; ++k)
         v[k] = (w[k] & m0) | (w[k + 1] & m1) | (w[k + 2] & m2) | (k + 3 < WIDE_DW ? w[k + 3] & m3 : 0u);
     v[0] = v[1] = v[2] = 0;
-    const uint32_t o3 = 14 + 4 * S;  // the L3 offset in the frame
-    uint32_t proto, o4, frag_off = 0;
+    // untagged IPv4 (IHL 5) -> GRE -> IPv4 (parse_ipv4_hdr :320-326, parse_gre :256-302): the
+    // outer header sets no field; the inner one starts 6 dwords later plus one per optional
+    // field (checksum, key, sequence number) -- with two or three, only its UDP ports fit
+    bool gre = false;
+    uint32_t gopt = 0;
+    if (l3 == ETH_P_IP && S == 0 && wb8<23>(w) == 47) {
+        const uint32_t gf = wbe16<34>(w);
+        if (wb8<14>(w) != 0x45 || wbe16<36>(w) != ETH_P_IP) return false;
+        gopt = ((gf & GRE_CHECKSUM) ? 1u : 0u) + ((gf & GRE_KEY) ? 1u : 0u) + ((gf & GRE_SEQNUM) ? 1u : 0u);
+        const uint32_t g0 = 0u - (gopt == 0), g1 = 0u - (gopt == 1), g2 = 0u - (gopt == 2), g3 = 0u - (gopt == 3);
+#pragma unroll
+        for (int k = 3; k < VD; ++k)
+            v[k] = (k + 6 < WIDE_DW ? w[k + 6] & g0 : 0u) | (k + 7 < WIDE_DW ? w[k + 7] & g1 : 0u) |
+                   (k + 8 < WIDE_DW ? w[k + 8] & g2 : 0u) | (k + 9 < WIDE_DW ? w[k + 9] & g3 : 0u);
+        gre = true;
+    }
+    const uint32_t o3 = 14 + 4 * S + (gre ? 24u + 4u * gopt : 0u);  // the L3 offset in the frame
+    uint32_t proto, o4, frag_off = 0, xh = 0;
     if (l3 == ETH_P_IP) {
         if (caplen < o3 + 20) return false;
         if (wb8<14>(v) != 0x45) return false;          // IHL 5 (options: the general walk)
         proto = wb8<23>(v);
-        if (proto == 47) return false;                 // GRE
+        if (proto == 47) return false;                 // GRE (in GRE: the general walk)
         const uint32_t fo = wbe16<20>(v);
         frag_off = fo & 0x1FFF;
         if (frag_enable && (fo & 0x3FFF)) return false;  // the fragmentation-cache path
@@ -666,7 +685,23 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     } else {
         if (caplen < o3 + 40) return false;
         proto = wb8<20>(v);
-        if (proto != 6 && proto != 17) return false;   // extension headers (or another L4)
+        // untagged only: up to two 8-byte hop-by-hop / routing / destination-options headers
+        // (length byte 0), the walk of skip_ipv6_ext_hdrs parser.cpp:365-412 for those types; its
+        // data-length checks are implied by the L4 caplen checks below
+        if (proto == 0 || proto == 43 || proto == 60) {
+            if (S != 0 || wb8<55>(w) != 0) return false;
+            const uint32_t p1 = wb8<54>(w);
+            if (p1 == 0 || p1 == 43 || p1 == 60) {
+                if (wb8<63>(w) != 0) return false;
+                proto = wb8<62>(w);
+                xh = 2;
+            } else {
+                proto = p1;
+                xh = 1;
+            }
+        }
+        if (proto != 6 && proto != 17) return false;   // other extension headers (or another L4)
+        if (xh == 2 && proto == 6) return false;        // its TCP header would end past the window
         p.ip_version = 6;
         p.ip_len = (uint16_t)(wbe16<18>(v) + 40);
         p.frag_id = 0;
@@ -680,26 +715,26 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
         p.dip[1] = wle32<42>(v);
         p.dip[2] = wle32<46>(v);
         p.dip[3] = wle32<50>(v);
-        o4 = o3 + 40;
+        o4 = o3 + 40 + 8 * xh;
     }
     const bool v6 = l3 == ETH_P_IPV6;
     uint32_t ports = 0, flags = 0;
     bool tcp_opt = false;
     if (frag_off == 0 && proto == 6) {
-        if (caplen < o4 + 20) return false;
-        const uint32_t w3 = v6 ? wle32<66>(v) : wle32<46>(v);  // L4 bytes 12..15
+        if (caplen < o4 + 20 || gopt > 1) return false;  // (past the window)
+        const uint32_t w3 = v6 ? (xh ? wle32<74>(w) : wle32<66>(v)) : wle32<46>(v);  // L4 bytes 12..15
         const uint32_t doff = (w3 & 0xFF) >> 4;
         if (doff > 5) {
-            if (v6 && S != 0) return false;  // the options would end past the window
+            if (gre || (v6 && (S != 0 || xh))) return false;  // the options would end past the window
             const uint32_t opt = v6 ? wle32<74>(w) : wle32<54>(v);  // L4 bytes 20..23
             if (doff != 8 || opt != 0x0A080101u || caplen < o4 + 32) return false;
             tcp_opt = true;
         }
         flags = (w3 >> 8) & 0xFF;
-        ports = v6 ? wle32<54>(v) : wle32<34>(v);
+        ports = v6 ? (xh ? wle32<62>(w) : wle32<54>(v)) : wle32<34>(v);
     } else if (frag_off == 0 && proto == 17) {
         if (caplen < o4 + 8) return false;
-        ports = v6 ? wle32<54>(v) : wle32<34>(v);
+        ports = v6 ? (xh == 2 ? wle32<70>(w) : (xh ? wle32<62>(w) : wle32<54>(v))) : wle32<34>(v);
     }
     p.ip_proto = (uint8_t)proto;
     p.tcp_flags = (uint8_t)flags;
@@ -708,7 +743,7 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     p.dst_port = bswap16(ports >> 16);
     p.l4 = (frag_off == 0 && (proto == 6 || proto == 17)) ? (uint8_t)proto : 0;
     p.vlan_id = vlan;
-    ext = S != 0 || v6 || tcp_opt;
+    ext = S != 0 || v6 || tcp_opt || gre;
     c.seen++;
     c.parsed++;
     const uint32_t e4 = et == ETH_P_IP ? 1u : 0u, e6 = et == ETH_P_IPV6 ? 1u : 0u;  // branch-free (see parse_frame)

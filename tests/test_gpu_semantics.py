@@ -381,3 +381,72 @@ def test_nonmonotonic_detected_at_wave_and_tile_boundaries(at):
     assert not d, d
     _, st0 = run_capture(arena, desc)
     assert st0["complex_flows"] == 0
+
+
+def _edge_frames():
+    """IPv6 extension chains (8- and 16-byte headers, the types the register walk takes and
+    others) and IPv4-in-GRE (optional fields, inner IPv6 / MPLS, IP options, fragments), each
+    also truncated at every caplen from 50 bytes: the shapes at the border of k_bin's wide
+    register walk, where a frame either parses in registers or falls back to the LDS walk."""
+    mac = b"\x02\0\0\0\0\x01", b"\x02\0\0\0\0\x02"
+    a6, b6 = bytes(range(16)), bytes(range(16, 32))
+    a4, b4 = b"\x0a\0\0\x01", b"\x0a\0\0\x02"
+    out = []
+    k = 0
+    for chain in ((0,), (60,), (43,), (0, 60), (0, 43), (60, 60), (0, 60, 43), (44,), (51,), (135,)):
+        for xlen in (0, 1):
+            for l4 in ("udp", "tcp", "tcp_ts"):
+                k += 1
+                body = (synth.udp(1000 + k, 443) if l4 == "udp" else
+                        synth.tcp(1000 + k, 443, 0x12, options=b"\x01\x01\x08\x0a" + b"\0" * 8 if l4 == "tcp_ts" else b""))
+                proto = 17 if l4 == "udp" else 6
+                ext = b""
+                for j in range(len(chain) - 1, -1, -1):
+                    nxt = chain[j + 1] if j + 1 < len(chain) else proto
+                    ln = xlen if j == 0 else 0
+                    ext = bytes([nxt, ln]) + b"\0" * (6 + 8 * ln) + ext
+                out.append(synth.eth(*mac, 0x86DD) + synth.ipv6(a6, b6, chain[0], ext + body))
+    for ihl in (5, 6):
+        for flags in ((False, False, False), (True, False, False), (False, True, False), (False, False, True),
+                      (True, True, False), (False, True, True), (True, True, True)):
+            for inner in ("v4udp", "v4tcp", "v4tcp_ts", "v4frag", "v6udp", "mpls"):
+                k += 1
+                if inner.startswith("v4"):
+                    l4 = (synth.udp(2000 + k, 53) if inner in ("v4udp", "v4frag") else
+                          synth.tcp(2000 + k, 80, 0x02, options=b"\x01\x01\x08\x0a" + b"\0" * 8 if inner == "v4tcp_ts" else b""))
+                    pay = synth.ipv4(a4, b4, 6 if "tcp" in inner else 17, l4, mf=1 if inner == "v4frag" else 0,
+                                     ident=k)
+                    pt = 0x0800
+                elif inner == "v6udp":
+                    pay, pt = synth.ipv6(a6, b6, 17, synth.udp(2000 + k, 53)), 0x86DD
+                else:
+                    pay, pt = synth.mpls([16], synth.ipv4(a4, b4, 17, synth.udp(2000 + k, 53))), 0x8847
+                out.append(synth.eth(*mac, 0x0800) +
+                           synth.ipv4(b"\xc0\0\0\x01", b"\xc0\0\0\x02", 47, synth.gre(pay, pt, *flags), ihl=ihl,
+                                      df=1, ident=k))
+    frames = []
+    for f in out:
+        f = synth.pad(f)
+        frames.append((f, len(f), len(f)))
+        for cl in range(50, len(f)):
+            frames.append((f[:cl], cl, len(f)))
+    return frames
+
+
+@pytest.mark.parametrize("walk", ["", "walk=wide"])
+@pytest.mark.parametrize("frag", [True, False])
+def test_wide_walk_ext_and_gre_edges(walk, frag):
+    """IPv6 extension headers and IPv4-in-GRE at the border of k_bin's register walk (untagged
+    IPv6 + one or two 8-byte extension headers, IPv4 + GRE + IPv4): flow records
+    and parser counters equal the oracle's, truncated copies included."""
+    from ipfixprobe_amd import run_capture
+    arena, desc = synth.to_batch(_edge_frames())
+    want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=20, frag_enable=frag)
+    got, gst = run_capture(arena, desc, params=";".join(x for x in (walk, "" if frag else "fe=false") if x))
+    if walk:
+        assert gst["walked_packets"] > 0
+    d = flowcmp.diff(got, want)
+    assert not d, d
+    for k in ("seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",
+              "tcp_packets", "udp_packets", "vlan_packets", "keyless_packets"):
+        assert gst[k] == wst[k], k
