@@ -121,9 +121,15 @@ __device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y,
 // frame and descriptor is read exactly once, so streaming them keeps L2 and the Infinity
 // Cache for the 160 MB of partition records that k_reduce reads back right after: measured
 // A/B on one box, k_bin -3 % and k_reduce -12 % against default-policy loads (sc0 alone:
-// no change; sc0|nt: as nt).
+// no change; sc0|nt: as nt).  Not so for the frame heads of the variable-length mixes (the
+// wide walk and k_bin_slow): there a head is 5-8 chunk loads into one or two lines of a large
+// frame, and with `nt` the lines were fetched again between the chunks -- default-policy
+// loads: k_bin's HBM fetch -23 % (imix) / -27 % (quic), imix 8.5 -> 9.3, quic 4.8 -> 5.2 Gpkt/s.
 #ifndef IPXG_LOAD_AUX
 #define IPXG_LOAD_AUX 2
+#endif
+#ifndef IPXG_WIDE_LOAD_AUX
+#define IPXG_WIDE_LOAD_AUX 0
 #endif
 // ok: load the frame's chunks (caplen >= 48: the first 3 always; in the wide walk the later
 // ones only below caplen -- a chunk past it reads as zeros with no memory traffic)
@@ -134,7 +140,8 @@ __device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, cons
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
         const uint32_t ok_k = k < 3 || (uint32_t)(16 * k) < d.caplen;
-        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, ok_k ? o + 16 * k : BUF_OOB, 0, IPXG_LOAD_AUX));
+        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, ok_k ? o + 16 * k : BUF_OOB, 0,
+                                                          NC > 3 ? IPXG_WIDE_LOAD_AUX : IPXG_LOAD_AUX));
     }
     return h;
 }
@@ -699,7 +706,7 @@ __device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t arena, const 
 #pragma unroll
     for (int k = 0; k < SLOW_NCH; ++k)
         w.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, (uint32_t)(16 * k) < cap ? o + 16 * k : BUF_OOB, 0,
-                                                          IPXG_LOAD_AUX));
+                                                          IPXG_WIDE_LOAD_AUX));
     return w;
 }
 

@@ -1,6 +1,16 @@
 set -u
-mkdir -p gpurun_out/r02n
-timeout -k 10 400 python -u -m pytest tests/test_strict.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r02n/pytest_strict.txt 2>&1; rc=$?; tail -3 gpurun_out/r02n/pytest_strict.txt; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 python bench.py --strict 17 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --verify > gpurun_out/r02n/bench_strict.json 2> gpurun_out/r02n/bench_strict.err || { tail -3 gpurun_out/r02n/bench_strict.err; exit 3; }
-python -c "
-import json; d=json.load(open('gpurun_out/r02n/bench_strict.json')); print(d['value'], d['ms_per_step'], d['verify'], d['strict'])"
+export TMPDIR=/tmp
+O=gpurun_out/r02nt
+mkdir -p $O
+for lib in default aux0; do
+  if [ $lib = default ]; then unset IPXG_LIB; else export IPXG_LIB=$PWD/ipfixprobe_amd/variants/$lib.so; fi
+  for W in imix quic; do
+    A="--workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
+    timeout -k 10 300 python bench.py $A > $O/${lib}_$W.json 2> $O/${lib}_$W.err || { tail -3 $O/${lib}_$W.err; exit 3; }
+    python -c "
+import json; d=json.load(open('$O/${lib}_$W.json')); print('$lib $W', d['value'], d['stage_ms_per_step'])"
+    timeout -k 10 -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_${lib}_$W/FETCH_SIZE -o run -- \
+        python3 bench.py $A > /dev/null 2> $O/pmc_${lib}_$W.err || { tail -3 $O/pmc_${lib}_$W.err; exit 4; }
+    python tools/pmc_summary.py $O/pmc_${lib}_$W | grep k_bin
+  done
+done
