@@ -157,47 +157,42 @@ class ExportGather:
     """The N > 1 step's only exchange (BASELINE.json configs[3]: "RCCL gather of per-GPU IPFIX
     export buffers over xGMI"): each rank's exports leave as the IPFIX message stream of its
     own observation domain (odid = rank), formatted on its GPU (ipxg_device_ipfix_messages,
-    no host round trip), copied into a fixed-size slot and gathered to rank 0 with one
-    dist.gather on a side stream -- behind the next step's kernels.  The engine's stream
-    waits only for the slot copy (its message buffer is then free); the slots alternate, and
-    the side stream is in order, so a slot is rewritten only after its gather."""
+    no host round trip), and move to rank 0 with shard.StreamGather on a side stream, behind
+    the next step's kernels: exactly the stream bytes, point to point over RCCL, sized by the
+    16-byte headers gathered the step before.  The engine's stream waits only for the copy of
+    its message buffer."""
 
-    def __init__(self, eng, rank, world, device, max_records):
+    def __init__(self, eng, rank, world, device):
         import torch
         from ipfixprobe_amd import shard
         self.eng, self.rank, self.world, self.device = eng, rank, world, device
         self.x = eng.ipfix_exporter(odid=rank, export_time=1_700_000_000)
-        self.slot_bytes = shard.SLOT_HEADER + shard.ipfix_stream_bound(max_records)
-        self.slots = [torch.zeros(self.slot_bytes, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.g = shard.StreamGather(rank, world, device)
         self.side = torch.cuda.Stream(device=device)
         self.eng_stream = torch.cuda.ExternalStream(eng.stream(), device=device)
         self.events = []
-        self.k = 0
-        self.records = self.bytes = 0
 
     def step(self):
         import torch
-        from ipfixprobe_amd import shard
         ptr, nb, nr, _ = self.eng.device_ipfix_messages(self.x)
         src = torch.as_tensor(_DevArray(ptr, max(nb, 1)), device=self.device)
-        slot = self.slots[self.k % 2]
-        self.k += 1
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         copied = torch.cuda.Event()
         self.side.wait_stream(self.eng_stream)
         with torch.cuda.stream(self.side):
             t0.record()
-            shard.pack_slot(slot, src, nb, nr)
-            copied.record()
-            shard.gather_slots(slot, self.rank, self.world)
+            self.g.push(src, nb, nr, copied=copied)
             t1.record()
         self.eng_stream.wait_event(copied)
         self.events.append((t0, t1))
-        self.records += nr
-        self.bytes += nb
+
+    def flush(self):
+        import torch
+        with torch.cuda.stream(self.side):
+            self.g.flush()
 
     def device_ms(self, reset=True):
-        """Side-stream time of the slot copies + gathers (synchronise first)."""
+        """Side-stream time of the copies + exchanges (synchronise first)."""
         ms = sum(a.elapsed_time(b) for a, b in self.events)
         if reset:
             self.events = []
@@ -377,7 +372,8 @@ class Workload:
 def make_workload(args, rank, world, device, local):
     import torch
     if args.workload == "udp64":
-        flows = gen_flows(args.flows, rank, world, args.seed, device_id=local)
+        sr, sw = args.shard if args.shard else (rank, world)
+        flows = gen_flows(args.flows, sr, sw, args.seed, device_id=local)
         if args.mode == "cold":
             fr, de = build_batch(flows, args.packets, args.seed + rank, device)
             desc = ("configs[1]: %d synthetic 64B Eth/IPv4/UDP packets over %d distinct biflows per GPU; step = "
@@ -393,32 +389,27 @@ def make_workload(args, rank, world, device, local):
         return Workload("udp64-stream", batches, args.flows, 1, False, desc)
     sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
     import synthgen
-    zipf = args.zipf if args.zipf is not None else (1.1 if args.workload == "imix" else None)
-    mix = synthgen.Mix(args.workload, args.flows * world if world > 1 else args.flows, seed=args.seed, zipf=zipf)
-    if world > 1:  # this rank's flows only (flow-hash-range shards, the NIC-RSS analogue)
-        own = rank_flows(mix, rank, world, local)
-        mix.flows = mix.flows[own]
-        if mix.cdf is not None:
-            mix.cdf, mix.rank_flow = zipf_cdf(len(mix.flows), zipf), np.random.default_rng(args.seed).permutation(
-                len(mix.flows)).astype(np.uint32)
-    gen = synthgen.Generator(mix, device, seed=args.seed + 7919 * rank)
+    # the flow-hash-range shard this process generates: its torch.distributed rank, or one rank's
+    # shard of an N-GPU job run alone on this GPU (--shard r/N: configs[3] at 1/N of its size)
+    srank, sworld = args.shard if args.shard else (rank, world)
+    mixname = "imix" if args.workload == "imix10m" else args.workload
+    zipf = args.zipf if args.zipf is not None else (1.1 if mixname == "imix" else None)
+    mix = synthgen.Mix(mixname, args.flows * sworld if sworld > 1 else args.flows, seed=args.seed, zipf=zipf)
+    if sworld > 1:  # this rank's flows only (flow-hash-range shards, the NIC-RSS analogue)
+        mix.restrict(rank_flows(mix, srank, sworld, local))
+    gen = synthgen.Generator(mix, device, seed=args.seed + 7919 * srank)
     batches = [gen.batch(k * args.packets, args.packets) for k in range(args.batches)]
     torch.cuda.synchronize()
+    cfg = {"imix": "configs[2]", "quic": "configs[4]", "imix10m": "configs[3]"}[args.workload]
+    if args.shard:
+        cfg += " shard %d/%d (one rank's slice of the %d-GPU job: %d of its %d flows, %d of its %d packets per step)" % (
+            srank, sworld, sworld, len(mix.flows), args.flows * sworld, args.packets * args.batches,
+            args.packets * args.batches * sworld)
     desc = ("%s: %s mix, %d packets per GPU per step (%d batches of %d, flows carried across batches) over %d "
             "flows%s; step = parse + XXH64 + biflow-cache update of every batch + finish"
-            % ({"imix": "configs[2]", "quic": "configs[4]"}[args.workload], args.workload,
-               args.packets * args.batches, args.batches, args.packets, len(mix.flows),
+            % (cfg, mixname, args.packets * args.batches, args.batches, args.packets, len(mix.flows),
                " (Zipf %.2f popularity)" % zipf if zipf else " (uniform popularity)"))
     return Workload(args.workload, batches, len(mix.flows), args.batches, True, desc)
-
-
-def zipf_cdf(F, s):
-    w = np.arange(1, F + 1, dtype=np.float64) ** (-float(s))
-    c = np.cumsum(w)
-    c /= c[-1]
-    cdf = np.floor(c * 18446744073709549568.0).astype(np.uint64)
-    cdf[-1] = np.uint64(0xFFFFFFFFFFFFFFFF)
-    return cdf
 
 
 def rank_flows(mix, rank, world, local):
@@ -462,12 +453,85 @@ def flow_canon(e, mix, fl):
     return out
 
 
+def engine_params(flows, ingest="binned", walk="auto"):
+    """The bench's engine: a table of >= 2 x flows slots (2^16 at least), the binned ingest, the
+    header walk chosen per batch."""
+    return "s=%d;ingest=%s;walk=%s" % (max(16, int(math.ceil(math.log2(2 * flows)))), ingest, walk)
+
+
+def launch_ranks(n):
+    """Start N ranks of this very command line under torch.distributed.run (one process per GPU,
+    rendezvous on 127.0.0.1) as a child process and return its exit code.  The parent has made no
+    GPU call (nothing here initialises HIP), and it never execs: it waits for the child."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the box's driver)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_selftest(args):
+    """The N > 1 plumbing without a GPU (gloo): every rank pushes, per step, a stream of a
+    different pseudo-random size and content through shard.StreamGather; rank 0 checks that it
+    received every rank's every stream byte for byte, and that the bytes it received are exactly
+    the streams' (no padding), then prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+    from ipfixprobe_amd import shard
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+
+    def stream(r, k):
+        g = np.random.default_rng(1000 * r + k)
+        n = int(g.integers(0, 5000)) if (r + k) % 5 else 0  # some empty streams
+        return g.integers(0, 256, n, dtype=np.uint8), n // 81
+
+    g = shard.StreamGather(rank, world, "cpu")
+    steps = args.steps or 5
+    sent = expect = 0
+    bad = []
+    for k in range(steps):
+        b, nr = stream(rank, k)
+        g.push(torch.from_numpy(b.copy()), len(b), nr)
+        sent += len(b)
+        if rank == 0 and k > 0:  # the previous step's streams arrived in this push
+            for r, t, rec in g.last:
+                want, wn = stream(r, k - 1)
+                if not np.array_equal(t.numpy(), want) or rec != wn:
+                    bad.append((k - 1, r))
+    g.flush()
+    if rank == 0:
+        for r, t, rec in g.last:
+            want, wn = stream(r, steps - 1)
+            if not np.array_equal(t.numpy(), want) or rec != wn:
+                bad.append((steps - 1, r))
+        expect = sum(len(stream(r, k)[0]) for r in range(world) for k in range(steps))
+        print(json.dumps({"selftest": "stream-gather", "n_ranks": world, "steps": steps,
+                          "received_bytes": g.received_bytes, "expected_bytes": expect,
+                          "header_bytes": g.header_bytes, "mismatches": bad}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 1 if bad or (rank == 0 and g.received_bytes != expect) else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="udp64", choices=["udp64", "imix", "quic"])
+    ap.add_argument("--workload", default="udp64", choices=["udp64", "imix", "quic", "imix10m"],
+                    help="udp64 = configs[1], imix = configs[2], imix10m = configs[3] (per GPU: 1/N of 1G packets "
+                         "over 10M flows), quic = configs[4]")
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="generate only rank R's flow-hash shard of an N-GPU job, on this one GPU (configs[3]'s "
+                         "per-GPU slice without the other N-1 GPUs)")
     ap.add_argument("--mode", default="cold", choices=["cold", "stream"], help="udp64 only")
     ap.add_argument("--packets", type=int, default=None, help="packets per batch")
     ap.add_argument("--batches", type=int, default=None, help="batches per step (imix / quic)")
@@ -483,9 +547,33 @@ def main():
     ap.add_argument("--strict", type=int, default=None, metavar="S",
                     help="strict mode with the reference's table of 2^S records (S=17: its default): "
                          "its evictions and sweep replayed exactly (ipxg_strict.hip)")
+    ap.add_argument("--plugins", default=None,
+                    help="process plugins through the bridge (native stand-ins, include/ipxg_stdplugins.h): a "
+                         "comma list of dns,http,tls,quic, or 'config' for the workload's own (configs[2]: "
+                         "dns,http,tls; configs[4]: quic)")
+    ap.add_argument("--cpu-selftest", action="store_true",
+                    help="no GPU: the N-rank launcher and the export exchange over gloo with synthetic streams "
+                         "(tests/test_launcher.py)")
     args = ap.parse_args()
+    # --gpus N: one process per GPU.  Under torchrun (the driver's N > 1 runs) WORLD_SIZE is set
+    # and must equal N; run directly with N > 1, bench.py starts the N ranks itself.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.stderr.write("bench.py: WORLD_SIZE=%s but --gpus %d\n" % (env_world, args.gpus))
+        sys.exit(2)
+    if args.cpu_selftest:
+        sys.exit(cpu_selftest(args))
+    if args.shard:
+        a, b = (int(x) for x in args.shard.split("/"))
+        if not 0 <= a < b:
+            ap.error("--shard R/N needs 0 <= R < N")
+        args.shard = (a, b)
+    # imix10m: configs[3] = 1G IMIX packets over 10M flows on 8 GPUs -> per GPU 125M packets (13 batches of
+    # 9,615,385: a batch's arena stays within the descriptors' 32-bit offsets) over 1.25M flows
     dflt = {"udp64": (10_000_000, 1, 100_000, 3000), "imix": (10_000_000, 10, 1_000_000, 5),
-            "quic": (5_000_000, 4, 1_000_000, 10)}[args.workload]
+            "quic": (5_000_000, 4, 1_000_000, 10), "imix10m": (9_615_385, 13, 1_250_000, 3)}[args.workload]
     args.packets = args.packets or dflt[0]
     args.batches = args.batches or dflt[1]
     args.flows = args.flows or dflt[2]
@@ -510,10 +598,18 @@ def main():
         wl.description += "; strict mode: the reference's table of 2^%d records in 16-way lines" % args.strict
         eng = Engine("strict=true;s=%d" % args.strict, device_id=local)
     else:
-        eng = Engine("s=%d;ingest=%s;walk=%s" % (max(16, int(math.ceil(math.log2(2 * wl.flows)))), args.ingest,
-                                                args.walk), device_id=local)
+        eng = Engine(engine_params(wl.flows, args.ingest, args.walk), device_id=local)
+    plugins = []
+    if args.plugins:
+        from ipfixprobe_amd.engine import StdPlugin
+        names = args.plugins.split(",") if args.plugins != "config" else \
+            {"imix": ["dns", "http", "tls"], "imix10m": ["dns", "http", "tls"], "quic": ["quic"]}.get(args.workload, [])
+        plugins = [StdPlugin(nm) for nm in names]
+        for pl in plugins:
+            eng.add_plugin(pl.struct)
+        wl.description += "; process plugins %s through the bridge (native stand-ins)" % ",".join(names)
     cursor = [0]
-    gather = ExportGather(eng, rank, world, device, wl.flows * 2) if world > 1 else None
+    gather = ExportGather(eng, rank, world, device) if world > 1 else None
 
     def step():
         if wl.finish:
@@ -544,6 +640,7 @@ def main():
     if gather is not None:
         torch.cuda.synchronize()
         gather.device_ms()
+        rx0 = (gather.g.received_bytes, gather.g.header_bytes, gather.g.sent_bytes, gather.g.k)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -557,6 +654,11 @@ def main():
     tm_in = eng.timing()
     st = eng.stats()
     gms = gather.device_ms() / args.steps if gather is not None else None
+    if gather is not None:  # per-step exchange volume over the timed steps (rank 0 received / this rank sent)
+        gx = gather.g
+        g_rx = (gx.received_bytes - rx0[0]) / args.steps
+        g_hdr = (gx.header_bytes - rx0[1]) / args.steps
+        g_tx = (gx.sent_bytes - rx0[2]) / max(gx.k - rx0[3], 1)
     eng.profile(1)  # stage breakdown (untimed)
     stage_steps = min(args.steps, 10)
     for _ in range(stage_steps):
@@ -568,6 +670,21 @@ def main():
         dt = float(t.item())
     pk_step = sum(wl.packets[:wl.per_step]) if wl.finish else wl.packets[0]
     alg_step = sum(wl.alg[:wl.per_step]) if wl.finish else wl.alg[0]
+    plug = None
+    if plugins:  # full caplen for the packets handed to process plugins
+        alg_step += tm_in["plugin_extra_bytes"] / args.steps
+        hw_ms = tm_in["plugin_ms"] / args.steps
+        plug = {"names": [p.name for p in plugins],
+                "host_walk": {"flows_per_step": round(tm_in["plugin_flows"] / args.steps),
+                              "packets_per_step": round(tm_in["plugin_packets"] / args.steps),
+                              "packet_share": round(tm_in["plugin_packets"] / args.steps / pk_step, 5),
+                              "bytes_per_step": round(tm_in["plugin_bytes"] / args.steps),
+                              "ms_per_step": round(hw_ms, 3),
+                              "share_of_step_time": round(hw_ms / (dt / args.steps * 1e3), 4)},
+                "hook_calls": {p.name: p.calls() for p in plugins},
+                "what": "flows with a plugin's packet in a batch (device pre-classifier) are replayed on the host "
+                        "through the hooks; ms_per_step = wall time of that host walk inside the step (pack, "
+                        "D2H of the packets, hooks, write-back)"}
     total_pkts = pk_step * args.steps * world
     value = total_pkts / dt / 1e6
     launches = max(tm_in["ingest_launches"], 1)
@@ -646,19 +763,26 @@ def main():
             "e2e_pcie": e2e,
             "spilled_packets": int(st["spilled_packets"]),
             "complex_flows": int(st["complex_flows"]),
-            "gather": {"what": "per-rank IPFIX stream (odid = rank) -> fixed-size slot -> dist.gather to rank 0 "
-                               "(RCCL) on a side stream, overlapped with the next step",
-                       "device_ms_per_step": round(gms, 4), "slot_bytes": gather.slot_bytes,
-                       "rank0_receives_bytes_per_step": gather.slot_bytes * world,
-                       "stream_bytes_per_step": round(gather.bytes / max(gather.k, 1))} if gather is not None else None,
+            "gather": {"what": "per-rank IPFIX stream (odid = rank) -> rank 0 over RCCL point to point, exactly "
+                               "the stream bytes, sized by 16-byte headers gathered the step before; on a side "
+                               "stream, overlapped with the next step",
+                       "device_ms_per_step": round(gms, 4),
+                       "rank0_receives_bytes_per_step": round(g_rx),
+                       "header_bytes_per_step": round(g_hdr),
+                       "rank0_stream_bytes_per_step": round(g_tx)} if gather is not None else None,
             "verify": verify,
             "cpu_baseline": cpu,
+            "plugins": plug,
             "strict": {"cache_exp": args.strict, "end_no_res_per_step": int(st["end_no_res"] // max(st["batches"], 1))}
             if args.strict is not None else None,
         }
         print(json.dumps(line))
+    if gather is not None:
+        gather.flush()
+        torch.cuda.synchronize()
     eng.close()
     if world > 1:
+        torch.distributed.barrier()
         torch.distributed.destroy_process_group()
 
 

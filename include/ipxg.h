@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 1
+#define IPXG_ABI_VERSION 2 /* 2: ipxg_plugin gained masked prefixes and follow_packets */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -336,13 +336,19 @@ typedef struct ipxg_packet_view {
 
 /* A process plugin: the device pre-classifier rule (a packet is the plugin's when it is
  * TCP/UDP -- proto_mask bit 0 TCP, bit 1 UDP -- with its source or destination port in
- * ports[], or its payload starts with one of prefixes[]), and the hooks.  Contract: on the
- * packets outside the rule every hook returns 0 and changes nothing (so flows with none of the
- * plugin's packets in a batch stay on the device).  A flow with one of them has all its packets
- * of the batch replayed in order on the host, through these hooks at put_pkt_recursive's call
- * sites.  The record's ext field (ipxg_flow_record.reserved[8..15], a 64-bit handle) is the
- * plugins' per-flow state -- RecordExt: zero on a new record, cleared by erase/reuse, carried by
- * the exported record.  Hooks return 0 or IPXG_FLOW_FLUSH / IPXG_FLOW_FLUSH_WITH_REINSERT. */
+ * ports[], or its payload starts with one of prefixes[]: byte k equal to prefix[q][k], or, when
+ * bit q of `masked` is set, equal under prefix_mask[q][k] -- e.g. QUIC's long-header bit,
+ * mask 0x80), and the hooks.  Contract: on the packets outside the rule every hook returns 0
+ * and changes nothing (so flows with none of the plugin's packets in a batch stay on the
+ * device) -- except, for a plugin with follow_packets > 0, on a flow whose record carries a
+ * non-zero ext while it holds fewer than follow_packets packets: such a flow stays on the host
+ * walk with all its packets, batch after batch, until it reaches follow_packets (QUIC stores
+ * every packet's type for the first QUIC_MAX_ELEMCOUNT packets of a flow it detected,
+ * quic.cpp:340-346,494-498).  A flow with one of them has all its packets of the batch replayed
+ * in order on the host, through these hooks at put_pkt_recursive's call sites.  The record's
+ * ext field (a 64-bit handle) is the plugins' per-flow state -- Flow::m_exts: zero on a new
+ * record, cleared by erase/reuse, carried by the exported record.  Hooks return 0 or
+ * IPXG_FLOW_FLUSH / IPXG_FLOW_FLUSH_WITH_REINSERT. */
 typedef struct ipxg_plugin {
     void* ctx;
     uint32_t proto_mask;
@@ -356,6 +362,10 @@ typedef struct ipxg_plugin {
     int (*pre_update)(void* ctx, ipxg_flow_record* flow, ipxg_packet_view* pkt);
     int (*post_update)(void* ctx, ipxg_flow_record* flow, const ipxg_packet_view* pkt);
     void (*pre_export)(void* ctx, ipxg_flow_record* flow);
+    /* ABI 2 */
+    uint32_t masked;          /* bit q: prefix q compares under prefix_mask[q]                 */
+    uint32_t follow_packets;  /* see above; 0 = the rule alone decides                          */
+    uint8_t prefix_mask[IPXG_PLUGIN_MAX_PREFIXES][IPXG_PLUGIN_PREFIX_LEN];
 } ipxg_plugin;
 
 /* Register a plugin (the order of registration is the order of the hook calls). */
@@ -376,6 +386,13 @@ typedef struct ipxg_timing {
     uint64_t slow_launches;
     uint64_t finish_launches;
     uint64_t ingest_packets;   /* packets covered by the timed ingest launches             */
+    /* the process-plugin bridge's host walk (wall clock, always counted; zeroed by ipxg_profile) */
+    double plugin_ms;          /* plugin flows: pack, copies of their packets, the walk, write-back */
+    uint64_t plugin_flows;     /* flow-batches walked on the host                               */
+    uint64_t plugin_packets;   /* packets handed to the hooks                                   */
+    uint64_t plugin_bytes;     /* their captured bytes (full caplen, copied to the host)        */
+    uint64_t plugin_extra_bytes; /* of which past each frame's first 128 (full caplen
+                                    for packets handed to process plugins)                    */
 } ipxg_timing;
 
 /* Per-phase shader-clock sums of the last batch's k_bin, k_reduce and k_bin_slow (16 values;

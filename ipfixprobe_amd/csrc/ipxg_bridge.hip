@@ -30,8 +30,10 @@ __device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, c
     for (uint32_t q = 0; q < r.n_prefixes; ++q) {
         const uint32_t n = r.prefix_len[q];
         if (n == 0 || n > pk.payload_len) continue;
+        const bool msk = (r.masked >> q) & 1u;
         bool eq = true;
-        for (uint32_t k = 0; k < n && eq; ++k) eq = s.b(pk.payload_off + k) == r.prefix[q][k];
+        for (uint32_t k = 0; k < n && eq; ++k)
+            eq = ((s.b(pk.payload_off + k) ^ r.prefix[q][k]) & (msk ? r.prefix_mask[q][k] : 0xFFu)) == 0;
         if (eq) return true;
     }
     return false;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx
     if (r >= ncx) return;
     const uint32_t s = cx.slot_of[r];
     const HotSlot h = t.hot[s];
-    if (!(h.state & SLOT_PLUGIN)) return;
+    if (!(h.state & SLOT_HOST)) return;
     const uint32_t pos = atomicAdd(count, 1u);
     PluginFlow f;
     f.slot = s;
@@ -143,13 +145,14 @@ void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx
     hipLaunchKernelGGL(k_plugin_bytes, dim3(g ? g : 1), dim3(256), 0, st, b, idx, off, m, out);
 }
 
-// The host walk's result for flow k: its slot (state LIVE with the record, or empty of records).
+// The host walk's result for flow k: its slot (state LIVE with the record -- and FOLLOW while a
+// plugin follows every packet of it --, or empty of records).
 __global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginFlow* in, uint32_t n) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
     const PluginFlow f = in[k];
     if (f.state & SLOT_LIVE) t.cold[f.slot] = f.rec;
-    clear_slot(&t.hot[f.slot], f.key, f.state & SLOT_LIVE);
+    clear_slot(&t.hot[f.slot], f.key, f.state & (SLOT_LIVE | SLOT_FOLLOW));
 }
 
 void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n) {

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 #include <cmath>
 #include <cstdio>
@@ -62,6 +63,7 @@ struct ipxg_engine {
     // process-plugin bridge: the registered plugins, their rules on the device, and what the
     // host walks add to the device-side counters (exports by reason, TopPorts)
     std::vector<ipxg_plugin> plugins;
+    uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
@@ -251,6 +253,9 @@ static Params params(ipxg_engine* e) {
     p.prev_usec = e->prev_usec;
     p.tile_agg = e->tile_agg ? 1 : 0;
     p.wide = wide_walk(e) ? 1 : 0;
+    p.spin_max = STRICT_SPIN_MAX;
+    if (const char* sm = std::getenv("IPXG_STRICT_SPIN_MAX"))  // test knob: a short watchdog
+        p.spin_max = std::max<uint32_t>(16, (uint32_t)std::strtoul(sm, nullptr, 0));
     return p;
 }
 
@@ -387,9 +392,27 @@ void ipxg_config_default(ipxg_config* cfg) {
     cfg->datalink = IPXG_DLT_EN10MB;
 }
 
+// Timing-experiment builds drop or fake work (-DIPXG_EXP_NOEMIT/NOHASH/LOADONLY) or add clock
+// probes (-DIPXG_PROBE); one such variant in round 2 (an atomic skipped in k_reduce) left slots
+// half-claimed and ipxg_finish then read past the table (an illegal memory access).  Their
+// engines only start for a tuning run that asks for them (IPXG_TUNING=1).
+#if defined(IPXG_TUNING_BUILD) || defined(IPXG_EXP_NOEMIT) || defined(IPXG_EXP_NOHASH) || \
+    defined(IPXG_EXP_LOADONLY) || defined(IPXG_PROBE)
+static constexpr bool kTuningBuild = true;
+#else
+static constexpr bool kTuningBuild = false;
+#endif
+
 int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (!cfg || !out) return IPXG_EINVAL;
     *out = nullptr;
+    if (kTuningBuild) {
+        const char* t = std::getenv("IPXG_TUNING");
+        if (!t || std::strcmp(t, "1") != 0) {
+            std::fprintf(stderr, "ipxg: timing-experiment build of libipxg refused (set IPXG_TUNING=1)\n");
+            return IPXG_ESTATE;
+        }
+    }
     if (cfg->cache_exp < 4 || cfg->cache_exp > 30) return IPXG_EINVAL;
     if (cfg->frag_enable && cfg->frag_size == 0) return IPXG_EINVAL;
     ipxg_engine* e = new ipxg_engine();
@@ -917,6 +940,12 @@ struct FlowWalk {
 // the plugin flows on the host and write them back.  *live_delta: records created - closed.
 static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, const ComplexView& cx, uint32_t ncx,
                        uint32_t npk, int64_t* live_delta) {
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Clock {  // the walk's wall time, however it returns
+        ipxg_engine* e;
+        std::chrono::steady_clock::time_point t0;
+        ~Clock() { e->tm.plugin_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } clock{e, t0};
     int rc;
     *live_delta = 0;
     if ((rc = ensure(e, e->pf_d, (size_t)ncx * sizeof(PluginFlow) + 16))) return rc;
@@ -962,6 +991,10 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     launch_plugin_bytes(e->st, bv, (const uint32_t*)e->pf_idx.p, (const uint64_t*)e->pf_off.p, m,
                         (uint8_t*)e->pf_bytes.p);
     HIPCHK(e, hipGetLastError());
+    e->tm.plugin_flows += nf;
+    e->tm.plugin_packets += m;
+    e->tm.plugin_bytes += off[m];
+    for (uint32_t k = 0; k < m; ++k) e->tm.plugin_extra_bytes += de[k].caplen > 128 ? de[k].caplen - 128u : 0u;
     std::vector<uint8_t> bytes(off[m] + 1);
     HIPCHK(e, hipMemcpyAsync(bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
@@ -988,7 +1021,10 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             v.index = idx[k];
             w.put(pk[k], &v);
         }
-        F.state = w.live ? SLOT_LIVE : 0;
+        // a plugin that follows every packet of a flow it claimed (ext set) keeps it on the host
+        // walk until the flow holds follow_packets packets (ipxg_plugin.follow_packets)
+        const bool follow = w.live && w.rec.ext && (uint64_t)w.rec.src_packets + w.rec.dst_packets < e->follow_max;
+        F.state = w.live ? (SLOT_LIVE | (follow ? SLOT_FOLLOW : 0u)) : 0u;
         F.rec = w.rec;
         *live_delta += (w.live ? 1 : 0) - (was_live ? 1 : 0);
         // TopPorts from the flow's packets (count_flow_ports: every packet counts both ports)
@@ -1035,6 +1071,7 @@ int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
         if (rc0) return rc0;
     }
     e->plugins.push_back(*pl);
+    e->follow_max = std::max<uint64_t>(e->follow_max, pl->follow_packets);
     std::vector<DevRule> rules(e->plugins.size());
     for (size_t k = 0; k < rules.size(); ++k) {
         const ipxg_plugin& q = e->plugins[k];
@@ -1046,6 +1083,8 @@ int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
         r.n_prefixes = q.n_prefixes;
         std::memcpy(r.prefix_len, q.prefix_len, sizeof(r.prefix_len));
         std::memcpy(r.prefix, q.prefix, sizeof(r.prefix));
+        r.masked = q.masked;
+        std::memcpy(r.prefix_mask, q.prefix_mask, sizeof(r.prefix_mask));
     }
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));

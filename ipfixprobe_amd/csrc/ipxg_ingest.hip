@@ -1326,6 +1326,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
     if (tid < 4) cnt[tid] = 0;
     __syncthreads();
     const bool force_cx = p.force_complex || ctl->nonmono;
+    const bool slot_clean = ctl->spilled == 0;  // no packet was folded into a slot directly (k_bin / k_reduce)
     uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0;
     for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
         const uint32_t k = base + tid;
@@ -1334,7 +1335,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
         RecW er;
         if (k < nf) {
             const HotSlot h = fin_list[k];  // the slot's merged image, its index in pad
-            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused);
+            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean);
             if (fr.status == FIN_COMPLEX) n_cx++;
             else if (!fused && fr.created) n_live++;
             do_export = fr.do_export || fr.fin_export;

@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
     if (r >= nranks) return;
     const uint32_t s = cx.slot_of[r];
     const HotSlot h = t.hot[s];
-    if (h.state & SLOT_PLUGIN) return;  // a process plugin's flow: the host walks it (plugin_walk)
+    if (h.state & SLOT_HOST) return;  // a process plugin's flow: the host walks it (plugin_walk)
     bool live = h.state & SLOT_LIVE;
     if (!live) atomicAdd(&ctl->cx_new_live, 1u);  // the slot ends the walk live
     ipxg_flow_record rec;
@@ -579,7 +579,7 @@ __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_ca
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < from_cap; s += gridDim.x * blockDim.x) {
         const HotSlot h = from.hot[s];
         if (h.key == 0) continue;
-        if (!(h.state & (SLOT_LIVE | SLOT_COMPLEX | SLOT_PLUGIN)) && h.last1 == 0) continue;  // dead slot
+        if (!(h.state & (SLOT_LIVE | SLOT_COMPLEX | SLOT_HOST)) && h.last1 == 0) continue;  // dead slot
         uint32_t ns = (uint32_t)h.key & to.mask;
         bool ok = false;
         for (uint32_t probe = 0; probe <= to.mask; ++probe) {

@@ -28,6 +28,9 @@ static_assert(sizeof(HotSlot) == 64, "hot slot must be one 64-byte line");
 
 constexpr uint32_t SLOT_LIVE = 1u, SLOT_COMPLEX = 2u;
 constexpr uint32_t SLOT_PLUGIN = 4u;  // a process plugin's packet in this batch: replayed on the host
+constexpr uint32_t SLOT_FOLLOW = 8u;  // a plugin follows every packet of the flow (ipxg_plugin.follow_packets):
+                                      // replayed on the host in every batch until the host walk drops it
+constexpr uint32_t SLOT_HOST = SLOT_PLUGIN | SLOT_FOLLOW;
 constexpr uint64_t ACC_BYTES_MASK = (1ull << 40) - 1;
 constexpr uint32_t MAX_PROBE = 64;
 
@@ -119,6 +122,7 @@ struct Params {
     uint32_t prev_sec, prev_usec;
     uint32_t tile_agg;       // k_bin / k_bin_slow aggregate frequent flows per tile (skewed traffic)
     uint32_t wide;           // k_bin's wide walk (96-byte loads, parse_medium)
+    uint32_t spin_max;       // strict replay: polling rounds without progress before giving up
 };
 
 // ---- strict mode (ipxg_strict.hip): the reference's line table -------------------------------
@@ -141,7 +145,10 @@ struct StrictPkt {          // what put_pkt_recursive reads of a keyed packet (h
 static_assert(sizeof(StrictPkt) == 32, "");
 constexpr uint32_t STRICT_LANES = 768;           // the replay's one workgroup (3 waves per SIMD; the DAG is ~260 packets wide at the reference default)
 constexpr uint32_t STRICT_NONE = 0xFFFFFFFFu;
-constexpr uint32_t STRICT_SPIN_MAX = 1u << 24;   // rounds a lane may wait for one queue entry before giving up
+#ifndef IPXG_STRICT_SPIN_MAX
+#define IPXG_STRICT_SPIN_MAX (1u << 24)
+#endif
+constexpr uint32_t STRICT_SPIN_MAX = IPXG_STRICT_SPIN_MAX;  // polling rounds without any packet finishing
 
 struct BatchView {
     const uint8_t* arena;
@@ -216,6 +223,8 @@ struct DevRule {
     uint32_t n_prefixes;
     uint8_t prefix_len[IPXG_PLUGIN_MAX_PREFIXES];
     uint8_t prefix[IPXG_PLUGIN_MAX_PREFIXES][IPXG_PLUGIN_PREFIX_LEN];
+    uint32_t masked;  // bit q: prefix q compares under prefix_mask[q]
+    uint8_t prefix_mask[IPXG_PLUGIN_MAX_PREFIXES][IPXG_PLUGIN_PREFIX_LEN];
 };
 
 // A plugin flow between the device and the host walk: its slot, packets (segment of the complex

@@ -361,7 +361,9 @@ __device__ void strict_packet(WalkCtx& w, const StrictPkt& s, const ipxg_flow_re
 
 // One workgroup: the DAG scheduler of the file comment.  An idle lane holds one ticket (a queue
 // position) and runs the ticket's packet once a predecessor (or k_strict_ready) has filled it.
-// A lane that waits STRICT_SPIN_MAX rounds gives up and stops the workgroup (ctl->strict_fail;
+// A lane that sees no packet of the workgroup finish for p.spin_max polling rounds gives up and
+// stops the workgroup (ctl->strict_fail; progress-based, so one long chain -- an elephant flow run
+// serially by the lane that owns it -- never trips it;
 // the scheduler cannot deadlock -- the lowest unfinished packet is always running or queued at
 // a position some lane's ticket reaches -- the bound guards engine bugs).
 __global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Params p, const StrictPkt* sp,
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Para
     // round trip and no wait for another wave's poll); further ready successors are queued.  An
     // idle lane holds one ticket; every lane stops when all K keyed packets are done.
     constexpr uint32_t NO_TICKET = 0xFFFFFFFFu;
-    uint32_t t = NO_TICKET, cur = STRICT_NONE, spins = 0;
+    uint32_t t = NO_TICKET, cur = STRICT_NONE, spins = 0, seen_done = 0;
     bool failed = false, fin = K == 0;
     while (__any(!fin)) {
         bool progressed = false;
@@ -404,13 +406,18 @@ __global__ __launch_bounds__(STRICT_LANES) void k_strict_walk(StrictView v, Para
                 t = NO_TICKET;
                 spins = 0;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            } else if (__hip_atomic_load(&done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= K ||
-                       __hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                fin = true;  // every packet done (this ticket is never filled), or a lane gave up
-            } else if (++spins > STRICT_SPIN_MAX) {
-                failed = true;  // engine bug: the host reports it
-                atomicOr(&stop, 1u);
-                fin = true;
+            } else {
+                const uint32_t dn = __hip_atomic_load(&done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (dn >= K || __hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                    fin = true;  // every packet done (this ticket is never filled), or a lane gave up
+                } else if (dn != seen_done) {
+                    seen_done = dn;  // the workgroup still makes progress (a long chain running on
+                    spins = 0;       // other lanes): waiting is legitimate, the bound restarts
+                } else if (++spins > p.spin_max) {
+                    failed = true;  // no packet finished for STRICT_SPIN_MAX rounds: engine bug
+                    atomicOr(&stop, 1u);
+                    fin = true;
+                }
             }
         }
         if (!fin && cur != STRICT_NONE) {

@@ -438,6 +438,37 @@ __device__ __forceinline__ RecW rec_load_w(const ipxg_flow_record* p) {
     }
     return r;
 }
+// The record's first 64 bytes (words 0-15: flow hash, times, byte and packet counters, TCP flags,
+// version/protocol, ports, the first word of src_ip) -- everything a continuing flow's batch reads
+// and updates; the second half (addresses, MACs, VLAN, extension handle) is written once, when the
+// record is created, and read again only when it is exported.
+__device__ __forceinline__ void rec_load_head_w(const ipxg_flow_record* p, RecW& r) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = q[i];
+        r.w[4 * i] = v.x;
+        r.w[4 * i + 1] = v.y;
+        r.w[4 * i + 2] = v.z;
+        r.w[4 * i + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void rec_load_tail_w(const ipxg_flow_record* p, RecW& r) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) {
+        const uint4 v = q[i];
+        r.w[4 * i] = v.x;
+        r.w[4 * i + 1] = v.y;
+        r.w[4 * i + 2] = v.z;
+        r.w[4 * i + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void rec_store_head_w(ipxg_flow_record* p, const RecW& r) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = make_uint4(r.w[4 * i], r.w[4 * i + 1], r.w[4 * i + 2], r.w[4 * i + 3]);
+}
 __device__ __forceinline__ void rec_store_w(ipxg_flow_record* p, const RecW& r) {
     uint4* q = reinterpret_cast<uint4*>(p);
 #pragma unroll
@@ -950,22 +981,31 @@ struct FinResult {
 // before the batch, so no boundary export can coincide): the completed record goes to er
 // (fin_export) instead of the table, and the slot is emptied.  One record out per slot either
 // way, so the caller holds one record, not two (two were kept in scratch).
+// slot_clean: the slot in memory holds only {key, state} (k_reduce listed its merged image
+// without writing it back, and no packet of the batch was accumulated into it directly): a
+// continuing flow whose state does not change then leaves the slot untouched.
+// A continuing flow reads and writes only the first half of its record (rec_load_head_w); the
+// creator's canonical direction comes from its flow hash (FlowRecord::create keys the record by
+// the creating packet's forward hash, cache.cpp:84-92: it is the slot's canonical key iff the
+// creator went in canonical direction 0 -- the rule rec_create_w / the host walk store in
+// reserved[0]), so the second half is read only for an export.
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
-                                                   bool force_cx, uint32_t* col, RecW& er, bool fuse = false) {
+                                                   bool force_cx, uint32_t* col, RecW& er, bool fuse = false,
+                                                   bool slot_clean = false) {
     FinResult res = {FIN_DONE, false, false, false, 0};
     const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
     RecW rec;
-    if (live) rec = rec_load_w(&t.cold[s]);
+    if (live) rec_load_head_w(&t.cold[s], rec);
     const ipxg_pkt_desc df = b.desc[first];
     const ipxg_pkt_desc dl = b.desc[last];
     const uint32_t cdf = p.split_biflow ? 0u : first_dir(h.first_n);
     const uint32_t I = p.inactive_s, A = p.active_s;
     uint8_t bsplit = 0;
+    const uint32_t creator = (live && !p.split_biflow && rw64(rec, RW_HASH) != h.key) ? 1u : 0u;
     if (live) {
-        const uint32_t creator = rw_creator(rec);
         const bool dsrc = p.split_biflow || cdf == creator;
         const uint32_t flw = dsrc ? rw_sflags(rec) : rw_dflags(rec);
         if (first_syn(h.first_n) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
@@ -973,7 +1013,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         else if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TFS] >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
     }
     const bool cont = live && !bsplit;
-    bool cx = force_cx || (h.state & SLOT_PLUGIN);  // a process plugin's flow: the host walks it
+    bool cx = force_cx || (h.state & SLOT_HOST);  // a process plugin's flow: the host walks it
     const uint32_t tb = h.tbits;
     if (tb >> 31) cx = true;
     else if (tb) {
@@ -986,7 +1026,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         if (!h.syn1[dd]) continue;
         const uint32_t sidx = h.syn1[dd] - 1;
         if (cont) {
-            const uint32_t cf = (uint32_t)dd == rw_creator(rec) ? rw_sflags(rec) : rw_dflags(rec);
+            const uint32_t cf = (uint32_t)dd == creator ? rw_sflags(rec) : rw_dflags(rec);
             if (cf & 0x05) cx = true;
         }
         if (h.fin_n[dd] && sidx > ~h.fin_n[dd]) cx = true;
@@ -1000,6 +1040,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         return res;
     }
     if (bsplit) {
+        rec_load_tail_w(&t.cold[s], rec);
         res.do_export = true;
         res.reason = bsplit;
         er = rec;
@@ -1014,7 +1055,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         canon(fp, p, lo, c2, hf);
         rec_create_w(rec, fp, df, hf, cdf);
     }
-    const uint32_t sd = rw_creator(rec);
+    const uint32_t sd = cont ? creator : rw_creator(rec);
     const uint64_t as = sd ? h.acc[1] : h.acc[0], ad = sd ? h.acc[0] : h.acc[1];  // (selects: no indexed copy)
     rec.w[RW_SPK] += (uint32_t)(as >> 40);
     rw64_set(rec, RW_SBYTES, rw64(rec, RW_SBYTES) + (as & ACC_BYTES_MASK));
@@ -1026,9 +1067,15 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     res.created = !live;
     count_flow_ports_w(t, rec, (uint32_t)(as >> 40) + (uint32_t)(ad >> 40));
     if (fuse && !res.do_export) {
+        if (cont) rec_load_tail_w(&t.cold[s], rec);  // (fused finishes follow an empty table: none)
         er = rec;
         res.fin_export = true;
         clear_slot(&t.hot[s], 0, 0);  // empty (every slot empties at the finish)
+        return res;
+    }
+    if (cont) {
+        rec_store_head_w(&t.cold[s], rec);
+        if (!(slot_clean && h.state == SLOT_LIVE)) clear_slot(&t.hot[s], h.key, SLOT_LIVE);
         return res;
     }
     rec_store_w(&t.cold[s], rec);

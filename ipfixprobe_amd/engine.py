@@ -75,7 +75,9 @@ class Timing(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in ("ingest_ms", "ingest_slow_ms", "reduce_ms", "fin_ms",
                                                "finalize_ms", "slow_ms", "finish_ms")] + \
         [(n, ctypes.c_uint64) for n in ("ingest_launches", "reduce_launches", "finalize_launches",
-                                        "slow_launches", "finish_launches", "ingest_packets")]
+                                        "slow_launches", "finish_launches", "ingest_packets")] + \
+        [("plugin_ms", ctypes.c_double)] + [(n, ctypes.c_uint64) for n in ("plugin_flows", "plugin_packets",
+                                                                             "plugin_bytes", "plugin_extra_bytes")]
 
 
 class Capture(ctypes.Structure):
@@ -125,7 +127,9 @@ class Plugin(ctypes.Structure):
                 ("ports", ctypes.c_uint16 * 16), ("n_prefixes", ctypes.c_uint32),
                 ("prefix_len", ctypes.c_uint8 * 16), ("prefix", (ctypes.c_uint8 * 16) * 16),
                 ("pre_create", PRE_CREATE_FN), ("post_create", FLOW_HOOK_FN), ("pre_update", FLOW_HOOK_FN),
-                ("post_update", FLOW_HOOK_FN), ("pre_export", PRE_EXPORT_FN)]
+                ("post_update", FLOW_HOOK_FN), ("pre_export", PRE_EXPORT_FN),
+                ("masked", ctypes.c_uint32), ("follow_packets", ctypes.c_uint32),
+                ("prefix_mask", (ctypes.c_uint8 * 16) * 16)]
 
 # ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),
@@ -206,6 +210,41 @@ def lib():
                 getattr(L, name).restype = ctypes.c_int
         _LIB = L
     return _LIB
+
+
+STD_LIB_PATH = os.path.join(_HERE, "libipxg_stdplugins.so")
+_STD = None
+
+
+class StdPlugin:
+    """A native stand-in process plugin (include/ipxg_stdplugins.h: "dns", "http", "tls", "quic"),
+    its ipxg_plugin in .struct (pass it to Engine.add_plugin or the oracle)."""
+
+    def __init__(self, name):
+        global _STD
+        if _STD is None:
+            if not os.path.exists(STD_LIB_PATH):
+                raise IpxgError("libipxg_stdplugins.so not built: run __graft_entry__.build()")
+            _STD = ctypes.CDLL(STD_LIB_PATH)
+            _STD.ipxg_std_plugin.argtypes = [ctypes.c_char_p, ctypes.POINTER(Plugin)]
+            _STD.ipxg_std_plugin_free.argtypes = [ctypes.POINTER(Plugin)]
+            _STD.ipxg_std_plugin_calls.argtypes = [ctypes.POINTER(Plugin), ctypes.c_void_p]
+        self.name = name
+        self.struct = Plugin()
+        if _STD.ipxg_std_plugin(name.encode(), ctypes.byref(self.struct)):
+            raise IpxgError("unknown stand-in plugin %r" % name)
+
+    def calls(self):
+        out = np.zeros(6, dtype=np.uint64)
+        _STD.ipxg_std_plugin_calls(ctypes.byref(self.struct), out.ctypes.data)
+        return dict(zip(("pre_create", "post_create", "pre_update", "post_update", "pre_export", "flushes"),
+                        (int(x) for x in out)))
+
+    def __del__(self):
+        try:
+            _STD.ipxg_std_plugin_free(ctypes.byref(self.struct))
+        except Exception:
+            pass
 
 
 def make_config(params: str = "", **kw) -> Config:

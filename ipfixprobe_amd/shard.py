@@ -7,10 +7,11 @@ Here: one process and one engine per GPU, and the canonical flow hash
 `lo = min(XXH64(key), XXH64(key_inv))` (the table key, cache.cpp:84-92 / ipxg_table.hpp)
 picks the rank, so both directions of a biflow land on the same GPU.  The only exchange is
 the gather of the per-GPU export buffers to rank 0: `gather_records` (an all-gather of the
-record counts, then point-to-point transfers) or, for IPFIX message streams formatted on each
-GPU, `gather_slots` (one fixed-size slot per rank -- the stream's length in its header -- so no
-rank waits on the host for the others' sizes and the gather can run on a side stream, behind
-the next step's kernels).  RCCL over xGMI on GPUs; gloo on CPU tensors in the tests.
+record counts, then point-to-point transfers) or, for the IPFIX message streams formatted on
+each GPU every step, `StreamGather` (the exact stream bytes, point to point, sized by headers
+gathered one step earlier, so no rank waits on the host for the others' sizes and the exchange
+runs on a side stream behind the next step's kernels).  RCCL over xGMI on GPUs; gloo on CPU
+tensors in the tests.
 """
 import numpy as np
 
@@ -61,50 +62,99 @@ def gather_records(buf, n, rank, world, device):
     return None
 
 
-SLOT_HEADER = 16  # little-endian u64 stream bytes, u64 records
+class StreamGather:
+    """Exact-size gather of every rank's per-step byte stream (its IPFIX messages) to rank 0 --
+    the path's only exchange.  Step k: each rank copies its stream into a buffer of
+    its own (the producer may then reuse its buffer) and gathers a 16-byte header (stream bytes,
+    records) to rank 0; the streams themselves move one step later, point to point, exactly the
+    bytes each rank produced, sized by the headers rank 0 gathered the step before -- by then
+    long complete, so rank 0's host reads them from pinned memory without waiting on the
+    exchange, and nothing is padded to a worst case.  A stream of any size fits (the buffers
+    grow), so no rank can fail alone inside a collective.
 
+    Every rank calls push() the same number of times and then flush() (collective).  On GPUs the
+    caller runs it inside `with torch.cuda.stream(side)`; `copied` (a torch.cuda.Event, optional)
+    is recorded once the stream has been copied.  On CPU tensors (gloo) every call is
+    synchronous.  Rank 0 keeps what it received of the last step (`last`: [(rank, uint8 tensor,
+    records)]) and the totals (`received_bytes`, `received_records`, `header_bytes`)."""
 
-def ipfix_stream_bound(records):
-    """Bytes of an IPFIX message stream of `records` basic records, templates included (at
-    least 13 records per message of 1458 bytes: 16 + 4 + 13 * 105; two more messages for the
-    template message and a flush that splits the two templates' sets)."""
-    return 196 + records * 105 + (records // 13 + 3) * 20
+    HEADER = 16  # two little-endian int64: stream bytes, records
 
+    def __init__(self, rank, world, device, keep_last=True):
+        import torch
+        self.rank, self.world, self.device = rank, world, torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.bufs = [torch.zeros(256, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self.hdr = [torch.zeros(2, dtype=torch.int64, device=self.device) for _ in range(2)]
+        self.hdrs = [[torch.zeros(2, dtype=torch.int64, device=self.device) for _ in range(world)]
+                     for _ in range(2)] if rank == 0 else None
+        self.hdr_host = [torch.zeros((world, 2), dtype=torch.int64, pin_memory=self.cuda) for _ in range(2)] \
+            if rank == 0 else None
+        self.hdr_ev = [None, None]
+        self.prev = None  # (buffer index, own bytes, own records)
+        self.k = 0
+        self.keep_last = keep_last
+        self.last = []
+        self.sent_bytes = self.sent_records = 0  # this rank's streams
+        self.received_bytes = self.received_records = self.header_bytes = 0  # rank 0
 
-def pack_slot(slot, stream, nbytes, records):
-    """Header + the first nbytes of `stream` (uint8 tensor) into `slot` (uint8 tensor of the
-    agreed slot size, same device), with stream-ordered copies (no host synchronisation)."""
-    if SLOT_HEADER + nbytes > slot.numel():
-        raise ValueError("IPFIX stream of %d bytes exceeds the slot (%d)" % (nbytes, slot.numel()))
-    hdr = slot[:SLOT_HEADER].view(torch_int64())  # two scalar fills on the device
-    hdr[0] = nbytes
-    hdr[1] = records
-    if nbytes:
-        slot[SLOT_HEADER:SLOT_HEADER + nbytes].copy_(stream[:nbytes])
+    def push(self, src, nbytes, records, copied=None):
+        import torch
+        import torch.distributed as dist
+        self._move_prev()
+        i = self.k % 2
+        if self.bufs[i].numel() < nbytes:
+            self.bufs[i] = torch.zeros(max(nbytes, 2 * self.bufs[i].numel()), dtype=torch.uint8, device=self.device)
+        if nbytes:
+            self.bufs[i][:nbytes].copy_(src[:nbytes])
+        if copied is not None:
+            copied.record()
+        self.hdr[i][0].fill_(int(nbytes))  # device-side fills: no host round trip
+        self.hdr[i][1].fill_(int(records))
+        if self.world > 1:
+            dist.gather(self.hdr[i], self.hdrs[i] if self.rank == 0 else None, dst=0)
+        if self.rank == 0:
+            self.hdr_host[i].copy_(torch.stack(self.hdrs[i]) if self.world > 1 else self.hdr[i].view(1, 2),
+                                   non_blocking=self.cuda)
+            if self.cuda:
+                self.hdr_ev[i] = torch.cuda.Event()
+                self.hdr_ev[i].record()
+            self.header_bytes += self.HEADER * self.world
+        self.prev = (i, int(nbytes), int(records))
+        self.sent_bytes += int(nbytes)
+        self.sent_records += int(records)
+        self.k += 1
 
+    def flush(self):
+        self._move_prev()
 
-def torch_int64():
-    import torch
-    return torch.int64
-
-
-def gather_slots(slot, rank, world):
-    """Every rank's slot into rank 0 (dist.gather on the current stream): a list of world
-    tensors on rank 0, None elsewhere.  Collective: every rank must call it."""
-    import torch
-    import torch.distributed as dist
-    if world == 1:
-        return [slot]
-    out = [torch.empty_like(slot) for _ in range(world)] if rank == 0 else None
-    dist.gather(slot, out, dst=0)
-    return out
-
-
-def unpack_slots(slots):
-    """[(stream bytes as a numpy uint8 array, records)] from gathered slots (host copies)."""
-    res = []
-    for s in slots:
-        a = s.cpu().numpy()
-        nb, nr = (int(v) for v in a[:SLOT_HEADER].view(np.int64))
-        res.append((a[SLOT_HEADER:SLOT_HEADER + nb], nr))
-    return res
+    def _move_prev(self):
+        import torch
+        import torch.distributed as dist
+        if self.prev is None:
+            return
+        i, nb, nr = self.prev
+        self.prev = None
+        ops = []
+        if self.rank == 0:
+            if self.hdr_ev[i] is not None:
+                self.hdr_ev[i].synchronize()  # the step-before's header gather: long complete
+            sizes = self.hdr_host[i].tolist()
+            got = [(0, self.bufs[i][:nb], nr)]
+            for r in range(1, self.world):
+                n, rec = int(sizes[r][0]), int(sizes[r][1])
+                t = torch.empty(n, dtype=torch.uint8, device=self.device)
+                if n:
+                    ops.append(dist.P2POp(dist.irecv, t, r))
+                got.append((r, t, rec))
+                self.received_bytes += n
+                self.received_records += rec
+            self.received_bytes += nb  # rank 0's own stream: local, not moved
+            self.received_records += nr
+            if self.keep_last:
+                self.last = got
+        elif nb:
+            ops.append(dist.P2POp(dist.isend, self.bufs[i][:nb], 0))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()

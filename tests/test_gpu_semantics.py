@@ -217,22 +217,30 @@ def test_nonmonotonic_conserves_packets():
 
 
 def test_bench_size_parity():
-    """The bench workload itself (10M 64 B packets, 100k biflows) against the oracle."""
+    """The bench workload itself (10M 64 B packets, 100k biflows) against the oracle, through
+    the bench's exact engine and step: its configuration (bench.engine_params: s=18, binned
+    ingest, walk=auto), the batch submitted asynchronously from the device with the finish right
+    behind it (the fused finish in k_fin_list), three steps in a row on the same engine (the
+    partition sizing and the walk choice come from the previous step from the second on)."""
     import torch
 
     import bench
     flows = bench.gen_flows(100_000, 0, 1, 1234)
     frames, desc = bench.build_batch(flows, 10_000_000, 1234, torch.device("cuda", 0))
-    from ipfixprobe_amd import Engine
-    with Engine("s=19") as e:
-        e.submit(frames, desc, device=True)
-        e.finish()
-        got = e.poll()
+    torch.cuda.synchronize()
     dn = desc.cpu().numpy().view(pcaputil.DESC_DTYPE)
     want, wst = oracle_py.run_capture(frames.cpu().numpy(), dn, 1, cache_exp=21)
     assert len(want) == 100_000 and wst["end_no_res"] == 0
-    d = flowcmp.diff(got, want)
-    assert not d, d
+    from ipfixprobe_amd import Engine
+    with Engine(bench.engine_params(100_000)) as e:
+        assert e.cfg.cache_exp == 18
+        for step in range(3):
+            e.submit(frames, desc, device=True, asynchronous=True, wait_producer=False)
+            e.finish()
+            got = e.poll()
+            d = flowcmp.diff(got, want)
+            assert not d, (step, d)
+        assert e.stats()["complex_flows"] == 0
 
 
 # ---- the binned ingest's fast and fallback paths (ipxg_ingest.hip) -------------------------

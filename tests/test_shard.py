@@ -138,9 +138,9 @@ def test_rccl_gather_single_rank_aliases_device_exports():
 
 
 def _gloo_ipfix_worker(rank, world, port, q):
-    """bench.py's N > 1 export step on CPU: each rank's flows exported as an IPFIX stream (the
-    oracle's exporter, observation domain = rank), packed into a fixed-size slot, gathered to
-    rank 0 (gather_slots), which decodes every stream."""
+    """bench.py's N > 1 export step on CPU: each rank's flows exported as IPFIX streams (the
+    oracle's exporter, observation domain = rank) over two steps, moved to rank 0 by
+    StreamGather, which decodes every stream."""
     import torch
     import torch.distributed as dist
     import ipfixdec
@@ -151,46 +151,52 @@ def _gloo_ipfix_worker(rank, world, port, q):
         arena, desc = _capture(seed=31)
         own = _owners(arena, desc, world)
         got, _ = oracle_py.run_capture(arena, np.ascontiguousarray(desc[own == rank]), 1, cache_exp=20)
-        stream, _ = oracle_py.ipfix_export(oracle_py.ipfix_exporter(odid=rank, export_time=5), got)
-        slot_bytes = shard.SLOT_HEADER + shard.ipfix_stream_bound(400)  # every rank: the same size
-        slot = torch.zeros(slot_bytes, dtype=torch.uint8)
-        shard.pack_slot(slot, torch.from_numpy(stream.copy()), len(stream), len(got))
-        out = shard.gather_slots(slot, rank, world)
+        x = oracle_py.ipfix_exporter(odid=rank, export_time=5)
+        half = len(got) // 2
+        g = shard.StreamGather(rank, world, "cpu")
+        streams = []
+        for part in (got[:half], got[half:]):  # two steps: the second without the template message
+            stream, _ = oracle_py.ipfix_export(x, part)
+            g.push(torch.from_numpy(stream.copy()), len(stream), len(part))
+            streams.append(len(stream))
+            if rank == 0 and len(streams) == 2:
+                first = [(r, t.numpy().copy(), nr) for r, t, nr in g.last]
+        g.flush()
         if rank == 0:
-            parts = shard.unpack_slots(out)
             recs, wire = [], 0
-            for r, (b, nr) in enumerate(parts):
-                msgs, _, rr, _, _ = ipfixdec.decode(b)
-                assert all(m["odid"] == r for m in msgs) and len(rr) == nr
-                recs.append(rr)
-                wire += len(b)
+            for (r, b0, n0), (r1, b1, n1) in zip(first, g.last):
+                assert r == r1
+                msgs, tm, rr0, _, _ = ipfixdec.decode(b0)
+                msgs1, _, rr1, _, _ = ipfixdec.decode(b1, tm)
+                assert all(m["odid"] == r for m in msgs + msgs1) and len(rr0) == n0 and len(rr1) == n1
+                recs += [rr0, rr1]
+                wire += len(b0) + len(b1)
             want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
             allr = np.concatenate(recs)
             assert ipfixdec.basic_view(allr) == ipfixdec.basic_view(want)
-            q.put((wire, sum(p[1] for p in parts), len(out) * slot_bytes))
+            q.put((wire, g.received_bytes, g.received_records))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [4, 8])
-def test_gloo_ipfix_slots_gather_to_rank0(world):
+def test_gloo_ipfix_streams_gather_to_rank0(world):
     """world_size 4 / 8 on CPU: the exact N > 1 export step of bench.py (IPFIX stream per rank
-    -> fixed-size slot -> gather to rank 0); the union of the decoded records is the whole
-    capture's, and rank 0 receives world slots (the volume DESIGN.md 6 budgets)."""
+    and step -> StreamGather to rank 0); the union of the decoded records is the whole capture's,
+    and rank 0 received exactly the streams' bytes (DESIGN.md 6's volume: no padding)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     mp.spawn(_gloo_ipfix_worker, args=(world, _free_port(), q), nprocs=world, join=True)
-    wire, nrec, moved = q.get(timeout=10)
-    assert nrec > 100 and wire < shard.ipfix_stream_bound(nrec) + world * 196
-    assert moved == world * (shard.SLOT_HEADER + shard.ipfix_stream_bound(400))
+    wire, moved, nrec = q.get(timeout=10)
+    assert nrec > 100 and moved == wire
 
 
 @pytest.mark.gpu
 def test_bench_export_gather_single_rank():
-    """bench.py's N > 1 export step (ExportGather: device IPFIX stream -> slot -> dist.gather on a
-    side stream) at world size 1 over RCCL: the gathered slot decodes to the engine's flows."""
+    """bench.py's N > 1 export step (ExportGather: device IPFIX stream -> StreamGather on a side
+    stream) at world size 1 over RCCL: the streams rank 0 holds decode to the engine's flows."""
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
@@ -205,21 +211,28 @@ def test_bench_export_gather_single_rank():
         arena, desc = _capture(seed=25)
         want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
         with Engine() as e:
-            g = bench.ExportGather(e, 0, 1, dev, 1000)
+            g = bench.ExportGather(e, 0, 1, dev)
+            got = []
             for _ in range(2):  # two steps: the second stream has no template message
                 e.submit(arena, desc)
                 e.finish()
                 g.step()
+                torch.cuda.synchronize()
+                got.append([(r, t.cpu().numpy().copy(), nr) for r, t, nr in g.g.last])
+            g.flush()
             torch.cuda.synchronize()
-            parts = shard.unpack_slots([g.slots[1]])
+            got.append([(r, t.cpu().numpy().copy(), nr) for r, t, nr in g.g.last])
             assert g.device_ms() > 0
-        b, nr = parts[0]
-        _, t0, _, _, _ = ipfixdec.decode(shard.unpack_slots([g.slots[0]])[0][0])
-        msgs, _, recs, _, _ = ipfixdec.decode(b, t0)
-        assert nr == len(want) == len(recs) and all(s[0] != 2 for m in msgs for s in m["sets"])
+        # got[1] holds step 0's stream (moved during step 1's push), got[2] step 1's (the flush)
+        (_, b0, n0), = got[1]
+        (_, b1, n1), = got[2]
+        _, t0, _, _, _ = ipfixdec.decode(b0)
+        msgs, _, recs, _, _ = ipfixdec.decode(b1, t0)
+        assert n1 == len(want) == len(recs) and all(s[0] != 2 for m in msgs for s in m["sets"])
         w = want.copy()
         w["end_reason"] = 0  # the oracle's sweep and the engine close open flows with different reasons
         recs["end_reason"] = 0
         assert ipfixdec.basic_view(recs) == ipfixdec.basic_view(w)
+        assert g.g.received_bytes == len(b0) + len(b1)
     finally:
         dist.destroy_process_group()

@@ -1,0 +1,180 @@
+"""Process plugins on the configs[2] / configs[4] mixes (BASELINE.json: "with TLS/HTTP/DNS
+process plugins enabled", "QUIC process plugin"): the native stand-ins of
+ipfixprobe_amd/host/ipxg_stdplugins.c (include/ipxg_stdplugins.h) registered through the
+bridge (ipxg_add_plugin), the engine against the oracle running the same hooks for every
+packet.
+
+The stand-ins are pinned by the reference's own goldens through the oracle (CPU): dns and http
+(every record equal), tls (the flows the plugin claims = tests/functional/outputs/tls, which keeps
+only flows with a TLS extension) and quic."""
+import os
+import sys
+from collections import Counter
+
+import numpy as np
+import pytest
+
+import flowcmp
+import oracle_py
+import pcaputil
+import plugins_py
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "tests", "golden", "reference")
+sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
+
+
+def _std(name):
+    from ipfixprobe_amd.engine import StdPlugin
+    return StdPlugin(name)
+
+
+def _capture(name):
+    dl, pk = pcaputil.read_capture(os.path.join(REF, name + ".pcap"))
+    arena, desc = pcaputil.to_batch(pk)
+    return dl, arena, desc
+
+
+@pytest.mark.parametrize("name,pcap", [("dns", "dns"), ("http", "http"), ("tls", "tls"),
+                                       ("quic", "quic_initial-sample")])
+def test_stand_in_reproduces_reference_golden(name, pcap):
+    dl, arena, desc = _capture(pcap)
+    pl = _std(name)
+    recs, _ = oracle_py.run_capture(arena, desc, dl, plugins=[pl.struct])
+    gold = Counter(pcaputil.read_golden(os.path.join(REF, "outputs", name)))
+    if name == "tls":  # the tls test's output keeps the flows with a TLS extension
+        recs = recs[recs["ext"] != 0]
+    assert Counter(pcaputil.format_records(recs)) == gold
+    assert pl.calls()["post_create"] > 0
+
+
+def test_stand_ins_agree_with_python_stand_ins():
+    """dns / http: the C stand-ins and tests/plugins_py.py (each restating dns.cpp / http.cpp)
+    end the same flows on the same captures and synthetic HTTP/DNS stream."""
+    import test_plugins
+    for name, py in (("dns", plugins_py.DnsFlush), ("http", plugins_py.HttpReinsert)):
+        for dl, arena, desc in (_capture(name), (1,) + tuple(test_plugins._http_stream())):
+            pa, pb = _std(name), py()  # (kept alive while the oracle calls their hooks)
+            a, _ = oracle_py.run_capture(arena, desc, dl, cache_exp=16, plugins=[pa.struct])
+            b, _ = oracle_py.run_capture(arena, desc, dl, cache_exp=16, plugins=[pb.struct])
+            assert not flowcmp.diff(a, b)
+
+
+def _mix(name, flows, seed=1234):
+    import synthgen
+    return synthgen.Mix(name, flows, seed=seed, zipf=1.1 if name == "imix" else None)
+
+
+def test_mix_plugin_shares():
+    """The generator's connections: opening flows (first messages: TLS ClientHello, HTTP request
+    line, QUIC long headers) are a small share of the packets, DNS flows rank last (short)."""
+    import synthgen
+
+    class G:
+        pass
+    for name, lo, hi in (("imix", 0.005, 0.03), ("quic", 0.03, 0.12)):
+        g = G()
+        g.mix, g.seed, g.t0_ns, g.dt_ns = _mix(name, 100_000), 5, 1_700_000_000 * 10**9, 100
+        g.q16 = [int(round(x * 65536)) for x in (0.55, 0.005, 0.045)]
+        f, _, _, lng, _ = synthgen.host_plan(g, 0, 200_000)
+        op = g.mix.flows["opening"][f] != 0
+        assert lo < op.mean() < hi, (name, op.mean())
+        if name == "quic":
+            assert np.array_equal(lng, op & (g.mix.layouts["size_mode"][g.mix.flows["layout"][f]] == 1))
+
+
+PLUGINS = {"imix": ("dns", "http", "tls"), "quic": ("quic", "dns")}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(PLUGINS))
+def test_plugins_on_workload_match_oracle(name):
+    """2M packets of the mix over 1M flows in four device batches with the configs' plugins
+    registered: every record (plugin flushes, REINSERTs and the plugins' ext bits included)
+    equals the oracle's, which calls the same hooks on every packet; the hooks saw only a small
+    share of the packets on the engine (the bridge kept the rest on the device)."""
+    import torch
+    import synthgen
+    from ipfixprobe_amd import Engine
+    gen = synthgen.Generator(_mix(name, 1_000_000), torch.device("cuda", 0), seed=1234)
+    n, nb = 500_000, 4
+    batches = [gen.batch(k * n, n) for k in range(nb)]
+    torch.cuda.synchronize()
+    pls = [_std(p) for p in PLUGINS[name]]
+    with Engine("s=21") as e:
+        for p in pls:
+            e.add_plugin(p.struct)
+        for fr, de in batches:
+            e.submit(fr, de, device=True)
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    ref = [_std(p) for p in PLUGINS[name]]
+    c = oracle_py.OracleCache(cache_exp=22)
+    for p in ref:
+        c.add_plugin(p.struct)
+    for fr, de in batches:
+        c.run(fr.cpu().numpy(), de.cpu().numpy().view(pcaputil.DESC_DTYPE), 1)
+    c.finish()
+    want = c.take()
+    c.close()
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+    assert (got["ext"] != 0).sum() > 100
+    seen = pls[0].calls()["pre_create"]
+    assert 0 < seen < 0.25 * n * nb, seen  # the host walk saw the plugin flows' packets only
+    assert st["complex_flows"] > 0
+
+
+class FollowProbe(plugins_py.PyPlugin):
+    """QUIC-shaped rule (UDP, long-header bit) with follow_packets = 6: claims a flow on a
+    long-header packet and records every later hook call on a claimed flow within its first 6
+    packets -- the calls the reference makes (every packet) and the bridge must reproduce."""
+    proto_mask = 2
+
+    def __init__(self):
+        super().__init__()
+        s = self.struct
+        s.n_prefixes = 1
+        s.prefix_len[0] = 1
+        s.prefix[0][0] = 0x80
+        s.masked = 1
+        s.prefix_mask[0][0] = 0x80
+        s.follow_packets = 6
+        self.seen = Counter()
+
+    def _note(self, rec, data):
+        if data[:1] and data[0] & 0x80:
+            rec["ext"] = 1
+        elif rec["ext"] and int(rec["src_packets"]) + int(rec["dst_packets"]) < 6:
+            self.seen[(int(rec["flow_hash"]), int(rec["src_packets"]) + int(rec["dst_packets"]))] += 1
+        return 0
+
+    def post_create(self, rec, p, data):
+        return self._note(rec, data)
+
+    def post_update(self, rec, p, data):
+        return self._note(rec, data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [7, 40])
+def test_follow_packets_keeps_claimed_flows_on_host(batch):
+    """A flow claimed in one batch keeps reaching the plugin's hooks in the next batches (short
+    headers, outside the rule) until it holds follow_packets packets; every such call the oracle
+    makes, the bridge makes."""
+    import synth
+    from ipfixprobe_amd import run_capture
+    cli, srv = synth.ip4(10), synth.ip4(200)
+    frames = []
+    for rnd in range(10):
+        for f in range(8):
+            first = b"\xc0" + b"\x00" * 20 if rnd == 0 and f % 2 == 0 else b"\x40" + b"\x01" * 20
+            ip = synth.ipv4(cli, srv, 17, synth.udp(30000 + f, 443, first))
+            frames.append(synth.pad(synth.eth(synth.mac(1), synth.mac(2), 0x0800) + ip))
+    arena, desc = synth.to_batch([(f, len(f), len(f)) for f in frames])
+    eng, orc = FollowProbe(), FollowProbe()
+    got, _ = run_capture(arena, desc, params="s=16", batch=batch, plugins=[eng.struct])
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=16, plugins=[orc.struct])
+    assert not flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert eng.seen == orc.seen and len(orc.seen) == 4 * 5

@@ -113,6 +113,18 @@ def test_strict_one_hot_line():
 
 
 @pytest.mark.gpu
+def test_strict_single_flow_watchdog(monkeypatch):
+    """One flow only: the whole batch is one dependent chain run serially by one lane while the
+    other 767 lanes wait.  The replay's watchdog is progress-based (it restarts whenever any
+    packet finishes), so a short bound (IPXG_STRICT_SPIN_MAX, 4096 polling rounds: well under a
+    millisecond, against the chain's ~0.1 s) must not give up on valid input."""
+    monkeypatch.setenv("IPXG_STRICT_SPIN_MAX", "4096")
+    arena, desc = synth.flow_stream(seed=36, n_flows=1, n_pkts=100000, frag=False).batch()
+    got, _ = _check(arena, desc, "s=10")
+    assert len(got) >= 1
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["basic", "vlan", "mqtt", "http", "quic"])
 def test_strict_reproduces_reference_golden(name):
     """At the reference's own defaults (s=17, l=4) the engine in strict mode gives the golden

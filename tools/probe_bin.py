@@ -1,5 +1,5 @@
 """Per-phase shader clocks of k_bin on the bench batch (library built with -DIPXG_PROBE:
-IPXG_LIB=ipfixprobe_amd/variants/probe.so python3 tools/probe_bin.py)."""
+IPXG_TUNING=1 IPXG_LIB=ipfixprobe_amd/variants/probe.so python3 tools/probe_bin.py)."""
 import math
 import os
 import sys

@@ -6,8 +6,8 @@
 // layout, addresses, ports and VLAN per flow).  Per packet, from a counter-based RNG keyed by
 // (seed, global packet index):
 //   k_synth_plan   flow (Zipf by CDF binary search, or uniform), direction, frame length (the
-//                  layout's size mode: IMIX 64/594/1518 at 7:4:1, QUIC long/short header),
-//                  TCP flags;
+//                  layout's size mode: IMIX 64/594/1518 at 7:4:1, QUIC long header for the
+//                  flows being opened / short header), TCP flags;
 //   (host)         frame offsets = exclusive prefix sum of the lengths rounded up to 64 B
 //                  (frames start on a cache line, as in a DPDK mbuf pool);
 //   k_synth_write  each workgroup builds 64 frames' headers in LDS (template + addresses,
@@ -32,14 +32,18 @@ struct SynthLayout {              // 256 bytes
     uint16_t size_mode;           // 0 IMIX 64/594/1518 7:4:1, 1 QUIC, 2 fixed 64 B
     uint16_t l7_off;              // QUIC: first byte of the QUIC header
     uint16_t min_len;             // shortest frame (>= hdr_len)
-    uint16_t pad[13];
+    uint16_t alt_len;             // bytes of alt[] written at l7_off in packets of established flows
+    uint8_t alt[8];               //   (the protocol's later messages: TLS application data, HTTP body)
+    uint16_t pad[8];
 };
 static_assert(sizeof(SynthLayout) == 256, "layout record");
 
 struct SynthFlow {                // 48 bytes
     uint8_t sip[16], dip[16];
     uint16_t sport, dport, layout, vlan;
-    uint32_t mac_id, pad;
+    uint32_t mac_id;
+    uint32_t opening;             // 1: a connection being opened (its packets carry the protocol's
+                                  // first message / QUIC long headers); 0: established
 };
 static_assert(sizeof(SynthFlow) == 48, "flow record");
 
@@ -91,8 +95,9 @@ __global__ __launch_bounds__(256) void k_synth_plan(SynthParams P, uint4* plan, 
     const uint32_t s12 = (uint32_t)(((r1 >> 32) & 0xFFFF) * 12u >> 16);
     if (L.size_mode == 0) {
         len = s12 < 7 ? 64u : (s12 < 11 ? 594u : 1518u);
-    } else if (L.size_mode == 1) {  // QUIC: 1 in 8 long-header Initial (>= 1200 B datagram)
-        lng = ((r1 >> 48) & 7) == 0;
+    } else if (L.size_mode == 1) {  // QUIC: an opening flow's packets are long-header Initials
+        lng = P.flows[f].opening ? 1u : 0u;  // (>= 1200 B datagrams), an established flow's short
+                                             // header 1-RTT packets
         len = lng ? L.l7_off + 1200u : (s12 < 6 ? 80u : 1350u);
     } else {
         len = 64u;
@@ -150,6 +155,8 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4*
             if (L.patch_off[k]) put16(h, L.patch_off[k], len - L.patch_bias[k]);
         if (L.tcp_flags_off) h[L.tcp_flags_off] = (uint8_t)pl.z;
         if (L.size_mode == 1 && !lng) h[L.l7_off] = 0x43;  // QUIC short header (1-RTT)
+        if (!F.opening)
+            for (uint32_t k = 0; k < L.alt_len; ++k) h[L.l7_off + k] = L.alt[k];
         meta[tid][0] = (uint32_t)off[i];
         meta[tid][1] = len;
         meta[tid][2] = L.hdr_len;

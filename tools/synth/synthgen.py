@@ -28,10 +28,10 @@ LAYOUT_DTYPE = np.dtype([
     ("tmpl", "u1", (192,)), ("hdr_len", "<u2"), ("addr_len", "<u2"), ("sip_off", "<u2"), ("dip_off", "<u2"),
     ("sport_off", "<u2"), ("dport_off", "<u2"), ("tcp_flags_off", "<u2"), ("vlan_off", "<u2"),
     ("patch_off", "<u2", (4,)), ("patch_bias", "<u2", (4,)), ("size_mode", "<u2"), ("l7_off", "<u2"),
-    ("min_len", "<u2"), ("pad", "<u2", (13,)),
+    ("min_len", "<u2"), ("alt_len", "<u2"), ("alt", "u1", (8,)), ("pad", "<u2", (8,)),
 ])
 FLOW_DTYPE = np.dtype([("sip", "u1", (16,)), ("dip", "u1", (16,)), ("sport", "<u2"), ("dport", "<u2"),
-                       ("layout", "<u2"), ("vlan", "<u2"), ("mac_id", "<u4"), ("pad", "<u4")])
+                       ("layout", "<u2"), ("vlan", "<u2"), ("mac_id", "<u4"), ("opening", "<u4")])
 assert LAYOUT_DTYPE.itemsize == 256 and FLOW_DTYPE.itemsize == 48
 
 SIZE_IMIX, SIZE_QUIC, SIZE_64 = 0, 1, 2
@@ -42,10 +42,13 @@ DNS_QUERY = struct.pack(">HHHHHH", 0x1234, 0x0100, 1, 0, 0, 0) + b"\x07example\x
 QUIC_INITIAL = (b"\xc3" + struct.pack(">I", 1) + b"\x08" + bytes(range(8)) + b"\x08" + bytes(range(8, 16)) +
                 b"\x00" + b"\x44\xb0" + b"\x00\x00\x00\x01")
 TCP_TS = b"\x01\x01\x08\x0a" + struct.pack(">II", 0x01020304, 0)
+# what established flows carry where an opening flow has its first message
+TLS_APPDATA = bytes.fromhex("1703030200")      # TLS application data record header
+HTTP_BODY = b"\x1f\x8b\x08\x00data"           # (gzip) body bytes -- no method, no status line
 
 
 def build_layout(ip=4, l4="udp", dport=0, vlan=0, mpls=0, pppoe=False, gre=False, ext=(), tcp_opts=b"",
-                 l7=b"", size_mode=SIZE_IMIX):
+                 l7=b"", size_mode=SIZE_IMIX, alt=b""):
     """One frame layout -> (LAYOUT_DTYPE record, server port).  vlan: 0 none, 1 802.1Q, 2 QinQ."""
     b = bytearray(b"\0" * 12)
     rec = np.zeros(1, dtype=LAYOUT_DTYPE)[0]
@@ -118,33 +121,35 @@ def build_layout(ip=4, l4="udp", dport=0, vlan=0, mpls=0, pppoe=False, gre=False
     rec["size_mode"] = size_mode
     rec["l7_off"] = l7o
     rec["min_len"] = max(len(b), 60)
+    rec["alt_len"] = len(alt)
+    rec["alt"][:len(alt)] = np.frombuffer(alt, dtype=np.uint8)
     return rec, dport
 
 
 # (share, layout kwargs).  dport 0 = a random well-known port per flow.
 MIXES = {
     "imix": [
-        (0.30, dict(ip=4, l4="tcp", dport=443, tcp_opts=TCP_TS, l7=TLS_HELLO)),
-        (0.15, dict(ip=4, l4="tcp", dport=80, tcp_opts=TCP_TS, l7=HTTP_GET)),
+        (0.30, dict(ip=4, l4="tcp", dport=443, tcp_opts=TCP_TS, l7=TLS_HELLO, alt=TLS_APPDATA)),
+        (0.15, dict(ip=4, l4="tcp", dport=80, tcp_opts=TCP_TS, l7=HTTP_GET, alt=HTTP_BODY)),
         (0.10, dict(ip=4, l4="tcp", dport=0)),
         (0.15, dict(ip=4, l4="udp", dport=53, l7=DNS_QUERY)),
         (0.15, dict(ip=4, l4="udp", dport=0)),
-        (0.08, dict(ip=6, l4="tcp", dport=443, tcp_opts=TCP_TS, l7=TLS_HELLO)),
+        (0.08, dict(ip=6, l4="tcp", dport=443, tcp_opts=TCP_TS, l7=TLS_HELLO, alt=TLS_APPDATA)),
         (0.04, dict(ip=6, l4="udp", dport=53, l7=DNS_QUERY)),
-        (0.03, dict(ip=4, l4="tcp", dport=443, vlan=1, tcp_opts=TCP_TS, l7=TLS_HELLO)),
+        (0.03, dict(ip=4, l4="tcp", dport=443, vlan=1, tcp_opts=TCP_TS, l7=TLS_HELLO, alt=TLS_APPDATA)),
     ],
     "quic": [
         (0.45, dict(ip=4, l4="udp", dport=443, l7=QUIC_INITIAL, size_mode=SIZE_QUIC)),
         (0.15, dict(ip=6, l4="udp", dport=443, l7=QUIC_INITIAL, size_mode=SIZE_QUIC)),
         (0.06, dict(ip=4, l4="udp", dport=443, vlan=1, l7=QUIC_INITIAL, size_mode=SIZE_QUIC)),
-        (0.05, dict(ip=4, l4="tcp", dport=443, vlan=2, tcp_opts=TCP_TS, l7=TLS_HELLO)),
+        (0.05, dict(ip=4, l4="tcp", dport=443, vlan=2, tcp_opts=TCP_TS, l7=TLS_HELLO, alt=TLS_APPDATA)),
         (0.03, dict(ip=4, l4="udp", dport=443, mpls=1, l7=QUIC_INITIAL, size_mode=SIZE_QUIC)),
         (0.03, dict(ip=4, l4="tcp", dport=443, mpls=2, tcp_opts=TCP_TS)),
         (0.02, dict(ip=6, l4="udp", dport=0, mpls=3)),
         (0.04, dict(ip=6, l4="udp", dport=443, ext=(0,), l7=QUIC_INITIAL, size_mode=SIZE_QUIC)),
         (0.03, dict(ip=6, l4="tcp", dport=443, ext=(0, 60), tcp_opts=TCP_TS)),
         (0.03, dict(ip=6, l4="udp", dport=0, ext=(0, 43, 60))),
-        (0.04, dict(ip=4, l4="tcp", dport=80, pppoe=True, tcp_opts=TCP_TS, l7=HTTP_GET)),
+        (0.04, dict(ip=4, l4="tcp", dport=80, pppoe=True, tcp_opts=TCP_TS, l7=HTTP_GET, alt=HTTP_BODY)),
         (0.02, dict(ip=6, l4="udp", dport=53, pppoe=True, l7=DNS_QUERY)),
         (0.03, dict(ip=4, l4="udp", dport=443, gre=True, l7=QUIC_INITIAL, size_mode=SIZE_QUIC)),
         (0.02, dict(ip=6, l4="tcp", dport=443, gre=True, tcp_opts=TCP_TS)),
@@ -153,9 +158,17 @@ MIXES = {
 
 
 class Mix:
-    """Layouts + flow table (+ Zipf CDF) of one mix, on the host."""
+    """Layouts + flow table (+ Zipf CDF) of one mix, on the host.
 
-    def __init__(self, name, n_flows, seed=1234, zipf=None):
+    Connections being opened vs established (what the process plugins see): an opening flow's
+    packets carry its protocol's first message (TLS ClientHello, HTTP request line, QUIC
+    long-header Initial); an established flow's carry later traffic (TLS application data, HTTP
+    body bytes, QUIC short headers).  With Zipf popularity the opening flows are the least
+    popular `open_share` of the flows (short connections; the popular ones are long-lived and
+    mid-connection), and DNS flows -- a query and its answer per flow -- rank last of all; with
+    uniform popularity a random `open_share` of the flows is opening."""
+
+    def __init__(self, name, n_flows, seed=1234, zipf=None, open_share=None):
         spec = MIXES[name]
         self.name = name
         self.zipf = zipf
@@ -200,7 +213,35 @@ class Mix:
             # 2^64 - 2048: the largest float64 below 2^64 (the last entry is set to 2^64 - 1)
             self.cdf = np.floor(c * 18446744073709549568.0).astype(np.uint64)
             self.cdf[-1] = np.uint64(0xFFFFFFFFFFFFFFFF)
-            self.rank_flow = rng.permutation(F).astype(np.uint32)
+            dns = np.isin(lay, [k for k, (_, kw) in enumerate(spec) if kw.get("l7") == DNS_QUERY])
+            # rank -> flow: the other flows in random order, then the DNS flows (the least popular)
+            self.rank_flow = np.concatenate([rng.permutation(np.nonzero(~dns)[0]),
+                                             rng.permutation(np.nonzero(dns)[0])]).astype(np.uint32)
+            share = 0.3 if open_share is None else open_share
+            fl["opening"][self.rank_flow[int(F * (1.0 - share)):]] = 1
+        else:
+            share = 1.0 / 16 if open_share is None else open_share
+            fl["opening"] = rng.random(F) < share
+
+
+    def restrict(self, keep):
+        """Keep only the flows `keep` (indices; one rank's flow-hash shard): their popularity
+        order is kept (Zipf over the kept flows, in the order the full mix ranked them), and
+        with it which are opening and where the DNS flows rank."""
+        keep = np.asarray(keep, dtype=np.int64)
+        if self.rank_flow is not None:
+            pos = np.empty(len(self.flows), dtype=np.int64)
+            pos[self.rank_flow] = np.arange(len(self.flows))
+            keep = keep[np.argsort(pos[keep], kind="stable")]  # in rank order
+        self.flows = self.flows[keep]
+        if self.cdf is not None:
+            F = len(self.flows)
+            w = np.arange(1, F + 1, dtype=np.float64) ** (-float(self.zipf))
+            c = np.cumsum(w)
+            c /= c[-1]
+            self.cdf = np.floor(c * 18446744073709549568.0).astype(np.uint64)
+            self.cdf[-1] = np.uint64(0xFFFFFFFFFFFFFFFF)
+            self.rank_flow = np.arange(F, dtype=np.uint32)
 
 
 class _Params(ctypes.Structure):
@@ -313,7 +354,7 @@ def host_plan(gen, first, n):
     u = (r1 & np.uint64(0xFFFF)).astype(np.int64)
     dirn = (((r1 >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.int64) >= gen.q16[0]).astype(np.int64)
     s12 = ((((r1 >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64) * 12) >> 16)
-    lng = (((r1 >> np.uint64(48)) & np.uint64(7)) == 0)
+    lng = mix.flows["opening"][f] != 0
     mode = L["size_mode"].astype(np.int64)
     imix = np.where(s12 < 7, 64, np.where(s12 < 11, 594, 1518))
     quic = np.where(lng, L["l7_off"].astype(np.int64) + 1200, np.where(s12 < 6, 80, 1350))
@@ -372,6 +413,9 @@ def host_batch(gen, first, n):
             h[lay["tcp_flags_off"]] = int(flags[i])
         if lay["size_mode"] == 1 and not lng[i]:
             h[lay["l7_off"]] = 0x43
+        if not fl["opening"][fi]:
+            o = int(lay["l7_off"])
+            h[o:o + int(lay["alt_len"])] = lay["alt"][:int(lay["alt_len"])].tobytes()
         hl = min(int(lay["hdr_len"]), int(ln[i]))
         arena[off[i]:off[i] + hl] = np.frombuffer(bytes(h[:hl]), dtype=np.uint8)
     return arena, desc

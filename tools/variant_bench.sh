@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 for v in ${VARIANTS:-$(ls ipfixprobe_amd/variants/*.so)}; do
   name=$(basename $v .so)
-  IPXG_LIB=$PWD/$v timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} \
+  IPXG_TUNING=1 IPXG_LIB=$PWD/$v timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} \
       > gpurun_out/var_$name.json 2> gpurun_out/var_$name.err
   rc=$?
   if [ $rc -gt 1 ]; then echo "$name: exit $rc"; tail -3 gpurun_out/var_$name.err; exit $rc; fi
