@@ -1,11 +1,15 @@
 // ipxg_probe -- minimal pipeline driver: pcap/pcapng file -> gpucache -> flow records.
 //
 //   ipxg_probe -i FILE [-s "s=20;a=300;i=30;..."] [-o csv|csv-vlan|ipfix:PATH] [--odid N]
-//              [--export-time SEC] [--mtu N]
+//              [--export-time SEC] [--mtu N] [-q BLOCK] [--mbuf]
 //
-// The input side mirrors ipfixprobe's pcap plugin + input_storage_worker
-// (workers.cpp:40-140): packets are read in arrival order and handed to the storage plugin
-// one by one (put_pkt); at end of file the storage is finished (workers.cpp:136).  Output is
+// The input side is ipfixprobe's input_storage_worker (workers.cpp:40-140) over the raw-ingest
+// input plugin "pcapraw" (rawinput.hpp: the pcap plugin without the CPU parser): blocks of -q
+// frames (default 64, ipfixprobe.cpp:56) in arrival order, each frame handed to the storage
+// plugin (put_pkt); at end of file the storage is finished (workers.cpp:136).  --mbuf: every
+// block goes through the DPDK burst adapter instead (burst_to_block), the frames copied into
+// mbufs of rte_mbuf's layout (a 128-byte headroom, data_off / data_len) as rte_eth_rx_burst
+// returns them.  Output is
 // the basic biflow columns in the text form of the reference's functional tests (UniRec
 // logger, tests/functional/scripts/run_test.sh), one line per exported flow, or (ipfix:PATH)
 // the IPFIX message stream of the reference's IPFIX output plugin (basic templates), written
@@ -16,10 +20,13 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gpucache.hpp"
+#include "rawinput.hpp"
 
 namespace {
 
@@ -70,16 +77,28 @@ struct FileMessages : ipxp::MessageSink {
     }
 };
 
+// rte_mbuf's fields that the burst adapter reads (rte_mbuf_core.h: buf_addr, data_off,
+// data_len, pkt_len), plus where this driver keeps the packet's timestamp (DPDK: a dynfield)
+struct MockMbuf {
+    void* buf_addr;
+    uint16_t data_off;
+    uint16_t data_len;
+    uint32_t pkt_len;
+    struct timeval ts;
+    uint8_t room[128 + 65536];  // RTE_PKTMBUF_HEADROOM + data
+};
+
 void usage() {
     fprintf(stderr, "usage: ipxg_probe -i FILE [-s CACHE_OPTIONS] [-o csv|csv-vlan|ipfix:PATH] [--odid N] "
-                    "[--export-time SEC] [--mtu N] [--stats]\n");
+                    "[--export-time SEC] [--mtu N] [--stats] [-q BLOCK] [--mbuf]\n");
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
     std::string in, opts, fmt = "csv";
-    bool stats = false;
+    bool stats = false, mbuf = false;
+    size_t qsize = 64;
     ipxg_ipfix_exporter x;
     ipxg_ipfix_exporter_init(&x);
     x.export_time = (uint32_t)time(nullptr);
@@ -92,6 +111,8 @@ int main(int argc, char** argv) {
         else if (a == "--export-time" && i + 1 < argc) x.export_time = (uint32_t)strtoul(argv[++i], nullptr, 0);
         else if (a == "--mtu" && i + 1 < argc) x.mtu = (uint16_t)strtoul(argv[++i], nullptr, 0);
         else if (a == "--stats") stats = true;
+        else if (a == "-q" && i + 1 < argc) qsize = std::max<size_t>(1, strtoul(argv[++i], nullptr, 0));
+        else if (a == "--mbuf") mbuf = true;
         else {
             usage();
             return 2;
@@ -101,10 +122,11 @@ int main(int argc, char** argv) {
         usage();
         return 2;
     }
-    ipxg_capture* cap = nullptr;
-    int rc = ipxg_capture_load(in.c_str(), &cap);
-    if (rc) {
-        fprintf(stderr, "ipxg_probe: cannot read %s (%d)\n", in.c_str(), rc);
+    ipxp::RawPcapReader input;
+    try {
+        input.init(("file=" + in).c_str());
+    } catch (const ipxp::PluginError& e) {
+        fprintf(stderr, "ipxg_probe: %s\n", e.what());
         return 1;
     }
     // the capture's link type, unless the option string names one
@@ -115,14 +137,13 @@ int main(int argc, char** argv) {
         fprintf(stderr, "ipxg_probe: invalid option string\n");
         return 2;
     }
-    if (probe_cfg.datalink == 0) opts += (opts.empty() ? "" : ";") + std::string("dlt=") + std::to_string(cap->datalink);
+    if (probe_cfg.datalink == 0) opts += (opts.empty() ? "" : ";") + std::string("dlt=") + std::to_string(input.datalink());
     CsvSink sink(stdout, fmt == "csv-vlan");
     FILE* ipfix_out = nullptr;
     if (fmt.rfind("ipfix:", 0) == 0) {
         ipfix_out = fopen(fmt.c_str() + 6, "wb");
         if (!ipfix_out) {
             fprintf(stderr, "ipxg_probe: cannot write %s\n", fmt.c_str() + 6);
-            ipxg_capture_free(cap);
             return 1;
         }
     }
@@ -130,15 +151,28 @@ int main(int argc, char** argv) {
     try {
         ipxp::GpuFlowCache cache(opts, &sink);
         if (ipfix_out) cache.set_ipfix(&msink, x);
-        for (uint32_t i = 0; i < cap->n; ++i) {
-            const ipxg_pkt_desc& d = cap->desc[i];
-            ipxp::RawPacket p;
-            p.ts.tv_sec = d.ts_sec;
-            p.ts.tv_usec = d.ts_usec;
-            p.packet = cap->arena + d.offset;
-            p.packet_len = d.caplen;
-            p.packet_len_wire = d.wirelen;
-            cache.put_pkt(p);
+        ipxp::RawPacketBlock block(qsize), burst(qsize);
+        std::vector<MockMbuf> pool(mbuf ? qsize : 0);
+        std::vector<MockMbuf*> rx(mbuf ? qsize : 0);
+        for (;;) {  // input_storage_worker (workers.cpp:66-122)
+            const ipxp::InputResult r = input.get(block);
+            if (r == ipxp::InputResult::END_OF_FILE) break;
+            const ipxp::RawPacketBlock* b = &block;
+            if (mbuf) {  // the frames as an rx burst of mbufs, back through the DPDK adapter
+                for (size_t k = 0; k < block.cnt; ++k) {
+                    MockMbuf& m = pool[k];
+                    m.buf_addr = m.room;
+                    m.data_off = 128;
+                    m.data_len = block.pkts[k].packet_len;
+                    m.pkt_len = block.pkts[k].packet_len_wire;
+                    m.ts = block.pkts[k].ts;
+                    std::memcpy(m.room + 128, block.pkts[k].packet, m.data_len);
+                    rx[k] = &m;
+                }
+                ipxp::burst_to_block(rx.data(), (uint16_t)block.cnt, [](const MockMbuf* m) { return m->ts; }, burst);
+                b = &burst;
+            }
+            for (size_t k = 0; k < b->cnt; ++k) cache.put_pkt(b->pkts[k]);
         }
         cache.finish();
         if (stats) {
@@ -153,13 +187,11 @@ int main(int argc, char** argv) {
     } catch (const ipxp::PluginError& e) {
         fprintf(stderr, "ipxg_probe: %s\n", e.what());
         if (ipfix_out) fclose(ipfix_out);
-        ipxg_capture_free(cap);
         return 1;
     }
     if (ipfix_out) {
         fclose(ipfix_out);
         if (stats) fprintf(stderr, "ipfix: %zu records in %zu messages\n", msink.records, msink.msgs);
     }
-    ipxg_capture_free(cap);
     return 0;
 }

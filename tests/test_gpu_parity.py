@@ -93,21 +93,41 @@ def test_flows_fixture(name, batch):
         assert gst[k] == wst[k], k
 
 
-def test_basic_golden_through_probe_cli():
-    """The C++ host path end to end: ipxg_probe (pcap reader -> GpuFlowCache::put_pkt ->
-    finish) reproduces the reference's outputs/basic for mixed.pcap."""
+@pytest.mark.parametrize("mode", [[], ["-q", "7"], ["--mbuf"], ["--mbuf", "-q", "32"]])
+def test_basic_golden_through_probe_cli(mode):
+    """The C++ host path end to end: ipxg_probe (the raw-ingest input plugin "pcapraw" ->
+    input_storage_worker blocks -> GpuFlowCache::put_pkt -> finish) reproduces the reference's
+    outputs/basic for mixed.pcap; --mbuf: every block as a DPDK rx burst of mbufs through the
+    burst adapter (rawinput.hpp burst_to_block, dpdk.cpp:196-225)."""
     exe = os.path.join(ROOT, "ipfixprobe_amd", "ipxg_probe")
-    out = subprocess.run([exe, "-i", os.path.join(REF, "mixed.pcap")], check=True,
+    out = subprocess.run([exe, "-i", os.path.join(REF, "mixed.pcap")] + mode, check=True,
                          stdout=subprocess.PIPE, text=True, timeout=120).stdout
     got = Counter(out.splitlines())
     gold = Counter(pcaputil.read_golden(os.path.join(REF, "outputs", "basic")))
     assert got == gold
 
 
-def test_vlan_golden_through_probe_cli():
+@pytest.mark.parametrize("mode", [[], ["--mbuf"]])
+def test_vlan_golden_through_probe_cli(mode):
     exe = os.path.join(ROOT, "ipfixprobe_amd", "ipxg_probe")
-    out = subprocess.run([exe, "-i", os.path.join(REF, "vlan.pcap"), "-o", "csv-vlan"], check=True,
+    out = subprocess.run([exe, "-i", os.path.join(REF, "vlan.pcap"), "-o", "csv-vlan"] + mode, check=True,
                          stdout=subprocess.PIPE, text=True, timeout=120).stdout
     cols = pcaputil.BASIC_COLUMNS[:13] + ["VLAN_ID"] + pcaputil.BASIC_COLUMNS[13:]
     gold = Counter(pcaputil.read_golden(os.path.join(REF, "outputs", "vlan"), cols))
     assert Counter(out.splitlines()) == gold
+
+
+@pytest.mark.parametrize("name", ["http", "quic", "mqtt"])
+def test_probe_cli_raw_and_mbuf_inputs_match_oracle(name):
+    """Other reference captures (one Linux-SLL, nanosecond) through both raw inputs: the basic
+    columns of every record equal the oracle's."""
+    from test_oracle_golden import PAIRS
+    exe = os.path.join(ROOT, "ipfixprobe_amd", "ipxg_probe")
+    path = os.path.join(REF, PAIRS[name] + ".pcap")
+    dl, pk = pcaputil.read_capture(path)
+    arena, desc = pcaputil.to_batch(pk)
+    want, _ = oracle_py.run_capture(arena, desc, dl)
+    for mode in ([], ["--mbuf"]):
+        out = subprocess.run([exe, "-i", path] + mode, check=True, stdout=subprocess.PIPE, text=True,
+                             timeout=120).stdout
+        assert Counter(out.splitlines()) == Counter(pcaputil.format_records(want)), mode

@@ -1,0 +1,170 @@
+"""The reference's own process plugins through the bridge: dns.cpp, http.cpp,
+tls.cpp and quic.cpp from /root/reference, compiled unmodified by oracle/Makefile (ref_plugins)
+into oracle/_ref/libref_plugins.so behind the product's adapter
+(ipfixprobe_amd/host/plugin_adapter.hpp: ipxg_plugin hooks -> ipxp::ProcessPlugin virtuals, the
+record's ext handle -> an ipxp::Flow holding the RecordExt chain), built against the unmodified
+reference headers processPlugin.hpp / packet.hpp / flowifc.hpp.
+
+CPU: the oracle with each real plugin reproduces the reference's golden output of its plugin
+test (tests/functional/outputs/<plugin>, basic columns: every record for dns / http / quic, the
+flows with a TLS extension for tls).  GPU: the engine's bridge with the real plugins gives the
+oracle's records and, record by record, the same extension contents (RecordExt::get_text) --
+on the golden captures and on the configs[2] / configs[4] mixes.
+
+The library exists only where the reference tree was present at build time (it travels to the
+GPU box in oracle/_ref); the tests skip without it."""
+import ctypes
+import os
+import sys
+from collections import Counter
+
+import numpy as np
+import pytest
+
+import flowcmp
+import oracle_py
+import pcaputil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "tests", "golden", "reference")
+LIB = os.path.join(ROOT, "oracle", "_ref", "libref_plugins.so")
+sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
+
+pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="oracle/_ref/libref_plugins.so not built")
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        from ipfixprobe_amd.engine import Plugin
+        _L = ctypes.CDLL(LIB)
+        _L.ref_plugin_create.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Plugin)]
+        _L.ref_plugin_destroy.argtypes = [ctypes.POINTER(Plugin)]
+        _L.ref_ext_text.argtypes = [ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
+        _L.ref_ext_free.argtypes = [ctypes.c_uint64]
+    return _L
+
+
+class RefPlugin:
+    """A fresh instance of the reference plugin `name` behind the adapter (.struct: its ipxg_plugin)."""
+
+    def __init__(self, name):
+        from ipfixprobe_amd.engine import Plugin
+        self.struct = Plugin()
+        rc = lib().ref_plugin_create(name.encode(), b"", ctypes.byref(self.struct))
+        assert rc == 0, (name, rc)
+
+    def __del__(self):
+        try:
+            lib().ref_plugin_destroy(ctypes.byref(self.struct))
+        except Exception:
+            pass
+
+
+def take_texts(recs):
+    """Each record's extension texts (then its Flow is released, as the consumer would)."""
+    out = []
+    buf = ctypes.create_string_buffer(1 << 16)
+    for e in recs["ext"]:
+        e = int(e)
+        if not e:
+            out.append("")
+            continue
+        n = lib().ref_ext_text(e, buf, len(buf))
+        assert n < len(buf)
+        out.append(buf.value.decode(errors="replace"))
+        lib().ref_ext_free(e)
+    return out
+
+
+def keyed(recs, texts):
+    return Counter((flowcmp.rec_key(r), t) for r, t in zip(recs, texts))
+
+
+GOLDEN = [("dns", "dns"), ("http", "http"), ("tls", "tls"), ("quic", "quic_initial-sample")]
+
+
+def _capture(pcap):
+    dl, pk = pcaputil.read_capture(os.path.join(REF, pcap + ".pcap"))
+    arena, desc = pcaputil.to_batch(pk)
+    return dl, arena, desc
+
+
+@pytest.mark.parametrize("name,pcap", GOLDEN)
+def test_oracle_with_reference_plugin_reproduces_golden(name, pcap):
+    dl, arena, desc = _capture(pcap)
+    pl = RefPlugin(name)
+    recs, _ = oracle_py.run_capture(arena, desc, dl, plugins=[pl.struct])
+    texts = take_texts(recs)
+    gold = Counter(pcaputil.read_golden(os.path.join(REF, "outputs", name)))
+    if name == "tls":  # the tls test's output keeps the flows with a TLS extension
+        recs = recs[np.array([t != "" for t in texts], dtype=bool)]
+    assert Counter(pcaputil.format_records(recs)) == gold
+    assert any(texts)
+
+
+@pytest.mark.parametrize("name,pcap", GOLDEN)
+def test_stand_in_decides_like_reference_plugin(name, pcap):
+    """The native stand-in (include/ipxg_stdplugins.h) ends and claims the same flows as the real
+    plugin on its golden capture."""
+    from ipfixprobe_amd.engine import StdPlugin
+    dl, arena, desc = _capture(pcap)
+    rp, sp = RefPlugin(name), StdPlugin(name)
+    a, _ = oracle_py.run_capture(arena, desc, dl, plugins=[rp.struct])
+    b, _ = oracle_py.run_capture(arena, desc, dl, plugins=[sp.struct])
+    claimed = np.array([t != "" for t in take_texts(a)], dtype=bool)
+    assert not flowcmp.diff(a, b)
+    assert not flowcmp.diff(a[claimed], b[b["ext"] != 0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [None, 5])
+@pytest.mark.parametrize("name,pcap", GOLDEN)
+def test_bridge_with_reference_plugin_matches_oracle(name, pcap, batch):
+    from ipfixprobe_amd import run_capture
+    dl, arena, desc = _capture(pcap)
+    ep, op = RefPlugin(name), RefPlugin(name)
+    got, _ = run_capture(arena, desc, datalink=dl, params="s=16", batch=batch, plugins=[ep.struct])
+    want, _ = oracle_py.run_capture(arena, desc, dl, cache_exp=16, plugins=[op.struct])
+    tg, tw = take_texts(got), take_texts(want)
+    assert keyed(got, tg) == keyed(want, tw)
+    gold = Counter(pcaputil.read_golden(os.path.join(REF, "outputs", name)))
+    if name == "tls":
+        got = got[np.array([t != "" for t in tg], dtype=bool)]
+    assert Counter(pcaputil.format_records(got)) == gold
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix,names", [("imix", ("dns", "http", "tls")), ("quic", ("quic", "dns"))])
+def test_bridge_with_reference_plugins_on_workload(mix, names):
+    """600k packets of the configs[2] / configs[4] mix (three device batches, flows carried across
+    them) with the configs' real plugins: records and extension contents equal the oracle's."""
+    import torch
+    import synthgen
+    from ipfixprobe_amd import Engine
+    m = synthgen.Mix(mix, 200_000, seed=77, zipf=1.1 if mix == "imix" else None)
+    gen = synthgen.Generator(m, torch.device("cuda", 0), seed=77)
+    n, nb = 200_000, 3
+    batches = [gen.batch(k * n, n) for k in range(nb)]
+    torch.cuda.synchronize()
+    eps = [RefPlugin(x) for x in names]
+    with Engine("s=19") as e:
+        for p in eps:
+            e.add_plugin(p.struct)
+        for fr, de in batches:
+            e.submit(fr, de, device=True)
+        e.finish()
+        got = e.poll()
+    ops = [RefPlugin(x) for x in names]
+    c = oracle_py.OracleCache(cache_exp=20)
+    for p in ops:
+        c.add_plugin(p.struct)
+    for fr, de in batches:
+        c.run(fr.cpu().numpy(), de.cpu().numpy().view(pcaputil.DESC_DTYPE), 1)
+    c.finish()
+    want = c.take()
+    c.close()
+    tg, tw = take_texts(got), take_texts(want)
+    assert sum(1 for t in tw if t) > 50
+    assert keyed(got, tg) == keyed(want, tw)
