@@ -3,6 +3,10 @@
 //   frame  : lane = packet; a 16-byte descriptor, then the frame's first 48 bytes at the
 //            descriptor's offset (3 x 16-byte loads, dependent on the descriptor)
 //   frame_nodesc : the same 48 bytes at i * stride, no descriptor
+//   frame_lds : the descriptors, then -- when a wave's 64 frames sit back to back at 64-byte
+//            stride (a ballot over the offsets) -- the wave's 4 KB read as 4 contiguous 1 KB
+//            loads (lane = 16 bytes) and transposed through the wave's LDS (frames at an 80-byte
+//            pitch: conflict-free 16-byte reads), each lane then holding its frame's 48 bytes
 // Usage: membench <n_packets> <stride> <blocks>
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -53,6 +57,52 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t* __restrict__ arena
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+__global__ __launch_bounds__(256) void k_frame_lds(const uint8_t* __restrict__ arena, const Desc* __restrict__ desc,
+                                                   uint32_t n, uint32_t* out) {
+    __shared__ uint4 xs[4][64 * 5];  // per wave: 64 frames x 80 bytes
+    uint32_t acc = 0;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256 * 4 + threadIdx.x; i0 < n; i0 += step * 4) {
+        uint32_t off[4];
+        bool seq[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = min(i0 + k * 256, n - 1);
+            const Desc d = desc[i];
+            off[k] = d.off;
+            acc ^= d.len ^ d.s;
+            const uint32_t o0 = __builtin_amdgcn_readfirstlane(d.off);
+            seq[k] = __all(d.off == o0 + 64u * lane);
+        }
+        uint4 h[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t o0 = __builtin_amdgcn_readfirstlane(off[k]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t a = seq[k] ? o0 + 1024u * c + 16u * lane : (c < 3 ? off[k] + 16u * c : off[k]);
+                h[k][c] = *reinterpret_cast<const uint4*>(arena + a);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (seq[k]) {  // chunk (lane & 3) of frame 16c + lane / 4 -> the frame's 80-byte slot
+#pragma unroll
+                for (int c = 0; c < 4; ++c) xs[w][(16 * c + lane / 4) * 5 + (lane & 3)] = h[k][c];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS stores
+#pragma unroll
+                for (int c = 0; c < 3; ++c) h[k][c] = xs[w][lane * 5 + c];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc ^= h[k][c].x ^ h[k][c].y ^ h[k][c].z ^ h[k][c].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 10000000;
     const uint32_t fs = argc > 2 ? atoi(argv[2]) : 64;
@@ -84,5 +134,6 @@ int main(int argc, char** argv) {
     run("contig", (double)n16 * 16, [&] { hipLaunchKernelGGL(k_contig, dim3(blocks), dim3(256), 0, 0, (const uint4*)arena, n16, out); });
     run("frame", (double)n * (48 + 16), [&] { hipLaunchKernelGGL(k_frame<true>, dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
     run("frame_nodesc", (double)n * 48, [&] { hipLaunchKernelGGL(k_frame<false>, dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    run("frame_lds", (double)n * (64 + 16), [&] { hipLaunchKernelGGL(k_frame_lds, dim3(blocks), dim3(256), 0, 0, arena, desc, n, out); });
     return 0;
 }
