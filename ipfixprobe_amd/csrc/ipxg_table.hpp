@@ -666,7 +666,6 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
         pppoe = true;
     }
     if (l3 != ETH_P_IP && l3 != ETH_P_IPV6) return false;
-    if (S == 3 && l3 == ETH_P_IPV6) return false;  // its L4 header would end past the window
     // the window re-based so that the L3 header starts at byte 14 of v
     constexpr int VD = WIDE_DW - 2;
     uint32_t v[VD];
@@ -733,6 +732,7 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
         }
         if (proto != 6 && proto != 17) return false;   // other extension headers (or another L4)
         if (xh == 2 && proto == 6) return false;        // its TCP header would end past the window
+        if (S == 3 && proto == 6) return false;         // under 3 MPLS labels: UDP fits, TCP does not
         p.ip_version = 6;
         p.ip_len = (uint16_t)(wbe16<18>(v) + 40);
         p.frag_id = 0;

@@ -393,7 +393,8 @@ def test_nonmonotonic_detected_at_wave_and_tile_boundaries(at):
 
 def _edge_frames():
     """IPv6 extension chains (8- and 16-byte headers, the types the register walk takes and
-    others) and IPv4-in-GRE (optional fields, inner IPv6 / MPLS, IP options, fragments), each
+    others), IPv4-in-GRE (optional fields, inner IPv6 / MPLS, IP options, fragments) and MPLS
+    stacks of 1-3 labels over IPv4 / IPv6 with UDP / TCP, each
     also truncated at every caplen from 50 bytes: the shapes at the border of k_bin's wide
     register walk, where a frame either parses in registers or falls back to the LDS walk."""
     mac = b"\x02\0\0\0\0\x01", b"\x02\0\0\0\0\x02"
@@ -432,6 +433,14 @@ def _edge_frames():
                 out.append(synth.eth(*mac, 0x0800) +
                            synth.ipv4(b"\xc0\0\0\x01", b"\xc0\0\0\x02", 47, synth.gre(pay, pt, *flags), ihl=ihl,
                                       df=1, ident=k))
+    for n in (1, 2, 3):  # MPLS stacks (IPv6 under three labels: UDP in the window, TCP past it)
+        for inner in ("v4udp", "v4tcp", "v6udp", "v6tcp", "v6tcp_ts"):
+            k += 1
+            l4 = (synth.udp(3000 + k, 443) if inner.endswith("udp") else
+                  synth.tcp(3000 + k, 443, 0x10, options=b"\x01\x01\x08\x0a" + b"\0" * 8 if inner == "v6tcp_ts" else b""))
+            proto = 17 if inner.endswith("udp") else 6
+            ip = synth.ipv4(a4, b4, proto, l4) if inner.startswith("v4") else synth.ipv6(a6, b6, proto, l4)
+            out.append(synth.eth(*mac, 0x8847) + synth.mpls([16 + j for j in range(n)], ip))
     frames = []
     for f in out:
         f = synth.pad(f)

@@ -8,7 +8,7 @@ OUT=gpurun_out/r03b
 mkdir -p $OUT
 stop() { case "$1" in 0|1) return 0 ;; *) echo "STOP: $2 exited $1"; exit "$1" ;; esac; }
 timeout -k 10 900 python -u -m pytest tests/test_stdplugins.py tests/test_ref_plugins.py tests/test_gpu_parity.py tests/test_shard.py tests/test_strict.py \
-    tests/test_gpu_workloads.py tests/test_gpu_semantics.py::test_bench_size_parity -m gpu -q -p no:cacheprovider \
+    tests/test_gpu_workloads.py tests/test_gpu_semantics.py::test_bench_size_parity tests/test_gpu_semantics.py::test_wide_walk_ext_and_gre_edges -m gpu -q -p no:cacheprovider \
     --timeout 240 --timeout-method thread > $OUT/pytest_new.txt 2>&1
 rc=$?; tail -15 $OUT/pytest_new.txt; stop $rc pytest
 for W in "udp64:--steps 50 --warmup 3 --no-cpu-baseline --no-e2e" \
