@@ -31,6 +31,11 @@ struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
 };
+// pinned host memory (the plugin walk's copies: DMA at full PCIe rate, no bounce buffer)
+struct HostBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
 
 struct ipxg_engine {
     ipxg_config cfg;
@@ -65,6 +70,7 @@ struct ipxg_engine {
     std::vector<ipxg_plugin> plugins;
     uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
+    HostBuf ph_sorted, ph_parsed, ph_desc, ph_bytes;  // their pinned host copies
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
     uint64_t host_unreasoned = 0;  // counted exports without an end reason (total_exported only)
@@ -157,6 +163,18 @@ static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
     b.p = nullptr;
     b.bytes = 0;
     if (hipMalloc(&b.p, nb) != hipSuccess) return set_err(e, IPXG_ENOMEM, "hipMalloc failed");
+    b.bytes = nb;
+    return IPXG_OK;
+}
+
+static int ensure_host(ipxg_engine* e, HostBuf& b, size_t need) {
+    if (b.bytes >= need && b.p) return IPXG_OK;
+    size_t nb = std::max<size_t>(need, b.bytes + b.bytes / 2);
+    if (nb < 4096) nb = 4096;
+    if (b.p) HIPCHK(e, hipHostFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipHostMalloc(&b.p, nb, hipHostMallocDefault) != hipSuccess) return set_err(e, IPXG_ENOMEM, "hipHostMalloc failed");
     b.bytes = nb;
     return IPXG_OK;
 }
@@ -502,6 +520,8 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
     if (e->plan_h) hipHostFree(e->plan_h);
+    for (HostBuf* h : {&e->ph_sorted, &e->ph_parsed, &e->ph_desc, &e->ph_bytes})
+        if (h->p) hipHostFree(h->p);
     if (e->plan_ev) (void)hipEventDestroy(e->plan_ev);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -958,9 +978,10 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipStreamSynchronize(e->st));
     if (!nf) return IPXG_OK;
     std::vector<PluginFlow> flows(nf);
-    std::vector<uint64_t> sorted(npk);
+    if ((rc = ensure_host(e, e->ph_sorted, (size_t)npk * 8 + 8))) return rc;
+    const uint64_t* sorted = (const uint64_t*)e->ph_sorted.p;
     HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(sorted.data(), cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->ph_sorted.p, cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     // the flows' packets, each flow's in arrival order (the sorted list: rank << 24 | index)
     std::vector<uint32_t> idx, first(nf + 1);
@@ -977,11 +998,12 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     launch_plugin_pkts(e->st, bv, p, frag_view(e), (const uint32_t*)e->pf_idx.p, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
                        (ipxg_pkt_desc*)e->pf_desc.p);
     HIPCHK(e, hipGetLastError());
-    std::vector<ipxg_parsed_pkt> pk(m);
-    std::vector<ipxg_pkt_desc> de(m);
-    HIPCHK(e, hipMemcpyAsync(pk.data(), e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost,
-                             e->st));
-    HIPCHK(e, hipMemcpyAsync(de.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
+    if ((rc = ensure_host(e, e->ph_parsed, (size_t)m * sizeof(ipxg_parsed_pkt) + 8))) return rc;
+    if ((rc = ensure_host(e, e->ph_desc, (size_t)m * sizeof(ipxg_pkt_desc) + 16))) return rc;
+    ipxg_parsed_pkt* pk = (ipxg_parsed_pkt*)e->ph_parsed.p;
+    const ipxg_pkt_desc* de = (const ipxg_pkt_desc*)e->ph_desc.p;
+    HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->ph_desc.p, e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     std::vector<uint64_t> off(m + 1, 0);
     for (uint32_t k = 0; k < m; ++k) off[k + 1] = off[k] + de[k].caplen;
@@ -995,8 +1017,9 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     e->tm.plugin_packets += m;
     e->tm.plugin_bytes += off[m];
     for (uint32_t k = 0; k < m; ++k) e->tm.plugin_extra_bytes += de[k].caplen > 128 ? de[k].caplen - 128u : 0u;
-    std::vector<uint8_t> bytes(off[m] + 1);
-    HIPCHK(e, hipMemcpyAsync(bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
+    if ((rc = ensure_host(e, e->ph_bytes, off[m] + 16))) return rc;
+    const uint8_t* bytes = (const uint8_t*)e->ph_bytes.p;
+    HIPCHK(e, hipMemcpyAsync(e->ph_bytes.p, e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     // the walks, flows in order of their first packet (export order is arbitrary otherwise)
     std::vector<uint32_t> order(nf);
@@ -1013,7 +1036,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             ipxg_packet_view v;
             std::memset(&v, 0, sizeof(v));
             v.pkt = &pk[k];
-            v.data = bytes.data() + off[k];
+            v.data = bytes + off[k];
             v.caplen = de[k].caplen;
             v.wirelen = de[k].wirelen;
             v.ts_sec = de[k].ts_sec;

@@ -147,6 +147,39 @@ __device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, cons
 }
 
 
+// The narrow walk's heads, transposed (IPXG_BIN_XPOSE): when a wave's 64 frames sit back to back
+// at a 64-byte pitch (a ballot over the descriptors' offsets -- the 64 B mixes), the wave reads
+// its 4 KB as four contiguous 1 KB loads (lane = 16 bytes: 8 lines per instruction instead of 32
+// per strided 16-byte load) and hands each lane its frame's first 48 bytes through the wave's
+// LDS (80-byte frame pitch: conflict-free 16-byte reads); otherwise the 3 strided loads.  Always
+// 4 loads, branch-free addresses: the same count in flight on every path.
+#ifndef IPXG_BIN_XPOSE
+#define IPXG_BIN_XPOSE 0
+#endif
+__device__ __forceinline__ Head<4> load_head_x(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok,
+                                               bool& seq) {
+    const uint32_t lane = lane_id();
+    const uint32_t o0 = __builtin_amdgcn_readfirstlane(d.offset);
+    seq = __ballot(ok && d.offset == o0 + 64u * lane) == ~0ull;  // wave-uniform
+    const uint32_t o = ok ? d.offset : BUF_OOB;
+    Head<4> h;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t a = seq ? o0 + 1024u * k + 16u * lane : (k < 3 ? o + 16u * k : BUF_OOB);
+        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, a, 0, IPXG_LOAD_AUX));
+    }
+    return h;
+}
+// chunk (lane & 3) of frame 16k + lane / 4 (load k) -> lane f's chunks 0..2, via xs (320 uint4)
+__device__ __forceinline__ void xpose_head(uint4* xs, Head<4>& h) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xs[(16u * k + (lane >> 2)) * 5u + (lane & 3u)] = h.c[k];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the wave's own LDS stores, in order)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) h.c[k] = xs[lane * 5u + k];
+}
+
 // descriptor i (zeros past the batch's end)
 __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, uint32_t i) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, IPXG_LOAD_AUX);
@@ -456,8 +489,11 @@ __device__ __forceinline__ uint32_t slow_class(const uint4 c0, const uint4 c1, c
 // frames from registers as well; the remaining shapes (MPLS, PPPoE, GRE, IPv6 extension
 // headers, other TCP options, ...) still go to the slow list.
 // The host picks the variants per batch (ipxg_engine.cpp: tile_agg, wide).
+#ifndef IPXG_BIN_NARROW_WPE
+#define IPXG_BIN_NARROW_WPE 3  // waves per SIMD of the narrow, non-aggregating k_bin (its register budget)
+#endif
 template <bool AGG, bool WIDE>
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : 3)))
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : IPXG_BIN_NARROW_WPE)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
@@ -491,7 +527,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     const uint64_t ts_before = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
     uint32_t spilled = 0, walked = 0, tb_or = 0;
-    constexpr int NC = WIDE ? WIDE_DW / 4 : 3;
+    constexpr bool XP = IPXG_BIN_XPOSE && !WIDE;
+    constexpr int NC = WIDE ? WIDE_DW / 4 : (XP ? 4 : 3);
+    // the wave's transpose area (XP): the stage array is free during the packet loop
+    uint4* const xs = reinterpret_cast<uint4*>(stage) + (tid >> 6) * 320u;
+    static_assert(IPXG_BLOCK / 64 * 320 <= BIN_TILE, "transpose areas fit the stage array");
     auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(d); };
     bool nonmono = false;
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
@@ -523,6 +563,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
     ipxg_pkt_desc Dr[DA];
     Head<NC> Hr[HA];
+    bool Xr[HA];  // XP: ring slot h holds a transposed (contiguous) head load
     // The prologue issues its loads in the order the last DA steps of a tile do, with dummy
     // stores where a tile issues heads of its own steps and its record stores: the loop's
     // first waits are shared by the first tile and all later ones, and the compiler sizes
@@ -533,7 +574,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         Dr[k] = load_desc(rs_desc, i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
-            Hr[h] = load_head<NC>(rs_arena, Dr[h], want(Dr[h]));
+            if constexpr (XP) Hr[h] = load_head_x(rs_arena, Dr[h], want(Dr[h]), Xr[h]);
+            else Hr[h] = load_head<NC>(rs_arena, Dr[h], want(Dr[h]));
         } else {
 #pragma unroll
             for (int q = 0; q < 3; ++q) g_dummy_rec[(k * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
@@ -573,7 +615,10 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t i = tile + j * IPXG_BLOCK + tid;
             // this step's packet, loaded HA (head) and DA (descriptor) steps ago
             const ipxg_pkt_desc dc = Dr[jj % DA];
-            const Head<NC> hc = Hr[jj % HA];
+            Head<NC> hc = Hr[jj % HA];
+            if constexpr (XP) {
+                if (Xr[jj % HA]) xpose_head(xs, hc);  // wave-uniform
+            }
             // bytes 40-43 are not parsed: keep their register live until here, or the compiler
             // reuses it while the load is in flight and must drain every load to do so
             asm volatile("" ::"v"(hc.c[2].z));
@@ -581,7 +626,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
             Dr[jj % DA] = load_desc(rs_desc, ia);
             const ipxg_pkt_desc dh = Dr[(jj + HA) % DA];
-            Hr[jj % HA] = load_head<NC>(rs_arena, dh, want(dh));
+            if constexpr (XP) Hr[jj % HA] = load_head_x(rs_arena, dh, want(dh), Xr[jj % HA]);
+            else Hr[jj % HA] = load_head<NC>(rs_arena, dh, want(dh));
             const bool act = i < b.n;
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
