@@ -69,6 +69,7 @@ struct ipxg_engine {
     // host walks add to the device-side counters (exports by reason, TopPorts)
     std::vector<ipxg_plugin> plugins;
     uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
+    double walk_phase_ms[6] = {0, 0, 0, 0, 0, 0};  // plugin_walk's phases (IPXG_WALK_TRACE)
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     HostBuf ph_sorted, ph_parsed, ph_desc, ph_bytes;  // their pinned host copies
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
@@ -499,6 +500,10 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
 }
 
 int ipxg_destroy(ipxg_engine* e) {
+    if (e && std::getenv("IPXG_WALK_TRACE") && e->tm.plugin_flows)
+        std::fprintf(stderr, "ipxg plugin walk ms: pack %.1f fetch %.1f parse %.1f bytes %.1f walk %.1f back %.1f\n",
+                     e->walk_phase_ms[0], e->walk_phase_ms[1], e->walk_phase_ms[2], e->walk_phase_ms[3],
+                     e->walk_phase_ms[4], e->walk_phase_ms[5]);
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
     hipFree(e->hot);
@@ -961,6 +966,15 @@ struct FlowWalk {
 static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, const ComplexView& cx, uint32_t ncx,
                        uint32_t npk, int64_t* live_delta) {
     const auto t0 = std::chrono::steady_clock::now();
+    auto tm = t0;
+    // IPXG_WALK_TRACE: the walk's phases (pack + count, flow images + sorted list, parsed
+    // packets, frame bytes, the host loop, write-back) summed, printed when the engine closes
+#define WALK_MARK(k)                                                                                         \
+    do {                                                                                                   \
+        const auto t_ = std::chrono::steady_clock::now();                                                  \
+        e->walk_phase_ms[k] += std::chrono::duration<double, std::milli>(t_ - tm).count();                 \
+        tm = t_;                                                                                           \
+    } while (0)
     struct Clock {  // the walk's wall time, however it returns
         ipxg_engine* e;
         std::chrono::steady_clock::time_point t0;
@@ -975,14 +989,14 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipGetLastError());
     uint32_t nf = 0;
     HIPCHK(e, hipMemcpyAsync(&nf, cnt_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(0);
     if (!nf) return IPXG_OK;
     std::vector<PluginFlow> flows(nf);
     if ((rc = ensure_host(e, e->ph_sorted, (size_t)npk * 8 + 8))) return rc;
     const uint64_t* sorted = (const uint64_t*)e->ph_sorted.p;
     HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->ph_sorted.p, cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(1);
     // the flows' packets, each flow's in arrival order (the sorted list: rank << 24 | index)
     std::vector<uint32_t> idx, first(nf + 1);
     for (uint32_t f = 0; f < nf; ++f) {
@@ -1004,7 +1018,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const ipxg_pkt_desc* de = (const ipxg_pkt_desc*)e->ph_desc.p;
     HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->ph_desc.p, e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(2);
     std::vector<uint64_t> off(m + 1, 0);
     for (uint32_t k = 0; k < m; ++k) off[k + 1] = off[k] + de[k].caplen;
     if ((rc = ensure(e, e->pf_off, (size_t)(m + 1) * 8))) return rc;
@@ -1020,7 +1034,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     if ((rc = ensure_host(e, e->ph_bytes, off[m] + 16))) return rc;
     const uint8_t* bytes = (const uint8_t*)e->ph_bytes.p;
     HIPCHK(e, hipMemcpyAsync(e->ph_bytes.p, e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(3);
     // the walks, flows in order of their first packet (export order is arbitrary otherwise)
     std::vector<uint32_t> order(nf);
     for (uint32_t f = 0; f < nf; ++f) order[f] = f;
@@ -1058,6 +1072,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             a[r.dst_port] += F.len;
         }
     }
+    WALK_MARK(4);
     // back to the device: the slots, then the exports after the batch's own
     HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows.data(), (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
     launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf);
@@ -1078,6 +1093,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
     for (int k = 0; k < 6; ++k) e->host_pkts[k] += wo.pkts[k];
     e->host_unreasoned += wo.unreasoned;
+    WALK_MARK(5);
+#undef WALK_MARK
     return IPXG_OK;
 }
 

@@ -14,8 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "tests", "golden", "reference")
 
 
-def _header_functions():
-    src = open(os.path.join(ROOT, "include", "ipxg.h")).read()
+def _header_functions(name="ipxg.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
     return sorted(set(re.findall(r"^\s*(?:[\w\*]+\s+)+\**(ipxg_\w+)\s*\(", src, re.M)))
 
 
@@ -27,6 +27,23 @@ def test_library_exports_every_declared_symbol():
     for f in funcs:
         assert hasattr(L, f), f
     assert set(engine.EXPORTED_SYMBOLS) <= set(funcs)
+
+
+def test_stdplugins_library_exports_its_header():
+    """libipxg_stdplugins.so (the native stand-in process plugins) exports every function
+    include/ipxg_stdplugins.h declares, and the plugin struct is ABI 2's (masked prefixes,
+    follow_packets appended)."""
+    from ipfixprobe_amd import engine
+    L = ctypes.CDLL(engine.STD_LIB_PATH)
+    funcs = _header_functions("ipxg_stdplugins.h")
+    assert funcs == ["ipxg_std_plugin", "ipxg_std_plugin_calls", "ipxg_std_plugin_free"]
+    for f in funcs:
+        assert hasattr(L, f), f
+    assert ctypes.sizeof(engine.Plugin) == 632  # = sizeof(ipxg_plugin), gcc x86-64
+    p = engine.StdPlugin("quic")
+    assert p.struct.masked == 1 and p.struct.prefix_mask[0][0] == 0x80 and p.struct.follow_packets == 30
+    with pytest.raises(engine.IpxgError):
+        engine.StdPlugin("nope")
 
 
 def test_struct_layouts_match_header_and_test_restatement():
