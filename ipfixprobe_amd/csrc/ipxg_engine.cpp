@@ -31,12 +31,6 @@ struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
 };
-// pinned host memory (the plugin walk's copies: DMA at full PCIe rate, no bounce buffer)
-struct HostBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-};
-
 struct ipxg_engine {
     ipxg_config cfg;
     hipStream_t st = nullptr;
@@ -71,7 +65,12 @@ struct ipxg_engine {
     uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
     double walk_phase_ms[6] = {0, 0, 0, 0, 0, 0};  // plugin_walk's phases (IPXG_WALK_TRACE)
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
-    HostBuf ph_sorted, ph_parsed, ph_desc, ph_bytes;  // their pinned host copies
+    // their host copies, kept across batches (pageable: the walk reads them on the CPU, and
+    // pinned hipHostMalloc memory read slower there -- measured: +58 % walk time on configs[2])
+    std::vector<uint64_t> hw_sorted;
+    std::vector<ipxg_parsed_pkt> hw_parsed;
+    std::vector<ipxg_pkt_desc> hw_desc;
+    std::vector<uint8_t> hw_bytes;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
     uint64_t host_unreasoned = 0;  // counted exports without an end reason (total_exported only)
@@ -164,18 +163,6 @@ static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
     b.p = nullptr;
     b.bytes = 0;
     if (hipMalloc(&b.p, nb) != hipSuccess) return set_err(e, IPXG_ENOMEM, "hipMalloc failed");
-    b.bytes = nb;
-    return IPXG_OK;
-}
-
-static int ensure_host(ipxg_engine* e, HostBuf& b, size_t need) {
-    if (b.bytes >= need && b.p) return IPXG_OK;
-    size_t nb = std::max<size_t>(need, b.bytes + b.bytes / 2);
-    if (nb < 4096) nb = 4096;
-    if (b.p) HIPCHK(e, hipHostFree(b.p));
-    b.p = nullptr;
-    b.bytes = 0;
-    if (hipHostMalloc(&b.p, nb, hipHostMallocDefault) != hipSuccess) return set_err(e, IPXG_ENOMEM, "hipHostMalloc failed");
     b.bytes = nb;
     return IPXG_OK;
 }
@@ -525,8 +512,6 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
     if (e->plan_h) hipHostFree(e->plan_h);
-    for (HostBuf* h : {&e->ph_sorted, &e->ph_parsed, &e->ph_desc, &e->ph_bytes})
-        if (h->p) hipHostFree(h->p);
     if (e->plan_ev) (void)hipEventDestroy(e->plan_ev);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -992,13 +977,18 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(0);
     if (!nf) return IPXG_OK;
     std::vector<PluginFlow> flows(nf);
-    if ((rc = ensure_host(e, e->ph_sorted, (size_t)npk * 8 + 8))) return rc;
-    const uint64_t* sorted = (const uint64_t*)e->ph_sorted.p;
+    e->hw_sorted.resize(npk);
+    const uint64_t* sorted = e->hw_sorted.data();
     HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->ph_sorted.p, cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_sorted.data(), cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(1);
     // the flows' packets, each flow's in arrival order (the sorted list: rank << 24 | index)
     std::vector<uint32_t> idx, first(nf + 1);
+    {
+        size_t total = 0;
+        for (uint32_t f = 0; f < nf; ++f) total += flows[f].len;
+        idx.reserve(total);
+    }
     for (uint32_t f = 0; f < nf; ++f) {
         first[f] = (uint32_t)idx.size();
         for (uint32_t k = 0; k < flows[f].len; ++k) idx.push_back((uint32_t)(sorted[flows[f].seg + k] & 0xFFFFFF));
@@ -1012,12 +1002,12 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     launch_plugin_pkts(e->st, bv, p, frag_view(e), (const uint32_t*)e->pf_idx.p, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
                        (ipxg_pkt_desc*)e->pf_desc.p);
     HIPCHK(e, hipGetLastError());
-    if ((rc = ensure_host(e, e->ph_parsed, (size_t)m * sizeof(ipxg_parsed_pkt) + 8))) return rc;
-    if ((rc = ensure_host(e, e->ph_desc, (size_t)m * sizeof(ipxg_pkt_desc) + 16))) return rc;
-    ipxg_parsed_pkt* pk = (ipxg_parsed_pkt*)e->ph_parsed.p;
-    const ipxg_pkt_desc* de = (const ipxg_pkt_desc*)e->ph_desc.p;
+    e->hw_parsed.resize(m);
+    e->hw_desc.resize(m);
+    ipxg_parsed_pkt* pk = e->hw_parsed.data();
+    const ipxg_pkt_desc* de = e->hw_desc.data();
     HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->ph_desc.p, e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(2);
     std::vector<uint64_t> off(m + 1, 0);
     for (uint32_t k = 0; k < m; ++k) off[k + 1] = off[k] + de[k].caplen;
@@ -1031,18 +1021,21 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     e->tm.plugin_packets += m;
     e->tm.plugin_bytes += off[m];
     for (uint32_t k = 0; k < m; ++k) e->tm.plugin_extra_bytes += de[k].caplen > 128 ? de[k].caplen - 128u : 0u;
-    if ((rc = ensure_host(e, e->ph_bytes, off[m] + 16))) return rc;
-    const uint8_t* bytes = (const uint8_t*)e->ph_bytes.p;
-    HIPCHK(e, hipMemcpyAsync(e->ph_bytes.p, e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
+    e->hw_bytes.resize(off[m] + 16);
+    const uint8_t* bytes = e->hw_bytes.data();
+    HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(3);
     // the walks, flows in order of their first packet (export order is arbitrary otherwise)
-    std::vector<uint32_t> order(nf);
-    for (uint32_t f = 0; f < nf; ++f) order[f] = f;
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return idx[first[a]] < idx[first[b]]; });
+    // (sorted as packed {first index, flow} words: contiguous keys, no indirection per compare)
+    std::vector<uint64_t> okey(nf);
+    for (uint32_t f = 0; f < nf; ++f) okey[f] = ((uint64_t)idx[first[f]] << 32) | f;
+    std::sort(okey.begin(), okey.end());
     WalkOut wo;
+    wo.ex.reserve(m + 16);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.empty()) e->host_ports.assign(2 * 65536, 0);
-    for (uint32_t f : order) {
+    for (const uint64_t ok : okey) {
+        const uint32_t f = (uint32_t)ok;
         PluginFlow& F = flows[f];
         FlowWalk w{e->plugins, p, wo, F.rec, (F.state & SLOT_LIVE) != 0};
         const bool was_live = w.live;
@@ -1185,6 +1178,20 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         nadef = e->ctl_h->agg_deferred;
         std::swap(e->defer_a, e->defer_b);
         std::swap(e->adefer_a, e->adefer_b);
+    }
+    // finalise-list flows whose table probe failed in k_fin_list (a batch of many new flows into
+    // a small table): grow the table and finalise just those, until none is left
+    uint32_t nfd = c1.fin_deferred;
+    while (nfd) {
+        if (!slow) ev_rec(e, 5);
+        slow = true;
+        if ((rc = rehash(e, e->cap * 2))) return rc;
+        HIPCHK(e, hipMemsetAsync(&e->ctl_d->fin_deferred, 0, sizeof(uint32_t), e->st));
+        launch_fin_list(e->st, bv, p, table_view(e), frag_view(e), export_view(e), e->ctl_d, (HotSlot*)e->fin_list.p,
+                        e->stats_d, c1.fin_count, false, true);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        nfd = e->ctl_h->fin_deferred;
     }
     if (slow) {
         ev_rec(e, 6);
@@ -1370,7 +1377,7 @@ int ipxg_finish(ipxg_engine* e) {
         if ((rc = check_ex(e))) return rc;
         if (fuse) {
             // complete unless k_fin_list could not fuse (host work) or left complex flows
-            const bool done = e->ctl_h->fused && !e->ctl_h->complex_count;
+            const bool done = e->ctl_h->fused && !e->ctl_h->complex_count && !e->ctl_h->fin_deferred;
             if ((rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, true))) return rc;
             if (done) {
                 e->keys = e->live = 0;

@@ -53,6 +53,9 @@ constexpr uint32_t BIN_TILE = BIN_TILE_PKTS;       // 2048 packets
 static_assert(BIN_TILE == BIN_K * IPXG_BLOCK, "k_bin tile = one packet per lane per step");
 constexpr uint32_t NO_REC = 0xFFFFFFFFu;
 constexpr uint32_t RED_U = IPXG_RED_U;            // records in flight per thread
+#ifndef IPXG_FIN_PROBE
+#define IPXG_FIN_PROBE 1  // k_fin_list probes the table for the flows k_reduce lists (see k_reduce)
+#endif
 constexpr uint32_t RED_MAX_PROBE = 256;
 constexpr uint32_t RED_FAILED = 0x80000000u;      // FlowAgg::tflags bit: table probe failed
 
@@ -1239,12 +1242,17 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     // deferred paths (spilled packets were accumulated by k_bin, before this kernel): then the
     // merged slot is complete and goes on the finalise list (k_fin_list).
     const bool fuse = ctl->frag_count == 0 && ctl->a_deferred == 0;
+    // (IPXG_FIN_PROBE=0: the slots probed here as before, the resolved images listed -- A/B knob)
+    const bool unresolved = fuse && IPXG_FIN_PROBE;
     uint32_t n_keys = 0, n_touch = 0, n_list = 0;
     constexpr uint32_t EPT = RED_ENTRIES / RED_THREADS;  // LDS entries per thread
     HotSlot img[EPT];
     bool listed[EPT];
     bool failed = false;
-    // The thread's entries' home slots are read, and the empty ones claimed, together (one
+    // fuse: the flows go on the finalise list as they are, unresolved -- k_fin_list probes the
+    // table for them, one lane per flow at its occupancy, so the random slot reads of a 1M-flow
+    // batch overlap there instead of stalling this LDS-bound workgroup (one per CU).  Otherwise
+    // the thread's entries' home slots are read, and the empty ones claimed, together (one
     // memory round trip for all of them, not one chain per entry); a home slot held by another
     // key continues with the general probe.
     uint64_t hkey[EPT];
@@ -1252,12 +1260,12 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q) {
         hkey[q] = ht[tid + q * RED_THREADS].key;
-        if (hkey[q]) img[q] = t.hot[(uint32_t)hkey[q] & t.mask];
+        if (hkey[q] && !unresolved) img[q] = t.hot[(uint32_t)hkey[q] & t.mask];
     }
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q) {
         old[q] = ~0ull;
-        if (hkey[q] && img[q].key == 0)
+        if (hkey[q] && !unresolved && img[q].key == 0)
             old[q] = atomicCAS((unsigned long long*)&t.hot[(uint32_t)hkey[q] & t.mask].key, 0ull,
                                (unsigned long long)hkey[q]);
     }
@@ -1267,7 +1275,16 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         FlowAgg a = ht[e];
         if (one_tb) a.tbits |= 1u;  // bucket 0 (lds_fold skipped the per-record OR)
         listed[q] = false;
-        if (a.key) {
+        if (a.key && unresolved) {  // the aggregate as a slot image, its slot probed by k_fin_list
+            n_touch++;
+            HotSlot u = {};
+            u.key = a.key;
+            agg_fold(u, a);
+            u.pad = FIN_UNRESOLVED;
+            img[q] = u;
+            listed[q] = true;
+            n_list++;
+        } else if (a.key) {
             n_touch++;
             bool claimed = false;
             HotSlot* hp = &t.hot[(uint32_t)a.key & t.mask];  // this workgroup is the slot's only writer here
@@ -1355,12 +1372,18 @@ void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSl
 // kernel completes is exported as FORCED and its slot emptied here -- the finish's export
 // folded into the finalise pass, so no table scan (k_finish) follows.  Flows it marks complex
 // stay; the host then runs the sequential path and a k_finish for them (ctl->fused tells it).
+// An unresolved entry (k_reduce's fuse mode) is probed here: its slot found or claimed
+// (probe_insert_full), the aggregate folded into the slot's image; a probe that fails (a table
+// full near the slot) marks the entry FIN_DEFERRED and counts it in ctl->fin_deferred -- the host
+// grows the table and runs this kernel again over those entries only (deferred_only), not
+// finishing.
 __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
-                                                         ExportView ex, BatchCtl* ctl, const HotSlot* fin_list,
-                                                         unsigned long long* stats, uint32_t finishing) {
+                                                         ExportView ex, BatchCtl* ctl, HotSlot* fin_list,
+                                                         unsigned long long* stats, uint32_t finishing,
+                                                         uint32_t deferred_only) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     __shared__ uint32_t sc[ST_COUNT];
-    __shared__ uint32_t cnt[4];  // new live, complex, exported, IPv6 exports
+    __shared__ uint32_t cnt[6];  // new live, complex, exported, IPv6 exports, new keys, deferred
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t ex_base;
     const uint32_t nf = ctl->fin_count;  // final: k_reduce has completed
@@ -1369,18 +1392,52 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
     if (blockIdx.x * IPXG_BLOCK >= nf) return;
     const uint32_t tid = threadIdx.x;
     if (tid < ST_COUNT) sc[tid] = 0;
-    if (tid < 4) cnt[tid] = 0;
+    if (tid < 6) cnt[tid] = 0;
     __syncthreads();
     const bool force_cx = p.force_complex || ctl->nonmono;
     const bool slot_clean = ctl->spilled == 0;  // no packet was folded into a slot directly (k_bin / k_reduce)
-    uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0;
+    uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0, n_keys = 0, n_def = 0;
     for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
         const uint32_t k = base + tid;
         bool do_export = false;  // er is exported with `reason` (a boundary split, or the fused finish)
         uint8_t reason = 0;
         RecW er;
-        if (k < nf) {
-            const HotSlot h = fin_list[k];  // the slot's merged image, its index in pad
+        HotSlot h;
+        bool go = k < nf;
+        if (go) {
+            h = fin_list[k];  // the slot's merged image and its index in pad, or an unresolved aggregate
+            if (deferred_only) go = h.pad == FIN_DEFERRED;
+            else if (h.pad == FIN_DEFERRED) go = false;  // (not from this batch's k_reduce)
+        }
+        if (go && h.pad >= FIN_DEFERRED) {
+            FlowAgg a;
+            a.key = h.key;
+            a.acc[0] = h.acc[0];
+            a.acc[1] = h.acc[1];
+            a.first_n = h.first_n;
+            a.last1 = h.last1;
+            a.tbits = h.tbits;
+            a.tflags = h.tflags;
+            a.fin_n[0] = h.fin_n[0];
+            a.fin_n[1] = h.fin_n[1];
+            a.syn1[0] = h.syn1[0];
+            a.syn1[1] = h.syn1[1];
+            HotSlot img;
+            bool claimed;
+            HotSlot* hp = probe_insert_full(t, a.key, img, claimed);
+            if (!hp) {  // the table is full near its slot: after a rehash, again
+                fin_list[k].pad = FIN_DEFERRED;
+                n_def++;
+                go = false;
+            } else {
+                n_keys += claimed ? 1u : 0u;
+                agg_fold(img, a);
+                img.pad = (uint32_t)(hp - t.hot);
+                h = img;
+                if (deferred_only) fin_list[k].pad = FIN_UNRESOLVED;  // done: later re-runs skip it
+            }
+        }
+        if (go) {
             const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean);
             if (fr.status == FIN_COMPLEX) n_cx++;
             else if (!fused && fr.created) n_live++;
@@ -1407,22 +1464,26 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
     if (n_cx) atomicAdd(&cnt[1], n_cx);
     if (n_ex) atomicAdd(&cnt[2], n_ex);
     if (n_v6) atomicAdd(&cnt[3], n_v6);
+    if (n_keys) atomicAdd(&cnt[4], n_keys);
+    if (n_def) atomicAdd(&cnt[5], n_def);
     flush_block_stats(sc, stats);
     if (tid == 0) {
         if (cnt[3] && ex.count6) atomicAdd(ex.count + 2, cnt[3]);  // count_v6_exports' counter
         if (cnt[0]) atomicAdd(&ctl->new_live, cnt[0]);
         if (cnt[1]) atomicAdd(&ctl->complex_count, cnt[1]);
         if (cnt[2]) atomicAdd(&ctl->exported, cnt[2]);
+        if (cnt[4]) atomicAdd(&ctl->new_keys, cnt[4]);
+        if (cnt[5]) atomicAdd(&ctl->fin_deferred, cnt[5]);
     }
 }
 
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
-                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
-                     bool finishing) {
+                     BatchCtl* ctl, HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
+                     bool finishing, bool deferred_only) {
     uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, ex, ctl, fin_list,
-                       stats, finishing ? 1u : 0u);
+                       stats, finishing ? 1u : 0u, deferred_only ? 1u : 0u);
 }
 
 }  // namespace ipxg

@@ -65,6 +65,7 @@ struct BatchCtl {
     int32_t strict_live;     // strict mode: records created - records exported
     uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
     uint32_t tb_any;         // OR of the time buckets of k_bin / k_bin_slow's records (0: all in bucket 0)
+    uint32_t fin_deferred;   // finalise-list aggregates whose table probe failed (k_fin_list: table full)
     uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -252,9 +253,11 @@ void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableV
 // fin_list: the merged images of the slots k_reduce completed (HotSlot::pad = slot index)
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                    uint32_t* deferred_list, uint4* agg_list);
+constexpr uint32_t FIN_UNRESOLVED = 0xFFFFFFFFu;  // a finalise-list entry's pad: the flow's slot not probed yet
+constexpr uint32_t FIN_DEFERRED = 0xFFFFFFFEu;    // ... its probe failed (table full): again after a rehash
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
-                     BatchCtl* ctl, const HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
-                     bool finishing);
+                     BatchCtl* ctl, HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
+                     bool finishing, bool deferred_only = false);
 void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
                      uint32_t nrules, BatchCtl* ctl);
 void launch_plugin_pack(hipStream_t st, TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out, uint32_t* count);
