@@ -264,8 +264,10 @@ def canon_of(eng, arena_np, desc_np):
 
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the newest profiles/*/pmc_summary[_<workload>].json:
-    FETCH_SIZE (KiB; doubled -- gfx950 tallies wide streaming reads at half, MI355X_MICROARCH.md
-    'HBM') + WRITE_SIZE (KiB), both per launch."""
+    the L2's fabric read requests by size (TCC_EA0_RDREQ_32B/64B/128B: 32, 64, 128 bytes each --
+    round 3 measured FETCH_SIZE = all requests x 64 B while ~99.9 % of k_bin's are 128 B, i.e.
+    FETCH_SIZE reads half, as MI355X_MICROARCH.md 'HBM' says) + WRITE_SIZE (KiB); summaries
+    without the request sizes: FETCH_SIZE x 2 + WRITE_SIZE."""
     best = None
     name = "pmc_summary.json" if workload == "udp64" else "pmc_summary_%s.json" % workload
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name))):
@@ -278,7 +280,12 @@ def pmc_traffic(kernel, workload):
         for kn, v in js.items():
             if kn.split("::")[-1].split("<")[0] == kernel and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                 if found is None or v.get("calls", 0) > found[0]:
-                    found = (v.get("calls", 0), (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0)
+                    if "TCC_EA0_RDREQ_128B_sum" in v:
+                        rd = (128 * v["TCC_EA0_RDREQ_128B_sum"] + 64 * v.get("TCC_EA0_RDREQ_64B_sum", 0) +
+                              32 * v.get("TCC_EA0_RDREQ_32B_sum", 0))
+                    else:
+                        rd = 2 * v["FETCH_SIZE"] * 1024.0
+                    found = (v.get("calls", 0), rd + v["WRITE_SIZE"] * 1024.0)
         if found is not None:
             best = (p, found[1])
     return best
