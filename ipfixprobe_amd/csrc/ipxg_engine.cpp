@@ -12,6 +12,7 @@
 //   -> grow the table if its load passed 1/2.
 // In the common case (no fragments, no overflow) that is four kernels and one host sync.
 #include <hip/hip_runtime.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <chrono>
@@ -63,7 +64,12 @@ struct ipxg_engine {
     // host walks add to the device-side counters (exports by reason, TopPorts)
     std::vector<ipxg_plugin> plugins;
     uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
-    double walk_phase_ms[6] = {0, 0, 0, 0, 0, 0};  // plugin_walk's phases (IPXG_WALK_TRACE)
+    double walk_phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};  // plugin_walk's phases (IPXG_WALK_TRACE)
+    long walk_faults[7] = {0, 0, 0, 0, 0, 0, 0};        // ... and the minor page faults in each
+    bool walk_trace = false;                             // IPXG_WALK_TRACE set at ipxg_create
+    bool strict_prune = true;                            // strict: idle-free sweep steps left out of the DAG
+    uint32_t strict_wgs = 0;                             // strict: replay workgroups per XCD (0: one workgroup)
+    uint32_t* st_sched = nullptr;                        // strict: the multi-workgroup scheduler block
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     // their host copies, kept across batches (pageable: the walk reads them on the CPU, and
     // pinned hipHostMalloc memory read slower there -- measured: +58 % walk time on configs[2])
@@ -71,6 +77,13 @@ struct ipxg_engine {
     std::vector<ipxg_parsed_pkt> hw_parsed;
     std::vector<ipxg_pkt_desc> hw_desc;
     std::vector<uint8_t> hw_bytes;
+    // the walk's own working vectors, kept too (a fresh 10-20 MB vector per batch cost its page
+    // faults on first touch inside the walk)
+    std::vector<PluginFlow> hw_flows;
+    std::vector<uint32_t> hw_idx, hw_first;
+    std::vector<uint64_t> hw_off, hw_okey, hw_okey2;
+    std::vector<PluginFlow> hw_flows2;
+    std::vector<ipxg_flow_record> hw_ex;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
     uint64_t host_unreasoned = 0;  // counted exports without an end reason (total_exported only)
@@ -423,6 +436,8 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     if (cfg->frag_enable && cfg->frag_size == 0) return IPXG_EINVAL;
     ipxg_engine* e = new ipxg_engine();
     e->cfg = *cfg;
+    e->walk_trace = std::getenv("IPXG_WALK_TRACE") != nullptr;
+    if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         delete e;
@@ -471,9 +486,16 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
         e->sv.lines = S >> cfg->line_exp;
         e->sv.slot_mask = S - 1;
         if (hipMalloc((void**)&e->sv.rec, (size_t)S * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
-        if (hipMalloc((void**)&e->sv.hash, (size_t)S * 8) != hipSuccess) return fail(IPXG_ENOMEM);
+        // (hash and time_last padded by 64 bytes: the multi-workgroup replay reads lines as 16-byte loads)
+        if (hipMalloc((void**)&e->sv.hash, (size_t)S * 8 + 64) != hipSuccess) return fail(IPXG_ENOMEM);
         if (hipMalloc((void**)&e->sv.perm, (size_t)e->sv.lines * 8) != hipSuccess) return fail(IPXG_ENOMEM);
-        if (hipMalloc((void**)&e->sv.tlast, (size_t)S * 4) != hipSuccess) return fail(IPXG_ENOMEM);
+        if (hipMalloc((void**)&e->sv.tlast, (size_t)S * 4 + 64) != hipSuccess) return fail(IPXG_ENOMEM);
+        if (hipMalloc((void**)&e->st_sched, STRICT_SCHED_BYTES) != hipSuccess) return fail(IPXG_ENOMEM);
+        // the replay on several workgroups of one XCD (IPXG_STRICT_WGS: workgroups per XCD, 0 = one
+        // workgroup); its buffer loads address the record array with 32-bit offsets
+        if (const char* w_env = std::getenv("IPXG_STRICT_WGS")) e->strict_wgs = (uint32_t)std::atoi(w_env);
+        if (e->strict_wgs > 32 || (size_t)S * sizeof(ipxg_flow_record) > 0x7FFFFFFFull) e->strict_wgs = 0;
+        if (hipMalloc((void**)&e->sv.lb, ((size_t)e->sv.lines + 1) * 4) != hipSuccess) return fail(IPXG_ENOMEM);
         launch_strict_clear(e->st, e->sv);
         if (hipGetLastError() != hipSuccess) return fail(IPXG_EDEVICE);
     }
@@ -487,10 +509,14 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
 }
 
 int ipxg_destroy(ipxg_engine* e) {
-    if (e && std::getenv("IPXG_WALK_TRACE") && e->tm.plugin_flows)
-        std::fprintf(stderr, "ipxg plugin walk ms: pack %.1f fetch %.1f parse %.1f bytes %.1f walk %.1f back %.1f\n",
+    if (e && e->walk_trace && e->tm.plugin_flows)
+        std::fprintf(stderr,
+                     "ipxg plugin walk ms: pack %.1f fetch %.1f parse %.1f bytes %.1f order %.1f walk %.1f back %.1f"
+                     " | minor faults: %ld %ld %ld %ld %ld %ld %ld\n",
                      e->walk_phase_ms[0], e->walk_phase_ms[1], e->walk_phase_ms[2], e->walk_phase_ms[3],
-                     e->walk_phase_ms[4], e->walk_phase_ms[5]);
+                     e->walk_phase_ms[4], e->walk_phase_ms[5], e->walk_phase_ms[6], e->walk_faults[0],
+                     e->walk_faults[1], e->walk_faults[2], e->walk_faults[3], e->walk_faults[4], e->walk_faults[5],
+                     e->walk_faults[6]);
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
     hipFree(e->hot);
@@ -509,6 +535,8 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->sv.hash);
     hipFree(e->sv.perm);
     hipFree(e->sv.tlast);
+    hipFree(e->sv.lb);
+    hipFree(e->st_sched);
     hipFree(e->frag_ent);
     hipFree(e->frag_cnt);
     if (e->plan_h) hipHostFree(e->plan_h);
@@ -610,7 +638,11 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     ipxg_flow_record* crec = (ipxg_flow_record*)e->st_crec.p;
     uint32_t* keyed = (uint32_t*)e->st_keyed.p;
     uint32_t* qx = (uint32_t*)e->st_qx.p;
-    launch_strict_prep2(e->st, bv, p, frag_view(e), sp, crec, keyed);
+    uint32_t* ts_acc = e->sv.lb + e->sv.lines;
+    HIPCHK(e, hipMemsetAsync(ts_acc, 0, 4, e->st));
+    launch_strict_prep2(e->st, bv, p, frag_view(e), sp, crec, keyed, ts_acc);
+    HIPCHK(e, hipGetLastError());
+    launch_strict_lb(e->st, e->sv);
     HIPCHK(e, hipGetLastError());
     size_t tb = 0, tb2 = 0;
     int bits = 1;
@@ -622,18 +654,23 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     HIPCHK(e, exclusive_scan_u32(e->sort_tmp.p, tb, keyed, qx, n, e->st));
     uint32_t *ks = (uint32_t*)e->st_keys.p, *vs = (uint32_t*)e->st_vals.p;
     uint32_t *ks2 = (uint32_t*)e->st_keys2.p, *vs2 = (uint32_t*)e->st_vals2.p;
-    launch_strict_events(e->st, e->sv, sp, keyed, qx, n, e->strict_q, p.split_biflow, ks, vs);
+    // (IPXG_STRICT_PRUNE=0: every sweep step kept as a DAG event -- a bound of 0 keeps them all)
+    launch_strict_events(e->st, e->sv, sp, keyed, qx, n, e->strict_q, p.split_biflow, e->strict_prune ? p.inactive_s : 0u,
+                         ks, vs);
     HIPCHK(e, hipGetLastError());
     tb = e->sort_tmp.bytes;
     HIPCHK(e, sort_pairs_u32(e->sort_tmp.p, tb, ks, ks2, vs, vs2, (uint32_t)m, bits, e->st));
     uint32_t* queue = (uint32_t*)e->st_queue.p;
-    uint32_t* q_count = queue + n;
+    // the ready count: the single workgroup's initial tail, or the scheduler block's tail word
+    uint32_t* sched = e->strict_wgs ? e->st_sched : queue + n;
+    uint32_t* q_count = e->strict_wgs ? e->st_sched + 1 : queue + n;
     HIPCHK(e, hipMemsetAsync(queue, 0xFF, (size_t)n * 4, e->st));  // STRICT_NONE: not filled yet
     HIPCHK(e, hipMemsetAsync(q_count, 0, 4, e->st));
+    if (e->strict_wgs) HIPCHK(e, hipMemsetAsync(e->st_sched, 0, STRICT_SCHED_BYTES, e->st));
     launch_strict_dag(e->st, ks2, vs2, (uint32_t)m, ks, keyed, n, e->sv.lines, (uint32_t*)e->st_succ.p,
                       (uint8_t*)e->st_pred.p, (uint32_t*)e->st_indeg.p, queue, q_count);
     launch_strict_walk(e->st, e->sv, p, sp, crec, keyed, qx, (const uint32_t*)e->st_succ.p, (uint32_t*)e->st_indeg.p,
-                       queue, q_count, n, e->strict_q, export_view(e), e->ctl_d, e->stats_d);
+                       queue, sched, n, e->strict_q, export_view(e), e->ctl_d, e->stats_d, e->strict_wgs);
     HIPCHK(e, hipGetLastError());
     ev_rec(e, 1);
     uint32_t tail[2] = {0, 0};  // the last packet's keyed rank and mark: keyed packets in the batch
@@ -786,7 +823,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 namespace {
 
 struct WalkOut {
-    std::vector<ipxg_flow_record> ex;  // exported records, in order
+    std::vector<ipxg_flow_record>& ex;  // exported records, in order
     uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
     uint64_t pkts[6] = {0, 0, 0, 0, 0, 0};  // FlowRecordStats buckets
     uint64_t unreasoned = 0;  // export_flow with end_reason 0 (post_create FLUSH of a new record)
@@ -953,12 +990,26 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const auto t0 = std::chrono::steady_clock::now();
     auto tm = t0;
     // IPXG_WALK_TRACE: the walk's phases (pack + count, flow images + sorted list, parsed
-    // packets, frame bytes, the host loop, write-back) summed, printed when the engine closes
+    // packets, frame bytes, flow order, the host loop, write-back) summed, with their minor page
+    // faults, printed when the engine closes
+    const bool trace = e->walk_trace;
+    long flt = 0;
+    auto faults = []() {
+        struct rusage u;
+        getrusage(RUSAGE_THREAD, &u);
+        return (long)u.ru_minflt;
+    };
+    if (trace) flt = faults();
 #define WALK_MARK(k)                                                                                         \
     do {                                                                                                   \
         const auto t_ = std::chrono::steady_clock::now();                                                  \
         e->walk_phase_ms[k] += std::chrono::duration<double, std::milli>(t_ - tm).count();                 \
         tm = t_;                                                                                           \
+        if (trace) {                                                                                       \
+            const long f_ = faults();                                                                      \
+            e->walk_faults[k] += f_ - flt;                                                                 \
+            flt = f_;                                                                                      \
+        }                                                                                                  \
     } while (0)
     struct Clock {  // the walk's wall time, however it returns
         ipxg_engine* e;
@@ -976,14 +1027,43 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipMemcpyAsync(&nf, cnt_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(0);
     if (!nf) return IPXG_OK;
-    std::vector<PluginFlow> flows(nf);
+    std::vector<PluginFlow>& flows = e->hw_flows;
+    flows.resize(nf);
     e->hw_sorted.resize(npk);
     const uint64_t* sorted = e->hw_sorted.data();
     HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_sorted.data(), cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(1);
+    // The walk takes the flows in order of their first packet (export order is arbitrary
+    // otherwise), and everything it reads is laid out in that order: the flow images permuted
+    // once here, then the packet list, the parsed packets and the frame bytes built from them --
+    // the walk streams through memory instead of a few dependent cache misses per flow.
+    // (LSD radix sort of {first index, flow} words on the 24-bit index: unique keys)
+    {
+        std::vector<uint64_t>& okey = e->hw_okey;
+        std::vector<uint64_t>& tmp = e->hw_okey2;
+        okey.resize(nf);
+        tmp.resize(nf);
+        for (uint32_t f = 0; f < nf; ++f) okey[f] = ((sorted[flows[f].seg] & 0xFFFFFFull) << 32) | f;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int sh = 32 + 8 * pass;
+            uint32_t cnt[257] = {0};
+            for (uint32_t f = 0; f < nf; ++f) cnt[((okey[f] >> sh) & 0xFF) + 1]++;
+            for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
+            for (uint32_t f = 0; f < nf; ++f) tmp[cnt[(okey[f] >> sh) & 0xFF]++] = okey[f];
+            okey.swap(tmp);
+        }
+        std::vector<PluginFlow>& fo = e->hw_flows2;
+        fo.resize(nf);
+        for (uint32_t k = 0; k < nf; ++k) fo[k] = flows[(uint32_t)okey[k]];
+        flows.swap(fo);
+    }
+    WALK_MARK(4);
     // the flows' packets, each flow's in arrival order (the sorted list: rank << 24 | index)
-    std::vector<uint32_t> idx, first(nf + 1);
+    std::vector<uint32_t>& idx = e->hw_idx;
+    std::vector<uint32_t>& first = e->hw_first;
+    idx.clear();
+    first.resize(nf + 1);
     {
         size_t total = 0;
         for (uint32_t f = 0; f < nf; ++f) total += flows[f].len;
@@ -1009,7 +1089,9 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(2);
-    std::vector<uint64_t> off(m + 1, 0);
+    std::vector<uint64_t>& off = e->hw_off;
+    off.resize(m + 1);
+    off[0] = 0;
     for (uint32_t k = 0; k < m; ++k) off[k + 1] = off[k] + de[k].caplen;
     if ((rc = ensure(e, e->pf_off, (size_t)(m + 1) * 8))) return rc;
     if ((rc = ensure(e, e->pf_bytes, off[m] + 16))) return rc;
@@ -1025,17 +1107,13 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const uint8_t* bytes = e->hw_bytes.data();
     HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(3);
-    // the walks, flows in order of their first packet (export order is arbitrary otherwise)
-    // (sorted as packed {first index, flow} words: contiguous keys, no indirection per compare)
-    std::vector<uint64_t> okey(nf);
-    for (uint32_t f = 0; f < nf; ++f) okey[f] = ((uint64_t)idx[first[f]] << 32) | f;
-    std::sort(okey.begin(), okey.end());
-    WalkOut wo;
+    // the walks, flows in order of their first packet (their order in `flows` now)
+    e->hw_ex.clear();
+    WalkOut wo{e->hw_ex};
     wo.ex.reserve(m + 16);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.empty()) e->host_ports.assign(2 * 65536, 0);
-    for (const uint64_t ok : okey) {
-        const uint32_t f = (uint32_t)ok;
+    for (uint32_t f = 0; f < nf; ++f) {
         PluginFlow& F = flows[f];
         FlowWalk w{e->plugins, p, wo, F.rec, (F.state & SLOT_LIVE) != 0};
         const bool was_live = w.live;
@@ -1065,7 +1143,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             a[r.dst_port] += F.len;
         }
     }
-    WALK_MARK(4);
+    WALK_MARK(5);
     // back to the device: the slots, then the exports after the batch's own
     HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows.data(), (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
     launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf);
@@ -1086,7 +1164,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
     for (int k = 0; k < 6; ++k) e->host_pkts[k] += wo.pkts[k];
     e->host_unreasoned += wo.unreasoned;
-    WALK_MARK(5);
+    WALK_MARK(6);
 #undef WALK_MARK
     return IPXG_OK;
 }

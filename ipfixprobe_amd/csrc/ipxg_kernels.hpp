@@ -132,6 +132,8 @@ struct StrictView {
     uint64_t* hash;         // their FlowRecord::m_hash (0 = empty)
     uint64_t* perm;         // per line: position j -> record slot, bits 4j..4j+3
     uint32_t* tlast;        // per slot: the record's time_last_sec, 0xFFFFFFFF while empty (the sweep's test)
+    uint32_t* lb;           // per line: a lower bound of every time_last it holds during the batch; [lines]:
+                            // ~(the batch's first second) (k_strict_prep2's atomicMax)
     uint32_t line_bits;     // l= (line size 2^l, at most 16)
     uint32_t lines;         // 2^s >> l
     uint32_t slot_mask;     // 2^s - 1
@@ -141,7 +143,7 @@ struct StrictPkt {          // what put_pkt_recursive reads of a keyed packet (h
     uint32_t ts_sec, ts_usec;
     uint16_t ip_len;
     uint8_t tcp_flags, ip_proto;
-    uint32_t pad;
+    uint32_t sweep;  // 1: its sweep step may export (k_strict_events); 0: provably exports nothing
 };
 static_assert(sizeof(StrictPkt) == 32, "");
 constexpr uint32_t STRICT_LANES = 768;           // the replay's one workgroup (3 waves per SIMD; the DAG is ~260 packets wide at the reference default)
@@ -322,17 +324,22 @@ hipError_t exclusive_scan_u32(void* temp, size_t& temp_bytes, const uint32_t* in
 void launch_strict_prep1(hipStream_t st, const BatchView& b, const Params& p, FragView f, BatchCtl* ctl,
                          unsigned long long* stats);
 void launch_strict_prep2(hipStream_t st, const BatchView& b, const Params& p, FragView f, StrictPkt* sp,
-                         ipxg_flow_record* crec, uint32_t* keyed);
-void launch_strict_events(hipStream_t st, StrictView v, const StrictPkt* sp, const uint32_t* keyed,
-                          const uint32_t* qx, uint32_t n, uint64_t q_base, uint32_t split, uint32_t* keys,
+                         ipxg_flow_record* crec, uint32_t* keyed, uint32_t* ts_acc);
+void launch_strict_lb(hipStream_t st, StrictView v);
+void launch_strict_events(hipStream_t st, StrictView v, StrictPkt* sp, const uint32_t* keyed, const uint32_t* qx,
+                          uint32_t n, uint64_t q_base, uint32_t split, uint32_t inactive, uint32_t* keys,
                           uint32_t* vals);
 void launch_strict_dag(hipStream_t st, const uint32_t* keys_sorted, const uint32_t* vals_sorted, uint32_t m,
                        const uint32_t* keys, const uint32_t* keyed, uint32_t n, uint32_t lines, uint32_t* succ,
                        uint8_t* pred, uint32_t* indeg, uint32_t* queue, uint32_t* q_count);
+// sched: one workgroup (wgs_per_xcd 0) -- the ready count k_strict_ready left; several
+// (8 x wgs_per_xcd launched, one XCD's take part) -- a zeroed STRICT_SCHED_BYTES block whose word 1
+// holds that count
+constexpr uint32_t STRICT_SCHED_BYTES = 512;
 void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const StrictPkt* sp,
                         const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx, const uint32_t* succ,
-                        uint32_t* indeg, uint32_t* queue, const uint32_t* q_count, uint32_t n, uint64_t q_base,
-                        ExportView ex, BatchCtl* ctl, unsigned long long* stats);
+                        uint32_t* indeg, uint32_t* queue, uint32_t* sched, uint32_t n, uint64_t q_base,
+                        ExportView ex, BatchCtl* ctl, unsigned long long* stats, uint32_t wgs_per_xcd);
 void launch_strict_expire(hipStream_t st, StrictView v, const Params& p, uint64_t q, int64_t now, ExportView ex,
                           BatchCtl* ctl, unsigned long long* stats);
 void launch_strict_finish(hipStream_t st, StrictView v, ExportView ex, BatchCtl* ctl, unsigned long long* stats);
