@@ -68,7 +68,7 @@ struct ipxg_engine {
     long walk_faults[7] = {0, 0, 0, 0, 0, 0, 0};        // ... and the minor page faults in each
     bool walk_trace = false;                             // IPXG_WALK_TRACE set at ipxg_create
     bool strict_prune = true;                            // strict: idle-free sweep steps left out of the DAG
-    uint32_t strict_wgs = 0;                             // strict: replay workgroups per XCD (0: one workgroup)
+    uint32_t strict_wgs = STRICT_WGS_DEFAULT;            // strict: replay workgroups per XCD (0: one workgroup)
     uint32_t* st_sched = nullptr;                        // strict: the multi-workgroup scheduler block
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     // their host copies, kept across batches (pageable: the walk reads them on the CPU, and
@@ -663,7 +663,7 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     uint32_t* queue = (uint32_t*)e->st_queue.p;
     // the ready count: the single workgroup's initial tail, or the scheduler block's tail word
     uint32_t* sched = e->strict_wgs ? e->st_sched : queue + n;
-    uint32_t* q_count = e->strict_wgs ? e->st_sched + 1 : queue + n;
+    uint32_t* q_count = e->strict_wgs ? e->st_sched + STRICT_SCHED_TAIL_WORD : queue + n;
     HIPCHK(e, hipMemsetAsync(queue, 0xFF, (size_t)n * 4, e->st));  // STRICT_NONE: not filled yet
     HIPCHK(e, hipMemsetAsync(q_count, 0, 4, e->st));
     if (e->strict_wgs) HIPCHK(e, hipMemsetAsync(e->st_sched, 0, STRICT_SCHED_BYTES, e->st));

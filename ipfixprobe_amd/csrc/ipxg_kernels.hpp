@@ -333,9 +333,11 @@ void launch_strict_dag(hipStream_t st, const uint32_t* keys_sorted, const uint32
                        const uint32_t* keys, const uint32_t* keyed, uint32_t n, uint32_t lines, uint32_t* succ,
                        uint8_t* pred, uint32_t* indeg, uint32_t* queue, uint32_t* q_count);
 // sched: one workgroup (wgs_per_xcd 0) -- the ready count k_strict_ready left; several
-// (8 x wgs_per_xcd launched, one XCD's take part) -- a zeroed STRICT_SCHED_BYTES block whose word 1
-// holds that count
+// (8 x wgs_per_xcd launched, one XCD's take part) -- a zeroed STRICT_SCHED_BYTES block whose word
+// STRICT_SCHED_TAIL_WORD holds that count
 constexpr uint32_t STRICT_SCHED_BYTES = 512;
+constexpr uint32_t STRICT_WGS_DEFAULT = 12;  // replay workgroups per XCD (of 256 lanes): 114 Mpkt/s at s=17
+constexpr uint32_t STRICT_SCHED_TAIL_WORD = 32;  // the ready count / queue tail (its own 128-byte line)
 void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const StrictPkt* sp,
                         const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx, const uint32_t* succ,
                         uint32_t* indeg, uint32_t* queue, uint32_t* sched, uint32_t n, uint64_t q_base,

@@ -814,14 +814,20 @@ void launch_strict_walk(hipStream_t st, StrictView v, const Params& p, const Str
                         const ipxg_flow_record* crec, const uint32_t* keyed, const uint32_t* qx, const uint32_t* succ,
                         uint32_t* indeg, uint32_t* queue, uint32_t* sched, uint32_t n, uint64_t q_base,
                         ExportView ex, BatchCtl* ctl, unsigned long long* stats, uint32_t wgs_per_xcd) {
-    static_assert(sizeof(StrictSched) == STRICT_SCHED_BYTES, "scheduler block");
-    static const char* lanes_env = std::getenv("IPXG_STRICT_MW_LANES");  // tuning: 256 or 768 lanes per workgroup
-    static const bool narrow = lanes_env && std::atoi(lanes_env) == 256;
-    if (wgs_per_xcd && narrow)  // 8 x wgs_per_xcd workgroups: those on the first XCD to arrive take part
-        hipLaunchKernelGGL((k_strict_walk<true, 256>), dim3(8 * wgs_per_xcd), dim3(256), 0, st, v, p, sp, crec, keyed,
+    static_assert(sizeof(StrictSched) == STRICT_SCHED_BYTES && offsetof(StrictSched, tail) == 4 * STRICT_SCHED_TAIL_WORD,
+                  "scheduler block");
+    // lanes per workgroup of the multi-workgroup replay: 256 (measured best at s=17: 12 x 256 per
+    // XCD 114 Mpkt/s, 6 x 768 76); IPXG_STRICT_MW_LANES=128/768 for tuning
+    static const char* lanes_env = std::getenv("IPXG_STRICT_MW_LANES");
+    static const int lanes = lanes_env ? std::atoi(lanes_env) : 256;
+    if (wgs_per_xcd && lanes == 128)  // 8 x wgs_per_xcd workgroups: those on the first XCD to arrive take part
+        hipLaunchKernelGGL((k_strict_walk<true, 128>), dim3(8 * wgs_per_xcd), dim3(128), 0, st, v, p, sp, crec, keyed,
+                           qx, succ, indeg, queue, sched, n, q_base, ex, ctl, stats);
+    else if (wgs_per_xcd && lanes == 768)
+        hipLaunchKernelGGL(k_strict_walk<true>, dim3(8 * wgs_per_xcd), dim3(STRICT_LANES), 0, st, v, p, sp, crec, keyed,
                            qx, succ, indeg, queue, sched, n, q_base, ex, ctl, stats);
     else if (wgs_per_xcd)
-        hipLaunchKernelGGL(k_strict_walk<true>, dim3(8 * wgs_per_xcd), dim3(STRICT_LANES), 0, st, v, p, sp, crec, keyed,
+        hipLaunchKernelGGL((k_strict_walk<true, 256>), dim3(8 * wgs_per_xcd), dim3(256), 0, st, v, p, sp, crec, keyed,
                            qx, succ, indeg, queue, sched, n, q_base, ex, ctl, stats);
     else
         hipLaunchKernelGGL(k_strict_walk<false>, dim3(1), dim3(STRICT_LANES), 0, st, v, p, sp, crec, keyed, qx, succ,

@@ -83,11 +83,12 @@ def test_strict_stream_parity(params, batch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wgs", ["2", "8", "32"])
+@pytest.mark.parametrize("wgs", ["0", "2", "8", "32"])
 @pytest.mark.parametrize("params", ["s=8", "s=12;l=4;i=5;a=20", "s=8;S", "s=7;l=2", "s=20"])
 def test_strict_multi_workgroup_parity(monkeypatch, params, wgs):
     """The replay on several workgroups of one XCD (IPXG_STRICT_WGS per XCD; sc1 table reads,
-    agent-scope scheduler): the same records, end reasons and statistics as the oracle."""
+    agent-scope scheduler; the default is 12) or on one workgroup (0): the same records, end
+    reasons and statistics as the oracle."""
     monkeypatch.setenv("IPXG_STRICT_WGS", wgs)
     arena, desc = synth.flow_stream(seed=41, n_flows=900, n_pkts=20000, v6_share=0.3, vlan_share=0.2).batch()
     _check(arena, desc, params, batch=6000)
