@@ -558,6 +558,8 @@ def main():
                     help="process plugins through the bridge (native stand-ins, include/ipxg_stdplugins.h): a "
                          "comma list of dns,http,tls,quic, or 'config' for the workload's own (configs[2]: "
                          "dns,http,tls; configs[4]: quic)")
+    ap.add_argument("--walk-threads", type=int, default=0,
+                    help="threads of the plugin flows' host walk (0: the host's threads, at most 16)")
     ap.add_argument("--cpu-selftest", action="store_true",
                     help="no GPU: the N-rank launcher and the export exchange over gloo with synthetic streams "
                          "(tests/test_launcher.py)")
@@ -612,6 +614,7 @@ def main():
         names = args.plugins.split(",") if args.plugins != "config" else \
             {"imix": ["dns", "http", "tls"], "imix10m": ["dns", "http", "tls"], "quic": ["quic"]}.get(args.workload, [])
         plugins = [StdPlugin(nm) for nm in names]
+        eng.set_walk_threads(args.walk_threads)
         for pl in plugins:
             eng.add_plugin(pl.struct)
         wl.description += "; process plugins %s through the bridge (native stand-ins)" % ",".join(names)
@@ -682,6 +685,7 @@ def main():
         alg_step += tm_in["plugin_extra_bytes"] / args.steps
         hw_ms = tm_in["plugin_ms"] / args.steps
         plug = {"names": [p.name for p in plugins],
+                "walk_threads": args.walk_threads or "default (host threads, at most 16)",
                 "host_walk": {"flows_per_step": round(tm_in["plugin_flows"] / args.steps),
                               "packets_per_step": round(tm_in["plugin_packets"] / args.steps),
                               "packet_share": round(tm_in["plugin_packets"] / args.steps / pk_step, 5),

@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 2 /* 2: ipxg_plugin gained masked prefixes and follow_packets */
+#define IPXG_ABI_VERSION 3 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+                              3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk) */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -366,10 +367,26 @@ typedef struct ipxg_plugin {
     uint32_t masked;          /* bit q: prefix q compares under prefix_mask[q]                 */
     uint32_t follow_packets;  /* see above; 0 = the rule alone decides                          */
     uint8_t prefix_mask[IPXG_PLUGIN_MAX_PREFIXES][IPXG_PLUGIN_PREFIX_LEN];
+    /* ABI 3: ProcessPlugin::copy() (processPlugin.hpp:50).  The host walk splits a batch's
+     * plugin flows over several threads (ipxg_set_walk_threads), each calling the hooks of its
+     * own instance of every plugin -- as the reference gives every storage pipeline its own copy
+     * of each process plugin (ipfixprobe.cpp:430-436).  copy_ctx returns a new context for another
+     * walk thread (NULL: out of memory), free_ctx releases one; the engine makes its copies on
+     * the first multi-threaded walk and frees them in ipxg_add_plugin and ipxg_destroy, so the
+     * original ctx must outlive the engine.  A NULL copy_ctx on any registered plugin keeps the
+     * walk on one thread. */
+    void* (*copy_ctx)(void* ctx);
+    void (*free_ctx)(void* ctx);
 } ipxg_plugin;
 
 /* Register a plugin (the order of registration is the order of the hook calls). */
 int ipxg_add_plugin(ipxg_engine* eng, const ipxg_plugin* plugin);
+/* Threads of the plugin flows' host walk: 0 = default (the host's hardware threads, at most
+ * 16), 1 = the calling thread only.  Flows are independent (the walk replays each flow's
+ * packets in order on one thread), so the records are the same for any thread count; the export
+ * order of the walked flows is the concatenation of the threads' (contiguous flow ranges in
+ * order of each flow's first packet). */
+int ipxg_set_walk_threads(ipxg_engine* eng, uint32_t threads);
 
 /* ---- stage timing (HIP events on the engine's stream) --------------------------------- */
 typedef struct ipxg_timing {

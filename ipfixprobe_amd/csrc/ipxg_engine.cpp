@@ -16,6 +16,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 #include <cmath>
 #include <cstdio>
@@ -31,6 +35,63 @@ using namespace ipxg;
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+};
+
+// The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
+// calling thread -- and returns when all have returned.  Persistent across batches (a batch of
+// configs[2] walks ~10^5 flows; spawning threads per batch would cost more than small walks).
+class WalkPool {
+public:
+    explicit WalkPool(unsigned n) {
+        for (unsigned t = 1; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~WalkPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    void run(const std::function<void(unsigned)>& f) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &f;
+            left_ = (unsigned)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(unsigned t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(t);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* job_ = nullptr;
+    unsigned left_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
 };
 struct ipxg_engine {
     ipxg_config cfg;
@@ -83,11 +144,17 @@ struct ipxg_engine {
     std::vector<uint32_t> hw_idx, hw_first;
     std::vector<uint64_t> hw_off, hw_okey, hw_okey2;
     std::vector<PluginFlow> hw_flows2;
-    std::vector<ipxg_flow_record> hw_ex;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
     uint64_t host_unreasoned = 0;  // counted exports without an end reason (total_exported only)
-    std::vector<uint64_t> host_ports;  // 2 x 65536 when ps=true and plugins walk flows
+    // the walk's threads (ipxg_set_walk_threads; 0 = default) and what each keeps across
+    // batches: its exports of the current batch, its TopPorts counts (2 x 65536 when ps=true;
+    // summed when read) and, for t >= 1, its copies of the plugins (ipxg_plugin.copy_ctx)
+    uint32_t walk_threads = 0;
+    WalkPool* pool = nullptr;
+    std::vector<std::vector<ipxg_flow_record>> hw_ex;   // [t]
+    std::vector<std::vector<uint64_t>> host_ports;      // [t]
+    std::vector<std::vector<ipxg_plugin>> walk_pl;      // [t - 1]: thread t's plugin instances
     // staging for host batches
     DevBuf arena, desc;
     // scratch
@@ -139,6 +206,8 @@ struct ipxg_engine {
     hipEvent_t ev[11] = {};
     ipxg_timing tm = {};
 };
+
+static void free_walk_copies(ipxg_engine* e);
 
 // events: 0 | k_bin | 1 | k_bin_slow | 2 | k_reduce | 3 | k_fin_list | 4;
 //         [5,6] slow paths, [7,8] k_finalize, [9,10] finish
@@ -519,6 +588,8 @@ int ipxg_destroy(ipxg_engine* e) {
                      e->walk_faults[6]);
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
+    delete e->pool;
+    free_walk_copies(e);
     hipFree(e->hot);
     hipFree(e->cold);
     hipFree(e->slot_rank);
@@ -983,6 +1054,53 @@ struct FlowWalk {
 
 }  // namespace
 
+// The walk threads' plugin copies (ipxg_plugin.copy_ctx), released.
+static void free_walk_copies(ipxg_engine* e) {
+    for (std::vector<ipxg_plugin>& v : e->walk_pl)
+        for (ipxg_plugin& q : v)
+            if (q.free_ctx && q.ctx) q.free_ctx(q.ctx);
+    e->walk_pl.clear();
+}
+
+// Threads for a walk of nf flows / m packets: the configured count (default: the host's hardware
+// threads, at most 16), fewer for a small walk (~2k packets per thread at least), one when a
+// plugin cannot be copied.  Starts the pool and makes every extra thread's plugin copies on
+// first use.
+static unsigned walk_pool(ipxg_engine* e, uint32_t nf, uint32_t m) {
+    unsigned want = e->walk_threads;
+    if (!want) want = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    for (const ipxg_plugin& q : e->plugins)
+        if (!q.copy_ctx || !q.free_ctx) want = 1;
+    const unsigned by_size = std::max<uint32_t>(1, m / 2048);
+    unsigned T = std::min<unsigned>({want, by_size, std::max<uint32_t>(nf, 1)});
+    if (T <= 1) return 1;
+    if (!e->pool || e->pool->size() != want) {
+        delete e->pool;
+        e->pool = new WalkPool(want);
+    }
+    while (e->walk_pl.size() + 1 < want) {
+        std::vector<ipxg_plugin> v = e->plugins;
+        bool ok = true;
+        for (ipxg_plugin& q : v) {
+            q.ctx = ok ? q.copy_ctx(q.ctx) : nullptr;
+            ok = ok && q.ctx;
+        }
+        if (!ok) {  // out of memory: the copies made so far serve, the rest of this walk
+            for (ipxg_plugin& q : v)
+                if (q.ctx) q.free_ctx(q.ctx);
+            break;
+        }
+        e->walk_pl.push_back(std::move(v));
+    }
+    return std::min<unsigned>(T, (unsigned)e->walk_pl.size() + 1);
+}
+
+int ipxg_set_walk_threads(ipxg_engine* e, uint32_t threads) {
+    if (!e || threads > 256) return IPXG_EINVAL;
+    e->walk_threads = threads;
+    return IPXG_OK;
+}
+
 // After the batch's complex path (its packets gathered and sorted, the device walk done): walk
 // the plugin flows on the host and write them back.  *live_delta: records created - closed.
 static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, const ComplexView& cx, uint32_t ncx,
@@ -1107,48 +1225,88 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const uint8_t* bytes = e->hw_bytes.data();
     HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(3);
-    // the walks, flows in order of their first packet (their order in `flows` now)
-    e->hw_ex.clear();
-    WalkOut wo{e->hw_ex};
-    wo.ex.reserve(m + 16);
+    // the walks, flows in order of their first packet (their order in `flows` now), split over
+    // the walk threads in contiguous flow ranges of about equal packet counts
+    const unsigned T = walk_pool(e, nf, m);
+    if (e->hw_ex.size() < T) e->hw_ex.resize(T);
     const bool ports = e->pstat_d != nullptr;
-    if (ports && e->host_ports.empty()) e->host_ports.assign(2 * 65536, 0);
-    for (uint32_t f = 0; f < nf; ++f) {
-        PluginFlow& F = flows[f];
-        FlowWalk w{e->plugins, p, wo, F.rec, (F.state & SLOT_LIVE) != 0};
-        const bool was_live = w.live;
-        for (uint32_t k = first[f]; k < first[f + 1]; ++k) {
-            ipxg_packet_view v;
-            std::memset(&v, 0, sizeof(v));
-            v.pkt = &pk[k];
-            v.data = bytes + off[k];
-            v.caplen = de[k].caplen;
-            v.wirelen = de[k].wirelen;
-            v.ts_sec = de[k].ts_sec;
-            v.ts_usec = de[k].ts_usec;
-            v.index = idx[k];
-            w.put(pk[k], &v);
-        }
-        // a plugin that follows every packet of a flow it claimed (ext set) keeps it on the host
-        // walk until the flow holds follow_packets packets (ipxg_plugin.follow_packets)
-        const bool follow = w.live && w.rec.ext && (uint64_t)w.rec.src_packets + w.rec.dst_packets < e->follow_max;
-        F.state = w.live ? (SLOT_LIVE | (follow ? SLOT_FOLLOW : 0u)) : 0u;
-        F.rec = w.rec;
-        *live_delta += (w.live ? 1 : 0) - (was_live ? 1 : 0);
-        // TopPorts from the flow's packets (count_flow_ports: every packet counts both ports)
-        const ipxg_flow_record& r = w.rec;
-        if (ports && (r.ip_proto == 6 || r.ip_proto == 17) && (r.src_port || r.dst_port)) {
-            uint64_t* a = e->host_ports.data() + (r.ip_proto == 17 ? 65536 : 0);
-            a[r.src_port] += F.len;
-            a[r.dst_port] += F.len;
-        }
+    if (ports && e->host_ports.size() < T) e->host_ports.resize(T);
+    std::vector<WalkOut> wos;
+    wos.reserve(T);
+    for (unsigned t = 0; t < T; ++t) {
+        e->hw_ex[t].clear();
+        wos.push_back(WalkOut{e->hw_ex[t]});
     }
+    std::vector<int64_t> dlive(T, 0);
+    auto walk_range = [&](unsigned t) {
+        // flows [f0, f1): the first flows whose first packet is at or past t/T of the packets
+        const uint32_t* fb = first.data();
+        const uint32_t f0 = t ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * t / T)) - fb) : 0;
+        const uint32_t f1 = t + 1 < T ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * (t + 1) / T)) - fb) : nf;
+        WalkOut& wo = wos[t];
+        wo.ex.reserve((size_t)(first[f1] - first[f0]) + 16);
+        const std::vector<ipxg_plugin>& pl = t ? e->walk_pl[t - 1] : e->plugins;
+        uint64_t* pa = nullptr;
+        if (ports) {
+            if (e->host_ports[t].empty()) e->host_ports[t].assign(2 * 65536, 0);
+            pa = e->host_ports[t].data();
+        }
+        int64_t dl = 0;
+        for (uint32_t f = f0; f < f1; ++f) {
+            PluginFlow& F = flows[f];
+            FlowWalk w{pl, p, wo, F.rec, (F.state & SLOT_LIVE) != 0};
+            const bool was_live = w.live;
+            for (uint32_t k = first[f]; k < first[f + 1]; ++k) {
+                ipxg_packet_view v;
+                std::memset(&v, 0, sizeof(v));
+                v.pkt = &pk[k];
+                v.data = bytes + off[k];
+                v.caplen = de[k].caplen;
+                v.wirelen = de[k].wirelen;
+                v.ts_sec = de[k].ts_sec;
+                v.ts_usec = de[k].ts_usec;
+                v.index = idx[k];
+                w.put(pk[k], &v);
+            }
+            // a plugin that follows every packet of a flow it claimed (ext set) keeps it on the
+            // host walk until the flow holds follow_packets packets (ipxg_plugin.follow_packets)
+            const bool follow =
+                w.live && w.rec.ext && (uint64_t)w.rec.src_packets + w.rec.dst_packets < e->follow_max;
+            F.state = w.live ? (SLOT_LIVE | (follow ? SLOT_FOLLOW : 0u)) : 0u;
+            F.rec = w.rec;
+            dl += (w.live ? 1 : 0) - (was_live ? 1 : 0);
+            // TopPorts from the flow's packets (count_flow_ports: every packet counts both ports)
+            const ipxg_flow_record& r = w.rec;
+            if (pa && (r.ip_proto == 6 || r.ip_proto == 17) && (r.src_port || r.dst_port)) {
+                uint64_t* a = pa + (r.ip_proto == 17 ? 65536 : 0);
+                a[r.src_port] += F.len;
+                a[r.dst_port] += F.len;
+            }
+        }
+        dlive[t] = dl;
+    };
+    if (T > 1) e->pool->run(walk_range);
+    else walk_range(0);
+    // the threads' exports, concatenated in thread order
+    size_t nx = 0;
+    for (unsigned t = 0; t < T; ++t) nx += wos[t].ex.size();
+    if (T > 1) {
+        std::vector<ipxg_flow_record>& all = e->hw_ex[0];
+        all.reserve(nx);
+        for (unsigned t = 1; t < T; ++t) all.insert(all.end(), wos[t].ex.begin(), wos[t].ex.end());
+    }
+    WalkOut& wo = wos[0];
+    for (unsigned t = 1; t < T; ++t) {
+        for (int k = 0; k < 5; ++k) wo.end[k] += wos[t].end[k];
+        for (int k = 0; k < 6; ++k) wo.pkts[k] += wos[t].pkts[k];
+        wo.unreasoned += wos[t].unreasoned;
+    }
+    for (unsigned t = 0; t < T; ++t) *live_delta += dlive[t];
     WALK_MARK(5);
     // back to the device: the slots, then the exports after the batch's own
     HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows.data(), (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
     launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf);
     HIPCHK(e, hipGetLastError());
-    const size_t nx = wo.ex.size();
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;
         HIPCHK(e, hipMemcpyAsync(e->ex + e->ex_count, wo.ex.data(), nx * sizeof(ipxg_flow_record),
@@ -1181,6 +1339,7 @@ int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
+    free_walk_copies(e);  // the walk threads copy the new set on their next walk
     e->plugins.push_back(*pl);
     e->follow_max = std::max<uint64_t>(e->follow_max, pl->follow_packets);
     std::vector<DevRule> rules(e->plugins.size());
@@ -1919,8 +2078,9 @@ int ipxg_parser_stats(ipxg_engine* e, uint64_t* tcp_ports, uint64_t* udp_ports, 
     HIPCHK(e, hipMemcpyAsync(h.data(), e->pstat_d, PSTAT_WORDS * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     static_assert(sizeof(ipxg_vlan_stats) == VS_N * 8, "VlanStats layout");
-    if (!e->host_ports.empty())
-        for (size_t k = 0; k < 2 * 65536; ++k) h[k] += e->host_ports[k];  // the plugin walks' flows
+    for (const std::vector<uint64_t>& hp : e->host_ports)  // the plugin walks' flows, per walk thread
+        if (!hp.empty())
+            for (size_t k = 0; k < 2 * 65536; ++k) h[k] += hp[k];
     if (tcp_ports) std::memcpy(tcp_ports, h.data(), 65536 * 8);
     if (udp_ports) std::memcpy(udp_ports, h.data() + 65536, 65536 * 8);
     if (vlans) std::memcpy(vlans, h.data() + PSTAT_PORTS, (size_t)IPXG_VLAN_IDS * VS_N * 8);

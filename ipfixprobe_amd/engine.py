@@ -101,7 +101,7 @@ EXPORTED_SYMBOLS = [
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
     "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
     "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
-    "ipxg_parser_stats", "ipxg_top_ports", "ipxg_add_plugin",
+    "ipxg_parser_stats", "ipxg_top_ports", "ipxg_add_plugin", "ipxg_set_walk_threads",
     "ipxg_demux", "ipxg_demux_arena_bytes", "ipxg_demux_split",
 ]
 
@@ -129,7 +129,8 @@ class Plugin(ctypes.Structure):
                 ("pre_create", PRE_CREATE_FN), ("post_create", FLOW_HOOK_FN), ("pre_update", FLOW_HOOK_FN),
                 ("post_update", FLOW_HOOK_FN), ("pre_export", PRE_EXPORT_FN),
                 ("masked", ctypes.c_uint32), ("follow_packets", ctypes.c_uint32),
-                ("prefix_mask", (ctypes.c_uint8 * 16) * 16)]
+                ("prefix_mask", (ctypes.c_uint8 * 16) * 16),
+                ("copy_ctx", ctypes.c_void_p), ("free_ctx", ctypes.c_void_p)]  # ABI 3 (C function pointers)
 
 # ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),
@@ -197,6 +198,7 @@ def lib():
                                                ctypes.POINTER(sz)]
         L.ipxg_parser_stats.argtypes = [vp, vp, vp, vp]
         L.ipxg_add_plugin.argtypes = [vp, ctypes.POINTER(Plugin)]
+        L.ipxg_set_walk_threads.argtypes = [vp, u32]
         L.ipxg_top_ports.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
         L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                  ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -415,6 +417,10 @@ class Engine:
     def add_plugin(self, plugin):
         """Register a Plugin (ctypes struct); the caller keeps it (and its callbacks) alive."""
         self._check(lib().ipxg_add_plugin(self._h, ctypes.byref(plugin)), "ipxg_add_plugin")
+
+    def set_walk_threads(self, n):
+        """Threads of the plugin flows' host walk (0 = default, 1 = the calling thread)."""
+        self._check(lib().ipxg_set_walk_threads(self._h, int(n)), "ipxg_set_walk_threads")
 
     def parser_stats(self):
         """(tcp port frequencies [65536], udp [65536], VlanStats [4096]) -- engine made with ps=true."""

@@ -9,9 +9,38 @@
 
 enum { C_PRE_CREATE, C_POST_CREATE, C_PRE_UPDATE, C_POST_UPDATE, C_PRE_EXPORT, C_FLUSH, C_N };
 
+/* A plugin instance's counters.  The walk threads' copies (copy_ctx, ProcessPlugin::copy) hang
+ * off the instance they were copied from; ipxg_std_plugin_calls sums them, and a copy released
+ * by the engine (free_ctx) folds its counts into it.  Copies are made and released by the
+ * engine's calling thread, between walks. */
 typedef struct std_ctx {
     uint64_t calls[C_N];
+    struct std_ctx* root;   /* NULL on the instance ipxg_std_plugin made */
+    struct std_ctx* next;   /* root: first copy; copy: next copy of the same root */
+    struct std_ctx* prev;
 } std_ctx;
+
+static void* std_copy(void* ctx) {
+    std_ctx* r = (std_ctx*)ctx;
+    if (r->root) r = r->root;
+    std_ctx* c = (std_ctx*)calloc(1, sizeof(std_ctx));
+    if (!c) return NULL;
+    c->root = r;
+    c->next = r->next;
+    c->prev = r;
+    if (r->next) r->next->prev = c;
+    r->next = c;
+    return c;
+}
+
+static void std_free_copy(void* ctx) {
+    std_ctx* c = (std_ctx*)ctx;
+    if (!c || !c->root) return; /* the original belongs to ipxg_std_plugin_free */
+    for (int k = 0; k < C_N; ++k) c->root->calls[k] += c->calls[k];
+    c->prev->next = c->next;
+    if (c->next) c->next->prev = c->prev;
+    free(c);
+}
 
 static const uint8_t* payload(const ipxg_packet_view* v, uint32_t* n) {
     const ipxg_parsed_pkt* p = v->pkt;
@@ -342,18 +371,29 @@ int ipxg_std_plugin(const char* name, ipxg_plugin* out) {
     } else {
         return IPXG_EINVAL;
     }
+    out->copy_ctx = std_copy;
+    out->free_ctx = std_free_copy;
     out->ctx = calloc(1, sizeof(std_ctx));
     return out->ctx ? IPXG_OK : IPXG_ENOMEM;
 }
 
 void ipxg_std_plugin_free(ipxg_plugin* pl) {
     if (pl && pl->ctx) {
-        free(pl->ctx);
+        std_ctx* r = (std_ctx*)pl->ctx;
+        while (r->next) { /* copies an engine still held (destroy the engine first) */
+            std_ctx* c = r->next;
+            r->next = c->next;
+            free(c);
+        }
+        free(r);
         pl->ctx = NULL;
     }
 }
 
 void ipxg_std_plugin_calls(const ipxg_plugin* pl, uint64_t* out6) {
     if (!pl || !pl->ctx || !out6) return;
-    memcpy(out6, ((const std_ctx*)pl->ctx)->calls, sizeof(uint64_t) * C_N);
+    const std_ctx* r = (const std_ctx*)pl->ctx;
+    memcpy(out6, r->calls, sizeof(uint64_t) * C_N);
+    for (const std_ctx* c = r->next; c; c = c->next)
+        for (int k = 0; k < C_N; ++k) out6[k] += c->calls[k];
 }

@@ -140,7 +140,12 @@ inline bool rule_for(const std::string& name, ipxg_plugin& q) {
 
 class Adapter {
 public:
-    explicit Adapter(ipxp::ProcessPlugin* p) : m_p(p) {}
+    explicit Adapter(ipxp::ProcessPlugin* p, bool owns = false) : m_p(p), m_owns(owns) {}
+    ~Adapter() {
+        if (m_owns) delete m_p;
+    }
+    Adapter(const Adapter&) = delete;
+    Adapter& operator=(const Adapter&) = delete;
 
     // The ipxg_plugin of this adapter (ctx = this): the rule of `kind` and the five hooks.
     bool make(const std::string& kind, ipxg_plugin& q) {
@@ -174,6 +179,16 @@ public:
             a->m_p->pre_export(f);
             a->adopt(*r, f);
         };
+        // a walk thread's own instance: ProcessPlugin::copy() (processPlugin.hpp:50), as the
+        // reference copies every process plugin per storage pipeline (ipfixprobe.cpp:430-436)
+        q.copy_ctx = [](void* c) -> void* {
+            try {
+                return new Adapter(static_cast<Adapter*>(c)->m_p->copy(), true);
+            } catch (...) {
+                return nullptr;
+            }
+        };
+        q.free_ctx = [](void* c) { delete static_cast<Adapter*>(c); };
         return true;
     }
 
@@ -203,6 +218,7 @@ private:
     }
 
     ipxp::ProcessPlugin* m_p;
+    bool m_owns;
     ipxp::Flow m_scratch{};  // the hooks' Flow for a record without extensions
 };
 

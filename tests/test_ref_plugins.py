@@ -136,10 +136,12 @@ def test_bridge_with_reference_plugin_matches_oracle(name, pcap, batch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 8])
 @pytest.mark.parametrize("mix,names", [("imix", ("dns", "http", "tls")), ("quic", ("quic", "dns"))])
-def test_bridge_with_reference_plugins_on_workload(mix, names):
+def test_bridge_with_reference_plugins_on_workload(mix, names, threads):
     """600k packets of the configs[2] / configs[4] mix (three device batches, flows carried across
-    them) with the configs' real plugins: records and extension contents equal the oracle's."""
+    them) with the configs' real plugins: records and extension contents equal the oracle's --
+    with the host walk on one thread and split over 8 (each with its own ProcessPlugin::copy())."""
     import torch
     import synthgen
     from ipfixprobe_amd import Engine
@@ -150,6 +152,7 @@ def test_bridge_with_reference_plugins_on_workload(mix, names):
     torch.cuda.synchronize()
     eps = [RefPlugin(x) for x in names]
     with Engine("s=19") as e:
+        e.set_walk_threads(threads)
         for p in eps:
             e.add_plugin(p.struct)
         for fr, de in batches:

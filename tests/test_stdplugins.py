@@ -84,15 +84,19 @@ def test_mix_plugin_shares():
 
 
 PLUGINS = {"imix": ("dns", "http", "tls"), "quic": ("quic", "dns")}
+_CALLS = {}  # hook calls of the single-threaded walk, per mix
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 4, 16])
 @pytest.mark.parametrize("name", sorted(PLUGINS))
-def test_plugins_on_workload_match_oracle(name):
+def test_plugins_on_workload_match_oracle(name, threads):
     """2M packets of the mix over 1M flows in four device batches with the configs' plugins
     registered: every record (plugin flushes, REINSERTs and the plugins' ext bits included)
     equals the oracle's, which calls the same hooks on every packet; the hooks saw only a small
-    share of the packets on the engine (the bridge kept the rest on the device)."""
+    share of the packets on the engine (the bridge kept the rest on the device).  The host walk
+    on 1, 4 and 16 threads (plugin copies per thread): the same records, and the hook calls of
+    all copies sum to the same counts."""
     import torch
     import synthgen
     from ipfixprobe_amd import Engine
@@ -102,6 +106,7 @@ def test_plugins_on_workload_match_oracle(name):
     torch.cuda.synchronize()
     pls = [_std(p) for p in PLUGINS[name]]
     with Engine("s=21") as e:
+        e.set_walk_threads(threads)
         for p in pls:
             e.add_plugin(p.struct)
         for fr, de in batches:
@@ -109,6 +114,11 @@ def test_plugins_on_workload_match_oracle(name):
         e.finish()
         got = e.poll()
         st = e.stats()
+    calls = [p.calls() for p in pls]  # copies folded back into the originals at engine destroy
+    if threads == 1:
+        _CALLS[name] = calls
+    elif name in _CALLS:
+        assert calls == _CALLS[name]
     ref = [_std(p) for p in PLUGINS[name]]
     c = oracle_py.OracleCache(cache_exp=22)
     for p in ref:
