@@ -371,10 +371,11 @@ typedef struct ipxg_plugin {
      * plugin flows over several threads (ipxg_set_walk_threads), each calling the hooks of its
      * own instance of every plugin -- as the reference gives every storage pipeline its own copy
      * of each process plugin (ipfixprobe.cpp:430-436).  copy_ctx returns a new context for another
-     * walk thread (NULL: out of memory), free_ctx releases one; the engine makes its copies on
-     * the first multi-threaded walk and frees them in ipxg_add_plugin and ipxg_destroy, so the
-     * original ctx must outlive the engine.  A NULL copy_ctx on any registered plugin keeps the
-     * walk on one thread. */
+     * walk thread (NULL: out of memory), free_ctx releases one.  The engine copies a plugin when
+     * it is registered (and in ipxg_set_walk_threads), before any walk has used it -- copy()
+     * copies a plugin's state, and the reference copies its prototypes before the pipelines
+     * start -- and frees the copies in ipxg_destroy, so the original ctx must outlive the
+     * engine.  A NULL copy_ctx on any registered plugin keeps the walk on one thread. */
     void* (*copy_ctx)(void* ctx);
     void (*free_ctx)(void* ctx);
 } ipxg_plugin;
@@ -382,7 +383,8 @@ typedef struct ipxg_plugin {
 /* Register a plugin (the order of registration is the order of the hook calls). */
 int ipxg_add_plugin(ipxg_engine* eng, const ipxg_plugin* plugin);
 /* Threads of the plugin flows' host walk: 0 = default (the host's hardware threads, at most
- * 16), 1 = the calling thread only.  Flows are independent (the walk replays each flow's
+ * 16), 1 = the calling thread only.  Raising it after the first plugin walk fails with
+ * IPXG_ESTATE (the new copies would copy used plugin instances).  Flows are independent (the walk replays each flow's
  * packets in order on one thread), so the records are the same for any thread count; the export
  * order of the walked flows is the concatenation of the threads' (contiguous flow ranges in
  * order of each flow's first packet). */

@@ -37,6 +37,47 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// Host memory for the walk's device-to-host copies: page-aligned malloc memory, page-locked with
+// hipHostRegister (so the DMA engine writes it directly, without the runtime's pageable staging)
+// and read by the CPU through its caches (hipHostMalloc'd memory read slower in the walk,
+// DESIGN 4.4).  Contents are not kept when it grows (each batch overwrites it).
+// IPXG_WALK_PAGEABLE=1 leaves it pageable (A/B).
+template <class T>
+struct HostVec {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    bool reg = false;
+    HostVec() = default;
+    HostVec(const HostVec&) = delete;
+    HostVec& operator=(const HostVec&) = delete;
+    ~HostVec() { release(); }
+    void release() {
+        if (p) {
+            if (reg) (void)hipHostUnregister(p);
+            std::free(p);
+        }
+        p = nullptr;
+        n = cap = 0;
+        reg = false;
+    }
+    bool resize(size_t k, bool pin) {
+        if (k > cap) {
+            const size_t want = std::max(k, cap + cap / 2 + 1024);
+            const size_t bytes = (want * sizeof(T) + 4095) & ~(size_t)4095;
+            release();
+            void* q = nullptr;
+            if (posix_memalign(&q, 4096, bytes)) return false;
+            p = static_cast<T*>(q);
+            cap = bytes / sizeof(T);
+            reg = pin && hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
+        }
+        n = k;
+        return true;
+    }
+    T* data() { return p; }
+    size_t size() const { return n; }
+};
+
 // The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
 // calling thread -- and returns when all have returned.  Persistent across batches (a batch of
 // configs[2] walks ~10^5 flows; spawning threads per batch would cost more than small walks).
@@ -134,10 +175,11 @@ struct ipxg_engine {
     DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
     // their host copies, kept across batches (pageable: the walk reads them on the CPU, and
     // pinned hipHostMalloc memory read slower there -- measured: +58 % walk time on configs[2])
-    std::vector<uint64_t> hw_sorted;
-    std::vector<ipxg_parsed_pkt> hw_parsed;
-    std::vector<ipxg_pkt_desc> hw_desc;
-    std::vector<uint8_t> hw_bytes;
+    HostVec<uint64_t> hw_sorted;
+    HostVec<ipxg_parsed_pkt> hw_parsed;
+    HostVec<ipxg_pkt_desc> hw_desc;
+    HostVec<uint8_t> hw_bytes;
+    bool walk_pin = true;  // HostVec page-locked (IPXG_WALK_PAGEABLE unset)
     // the walk's own working vectors, kept too (a fresh 10-20 MB vector per batch cost its page
     // faults on first touch inside the walk)
     std::vector<PluginFlow> hw_flows;
@@ -151,6 +193,7 @@ struct ipxg_engine {
     // batches: its exports of the current batch, its TopPorts counts (2 x 65536 when ps=true;
     // summed when read) and, for t >= 1, its copies of the plugins (ipxg_plugin.copy_ctx)
     uint32_t walk_threads = 0;
+    bool walked = false;  // a plugin walk has called hooks (plugin instances no longer pristine)
     WalkPool* pool = nullptr;
     std::vector<std::vector<ipxg_flow_record>> hw_ex;   // [t]
     std::vector<std::vector<uint64_t>> host_ports;      // [t]
@@ -506,6 +549,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     ipxg_engine* e = new ipxg_engine();
     e->cfg = *cfg;
     e->walk_trace = std::getenv("IPXG_WALK_TRACE") != nullptr;
+    e->walk_pin = std::getenv("IPXG_WALK_PAGEABLE") == nullptr;
     if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -1062,43 +1106,62 @@ static void free_walk_copies(ipxg_engine* e) {
     e->walk_pl.clear();
 }
 
-// Threads for a walk of nf flows / m packets: the configured count (default: the host's hardware
-// threads, at most 16), fewer for a small walk (~2k packets per thread at least), one when a
-// plugin cannot be copied.  Starts the pool and makes every extra thread's plugin copies on
-// first use.
-static unsigned walk_pool(ipxg_engine* e, uint32_t nf, uint32_t m) {
-    unsigned want = e->walk_threads;
-    if (!want) want = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+// Walk threads wanted: the configured count (default: the host's hardware threads, at most 16);
+// one when a registered plugin cannot be copied.
+static unsigned walk_want(const ipxg_engine* e) {
     for (const ipxg_plugin& q : e->plugins)
-        if (!q.copy_ctx || !q.free_ctx) want = 1;
+        if (!q.copy_ctx || !q.free_ctx) return 1;
+    return e->walk_threads ? e->walk_threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// Every registered plugin copied for walk threads 1 .. want-1 (walk_pl[t-1][k]: thread t's copy
+// of plugin k).  Copies are made from instances no walk has used yet, at registration: a
+// ProcessPlugin's copy() copies its state, and the reference copies its prototypes before the
+// pipelines start (ipfixprobe.cpp:430-436) -- TLSPlugin / HTTPPlugin keep a preallocated
+// extension pointer (tls.cpp:412-425, http.cpp:592-598) that a copy of a used instance would
+// share with it.
+static int make_walk_copies(ipxg_engine* e) {
+    const unsigned want = walk_want(e);
+    if (want <= 1) return IPXG_OK;
+    if (e->walk_pl.size() + 1 < want) e->walk_pl.resize(want - 1);
+    for (unsigned t = 0; t + 1 < want; ++t) {
+        std::vector<ipxg_plugin>& v = e->walk_pl[t];
+        while (v.size() < e->plugins.size()) {
+            ipxg_plugin q = e->plugins[v.size()];
+            q.ctx = q.copy_ctx(q.ctx);
+            if (!q.ctx) return set_err(e, IPXG_ENOMEM, "a process plugin's copy_ctx failed");
+            v.push_back(q);
+        }
+    }
+    return IPXG_OK;
+}
+
+// Threads for a walk of nf flows / m packets: the wanted count, fewer for a small walk (~2k
+// packets per thread at least).  Starts the pool on first use.
+static unsigned walk_pool(ipxg_engine* e, uint32_t nf, uint32_t m) {
+    const unsigned want = walk_want(e);
     const unsigned by_size = std::max<uint32_t>(1, m / 2048);
     unsigned T = std::min<unsigned>({want, by_size, std::max<uint32_t>(nf, 1)});
+    for (unsigned t = 1; t < T; ++t)
+        if (t > e->walk_pl.size() || e->walk_pl[t - 1].size() != e->plugins.size()) T = t;
     if (T <= 1) return 1;
-    if (!e->pool || e->pool->size() != want) {
+    if (!e->pool || e->pool->size() < T) {
         delete e->pool;
         e->pool = new WalkPool(want);
     }
-    while (e->walk_pl.size() + 1 < want) {
-        std::vector<ipxg_plugin> v = e->plugins;
-        bool ok = true;
-        for (ipxg_plugin& q : v) {
-            q.ctx = ok ? q.copy_ctx(q.ctx) : nullptr;
-            ok = ok && q.ctx;
-        }
-        if (!ok) {  // out of memory: the copies made so far serve, the rest of this walk
-            for (ipxg_plugin& q : v)
-                if (q.ctx) q.free_ctx(q.ctx);
-            break;
-        }
-        e->walk_pl.push_back(std::move(v));
-    }
-    return std::min<unsigned>(T, (unsigned)e->walk_pl.size() + 1);
+    return T;
 }
 
 int ipxg_set_walk_threads(ipxg_engine* e, uint32_t threads) {
     if (!e || threads > 256) return IPXG_EINVAL;
+    const uint32_t old = e->walk_threads;
     e->walk_threads = threads;
-    return IPXG_OK;
+    const unsigned want = walk_want(e);
+    if (want > e->walk_pl.size() + 1 && e->walked) {  // the new copies would copy used instances
+        e->walk_threads = old;
+        return set_err(e, IPXG_ESTATE, "walk threads raised after the first plugin walk");
+    }
+    return make_walk_copies(e);
 }
 
 // After the batch's complex path (its packets gathered and sorted, the device walk done): walk
@@ -1147,7 +1210,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     if (!nf) return IPXG_OK;
     std::vector<PluginFlow>& flows = e->hw_flows;
     flows.resize(nf);
-    e->hw_sorted.resize(npk);
+    if (!e->hw_sorted.resize(npk, e->walk_pin)) return set_err(e, IPXG_ENOMEM, "host walk buffers");
     const uint64_t* sorted = e->hw_sorted.data();
     HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_sorted.data(), cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
@@ -1200,8 +1263,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     launch_plugin_pkts(e->st, bv, p, frag_view(e), (const uint32_t*)e->pf_idx.p, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
                        (ipxg_pkt_desc*)e->pf_desc.p);
     HIPCHK(e, hipGetLastError());
-    e->hw_parsed.resize(m);
-    e->hw_desc.resize(m);
+    if (!e->hw_parsed.resize(m, e->walk_pin) || !e->hw_desc.resize(m, e->walk_pin))
+        return set_err(e, IPXG_ENOMEM, "host walk buffers");
     ipxg_parsed_pkt* pk = e->hw_parsed.data();
     const ipxg_pkt_desc* de = e->hw_desc.data();
     HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
@@ -1221,13 +1284,14 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     e->tm.plugin_packets += m;
     e->tm.plugin_bytes += off[m];
     for (uint32_t k = 0; k < m; ++k) e->tm.plugin_extra_bytes += de[k].caplen > 128 ? de[k].caplen - 128u : 0u;
-    e->hw_bytes.resize(off[m] + 16);
+    if (!e->hw_bytes.resize(off[m] + 16, e->walk_pin)) return set_err(e, IPXG_ENOMEM, "host walk buffers");
     const uint8_t* bytes = e->hw_bytes.data();
     HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(3);
     // the walks, flows in order of their first packet (their order in `flows` now), split over
     // the walk threads in contiguous flow ranges of about equal packet counts
     const unsigned T = walk_pool(e, nf, m);
+    e->walked = true;
     if (e->hw_ex.size() < T) e->hw_ex.resize(T);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.size() < T) e->host_ports.resize(T);
@@ -1339,8 +1403,11 @@ int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
-    free_walk_copies(e);  // the walk threads copy the new set on their next walk
     e->plugins.push_back(*pl);
+    if (const int rc1 = make_walk_copies(e)) {  // the walk threads' copies of the new plugin
+        e->plugins.pop_back();
+        return rc1;
+    }
     e->follow_max = std::max<uint64_t>(e->follow_max, pl->follow_packets);
     std::vector<DevRule> rules(e->plugins.size());
     for (size_t k = 0; k < rules.size(); ++k) {
