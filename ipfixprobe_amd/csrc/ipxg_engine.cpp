@@ -1303,6 +1303,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     }
     std::vector<int64_t> dlive(T, 0);
     auto walk_range = [&](unsigned t) {
+        if (t >= T) return;  // (the pool may hold more threads than this walk uses)
         // flows [f0, f1): the first flows whose first packet is at or past t/T of the packets
         const uint32_t* fb = first.data();
         const uint32_t f0 = t ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * t / T)) - fb) : 0;
