@@ -79,28 +79,100 @@ void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableV
     hipLaunchKernelGGL(k_classify, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, rules, nrules, ctl);
 }
 
-// The plugin flows among the ncx complex ones (rank order is arbitrary; the host sorts).
-__global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out,
+// The plugin flows among the ncx complex ones, put in the order the host walks them -- by their
+// first packet in the batch -- and everything the walk reads laid out in that order, so the host
+// streams through memory and splits the flows over its threads by contiguous ranges:
+//   k_plugin_keys   key[r] = first packet index << 32 | rank for a plugin flow, PF_NONE otherwise
+//   (radix sort of the keys, 56 bits)
+//   k_plugin_pack   flow k of the sorted keys -> PluginFlow out[k], its packet count flen[k]
+//   (exclusive scan of flen: the flows' first positions in the packet list)
+//   k_plugin_idx    the packet list (batch indices, flows in order, each flow's in arrival order)
+//                   and each listed packet's captured length (exclusive scan: byte offsets)
+//   k_plugin_totals {plugin flows, packets, bytes} for the host
+constexpr uint64_t PF_NONE = (1ull << 56) - 1;
+
+__global__ __launch_bounds__(256) void k_plugin_keys(TableView t, ComplexView cx, uint32_t ncx, uint64_t* keys,
                                                      uint32_t* count) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= ncx) return;
+    const bool host = (t.hot[cx.slot_of[r]].state & SLOT_HOST) != 0;
+    keys[r] = host ? ((cx.sorted[cx.seg[r]] & 0xFFFFFFull) << 32) | r : PF_NONE;
+    // one atomic per wave
+    const uint64_t m = __ballot(host);
+    if (m && threadIdx.x % 64 == (uint32_t)__builtin_ctzll(m)) atomicAdd(count, (uint32_t)__popcll(m));
+}
+
+__global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx, const uint64_t* skeys, uint32_t ncx,
+                                                     const uint32_t* count, PluginFlow* out, uint32_t* flen) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k > ncx) return;
+    if (k >= *count) {
+        flen[k] = 0;  // (the scan's tail: first[k] = packets for k >= flows)
+        return;
+    }
+    const uint32_t r = (uint32_t)skeys[k];
     const uint32_t s = cx.slot_of[r];
     const HotSlot h = t.hot[s];
-    if (!(h.state & SLOT_HOST)) return;
-    const uint32_t pos = atomicAdd(count, 1u);
     PluginFlow f;
     f.slot = s;
     f.seg = cx.seg[r];
     f.len = cx.len[r];
     f.state = h.state;
     f.key = h.key;
+    f.pad = 0;
     f.rec = t.cold[s];
-    out[pos] = f;
+    out[k] = f;
+    flen[k] = f.len;
 }
 
-void launch_plugin_pack(hipStream_t st, TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out,
-                        uint32_t* count) {
-    hipLaunchKernelGGL(k_plugin_pack, dim3((ncx + 255) / 256), dim3(256), 0, st, t, cx, ncx, out, count);
+// One wave per flow: its packets' batch indices and captured lengths at first[k] ...
+__global__ __launch_bounds__(256) void k_plugin_idx(BatchView b, ComplexView cx, const PluginFlow* flows,
+                                                    const uint32_t* count, const uint32_t* first, uint32_t* idx,
+                                                    uint64_t* clen) {
+    const uint32_t lane = threadIdx.x % 64;
+    const uint32_t nf = *count;
+    for (uint32_t k = (blockIdx.x * 256 + threadIdx.x) / 64; k < nf; k += gridDim.x * 4) {
+        const uint32_t seg = flows[k].seg, len = flows[k].len, at = first[k];
+        for (uint32_t j = lane; j < len; j += 64) {
+            const uint32_t i = (uint32_t)(cx.sorted[seg + j] & 0xFFFFFFu);
+            idx[at + j] = i;
+            clen[at + j] = b.desc[i].caplen;
+        }
+    }
+}
+
+__global__ void k_plugin_totals(const uint32_t* count, const uint32_t* first, const uint64_t* off, uint64_t* tot) {
+    const uint32_t nf = *count, m = first[nf];
+    tot[0] = nf;
+    tot[1] = m;
+    tot[2] = off[m];
+}
+
+void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, ComplexView cx, uint32_t ncx, uint32_t npk,
+                         const PluginOrder& o) {
+    hipLaunchKernelGGL(k_plugin_keys, dim3((ncx + 255) / 256), dim3(256), 0, st, t, cx, ncx, o.keys, o.count);
+    size_t tb = o.temp_bytes;
+    (void)sort_keys_u64(o.temp, tb, o.keys, o.skeys, ncx, 56, st);
+    hipLaunchKernelGGL(k_plugin_pack, dim3((ncx + 1 + 255) / 256), dim3(256), 0, st, t, cx, o.skeys, ncx, o.count,
+                       o.flows, o.flen);
+    tb = o.temp_bytes;
+    (void)exclusive_scan_u32(o.temp, tb, o.flen, o.first, ncx + 1, st);
+    uint32_t g = (ncx + 3) / 4;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_plugin_idx, dim3(g ? g : 1), dim3(256), 0, st, b, cx, o.flows, o.count, o.first, o.idx,
+                       o.clen);
+    tb = o.temp_bytes;
+    (void)exclusive_scan_u64(o.temp, tb, o.clen, o.off, npk + 1, st);
+    hipLaunchKernelGGL(k_plugin_totals, dim3(1), dim3(1), 0, st, o.count, o.first, o.off, o.tot);
+}
+
+// Scratch bytes launch_plugin_order needs for ncx flows / npk packets (radix sort + scans).
+size_t plugin_order_temp(uint32_t ncx, uint32_t npk) {
+    size_t a = 0, c = 0, d = 0;
+    (void)sort_keys_u64(nullptr, a, nullptr, nullptr, ncx, 56, nullptr);
+    (void)exclusive_scan_u32(nullptr, c, nullptr, nullptr, ncx + 1, nullptr);
+    (void)exclusive_scan_u64(nullptr, d, nullptr, nullptr, npk + 1, nullptr);
+    return std::max(a, std::max(c, d));
 }
 
 // Packet idx[k] (k < m): every field a hook reads (ipxg_parsed_pkt, FULL parse) and its descriptor.

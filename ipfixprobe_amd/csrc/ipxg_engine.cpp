@@ -78,6 +78,11 @@ struct HostVec {
     size_t size() const { return n; }
 };
 
+// A walk thread's exports, on a cache line of its own (the threads append concurrently).
+struct alignas(128) ExportVec {
+    std::vector<ipxg_flow_record> v;
+};
+
 // The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
 // calling thread -- and returns when all have returned.  Persistent across batches (a batch of
 // configs[2] walks ~10^5 flows; spawning threads per batch would cost more than small walks).
@@ -172,20 +177,15 @@ struct ipxg_engine {
     bool strict_prune = true;                            // strict: idle-free sweep steps left out of the DAG
     uint32_t strict_wgs = STRICT_WGS_DEFAULT;            // strict: replay workgroups per XCD (0: one workgroup)
     uint32_t* st_sched = nullptr;                        // strict: the multi-workgroup scheduler block
-    DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes;
-    // their host copies, kept across batches (pageable: the walk reads them on the CPU, and
-    // pinned hipHostMalloc memory read slower there -- measured: +58 % walk time on configs[2])
-    HostVec<uint64_t> hw_sorted;
+    DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes, pf_keys, pf_flen, pf_tmp;
+    // their host copies, kept across batches (HostVec: page-locked malloc memory)
+    HostVec<PluginFlow> hw_flows;
+    HostVec<uint32_t> hw_first, hw_idx;
+    HostVec<uint64_t> hw_off;
     HostVec<ipxg_parsed_pkt> hw_parsed;
     HostVec<ipxg_pkt_desc> hw_desc;
     HostVec<uint8_t> hw_bytes;
     bool walk_pin = true;  // HostVec page-locked (IPXG_WALK_PAGEABLE unset)
-    // the walk's own working vectors, kept too (a fresh 10-20 MB vector per batch cost its page
-    // faults on first touch inside the walk)
-    std::vector<PluginFlow> hw_flows;
-    std::vector<uint32_t> hw_idx, hw_first;
-    std::vector<uint64_t> hw_off, hw_okey, hw_okey2;
-    std::vector<PluginFlow> hw_flows2;
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
     uint64_t host_pkts[6] = {0, 0, 0, 0, 0, 0};
     uint64_t host_unreasoned = 0;  // counted exports without an end reason (total_exported only)
@@ -195,7 +195,7 @@ struct ipxg_engine {
     uint32_t walk_threads = 0;
     bool walked = false;  // a plugin walk has called hooks (plugin instances no longer pristine)
     WalkPool* pool = nullptr;
-    std::vector<std::vector<ipxg_flow_record>> hw_ex;   // [t]
+    std::vector<ExportVec> hw_ex;                        // [t]
     std::vector<std::vector<uint64_t>> host_ports;      // [t]
     std::vector<std::vector<ipxg_plugin>> walk_pl;      // [t - 1]: thread t's plugin instances
     // staging for host batches
@@ -624,12 +624,10 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
 int ipxg_destroy(ipxg_engine* e) {
     if (e && e->walk_trace && e->tm.plugin_flows)
         std::fprintf(stderr,
-                     "ipxg plugin walk ms: pack %.1f fetch %.1f parse %.1f bytes %.1f order %.1f walk %.1f back %.1f"
-                     " | minor faults: %ld %ld %ld %ld %ld %ld %ld\n",
-                     e->walk_phase_ms[0], e->walk_phase_ms[1], e->walk_phase_ms[2], e->walk_phase_ms[3],
-                     e->walk_phase_ms[4], e->walk_phase_ms[5], e->walk_phase_ms[6], e->walk_faults[0],
-                     e->walk_faults[1], e->walk_faults[2], e->walk_faults[3], e->walk_faults[4], e->walk_faults[5],
-                     e->walk_faults[6]);
+                     "ipxg plugin walk ms: order %.1f copies %.1f walk %.1f back %.1f"
+                     " | minor faults: %ld %ld %ld %ld\n",
+                     e->walk_phase_ms[0], e->walk_phase_ms[1], e->walk_phase_ms[5], e->walk_phase_ms[6],
+                     e->walk_faults[0], e->walk_faults[1], e->walk_faults[5], e->walk_faults[6]);
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
@@ -937,11 +935,12 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 // differ) and the 16-way line (no NO_RES evictions).
 namespace {
 
-struct WalkOut {
+struct alignas(128) WalkOut {  // one per walk thread, on cache lines of its own
     std::vector<ipxg_flow_record>& ex;  // exported records, in order
     uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
     uint64_t pkts[6] = {0, 0, 0, 0, 0, 0};  // FlowRecordStats buckets
     uint64_t unreasoned = 0;  // export_flow with end_reason 0 (post_create FLUSH of a new record)
+    uint64_t v6 = 0;          // IPv6 records among ex
 };
 
 struct FlowWalk {
@@ -986,6 +985,7 @@ struct FlowWalk {
         o.reserved0 = 0;
         std::memset(o.reserved, 0, sizeof(o.reserved));
         out.ex.push_back(o);
+        out.v6 += o.ip_version == 6 ? 1 : 0;
         // m_total_exported and update_flow_record_stats count every export_flow;
         // update_flow_end_reason_stats ignores a reason outside 1..5 (cache.cpp:264-267,618-638)
         if (!counted) return;
@@ -1170,8 +1170,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
                        uint32_t npk, int64_t* live_delta) {
     const auto t0 = std::chrono::steady_clock::now();
     auto tm = t0;
-    // IPXG_WALK_TRACE: the walk's phases (pack + count, flow images + sorted list, parsed
-    // packets, frame bytes, flow order, the host loop, write-back) summed, with their minor page
+    // IPXG_WALK_TRACE: the walk's phases (0: the device ordering + the sizes' round trip, 1: the
+    // copies to the host, 5: the host loop, 6: the write-back) summed, with their minor page
     // faults, printed when the engine closes
     const bool trace = e->walk_trace;
     long flt = 0;
@@ -1199,95 +1199,72 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     } clock{e, t0};
     int rc;
     *live_delta = 0;
+    // on the device: the plugin flows in order of their first packet, their packets' list and
+    // byte offsets (launch_plugin_order), then the parsed packets and the frame bytes in that
+    // order; one round trip for the sizes
+    const size_t tmp_b = plugin_order_temp(ncx, npk);
+    if ((rc = ensure(e, e->pf_keys, (size_t)ncx * 16 + 16))) return rc;
     if ((rc = ensure(e, e->pf_d, (size_t)ncx * sizeof(PluginFlow) + 16))) return rc;
-    uint32_t* cnt_d = (uint32_t*)((char*)e->pf_d.p + (size_t)ncx * sizeof(PluginFlow));
-    HIPCHK(e, hipMemsetAsync(cnt_d, 0, sizeof(uint32_t), e->st));
-    launch_plugin_pack(e->st, table_view(e), cx, ncx, (PluginFlow*)e->pf_d.p, cnt_d);
+    if ((rc = ensure(e, e->pf_flen, ((size_t)ncx + 1) * 8 + 16))) return rc;
+    if ((rc = ensure(e, e->pf_idx, (size_t)npk * 4 + 16))) return rc;
+    if ((rc = ensure(e, e->pf_off, ((size_t)npk + 1) * 16 + 16))) return rc;
+    if ((rc = ensure(e, e->pf_tmp, tmp_b + 64))) return rc;
+    PluginOrder o;
+    o.keys = (uint64_t*)e->pf_keys.p;
+    o.skeys = o.keys + ncx;
+    o.flows = (PluginFlow*)e->pf_d.p;
+    o.flen = (uint32_t*)e->pf_flen.p;
+    o.first = o.flen + ncx + 1;
+    o.idx = (uint32_t*)e->pf_idx.p;
+    o.off = (uint64_t*)e->pf_off.p;
+    o.clen = o.off + npk + 1;
+    o.tot = (uint64_t*)e->pf_tmp.p;
+    o.count = (uint32_t*)(o.tot + 4);
+    o.temp = (char*)e->pf_tmp.p + 64;
+    o.temp_bytes = tmp_b;
+    HIPCHK(e, hipMemsetAsync(o.count, 0, sizeof(uint32_t), e->st));
+    HIPCHK(e, hipMemsetAsync(o.clen, 0, ((size_t)npk + 1) * 8, e->st));
+    launch_plugin_order(e->st, bv, table_view(e), cx, ncx, npk, o);
     HIPCHK(e, hipGetLastError());
-    uint32_t nf = 0;
-    HIPCHK(e, hipMemcpyAsync(&nf, cnt_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+    uint64_t tot[3] = {0, 0, 0};
+    HIPCHK(e, hipMemcpyAsync(tot, o.tot, sizeof(tot), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(0);
+    const uint32_t nf = (uint32_t)tot[0], m = (uint32_t)tot[1];
+    const uint64_t nbytes = tot[2];
     if (!nf) return IPXG_OK;
-    std::vector<PluginFlow>& flows = e->hw_flows;
-    flows.resize(nf);
-    if (!e->hw_sorted.resize(npk, e->walk_pin)) return set_err(e, IPXG_ENOMEM, "host walk buffers");
-    const uint64_t* sorted = e->hw_sorted.data();
-    HIPCHK(e, hipMemcpyAsync(flows.data(), e->pf_d.p, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->hw_sorted.data(), cx.sorted, (size_t)npk * 8, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(1);
-    // The walk takes the flows in order of their first packet (export order is arbitrary
-    // otherwise), and everything it reads is laid out in that order: the flow images permuted
-    // once here, then the packet list, the parsed packets and the frame bytes built from them --
-    // the walk streams through memory instead of a few dependent cache misses per flow.
-    // (LSD radix sort of {first index, flow} words on the 24-bit index: unique keys)
-    {
-        std::vector<uint64_t>& okey = e->hw_okey;
-        std::vector<uint64_t>& tmp = e->hw_okey2;
-        okey.resize(nf);
-        tmp.resize(nf);
-        for (uint32_t f = 0; f < nf; ++f) okey[f] = ((sorted[flows[f].seg] & 0xFFFFFFull) << 32) | f;
-        for (int pass = 0; pass < 3; ++pass) {
-            const int sh = 32 + 8 * pass;
-            uint32_t cnt[257] = {0};
-            for (uint32_t f = 0; f < nf; ++f) cnt[((okey[f] >> sh) & 0xFF) + 1]++;
-            for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
-            for (uint32_t f = 0; f < nf; ++f) tmp[cnt[(okey[f] >> sh) & 0xFF]++] = okey[f];
-            okey.swap(tmp);
-        }
-        std::vector<PluginFlow>& fo = e->hw_flows2;
-        fo.resize(nf);
-        for (uint32_t k = 0; k < nf; ++k) fo[k] = flows[(uint32_t)okey[k]];
-        flows.swap(fo);
-    }
-    WALK_MARK(4);
-    // the flows' packets, each flow's in arrival order (the sorted list: rank << 24 | index)
-    std::vector<uint32_t>& idx = e->hw_idx;
-    std::vector<uint32_t>& first = e->hw_first;
-    idx.clear();
-    first.resize(nf + 1);
-    {
-        size_t total = 0;
-        for (uint32_t f = 0; f < nf; ++f) total += flows[f].len;
-        idx.reserve(total);
-    }
-    for (uint32_t f = 0; f < nf; ++f) {
-        first[f] = (uint32_t)idx.size();
-        for (uint32_t k = 0; k < flows[f].len; ++k) idx.push_back((uint32_t)(sorted[flows[f].seg + k] & 0xFFFFFF));
-    }
-    first[nf] = (uint32_t)idx.size();
-    const uint32_t m = (uint32_t)idx.size();
-    if ((rc = ensure(e, e->pf_idx, (size_t)m * 4 + 4))) return rc;
     if ((rc = ensure(e, e->pf_parsed, (size_t)m * sizeof(ipxg_parsed_pkt) + 8))) return rc;
     if ((rc = ensure(e, e->pf_desc, (size_t)m * sizeof(ipxg_pkt_desc) + 16))) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->pf_idx.p, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice, e->st));
-    launch_plugin_pkts(e->st, bv, p, frag_view(e), (const uint32_t*)e->pf_idx.p, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
+    if ((rc = ensure(e, e->pf_bytes, nbytes + 16))) return rc;
+    launch_plugin_pkts(e->st, bv, p, frag_view(e), o.idx, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
                        (ipxg_pkt_desc*)e->pf_desc.p);
+    launch_plugin_bytes(e->st, bv, o.idx, o.off, m, (uint8_t*)e->pf_bytes.p);
     HIPCHK(e, hipGetLastError());
-    if (!e->hw_parsed.resize(m, e->walk_pin) || !e->hw_desc.resize(m, e->walk_pin))
+    const bool pin = e->walk_pin;
+    if (!e->hw_flows.resize(nf, pin) || !e->hw_first.resize(nf + 1, pin) || !e->hw_idx.resize(m, pin) ||
+        !e->hw_parsed.resize(m, pin) || !e->hw_desc.resize(m, pin) || !e->hw_off.resize((size_t)m + 1, pin) ||
+        !e->hw_bytes.resize(nbytes + 16, pin))
         return set_err(e, IPXG_ENOMEM, "host walk buffers");
+    PluginFlow* flows = e->hw_flows.data();
+    const uint32_t* first = e->hw_first.data();
+    const uint32_t* idx = e->hw_idx.data();
     ipxg_parsed_pkt* pk = e->hw_parsed.data();
     const ipxg_pkt_desc* de = e->hw_desc.data();
+    const uint64_t* off = e->hw_off.data();
+    const uint8_t* bytes = e->hw_bytes.data();
+    HIPCHK(e, hipMemcpyAsync(flows, o.flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_first.data(), o.first, ((size_t)nf + 1) * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_idx.data(), o.idx, (size_t)m * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_off.data(), o.off, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(2);
-    std::vector<uint64_t>& off = e->hw_off;
-    off.resize(m + 1);
-    off[0] = 0;
-    for (uint32_t k = 0; k < m; ++k) off[k + 1] = off[k] + de[k].caplen;
-    if ((rc = ensure(e, e->pf_off, (size_t)(m + 1) * 8))) return rc;
-    if ((rc = ensure(e, e->pf_bytes, off[m] + 16))) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->pf_off.p, off.data(), (size_t)(m + 1) * 8, hipMemcpyHostToDevice, e->st));
-    launch_plugin_bytes(e->st, bv, (const uint32_t*)e->pf_idx.p, (const uint64_t*)e->pf_off.p, m,
-                        (uint8_t*)e->pf_bytes.p);
-    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost,
+                             e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, nbytes, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
     e->tm.plugin_flows += nf;
     e->tm.plugin_packets += m;
-    e->tm.plugin_bytes += off[m];
+    e->tm.plugin_bytes += nbytes;
     for (uint32_t k = 0; k < m; ++k) e->tm.plugin_extra_bytes += de[k].caplen > 128 ? de[k].caplen - 128u : 0u;
-    if (!e->hw_bytes.resize(off[m] + 16, e->walk_pin)) return set_err(e, IPXG_ENOMEM, "host walk buffers");
-    const uint8_t* bytes = e->hw_bytes.data();
-    HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, off[m], hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(3);
+    WALK_MARK(1);
     // the walks, flows in order of their first packet (their order in `flows` now), split over
     // the walk threads in contiguous flow ranges of about equal packet counts
     const unsigned T = walk_pool(e, nf, m);
@@ -1298,14 +1275,14 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     std::vector<WalkOut> wos;
     wos.reserve(T);
     for (unsigned t = 0; t < T; ++t) {
-        e->hw_ex[t].clear();
-        wos.push_back(WalkOut{e->hw_ex[t]});
+        e->hw_ex[t].v.clear();
+        wos.push_back(WalkOut{e->hw_ex[t].v});
     }
     std::vector<int64_t> dlive(T, 0);
     auto walk_range = [&](unsigned t) {
         if (t >= T) return;  // (the pool may hold more threads than this walk uses)
         // flows [f0, f1): the first flows whose first packet is at or past t/T of the packets
-        const uint32_t* fb = first.data();
+        const uint32_t* fb = first;
         const uint32_t f0 = t ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * t / T)) - fb) : 0;
         const uint32_t f1 = t + 1 < T ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * (t + 1) / T)) - fb) : nf;
         WalkOut& wo = wos[t];
@@ -1352,32 +1329,33 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     };
     if (T > 1) e->pool->run(walk_range);
     else walk_range(0);
-    // the threads' exports, concatenated in thread order
+    // the threads' exports follow each other in thread order (copied to the device below)
     size_t nx = 0;
-    for (unsigned t = 0; t < T; ++t) nx += wos[t].ex.size();
-    if (T > 1) {
-        std::vector<ipxg_flow_record>& all = e->hw_ex[0];
-        all.reserve(nx);
-        for (unsigned t = 1; t < T; ++t) all.insert(all.end(), wos[t].ex.begin(), wos[t].ex.end());
-    }
     WalkOut& wo = wos[0];
+    for (unsigned t = 0; t < T; ++t) nx += wos[t].ex.size();
     for (unsigned t = 1; t < T; ++t) {
         for (int k = 0; k < 5; ++k) wo.end[k] += wos[t].end[k];
         for (int k = 0; k < 6; ++k) wo.pkts[k] += wos[t].pkts[k];
         wo.unreasoned += wos[t].unreasoned;
+        wo.v6 += wos[t].v6;
     }
     for (unsigned t = 0; t < T; ++t) *live_delta += dlive[t];
     WALK_MARK(5);
     // back to the device: the slots, then the exports after the batch's own
-    HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows.data(), (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
     launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf);
     HIPCHK(e, hipGetLastError());
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;
-        HIPCHK(e, hipMemcpyAsync(e->ex + e->ex_count, wo.ex.data(), nx * sizeof(ipxg_flow_record),
-                                 hipMemcpyHostToDevice, e->st));
-        uint32_t c3[3] = {e->ex_count + (uint32_t)nx, 0, e->ex_count6};
-        for (const ipxg_flow_record& r : wo.ex) c3[2] += r.ip_version == 6 ? 1 : 0;
+        size_t at = e->ex_count;
+        for (unsigned t = 0; t < T; ++t) {
+            const std::vector<ipxg_flow_record>& x = wos[t].ex;
+            if (x.empty()) continue;
+            HIPCHK(e, hipMemcpyAsync(e->ex + at, x.data(), x.size() * sizeof(ipxg_flow_record), hipMemcpyHostToDevice,
+                                     e->st));
+            at += x.size();
+        }
+        uint32_t c3[3] = {e->ex_count + (uint32_t)nx, 0, e->ex_count6 + (uint32_t)wo.v6};
         HIPCHK(e, hipMemcpyAsync(e->ex_count_d, c3, sizeof(c3), hipMemcpyHostToDevice, e->st));
         e->ex_zero_pending = false;  // all three counters written
         e->ex_count = c3[0];

@@ -262,7 +262,20 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
                      bool finishing, bool deferred_only = false);
 void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
                      uint32_t nrules, BatchCtl* ctl);
-void launch_plugin_pack(hipStream_t st, TableView t, ComplexView cx, uint32_t ncx, PluginFlow* out, uint32_t* count);
+// The host walk's inputs on the device, flows in order of their first packet (ipxg_bridge.hip):
+// keys / skeys [ncx], flows [ncx], flen / first [ncx + 1], idx [npk], clen / off [npk + 1],
+// count (zeroed by the caller), tot [3] = {flows, packets, bytes}
+struct PluginOrder {
+    uint64_t *keys, *skeys;
+    PluginFlow* flows;
+    uint32_t *flen, *first, *idx, *count;
+    uint64_t *clen, *off, *tot;
+    void* temp;
+    size_t temp_bytes;
+};
+void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, ComplexView cx, uint32_t ncx, uint32_t npk,
+                         const PluginOrder& o);
+size_t plugin_order_temp(uint32_t ncx, uint32_t npk);
 void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
                         uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout);
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
@@ -319,6 +332,8 @@ void launch_xxh64(hipStream_t st, const uint8_t* keys, uint32_t keylen, uint32_t
 // rocPRIM radix sort of 64-bit keys (slow paths only).  temp may be null to query size.
 hipError_t sort_pairs_u32(void* temp, size_t& temp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
                           uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
+hipError_t exclusive_scan_u64(void* temp, size_t& temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
+                              hipStream_t st);
 hipError_t exclusive_scan_u32(void* temp, size_t& temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
                               hipStream_t st);
 void launch_strict_prep1(hipStream_t st, const BatchView& b, const Params& p, FragView f, BatchCtl* ctl,

@@ -29,4 +29,10 @@ hipError_t exclusive_scan_u32(void* temp, size_t& temp_bytes, const uint32_t* in
     return rocprim::exclusive_scan(temp, temp_bytes, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), st);
 }
 
+// process-plugin bridge: byte offsets of the walked packets' frames
+hipError_t exclusive_scan_u64(void* temp, size_t& temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
+                              hipStream_t st) {
+    return rocprim::exclusive_scan(temp, temp_bytes, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), st);
+}
+
 }  // namespace ipxg
