@@ -18,6 +18,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -60,27 +61,41 @@ struct HostVec {
         n = cap = 0;
         reg = false;
     }
+    // capacity for k elements; keep: the first n survive a reallocation
+    bool reserve(size_t k, bool pin, bool keep = false) {
+        if (k <= cap) return true;
+        const size_t want = std::max(k, cap + cap / 2 + 1024);
+        const size_t bytes = (want * sizeof(T) + 4095) & ~(size_t)4095;
+        void* q = nullptr;
+        if (posix_memalign(&q, 4096, bytes)) return false;
+        const size_t kept = keep ? n : 0;
+        if (kept) std::memcpy(q, p, kept * sizeof(T));
+        release();
+        p = static_cast<T*>(q);
+        cap = bytes / sizeof(T);
+        n = kept;
+        reg = pin && hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
+        return true;
+    }
     bool resize(size_t k, bool pin) {
-        if (k > cap) {
-            const size_t want = std::max(k, cap + cap / 2 + 1024);
-            const size_t bytes = (want * sizeof(T) + 4095) & ~(size_t)4095;
-            release();
-            void* q = nullptr;
-            if (posix_memalign(&q, 4096, bytes)) return false;
-            p = static_cast<T*>(q);
-            cap = bytes / sizeof(T);
-            reg = pin && hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
-        }
+        if (!reserve(k, pin)) return false;
         n = k;
         return true;
     }
+    void push_back(const T& v) {  // (grows page-locked; std::bad_alloc when the host is out of memory)
+        if (n == cap && !reserve(n + 1, reg || !p, true)) throw std::bad_alloc();
+        p[n++] = v;
+    }
+    void clear() { n = 0; }
+    bool empty() const { return n == 0; }
     T* data() { return p; }
+    const T* data() const { return p; }
     size_t size() const { return n; }
 };
 
 // A walk thread's exports, on a cache line of its own (the threads append concurrently).
 struct alignas(128) ExportVec {
-    std::vector<ipxg_flow_record> v;
+    HostVec<ipxg_flow_record> v;  // page-locked: copied to the device's export buffer directly
 };
 
 // The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
@@ -195,7 +210,8 @@ struct ipxg_engine {
     uint32_t walk_threads = 0;
     bool walked = false;  // a plugin walk has called hooks (plugin instances no longer pristine)
     WalkPool* pool = nullptr;
-    std::vector<ExportVec> hw_ex;                        // [t]
+    std::vector<std::unique_ptr<ExportVec>> hw_ex;       // [t]
+    std::vector<hipEvent_t> walk_ev;                     // [t]: thread t's share copied
     std::vector<std::vector<uint64_t>> host_ports;      // [t]
     std::vector<std::vector<ipxg_plugin>> walk_pl;      // [t - 1]: thread t's plugin instances
     // staging for host batches
@@ -632,6 +648,7 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
     free_walk_copies(e);
+    for (hipEvent_t ev : e->walk_ev) hipEventDestroy(ev);
     hipFree(e->hot);
     hipFree(e->cold);
     hipFree(e->slot_rank);
@@ -936,7 +953,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 namespace {
 
 struct alignas(128) WalkOut {  // one per walk thread, on cache lines of its own
-    std::vector<ipxg_flow_record>& ex;  // exported records, in order
+    HostVec<ipxg_flow_record>& ex;  // exported records, in order
     uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
     uint64_t pkts[6] = {0, 0, 0, 0, 0, 0};  // FlowRecordStats buckets
     uint64_t unreasoned = 0;  // export_flow with end_reason 0 (post_create FLUSH of a new record)
@@ -1251,42 +1268,73 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const ipxg_pkt_desc* de = e->hw_desc.data();
     const uint64_t* off = e->hw_off.data();
     const uint8_t* bytes = e->hw_bytes.data();
-    HIPCHK(e, hipMemcpyAsync(flows, o.flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
+    // first and off come over first (they split the walk); then each walk thread's share of the
+    // rest -- its flows, packets and frame bytes, contiguous in flow order -- in thread order,
+    // each behind an event its thread waits for: the walks of the first ranges overlap the copies
+    // of the later ones
     HIPCHK(e, hipMemcpyAsync(e->hw_first.data(), o.first, ((size_t)nf + 1) * 4, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->hw_idx.data(), o.idx, (size_t)m * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_off.data(), o.off, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost,
-                             e->st));
-    HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, nbytes, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->tm.plugin_flows += nf;
     e->tm.plugin_packets += m;
     e->tm.plugin_bytes += nbytes;
-    for (uint32_t k = 0; k < m; ++k) e->tm.plugin_extra_bytes += de[k].caplen > 128 ? de[k].caplen - 128u : 0u;
-    WALK_MARK(1);
-    // the walks, flows in order of their first packet (their order in `flows` now), split over
-    // the walk threads in contiguous flow ranges of about equal packet counts
+    for (uint32_t k = 0; k < m; ++k) {
+        const uint64_t cl = off[k + 1] - off[k];
+        e->tm.plugin_extra_bytes += cl > 128 ? cl - 128 : 0;
+    }
+    // the walk threads: contiguous flow ranges of about equal packet counts (flows in order of
+    // their first packet)
     const unsigned T = walk_pool(e, nf, m);
     e->walked = true;
-    if (e->hw_ex.size() < T) e->hw_ex.resize(T);
+    std::vector<uint32_t> fr(T + 1);
+    for (unsigned t = 0; t <= T; ++t)
+        fr[t] = t == 0 ? 0 : t == T ? nf
+                       : (uint32_t)(std::lower_bound(first, first + nf, (uint32_t)((uint64_t)m * t / T)) - first);
+    while (e->walk_ev.size() < T) {
+        hipEvent_t ev;
+        HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        e->walk_ev.push_back(ev);
+    }
+    for (unsigned t = 0; t < T; ++t) {
+        const uint32_t f0 = fr[t], f1 = fr[t + 1], a = first[f0], b = first[f1];
+        if (f1 > f0)
+            HIPCHK(e, hipMemcpyAsync(flows + f0, o.flows + f0, (size_t)(f1 - f0) * sizeof(PluginFlow),
+                                     hipMemcpyDeviceToHost, e->st));
+        if (b > a) {
+            HIPCHK(e, hipMemcpyAsync(e->hw_idx.data() + a, o.idx + a, (size_t)(b - a) * 4, hipMemcpyDeviceToHost, e->st));
+            HIPCHK(e, hipMemcpyAsync(pk + a, (ipxg_parsed_pkt*)e->pf_parsed.p + a, (size_t)(b - a) * sizeof(ipxg_parsed_pkt),
+                                     hipMemcpyDeviceToHost, e->st));
+            HIPCHK(e, hipMemcpyAsync(e->hw_desc.data() + a, (ipxg_pkt_desc*)e->pf_desc.p + a,
+                                     (size_t)(b - a) * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
+            if (off[b] > off[a])
+                HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data() + off[a], (uint8_t*)e->pf_bytes.p + off[a], off[b] - off[a],
+                                         hipMemcpyDeviceToHost, e->st));
+        }
+        HIPCHK(e, hipEventRecord(e->walk_ev[t], e->st));
+    }
+    WALK_MARK(1);
+    if (e->hw_ex.size() < T)
+        while (e->hw_ex.size() < T) e->hw_ex.emplace_back(new ExportVec);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.size() < T) e->host_ports.resize(T);
     std::vector<WalkOut> wos;
     wos.reserve(T);
     for (unsigned t = 0; t < T; ++t) {
-        e->hw_ex[t].v.clear();
-        wos.push_back(WalkOut{e->hw_ex[t].v});
+        e->hw_ex[t]->v.clear();
+        wos.push_back(WalkOut{e->hw_ex[t]->v});
     }
     std::vector<int64_t> dlive(T, 0);
+    std::vector<int> wfail(T, 0);
     auto walk_range = [&](unsigned t) {
         if (t >= T) return;  // (the pool may hold more threads than this walk uses)
-        // flows [f0, f1): the first flows whose first packet is at or past t/T of the packets
-        const uint32_t* fb = first;
-        const uint32_t f0 = t ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * t / T)) - fb) : 0;
-        const uint32_t f1 = t + 1 < T ? (uint32_t)(std::lower_bound(fb, fb + nf, (uint32_t)((uint64_t)m * (t + 1) / T)) - fb) : nf;
+        const uint32_t f0 = fr[t], f1 = fr[t + 1];
         WalkOut& wo = wos[t];
-        wo.ex.reserve((size_t)(first[f1] - first[f0]) + 16);
+        if (hipEventSynchronize(e->walk_ev[t]) != hipSuccess ||
+            !wo.ex.reserve((size_t)(first[f1] - first[f0]) + 16, e->walk_pin)) {
+            wfail[t] = 1;
+            return;
+        }
+        try {
         const std::vector<ipxg_plugin>& pl = t ? e->walk_pl[t - 1] : e->plugins;
         uint64_t* pa = nullptr;
         if (ports) {
@@ -1326,9 +1374,17 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             }
         }
         dlive[t] = dl;
+        } catch (const std::bad_alloc&) {
+            wfail[t] = 2;
+        }
     };
     if (T > 1) e->pool->run(walk_range);
     else walk_range(0);
+    for (unsigned t = 0; t < T; ++t)
+        if (wfail[t]) {
+            (void)hipStreamSynchronize(e->st);
+            return set_err(e, wfail[t] == 1 ? IPXG_EDEVICE : IPXG_ENOMEM, "plugin walk: copies or export buffer");
+        }
     // the threads' exports follow each other in thread order (copied to the device below)
     size_t nx = 0;
     WalkOut& wo = wos[0];
@@ -1349,7 +1405,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         if ((rc = ensure_export(e, nx))) return rc;
         size_t at = e->ex_count;
         for (unsigned t = 0; t < T; ++t) {
-            const std::vector<ipxg_flow_record>& x = wos[t].ex;
+            const HostVec<ipxg_flow_record>& x = wos[t].ex;
             if (x.empty()) continue;
             HIPCHK(e, hipMemcpyAsync(e->ex + at, x.data(), x.size() * sizeof(ipxg_flow_record), hipMemcpyHostToDevice,
                                      e->st));
