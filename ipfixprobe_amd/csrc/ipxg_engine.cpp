@@ -1292,7 +1292,9 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
                        : (uint32_t)(std::lower_bound(first, first + nf, (uint32_t)((uint64_t)m * t / T)) - first);
     while (e->walk_ev.size() < T) {
         hipEvent_t ev;
-        HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        // (IPXG_WALK_SPIN: the waits poll instead of sleeping on the completion signal -- A/B)
+        const unsigned fl = hipEventDisableTiming | (std::getenv("IPXG_WALK_SPIN") ? 0u : (unsigned)hipEventBlockingSync);
+        HIPCHK(e, hipEventCreateWithFlags(&ev, fl));
         e->walk_ev.push_back(ev);
     }
     for (unsigned t = 0; t < T; ++t) {

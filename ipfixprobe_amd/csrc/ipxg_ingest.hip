@@ -1486,4 +1486,66 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
                        stats, finishing ? 1u : 0u, deferred_only ? 1u : 0u);
 }
 
+// ---- complex flows: their packets ----------------------------------------------------------
+// Every packet of the batch is parsed again to find the complex flows' packets (k_complex_rank
+// has put their keys in cx.keys) and listed in its flow's segment.  Frames of the shapes k_bin's
+// wide walk takes go through the same register parser (80-byte head by buffer loads); the rest
+// through the general parser -- the gather used to parse every frame with the general LDS
+// parser, twice k_bin's time per batch on the configs[2] mix with its plugins registered.
+__global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Params p, FragView f, ComplexView cx) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    uint32_t* col = &win[threadIdx.x];
+    const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
+        const ipxg_pkt_desc d = load_desc(rs_desc, i);
+        DevPkt pk;
+        ParseCounts c = {};
+        bool ok = false;
+        const bool reg = eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim;
+        if (reg) {
+            const Head<5> h = load_head<5>(rs_arena, d, true);
+            uint32_t w[WIDE_DW];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                w[4 * k] = h.c[k].x;
+                w[4 * k + 1] = h.c[k].y;
+                w[4 * k + 2] = h.c[k].z;
+                w[4 * k + 3] = h.c[k].w;
+            }
+            bool ext = false;
+            ok = parse_medium(w, d.caplen, p.frag_enable, pk, c, ext);
+        }
+        if (!ok) {
+            DevPkt q;
+            stage_frame(col, b.arena, d.offset, d.caplen);
+            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+            if (!parse_frame<false>(S, d.caplen, p.dlt, q, c)) continue;
+            pk = q;
+        }
+        if (pk.ip_version != 4 && pk.ip_version != 6) continue;
+        if (p.frag_enable && (pk.frag_off || pk.more_fragments)) apply_frag_ports(p, f, i, pk);
+        uint64_t lo, hf;
+        uint32_t cdir;
+        canon(pk, p, lo, cdir, hf);
+        const int64_t rr = complex_rank_of(cx, lo);
+        if (rr >= 0) {
+            const uint32_t r = (uint32_t)rr;
+            const uint32_t pos = atomicAdd(&cx.cursor[r], 1u);
+            cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
+        }
+    }
+}
+
+void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                           ComplexView cx) {
+    (void)t;
+    uint32_t g = (b.n + IPXG_BLOCK - 1) / IPXG_BLOCK;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_complex_gather, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, f, cx);
+}
+
 }  // namespace ipxg

@@ -31,15 +31,6 @@ __device__ __forceinline__ bool flow_accumulate(const TableView& t, const Params
 // ---- K1: ingest ------------------------------------------------------------------------
 enum IngestMode { MODE_INGEST = 0, MODE_GATHER = 1 };
 
-// rank of the complex flow with canonical key lo, or -1
-__device__ __forceinline__ int64_t complex_rank_of(const ComplexView& cx, uint64_t lo) {
-    for (uint32_t e = (uint32_t)lo & cx.kmask;; e = (e + 1) & cx.kmask) {
-        const unsigned long long k = cx.keys[e];
-        if (k == lo) return cx.key_rank[e];
-        if (k == 0ull) return -1;
-    }
-}
-
 template <int MODE>
 __global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, TableView t, FragView f,
                                                        BatchCtl* ctl, uint32_t* deferred_list,
@@ -130,11 +121,6 @@ void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableVie
                        t, f, ctl, deferred_list, stats, cx);
 }
 
-void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t,
-                           FragView f, ComplexView cx) {
-    hipLaunchKernelGGL(k_ingest<MODE_GATHER>, dim3(grid_for(b.n, 1024)), dim3(IPXG_BLOCK), 0, st, b, p,
-                       t, f, nullptr, nullptr, nullptr, cx);
-}
 
 // ---- fragmentation cache -----------------------------------------------------------------
 __device__ __forceinline__ void frag_words(const DevPkt& pk, uint64_t w[5]) {
@@ -343,13 +329,38 @@ void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableV
 }
 
 // ---- complex flows: sequential replay of put_pkt_recursive ------------------------------
+// Each complex flow gets a rank and a segment of its packet count: one returning atomic per wave
+// on the {ranks, packets} counter (a returning atomic per lane on that one word serialised the
+// configs[2] plugin batches' ~10^5 complex flows), the lanes' offsets by a wave prefix sum.
 __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView cx, BatchCtl* ctl,
                                                       uint32_t cap) {
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const HotSlot& h = t.hot[s];
-        if (h.key == 0 || !(h.state & SLOT_COMPLEX)) continue;
-        const uint32_t npk = (uint32_t)(h.acc[0] >> 40) + (uint32_t)(h.acc[1] >> 40);
-        unsigned long long old = atomicAdd((unsigned long long*)&ctl->cx_alloc, (1ull << 32) | npk);
+    const uint32_t lane = lane_id();
+    for (uint32_t base = blockIdx.x * blockDim.x; base < cap; base += gridDim.x * blockDim.x) {  // wave-uniform
+        const uint32_t s = base + threadIdx.x;
+        bool cxf = false;
+        HotSlot h;
+        if (s < cap) {
+            h = t.hot[s];
+            cxf = h.key != 0 && (h.state & SLOT_COMPLEX);
+        }
+        const uint64_t m = __ballot(cxf);
+        if (m == 0) continue;
+        const uint32_t npk = cxf ? (uint32_t)(h.acc[0] >> 40) + (uint32_t)(h.acc[1] >> 40) : 0u;
+        uint32_t x = npk;  // inclusive wave scan of the packet counts
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= (uint32_t)d) x += y;
+        }
+        const uint32_t tot = __shfl(x, 63);
+        const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+        unsigned long long old0 = 0;
+        if (lane == leader)
+            old0 = atomicAdd((unsigned long long*)&ctl->cx_alloc, ((unsigned long long)__popcll(m) << 32) | tot);
+        old0 = __shfl(old0, (int)leader);
+        if (!cxf) continue;
+        const uint64_t below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+        const unsigned long long old = old0 + ((unsigned long long)__popcll(below) << 32) + (x - npk);
         const uint32_t r = (uint32_t)(old >> 32);
         t.slot_rank[s] = r;
         cx.slot_of[r] = s;

@@ -13,6 +13,15 @@ namespace ipxg {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// rank of the complex flow with canonical key lo, or -1
+__device__ __forceinline__ int64_t complex_rank_of(const ComplexView& cx, uint64_t lo) {
+    for (uint32_t e = (uint32_t)lo & cx.kmask;; e = (e + 1) & cx.kmask) {
+        const unsigned long long k = cx.keys[e];
+        if (k == lo) return cx.key_rank[e];
+        if (k == 0ull) return -1;
+    }
+}
+
 // Wave-aggregated append: one atomic per wave instead of one per lane.  Every lane of the
 // wave must call it (convergent).
 __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
