@@ -20,9 +20,9 @@
 
 namespace ipxg {
 
-// Does the parsed packet match rule r?  Its frame is staged in S (LDS window + global).
-template <class S>
-__device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, const S& s) {
+// Does the parsed packet match rule r?  pay(k): byte k of its payload (k < 16, within payload_len).
+template <class B>
+__device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, const B& pay) {
     const bool tcp = pk.l4 == 6, udp = pk.l4 == 17;
     if (!((tcp && (r.proto_mask & 1)) || (udp && (r.proto_mask & 2)))) return false;
     for (uint32_t k = 0; k < r.n_ports; ++k)
@@ -33,28 +33,83 @@ __device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, c
         const bool msk = (r.masked >> q) & 1u;
         bool eq = true;
         for (uint32_t k = 0; k < n && eq; ++k)
-            eq = ((s.b(pk.payload_off + k) ^ r.prefix[q][k]) & (msk ? r.prefix_mask[q][k] : 0xFFu)) == 0;
+            eq = ((pay(k) ^ r.prefix[q][k]) & (msk ? r.prefix_mask[q][k] : 0xFFu)) == 0;
         if (eq) return true;
     }
     return false;
 }
 
+typedef uint32_t bridge_u32x4 __attribute__((ext_vector_type(4)));
+
+// The 16 payload bytes at byte p of a frame at a 16-byte aligned offset o (two aligned 16-byte
+// buffer loads, re-based by p & 15; zeros past the arena)
+__device__ __forceinline__ uint4 payload16(__amdgpu_buffer_rsrc_t arena, uint32_t o, uint32_t p) {
+    const uint32_t a = o + (p & ~15u);
+    const bridge_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(arena, a, 0, 0);
+    const bridge_u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(arena, a + 16u, 0, 0);
+    const uint32_t d[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    const uint32_t q = (p >> 2) & 3u, sh = p & 3u;
+    uint32_t o4[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)  // dwords q .. q + 4 (selects: no dynamic register index)
+        o4[j] = q == 0 ? d[j] : q == 1 ? d[j + 1] : q == 2 ? d[j + 2] : d[j + 3];
+    uint4 r;
+    r.x = __builtin_amdgcn_alignbyte(o4[1], o4[0], sh);
+    r.y = __builtin_amdgcn_alignbyte(o4[2], o4[1], sh);
+    r.z = __builtin_amdgcn_alignbyte(o4[3], o4[2], sh);
+    r.w = __builtin_amdgcn_alignbyte(o4[4], o4[3], sh);
+    return r;
+}
+
+// Pre-classification of every packet against the plugins' rules.  Frames of the shapes k_bin's
+// wide walk takes are parsed from an 80-byte register window (and their payload's first 16 bytes
+// loaded for the prefix rules); the others by the general parser in LDS -- which parsed every
+// frame before: 0.9 ms per 10M-packet batch of the configs[2] mix, more than k_bin.
 __global__ __launch_bounds__(IPXG_BLOCK) void k_classify(BatchView b, Params p, TableView t, const DevRule* rules,
                                                          uint32_t nrules, BatchCtl* ctl) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     uint32_t* col = &win[threadIdx.x];
+    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
     uint32_t claimed_n = 0;
     for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
         const ipxg_pkt_desc d = b.desc[i];
-        stage_frame(col, b.arena, d.offset, d.caplen);
-        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
         DevPkt pk;
         ParseCounts dummy = {};
-        if (!parse_frame<true>(S, d.caplen, p.dlt, pk, dummy)) continue;
-        if (pk.ip_version != 4 && pk.ip_version != 6) continue;
-        if (pk.frag_off) continue;  // no L4 header (its ports come from the fragmentation cache)
-        bool hit = false;
-        for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, S);
+        bool reg = false, hit = false;
+        if (eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim) {
+            uint32_t w[WIDE_DW];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const bridge_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_arena, d.offset + 16u * k, 0, 0);
+                w[4 * k] = x.x;
+                w[4 * k + 1] = x.y;
+                w[4 * k + 2] = x.z;
+                w[4 * k + 3] = x.w;
+            }
+            bool ext = false;
+            reg = parse_medium<true>(w, d.caplen, p.frag_enable, pk, dummy, ext);
+            if (reg && (pk.l4 == 6 || pk.l4 == 17)) {
+                const uint4 pw = payload16(rs_arena, d.offset, pk.payload_off);
+                const uint32_t pd[4] = {pw.x, pw.y, pw.z, pw.w};
+                auto pay = [&](uint32_t k) {  // (bytes at or past caplen read as 0, as in the LDS walk)
+                    const uint32_t dw = k >> 2;
+                    const uint32_t v = dw == 0 ? pd[0] : dw == 1 ? pd[1] : dw == 2 ? pd[2] : pd[3];
+                    return (uint32_t)pk.payload_off + k < d.caplen ? (v >> (8 * (k & 3))) & 0xFFu : 0u;
+                };
+                for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, pay);
+            }
+        }
+        if (!reg) {
+            stage_frame(col, b.arena, d.offset, d.caplen);
+            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+            if (!parse_frame<true>(S, d.caplen, p.dlt, pk, dummy)) continue;
+            if (pk.ip_version != 4 && pk.ip_version != 6) continue;
+            if (pk.frag_off) continue;  // no L4 header (its ports come from the fragmentation cache)
+            auto pay = [&](uint32_t k) { return S.b(pk.payload_off + k); };
+            for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, pay);
+        }
         if (!hit) continue;
         uint64_t lo, hf;
         uint32_t cdir;

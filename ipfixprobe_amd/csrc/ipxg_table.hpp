@@ -640,6 +640,9 @@ __device__ __forceinline__ uint32_t wb8(const uint32_t* w) { return (w[O / 4] >>
 template <int O>
 __device__ __forceinline__ uint32_t wbe16(const uint32_t* w) { return bswap16(wle32<O>(w)); }
 
+// PAY: also Packet::payload / payload_len as parse_frame<true> gives them (parser.cpp:780-797;
+// the pre-classifier of the plugin bridge compares payload prefixes)
+template <bool PAY = false>
 __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint32_t caplen, bool frag_enable,
                                              DevPkt& p, ParseCounts& c, bool& ext) {
     // Ethernet + tags (parse_eth_hdr): only the outermost tag's VLAN id is kept
@@ -758,12 +761,13 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
         o4 = o3 + 40 + 8 * xh;
     }
     const bool v6 = l3 == ETH_P_IPV6;
-    uint32_t ports = 0, flags = 0;
+    uint32_t ports = 0, flags = 0, l4h = 0;
     bool tcp_opt = false;
     if (frag_off == 0 && proto == 6) {
         if (caplen < o4 + 20 || gopt > 1) return false;  // (past the window)
         const uint32_t w3 = v6 ? (xh ? wle32<74>(w) : wle32<66>(v)) : wle32<46>(v);  // L4 bytes 12..15
         const uint32_t doff = (w3 & 0xFF) >> 4;
+        l4h = 4 * doff;
         if (doff > 5) {
             if (gre || (v6 && (S != 0 || xh))) return false;  // the options would end past the window
             const uint32_t opt = v6 ? wle32<74>(w) : wle32<54>(v);  // L4 bytes 20..23
@@ -775,6 +779,17 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     } else if (frag_off == 0 && proto == 17) {
         if (caplen < o4 + 8) return false;
         ports = v6 ? (xh == 2 ? wle32<70>(w) : (xh ? wle32<62>(w) : wle32<54>(v))) : wle32<34>(v);
+        l4h = 8;
+    }
+    if constexpr (PAY) {  // parser.cpp:780-797 in its uint16_t arithmetic (l4 offset o4 != l3 offset)
+        const uint32_t ipl = v6 ? ((uint32_t)p.ip_len - 40u - 8u * xh) & 0xFFFF : ((uint32_t)p.ip_len - 20u) & 0xFFFF;
+        const uint32_t off = o4 + l4h;
+        uint32_t pkt_len = caplen;
+        if (o4 + ipl < 64) pkt_len = (o4 + ipl) & 0xFFFF;
+        uint32_t plen = (ipl - l4h) & 0xFFFF;
+        if (plen + off > pkt_len) plen = (pkt_len - off) & 0xFFFF;
+        p.payload_off = (uint16_t)off;
+        p.payload_len = (uint16_t)plen;
     }
     p.ip_proto = (uint8_t)proto;
     p.tcp_flags = (uint8_t)flags;

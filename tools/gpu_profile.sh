@@ -15,6 +15,9 @@ for W in ${WORKLOADS:-udp64 imix quic}; do
     stream) ARGS="--mode stream --steps 20 --warmup 3" ;;
     imix) ARGS="--workload imix --steps 3 --warmup 1" ;;
     quic) ARGS="--workload quic --steps 5 --warmup 1" ;;
+    imix_plugins) ARGS="--workload imix --plugins dns,http,tls --steps 2 --warmup 1" ;;
+    quic_plugins) ARGS="--workload quic --plugins quic --steps 3 --warmup 1" ;;
+    imix10m) ARGS="--workload imix10m --shard 0/8 --steps 2 --warmup 1" ;;
   esac
   echo "== kernel trace $W"; date
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$W -o run -- \
