@@ -274,16 +274,20 @@ void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx
 
 // The host walk's result for flow k: its slot (state LIVE with the record -- and FOLLOW while a
 // plugin follows every packet of it --, or empty of records).
-__global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginFlow* in, uint32_t n) {
+__global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginFlow* in, uint32_t n, BatchCtl* ctl) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
     const PluginFlow f = in[k];
+    if (f.slot > t.mask) {  // (guard: never, unless the host handed back a corrupt image)
+        atomicOr(&ctl->guard, 4u);
+        return;
+    }
     if (f.state & SLOT_LIVE) t.cold[f.slot] = f.rec;
     clear_slot(&t.hot[f.slot], f.key, f.state & (SLOT_LIVE | SLOT_FOLLOW));
 }
 
-void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n) {
-    hipLaunchKernelGGL(k_plugin_apply, dim3((n + 255) / 256), dim3(256), 0, st, t, in, n);
+void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n, BatchCtl* ctl) {
+    hipLaunchKernelGGL(k_plugin_apply, dim3((n + 255) / 256), dim3(256), 0, st, t, in, n, ctl);
 }
 
 }  // namespace ipxg

@@ -1401,7 +1401,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     WALK_MARK(5);
     // back to the device: the slots, then the exports after the batch's own
     HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
-    launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf);
+    launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf, e->ctl_d);
     HIPCHK(e, hipGetLastError());
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;
@@ -1570,17 +1570,17 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         HIPCHK(e, hipMemsetAsync(ck, 0, (size_t)kcap * 8, e->st));
         ComplexView cx = {nullptr, nullptr, cr, cr + ncx, cr + 2 * (size_t)ncx, cr + 3 * (size_t)ncx,
                           ck, reinterpret_cast<uint32_t*>(ck + kcap), kcap - 1};
-        launch_complex_rank(e->st, table_view(e), cx, e->ctl_d, e->cap);
+        launch_complex_rank(e->st, table_view(e), cx, e->ctl_d, e->cap, ncx);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
-        if ((uint32_t)(e->ctl_h->cx_alloc >> 32) != ncx)
+        if ((uint32_t)(e->ctl_h->cx_alloc >> 32) != ncx || e->ctl_h->guard)
             return set_err(e, IPXG_EDEVICE, "complex-flow count mismatch (engine bug)");
         const uint32_t npk = (uint32_t)(e->ctl_h->cx_alloc & 0xFFFFFFFFu);
         if ((rc = ensure(e, e->cx_list, (size_t)npk * 8 + 8))) return rc;
         if ((rc = ensure(e, e->cx_sorted, (size_t)npk * 8 + 8))) return rc;
         cx.list = (uint64_t*)e->cx_list.p;
         cx.sorted = (uint64_t*)e->cx_sorted.p;
-        launch_complex_gather(e->st, bv, p, table_view(e), frag_view(e), cx);
+        launch_complex_gather(e->st, bv, p, table_view(e), frag_view(e), cx, e->ctl_d);
         HIPCHK(e, hipGetLastError());
         int bits = 24;
         while ((1ull << (bits - 24)) < ncx) bits++;
@@ -1594,10 +1594,13 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ev_rec(e, 6);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
+        if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "a complex flow's packets overran its segment (engine bug)");
         if (!e->plugins.empty()) {  // the process plugins' flows: walked on the host
             int64_t dl = 0;
             if ((rc = plugin_walk(e, bv, p, cx, ncx, npk, &dl))) return rc;
             plugin_live += dl;
+            if ((rc = sync_ctl(e))) return rc;
+            if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
         }
         if (e->prof && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);

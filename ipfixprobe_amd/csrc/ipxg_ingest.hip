@@ -1492,7 +1492,8 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
 // wide walk takes go through the same register parser (80-byte head by buffer loads); the rest
 // through the general parser -- the gather used to parse every frame with the general LDS
 // parser, twice k_bin's time per batch on the configs[2] mix with its plugins registered.
-__global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Params p, FragView f, ComplexView cx) {
+__global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Params p, FragView f, ComplexView cx,
+                                                               BatchCtl* ctl) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     uint32_t* col = &win[threadIdx.x];
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
@@ -1535,17 +1536,18 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Para
         if (rr >= 0) {
             const uint32_t r = (uint32_t)rr;
             const uint32_t pos = atomicAdd(&cx.cursor[r], 1u);
-            cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
+            if (pos < cx.len[r]) cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
+            else atomicOr(&ctl->guard, 2u);  // more packets than the flow's slot counted (guard)
         }
     }
 }
 
 void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
-                           ComplexView cx) {
+                           ComplexView cx, BatchCtl* ctl) {
     (void)t;
     uint32_t g = (b.n + IPXG_BLOCK - 1) / IPXG_BLOCK;
     if (g > 2048) g = 2048;
-    hipLaunchKernelGGL(k_complex_gather, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, f, cx);
+    hipLaunchKernelGGL(k_complex_gather, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, f, cx, ctl);
 }
 
 }  // namespace ipxg

@@ -336,7 +336,7 @@ void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableV
 // the configs[2] mix with its plugins, 0.37 ms per batch at one atomic per wave).
 constexpr uint32_t CXR_SPAN = 4096;  // slots per workgroup (LDS list: 8 bytes per entry)
 __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap,
-                                                      uint32_t span) {
+                                                      uint32_t span, uint32_t ncx) {
     __shared__ uint32_t l_slot[CXR_SPAN], l_npk[CXR_SPAN];
     __shared__ uint32_t l_n, scan_s[256 / 64 + 1];
     __shared__ unsigned long long l_base;
@@ -365,6 +365,10 @@ __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView c
     if (tid == 0) l_base = atomicAdd((unsigned long long*)&ctl->cx_alloc, ((unsigned long long)n << 32) | tot);
     __syncthreads();
     const uint32_t r0 = (uint32_t)(l_base >> 32), p0 = (uint32_t)l_base;
+    if (r0 + n > ncx) {  // more complex slots than the finalisers counted (guard; the host reports it)
+        if (tid == 0) atomicOr(&ctl->guard, 1u);
+        return;
+    }
     for (uint32_t k = k0; k < k1; ++k) {
         const uint32_t sl = l_slot[k], npk = l_npk[k], r = r0 + k;
         t.slot_rank[sl] = r;
@@ -380,12 +384,12 @@ __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView c
     }
 }
 
-void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap) {
+void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap, uint32_t ncx) {
     // at least 2048 workgroups, at most CXR_SPAN slots each
     uint32_t g = std::max<uint32_t>(std::min<uint32_t>(2048, (cap + 255) / 256), (cap + CXR_SPAN - 1) / CXR_SPAN);
     const uint32_t span = ((cap + g - 1) / g + 255) & ~255u;
     g = (cap + span - 1) / span;
-    hipLaunchKernelGGL(k_complex_rank, dim3(g ? g : 1), dim3(256), 0, st, t, cx, ctl, cap, span);
+    hipLaunchKernelGGL(k_complex_rank, dim3(g ? g : 1), dim3(256), 0, st, t, cx, ctl, cap, span, ncx);
 }
 
 __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, TableView t, FragView f,

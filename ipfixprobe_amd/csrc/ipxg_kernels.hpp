@@ -66,6 +66,9 @@ struct BatchCtl {
     uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
     uint32_t tb_any;         // OR of the time buckets of k_bin / k_bin_slow's records (0: all in bucket 0)
     uint32_t fin_deferred;   // finalise-list aggregates whose table probe failed (k_fin_list: table full)
+    uint32_t guard;          // bounds guards that fired (engine bug, reported as IPXG_EDEVICE): 1 more complex
+                             // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
+                             // past the table
     uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -280,7 +283,7 @@ void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, Fra
                         uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout);
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
                          uint8_t* out);
-void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n);
+void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n, BatchCtl* ctl);
 void launch_pstats(hipStream_t st, const BatchView& b, const Params& p, unsigned long long* pstat);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
@@ -294,9 +297,9 @@ void launch_deferred_agg(hipStream_t st, TableView t, const uint4* in_list, uint
                          uint4* out_list);
 void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                      ExportView ex, BatchCtl* ctl, unsigned long long* stats);
-void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap);
-void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t,
-                           FragView f, ComplexView cx);
+void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap, uint32_t ncx);
+void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
+                           ComplexView cx, BatchCtl* ctl);
 void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                          ComplexView cx, uint32_t nranks, ExportView ex, BatchCtl* ctl,
                          unsigned long long* stats);
