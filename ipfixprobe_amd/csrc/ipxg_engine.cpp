@@ -95,7 +95,8 @@ struct HostVec {
 
 // A walk thread's exports, on a cache line of its own (the threads append concurrently).
 struct alignas(128) ExportVec {
-    HostVec<ipxg_flow_record> v;  // page-locked: copied to the device's export buffer directly
+    HostVec<ipxg_flow_record> v;              // page-locked, sized by the engine's thread before the walk
+    std::vector<ipxg_flow_record> spill;      // what did not fit (the walk threads make no HIP call)
 };
 
 // The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
@@ -211,7 +212,6 @@ struct ipxg_engine {
     bool walked = false;  // a plugin walk has called hooks (plugin instances no longer pristine)
     WalkPool* pool = nullptr;
     std::vector<std::unique_ptr<ExportVec>> hw_ex;       // [t]
-    std::vector<hipEvent_t> walk_ev;                     // [t]: thread t's share copied
     std::vector<std::vector<uint64_t>> host_ports;      // [t]
     std::vector<std::vector<ipxg_plugin>> walk_pl;      // [t - 1]: thread t's plugin instances
     // staging for host batches
@@ -648,7 +648,6 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
     free_walk_copies(e);
-    for (hipEvent_t ev : e->walk_ev) hipEventDestroy(ev);
     hipFree(e->hot);
     hipFree(e->cold);
     hipFree(e->slot_rank);
@@ -953,7 +952,8 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
 namespace {
 
 struct alignas(128) WalkOut {  // one per walk thread, on cache lines of its own
-    HostVec<ipxg_flow_record>& ex;  // exported records, in order
+    HostVec<ipxg_flow_record>& ex;  // exported records, in order (then spill)
+    std::vector<ipxg_flow_record>& spill;
     uint64_t end[5] = {0, 0, 0, 0, 0};   // by end reason (export statistics)
     uint64_t pkts[6] = {0, 0, 0, 0, 0, 0};  // FlowRecordStats buckets
     uint64_t unreasoned = 0;  // export_flow with end_reason 0 (post_create FLUSH of a new record)
@@ -1001,7 +1001,8 @@ struct FlowWalk {
         o.end_reason = reason;
         o.reserved0 = 0;
         std::memset(o.reserved, 0, sizeof(o.reserved));
-        out.ex.push_back(o);
+        if (out.ex.size() < out.ex.cap) out.ex.push_back(o);
+        else out.spill.push_back(o);
         out.v6 += o.ip_version == 6 ? 1 : 0;
         // m_total_exported and update_flow_record_stats count every export_flow;
         // update_flow_end_reason_stats ignores a reason outside 1..5 (cache.cpp:264-267,618-638)
@@ -1268,12 +1269,17 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const ipxg_pkt_desc* de = e->hw_desc.data();
     const uint64_t* off = e->hw_off.data();
     const uint8_t* bytes = e->hw_bytes.data();
-    // first and off come over first (they split the walk); then each walk thread's share of the
-    // rest -- its flows, packets and frame bytes, contiguous in flow order -- in thread order,
-    // each behind an event its thread waits for: the walks of the first ranges overlap the copies
-    // of the later ones
+    // everything the walk reads, in one round of copies (page-locked host buffers); the walk
+    // threads make no HIP call (per-range copies behind events, waited on by each thread, gained
+    // nothing measurable: the copies of the first range hold up the last one anyway)
     HIPCHK(e, hipMemcpyAsync(e->hw_first.data(), o.first, ((size_t)nf + 1) * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_off.data(), o.off, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(flows, o.flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_idx.data(), o.idx, (size_t)m * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost,
+                             e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, nbytes, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->tm.plugin_flows += nf;
     e->tm.plugin_packets += m;
@@ -1282,60 +1288,35 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         const uint64_t cl = off[k + 1] - off[k];
         e->tm.plugin_extra_bytes += cl > 128 ? cl - 128 : 0;
     }
+    WALK_MARK(1);
     // the walk threads: contiguous flow ranges of about equal packet counts (flows in order of
-    // their first packet)
+    // their first packet); each thread's export buffer sized here for two exports per packet
+    // (more -- REINSERT chains -- go to its overflow vector)
     const unsigned T = walk_pool(e, nf, m);
     e->walked = true;
     std::vector<uint32_t> fr(T + 1);
     for (unsigned t = 0; t <= T; ++t)
         fr[t] = t == 0 ? 0 : t == T ? nf
                        : (uint32_t)(std::lower_bound(first, first + nf, (uint32_t)((uint64_t)m * t / T)) - first);
-    while (e->walk_ev.size() < T) {
-        hipEvent_t ev;
-        // (IPXG_WALK_SPIN: the waits poll instead of sleeping on the completion signal -- A/B)
-        const unsigned fl = hipEventDisableTiming | (std::getenv("IPXG_WALK_SPIN") ? 0u : (unsigned)hipEventBlockingSync);
-        HIPCHK(e, hipEventCreateWithFlags(&ev, fl));
-        e->walk_ev.push_back(ev);
-    }
-    for (unsigned t = 0; t < T; ++t) {
-        const uint32_t f0 = fr[t], f1 = fr[t + 1], a = first[f0], b = first[f1];
-        if (f1 > f0)
-            HIPCHK(e, hipMemcpyAsync(flows + f0, o.flows + f0, (size_t)(f1 - f0) * sizeof(PluginFlow),
-                                     hipMemcpyDeviceToHost, e->st));
-        if (b > a) {
-            HIPCHK(e, hipMemcpyAsync(e->hw_idx.data() + a, o.idx + a, (size_t)(b - a) * 4, hipMemcpyDeviceToHost, e->st));
-            HIPCHK(e, hipMemcpyAsync(pk + a, (ipxg_parsed_pkt*)e->pf_parsed.p + a, (size_t)(b - a) * sizeof(ipxg_parsed_pkt),
-                                     hipMemcpyDeviceToHost, e->st));
-            HIPCHK(e, hipMemcpyAsync(e->hw_desc.data() + a, (ipxg_pkt_desc*)e->pf_desc.p + a,
-                                     (size_t)(b - a) * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
-            if (off[b] > off[a])
-                HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data() + off[a], (uint8_t*)e->pf_bytes.p + off[a], off[b] - off[a],
-                                         hipMemcpyDeviceToHost, e->st));
-        }
-        HIPCHK(e, hipEventRecord(e->walk_ev[t], e->st));
-    }
-    WALK_MARK(1);
-    if (e->hw_ex.size() < T)
-        while (e->hw_ex.size() < T) e->hw_ex.emplace_back(new ExportVec);
+    while (e->hw_ex.size() < T) e->hw_ex.emplace_back(new ExportVec);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.size() < T) e->host_ports.resize(T);
     std::vector<WalkOut> wos;
     wos.reserve(T);
     for (unsigned t = 0; t < T; ++t) {
-        e->hw_ex[t]->v.clear();
-        wos.push_back(WalkOut{e->hw_ex[t]->v});
+        ExportVec& xv = *e->hw_ex[t];
+        xv.v.clear();
+        xv.spill.clear();
+        if (!xv.v.reserve(2 * (size_t)(first[fr[t + 1]] - first[fr[t]]) + 16, e->walk_pin))
+            return set_err(e, IPXG_ENOMEM, "host walk export buffers");
+        wos.push_back(WalkOut{xv.v, xv.spill});
     }
     std::vector<int64_t> dlive(T, 0);
-    std::vector<int> wfail(T, 0);
+    std::vector<int> wfail(T, 0);  // a walk thread ran out of host memory
     auto walk_range = [&](unsigned t) {
         if (t >= T) return;  // (the pool may hold more threads than this walk uses)
         const uint32_t f0 = fr[t], f1 = fr[t + 1];
         WalkOut& wo = wos[t];
-        if (hipEventSynchronize(e->walk_ev[t]) != hipSuccess ||
-            !wo.ex.reserve((size_t)(first[f1] - first[f0]) + 16, e->walk_pin)) {
-            wfail[t] = 1;
-            return;
-        }
         try {
         const std::vector<ipxg_plugin>& pl = t ? e->walk_pl[t - 1] : e->plugins;
         uint64_t* pa = nullptr;
@@ -1385,12 +1366,12 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     for (unsigned t = 0; t < T; ++t)
         if (wfail[t]) {
             (void)hipStreamSynchronize(e->st);
-            return set_err(e, wfail[t] == 1 ? IPXG_EDEVICE : IPXG_ENOMEM, "plugin walk: copies or export buffer");
+            return set_err(e, IPXG_ENOMEM, "plugin walk: host memory for the exports");
         }
     // the threads' exports follow each other in thread order (copied to the device below)
     size_t nx = 0;
     WalkOut& wo = wos[0];
-    for (unsigned t = 0; t < T; ++t) nx += wos[t].ex.size();
+    for (unsigned t = 0; t < T; ++t) nx += wos[t].ex.size() + wos[t].spill.size();
     for (unsigned t = 1; t < T; ++t) {
         for (int k = 0; k < 5; ++k) wo.end[k] += wos[t].end[k];
         for (int k = 0; k < 6; ++k) wo.pkts[k] += wos[t].pkts[k];
@@ -1408,10 +1389,15 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         size_t at = e->ex_count;
         for (unsigned t = 0; t < T; ++t) {
             const HostVec<ipxg_flow_record>& x = wos[t].ex;
-            if (x.empty()) continue;
-            HIPCHK(e, hipMemcpyAsync(e->ex + at, x.data(), x.size() * sizeof(ipxg_flow_record), hipMemcpyHostToDevice,
-                                     e->st));
+            const std::vector<ipxg_flow_record>& y = wos[t].spill;
+            if (!x.empty())
+                HIPCHK(e, hipMemcpyAsync(e->ex + at, x.data(), x.size() * sizeof(ipxg_flow_record),
+                                         hipMemcpyHostToDevice, e->st));
             at += x.size();
+            if (!y.empty())
+                HIPCHK(e, hipMemcpyAsync(e->ex + at, y.data(), y.size() * sizeof(ipxg_flow_record),
+                                         hipMemcpyHostToDevice, e->st));
+            at += y.size();
         }
         uint32_t c3[3] = {e->ex_count + (uint32_t)nx, 0, e->ex_count6 + (uint32_t)wo.v6};
         HIPCHK(e, hipMemcpyAsync(e->ex_count_d, c3, sizeof(c3), hipMemcpyHostToDevice, e->st));
