@@ -27,13 +27,16 @@ if [[ " $STAGES " == *" test "* ]]; then
   rc=$?; tail -1 $OUT/smoke.txt; stop_on_fault $rc smoke
 fi
 if [[ " $STAGES " == *" bench "* ]]; then
-  for W in ${BENCHES:-udp64 stream imix quic strict}; do
+  for W in ${BENCHES:-udp64 stream imix quic strict imix10m imix_plugins quic_plugins}; do
     case $W in
-      udp64) ARGS="--steps 50 --warmup 3" ;;
+      udp64) ARGS="" ;;  # the driver's default invocation
       stream) ARGS="--mode stream --steps 50 --warmup 3 --no-cpu-baseline --no-e2e" ;;
       imix) ARGS="--workload imix --steps 3 --warmup 1 --no-cpu-baseline --no-e2e" ;;
       quic) ARGS="--workload quic --steps 5 --warmup 1 --no-cpu-baseline --no-e2e" ;;
       strict) ARGS="--strict 17 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --verify" ;;
+      imix10m) ARGS="--workload imix10m --shard 0/8 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e" ;;
+      imix_plugins) ARGS="--workload imix --plugins dns,http,tls --steps 3 --warmup 1 --no-cpu-baseline --no-e2e" ;;
+      quic_plugins) ARGS="--workload quic --plugins quic --steps 5 --warmup 1 --no-cpu-baseline --no-e2e" ;;
     esac
     echo "== bench $W"; date
     timeout -k 10 500 python bench.py $ARGS > $OUT/bench_$W.json 2> $OUT/bench_$W.err
@@ -41,7 +44,7 @@ if [[ " $STAGES " == *" bench "* ]]; then
   done
 fi
 if [[ " $STAGES " == *" prof "* ]]; then
-  TAG=$TAG bash tools/gpu_profile.sh
+  TAG=$TAG PMC=${PMC:-0} WORKLOADS="${PROF_WORKLOADS:-udp64 imix quic imix_plugins quic_plugins}" bash tools/gpu_profile.sh
   rc=$?; stop_on_fault $rc profile
 fi
 echo "== round done"; date
