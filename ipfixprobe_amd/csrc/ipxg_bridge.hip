@@ -158,11 +158,13 @@ __global__ __launch_bounds__(256) void k_plugin_keys(TableView t, ComplexView cx
 }
 
 __global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx, const uint64_t* skeys, uint32_t ncx,
-                                                     const uint32_t* count, PluginFlow* out, uint32_t* flen) {
+                                                     const uint32_t* count, PluginFlow* out, uint32_t* flen,
+                                                     uint32_t* hstate, uint32_t* lflag) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k > ncx) return;
     if (k >= *count) {
-        flen[k] = 0;  // (the scan's tail: first[k] = packets for k >= flows)
+        flen[k] = 0;  // (the scans' tails: first[k] = packets, lpos[k] = live flows for k >= flows)
+        lflag[k] = 0;
         return;
     }
     const uint32_t r = (uint32_t)skeys[k];
@@ -178,6 +180,18 @@ __global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx
     f.rec = t.cold[s];
     out[k] = f;
     flen[k] = f.len;
+    hstate[k] = f.state;
+    lflag[k] = (f.state & SLOT_LIVE) ? 1u : 0u;
+}
+
+// The records of the flows live before the walk, compacted (rec[lpos[k]]): the host gets the
+// records it needs, not 160-byte images of every flow.
+__global__ __launch_bounds__(256) void k_plugin_recs(const PluginFlow* flows, const uint32_t* count,
+                                                     const uint32_t* lflag, const uint32_t* lpos,
+                                                     ipxg_flow_record* recs) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= *count || !lflag[k]) return;
+    recs[lpos[k]] = flows[k].rec;
 }
 
 // One wave per flow: its packets' batch indices and captured lengths at first[k] ...
@@ -196,11 +210,13 @@ __global__ __launch_bounds__(256) void k_plugin_idx(BatchView b, ComplexView cx,
     }
 }
 
-__global__ void k_plugin_totals(const uint32_t* count, const uint32_t* first, const uint64_t* off, uint64_t* tot) {
+__global__ void k_plugin_totals(const uint32_t* count, const uint32_t* first, const uint64_t* off,
+                                const uint32_t* lpos, uint64_t* tot) {
     const uint32_t nf = *count, m = first[nf];
     tot[0] = nf;
     tot[1] = m;
     tot[2] = off[m];
+    tot[3] = lpos[nf];
 }
 
 void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, ComplexView cx, uint32_t ncx, uint32_t npk,
@@ -209,16 +225,20 @@ void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, Comple
     size_t tb = o.temp_bytes;
     (void)sort_keys_u64(o.temp, tb, o.keys, o.skeys, ncx, 56, st);
     hipLaunchKernelGGL(k_plugin_pack, dim3((ncx + 1 + 255) / 256), dim3(256), 0, st, t, cx, o.skeys, ncx, o.count,
-                       o.flows, o.flen);
+                       o.flows, o.flen, o.hstate, o.lflag);
     tb = o.temp_bytes;
     (void)exclusive_scan_u32(o.temp, tb, o.flen, o.first, ncx + 1, st);
+    tb = o.temp_bytes;
+    (void)exclusive_scan_u32(o.temp, tb, o.lflag, o.lpos, ncx + 1, st);
+    hipLaunchKernelGGL(k_plugin_recs, dim3((ncx + 255) / 256), dim3(256), 0, st, o.flows, o.count, o.lflag, o.lpos,
+                       o.recs);
     uint32_t g = (ncx + 3) / 4;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_plugin_idx, dim3(g ? g : 1), dim3(256), 0, st, b, cx, o.flows, o.count, o.first, o.idx,
                        o.clen);
     tb = o.temp_bytes;
     (void)exclusive_scan_u64(o.temp, tb, o.clen, o.off, npk + 1, st);
-    hipLaunchKernelGGL(k_plugin_totals, dim3(1), dim3(1), 0, st, o.count, o.first, o.off, o.tot);
+    hipLaunchKernelGGL(k_plugin_totals, dim3(1), dim3(1), 0, st, o.count, o.first, o.off, o.lpos, o.tot);
 }
 
 // Scratch bytes launch_plugin_order needs for ncx flows / npk packets (radix sort + scans).
@@ -272,22 +292,40 @@ void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx
     hipLaunchKernelGGL(k_plugin_bytes, dim3(g ? g : 1), dim3(256), 0, st, b, idx, off, m, out);
 }
 
-// The host walk's result for flow k: its slot (state LIVE with the record -- and FOLLOW while a
-// plugin follows every packet of it --, or empty of records).
-__global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginFlow* in, uint32_t n, BatchCtl* ctl) {
+// The host walk's result: flow k's new slot state (LIVE -- and FOLLOW while a plugin follows every
+// packet of it -- or empty of records), and the records of the flows live after the walk
+// (out_recs[j] for flow out_idx[j]).
+__global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginFlow* flows, const uint32_t* state,
+                                                      uint32_t n, BatchCtl* ctl) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
-    const PluginFlow f = in[k];
-    if (f.slot > t.mask) {  // (guard: never, unless the host handed back a corrupt image)
+    const uint32_t slot = flows[k].slot;
+    if (slot > t.mask) {  // (guard: never, unless the flow images were overwritten)
         atomicOr(&ctl->guard, 4u);
         return;
     }
-    if (f.state & SLOT_LIVE) t.cold[f.slot] = f.rec;
-    clear_slot(&t.hot[f.slot], f.key, f.state & (SLOT_LIVE | SLOT_FOLLOW));
+    clear_slot(&t.hot[slot], flows[k].key, state[k] & (SLOT_LIVE | SLOT_FOLLOW));
 }
 
-void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n, BatchCtl* ctl) {
-    hipLaunchKernelGGL(k_plugin_apply, dim3((n + 255) / 256), dim3(256), 0, st, t, in, n, ctl);
+__global__ __launch_bounds__(256) void k_plugin_apply_recs(TableView t, const PluginFlow* flows, uint32_t nf,
+                                                           const uint32_t* idx, const ipxg_flow_record* recs,
+                                                           uint32_t n, BatchCtl* ctl) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t k = idx[j];
+    if (k >= nf || flows[k].slot > t.mask) {  // (guard: the host handed back a bad index)
+        atomicOr(&ctl->guard, 4u);
+        return;
+    }
+    t.cold[flows[k].slot] = recs[j];
+}
+
+void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* flows, const uint32_t* state, uint32_t nf,
+                         const uint32_t* idx, const ipxg_flow_record* recs, uint32_t nrec, BatchCtl* ctl) {
+    if (nrec)
+        hipLaunchKernelGGL(k_plugin_apply_recs, dim3((nrec + 255) / 256), dim3(256), 0, st, t, flows, nf, idx, recs, nrec,
+                           ctl);
+    hipLaunchKernelGGL(k_plugin_apply, dim3((nf + 255) / 256), dim3(256), 0, st, t, flows, state, nf, ctl);
 }
 
 }  // namespace ipxg

@@ -97,6 +97,8 @@ struct HostVec {
 struct alignas(128) ExportVec {
     HostVec<ipxg_flow_record> v;              // page-locked, sized by the engine's thread before the walk
     std::vector<ipxg_flow_record> spill;      // what did not fit (the walk threads make no HIP call)
+    HostVec<uint32_t> oidx;                   // the flows of its range live after the walk ...
+    HostVec<ipxg_flow_record> orec;           // ... and their records (one per flow at most)
 };
 
 // The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
@@ -193,9 +195,10 @@ struct ipxg_engine {
     bool strict_prune = true;                            // strict: idle-free sweep steps left out of the DAG
     uint32_t strict_wgs = STRICT_WGS_DEFAULT;            // strict: replay workgroups per XCD (0: one workgroup)
     uint32_t* st_sched = nullptr;                        // strict: the multi-workgroup scheduler block
-    DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes, pf_keys, pf_flen, pf_tmp;
+    DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes, pf_keys, pf_flen, pf_tmp, pf_live, pf_recs;
     // their host copies, kept across batches (HostVec: page-locked malloc memory)
-    HostVec<PluginFlow> hw_flows;
+    HostVec<uint32_t> hw_state, hw_lpos;  // the flows' slot states (then their new ones); live record positions
+    HostVec<ipxg_flow_record> hw_recs;    // the live flows' records
     HostVec<uint32_t> hw_first, hw_idx;
     HostVec<uint64_t> hw_off;
     HostVec<ipxg_parsed_pkt> hw_parsed;
@@ -1227,6 +1230,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     if ((rc = ensure(e, e->pf_idx, (size_t)npk * 4 + 16))) return rc;
     if ((rc = ensure(e, e->pf_off, ((size_t)npk + 1) * 16 + 16))) return rc;
     if ((rc = ensure(e, e->pf_tmp, tmp_b + 64))) return rc;
+    if ((rc = ensure(e, e->pf_live, (3 * (size_t)ncx + 2) * 4 + 16))) return rc;
+    if ((rc = ensure(e, e->pf_recs, (size_t)ncx * sizeof(ipxg_flow_record) + 16))) return rc;
     PluginOrder o;
     o.keys = (uint64_t*)e->pf_keys.p;
     o.skeys = o.keys + ncx;
@@ -1238,17 +1243,22 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     o.clen = o.off + npk + 1;
     o.tot = (uint64_t*)e->pf_tmp.p;
     o.count = (uint32_t*)(o.tot + 4);
+    o.hstate = (uint32_t*)e->pf_live.p;
+    o.lflag = o.hstate + ncx;
+    o.lpos = o.lflag + ncx + 1;
+    o.recs = (ipxg_flow_record*)e->pf_recs.p;
     o.temp = (char*)e->pf_tmp.p + 64;
     o.temp_bytes = tmp_b;
     HIPCHK(e, hipMemsetAsync(o.count, 0, sizeof(uint32_t), e->st));
     HIPCHK(e, hipMemsetAsync(o.clen, 0, ((size_t)npk + 1) * 8, e->st));
     launch_plugin_order(e->st, bv, table_view(e), cx, ncx, npk, o);
     HIPCHK(e, hipGetLastError());
-    uint64_t tot[3] = {0, 0, 0};
+    uint64_t tot[4] = {0, 0, 0, 0};
     HIPCHK(e, hipMemcpyAsync(tot, o.tot, sizeof(tot), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));  WALK_MARK(0);
     const uint32_t nf = (uint32_t)tot[0], m = (uint32_t)tot[1];
     const uint64_t nbytes = tot[2];
+    const uint32_t nlive = (uint32_t)tot[3];
     if (!nf) return IPXG_OK;
     if ((rc = ensure(e, e->pf_parsed, (size_t)m * sizeof(ipxg_parsed_pkt) + 8))) return rc;
     if ((rc = ensure(e, e->pf_desc, (size_t)m * sizeof(ipxg_pkt_desc) + 16))) return rc;
@@ -1258,11 +1268,13 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     launch_plugin_bytes(e->st, bv, o.idx, o.off, m, (uint8_t*)e->pf_bytes.p);
     HIPCHK(e, hipGetLastError());
     const bool pin = e->walk_pin;
-    if (!e->hw_flows.resize(nf, pin) || !e->hw_first.resize(nf + 1, pin) || !e->hw_idx.resize(m, pin) ||
-        !e->hw_parsed.resize(m, pin) || !e->hw_desc.resize(m, pin) || !e->hw_off.resize((size_t)m + 1, pin) ||
-        !e->hw_bytes.resize(nbytes + 16, pin))
+    if (!e->hw_state.resize(nf, pin) || !e->hw_recs.resize(nlive, pin) || !e->hw_first.resize(nf + 1, pin) ||
+        !e->hw_idx.resize(m, pin) || !e->hw_parsed.resize(m, pin) || !e->hw_desc.resize(m, pin) ||
+        !e->hw_off.resize((size_t)m + 1, pin) || !e->hw_bytes.resize(nbytes + 16, pin) || !e->hw_lpos.resize(nf + 1, pin))
         return set_err(e, IPXG_ENOMEM, "host walk buffers");
-    PluginFlow* flows = e->hw_flows.data();
+    uint32_t* fstate = e->hw_state.data();
+    const ipxg_flow_record* recs_in = e->hw_recs.data();
+    uint32_t* lpos = e->hw_lpos.data();
     const uint32_t* first = e->hw_first.data();
     const uint32_t* idx = e->hw_idx.data();
     ipxg_parsed_pkt* pk = e->hw_parsed.data();
@@ -1274,7 +1286,12 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     // nothing measurable: the copies of the first range hold up the last one anyway)
     HIPCHK(e, hipMemcpyAsync(e->hw_first.data(), o.first, ((size_t)nf + 1) * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_off.data(), o.off, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(flows, o.flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyDeviceToHost, e->st));
+    // (the flows' slot states, and the records of the live ones only: the 160-byte flow images
+    // stay on the device for the write-back)
+    HIPCHK(e, hipMemcpyAsync(fstate, o.hstate, (size_t)nf * 4, hipMemcpyDeviceToHost, e->st));
+    if (nlive)
+        HIPCHK(e, hipMemcpyAsync(e->hw_recs.data(), o.recs, (size_t)nlive * sizeof(ipxg_flow_record),
+                                 hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_idx.data(), o.idx, (size_t)m * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost,
@@ -1288,6 +1305,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         const uint64_t cl = off[k + 1] - off[k];
         e->tm.plugin_extra_bytes += cl > 128 ? cl - 128 : 0;
     }
+    lpos[0] = 0;  // flow f's record in recs_in, when it is live
+    for (uint32_t f = 0; f < nf; ++f) lpos[f + 1] = lpos[f] + ((fstate[f] & SLOT_LIVE) ? 1u : 0u);
     WALK_MARK(1);
     // the walk threads: contiguous flow ranges of about equal packet counts (flows in order of
     // their first packet); each thread's export buffer sized here for two exports per packet
@@ -1307,7 +1326,11 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         ExportVec& xv = *e->hw_ex[t];
         xv.v.clear();
         xv.spill.clear();
-        if (!xv.v.reserve(2 * (size_t)(first[fr[t + 1]] - first[fr[t]]) + 16, e->walk_pin))
+        xv.oidx.clear();
+        xv.orec.clear();
+        const size_t nft = fr[t + 1] - fr[t];
+        if (!xv.v.reserve(2 * (size_t)(first[fr[t + 1]] - first[fr[t]]) + 16, e->walk_pin) ||
+            !xv.oidx.reserve(nft + 1, e->walk_pin) || !xv.orec.reserve(nft + 1, e->walk_pin))
             return set_err(e, IPXG_ENOMEM, "host walk export buffers");
         wos.push_back(WalkOut{xv.v, xv.spill});
     }
@@ -1325,9 +1348,13 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             pa = e->host_ports[t].data();
         }
         int64_t dl = 0;
+        ExportVec& xv = *e->hw_ex[t];
         for (uint32_t f = f0; f < f1; ++f) {
-            PluginFlow& F = flows[f];
-            FlowWalk w{pl, p, wo, F.rec, (F.state & SLOT_LIVE) != 0};
+            const bool live0 = (fstate[f] & SLOT_LIVE) != 0;
+            ipxg_flow_record r0;
+            if (live0) r0 = recs_in[lpos[f]];
+            else std::memset(&r0, 0, sizeof(r0));
+            FlowWalk w{pl, p, wo, r0, live0};
             const bool was_live = w.live;
             for (uint32_t k = first[f]; k < first[f + 1]; ++k) {
                 ipxg_packet_view v;
@@ -1345,15 +1372,19 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             // host walk until the flow holds follow_packets packets (ipxg_plugin.follow_packets)
             const bool follow =
                 w.live && w.rec.ext && (uint64_t)w.rec.src_packets + w.rec.dst_packets < e->follow_max;
-            F.state = w.live ? (SLOT_LIVE | (follow ? SLOT_FOLLOW : 0u)) : 0u;
-            F.rec = w.rec;
+            fstate[f] = w.live ? (SLOT_LIVE | (follow ? SLOT_FOLLOW : 0u)) : 0u;
+            if (w.live) {  // (capacity: one record per flow of the range)
+                xv.oidx.push_back(f);
+                xv.orec.push_back(w.rec);
+            }
             dl += (w.live ? 1 : 0) - (was_live ? 1 : 0);
+            const uint32_t flen = first[f + 1] - first[f];
             // TopPorts from the flow's packets (count_flow_ports: every packet counts both ports)
             const ipxg_flow_record& r = w.rec;
             if (pa && (r.ip_proto == 6 || r.ip_proto == 17) && (r.src_port || r.dst_port)) {
                 uint64_t* a = pa + (r.ip_proto == 17 ? 65536 : 0);
-                a[r.src_port] += F.len;
-                a[r.dst_port] += F.len;
+                a[r.src_port] += flen;
+                a[r.dst_port] += flen;
             }
         }
         dlive[t] = dl;
@@ -1380,9 +1411,24 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     }
     for (unsigned t = 0; t < T; ++t) *live_delta += dlive[t];
     WALK_MARK(5);
-    // back to the device: the slots, then the exports after the batch's own
-    HIPCHK(e, hipMemcpyAsync(e->pf_d.p, flows, (size_t)nf * sizeof(PluginFlow), hipMemcpyHostToDevice, e->st));
-    launch_plugin_apply(e->st, table_view(e), (const PluginFlow*)e->pf_d.p, nf, e->ctl_d);
+    // back to the device: the slot states, the live flows' records, then the exports after the
+    // batch's own
+    HIPCHK(e, hipMemcpyAsync(o.hstate, fstate, (size_t)nf * 4, hipMemcpyHostToDevice, e->st));
+    uint32_t nout = 0;
+    {
+        uint32_t* oidx_d = o.lflag;  // (free now: nf + 1 words)
+        ipxg_flow_record* orec_d = o.recs;
+        for (unsigned t = 0; t < T; ++t) {
+            const ExportVec& xv = *e->hw_ex[t];
+            const size_t k = xv.oidx.size();
+            if (!k) continue;
+            HIPCHK(e, hipMemcpyAsync(oidx_d + nout, xv.oidx.data(), k * 4, hipMemcpyHostToDevice, e->st));
+            HIPCHK(e, hipMemcpyAsync(orec_d + nout, xv.orec.data(), k * sizeof(ipxg_flow_record), hipMemcpyHostToDevice,
+                                     e->st));
+            nout += (uint32_t)k;
+        }
+        launch_plugin_apply(e->st, table_view(e), o.flows, o.hstate, nf, oidx_d, orec_d, nout, e->ctl_d);
+    }
     HIPCHK(e, hipGetLastError());
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;

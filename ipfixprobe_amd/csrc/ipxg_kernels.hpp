@@ -267,11 +267,14 @@ void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableV
                      uint32_t nrules, BatchCtl* ctl);
 // The host walk's inputs on the device, flows in order of their first packet (ipxg_bridge.hip):
 // keys / skeys [ncx], flows [ncx], flen / first [ncx + 1], idx [npk], clen / off [npk + 1],
-// count (zeroed by the caller), tot [3] = {flows, packets, bytes}
+// hstate [ncx] (slot states), lflag / lpos [ncx + 1] (live flags, their exclusive prefix),
+// recs [ncx] (the live flows' records, compacted), count (zeroed by the caller),
+// tot [4] = {flows, packets, bytes, live flows}
 struct PluginOrder {
     uint64_t *keys, *skeys;
     PluginFlow* flows;
-    uint32_t *flen, *first, *idx, *count;
+    uint32_t *flen, *first, *idx, *count, *hstate, *lflag, *lpos;
+    ipxg_flow_record* recs;
     uint64_t *clen, *off, *tot;
     void* temp;
     size_t temp_bytes;
@@ -283,7 +286,8 @@ void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, Fra
                         uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout);
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
                          uint8_t* out);
-void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* in, uint32_t n, BatchCtl* ctl);
+void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* flows, const uint32_t* state, uint32_t nf,
+                         const uint32_t* idx, const ipxg_flow_record* recs, uint32_t nrec, BatchCtl* ctl);
 void launch_pstats(hipStream_t st, const BatchView& b, const Params& p, unsigned long long* pstat);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
