@@ -15,6 +15,7 @@
 #include <sys/resource.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -43,6 +44,7 @@ struct DevBuf {
 // and read by the CPU through its caches (hipHostMalloc'd memory read slower in the walk,
 // DESIGN 4.4).  Contents are not kept when it grows (each batch overwrites it).
 // IPXG_WALK_PAGEABLE=1 leaves it pageable (A/B).
+static std::atomic<uint64_t> g_hostvec_allocs{0}, g_hostvec_unpinned{0};  // (IPXG_WALK_TRACE)
 template <class T>
 struct HostVec {
     T* p = nullptr;
@@ -75,6 +77,8 @@ struct HostVec {
         cap = bytes / sizeof(T);
         n = kept;
         reg = pin && hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
+        g_hostvec_allocs++;
+        if (pin && !reg) g_hostvec_unpinned++;
         return true;
     }
     bool resize(size_t k, bool pin) {
@@ -644,9 +648,10 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e && e->walk_trace && e->tm.plugin_flows)
         std::fprintf(stderr,
                      "ipxg plugin walk ms: order %.1f copies %.1f walk %.1f back %.1f"
-                     " | minor faults: %ld %ld %ld %ld\n",
+                     " | minor faults: %ld %ld %ld %ld | host buffers allocated %lu, not page-locked %lu\n",
                      e->walk_phase_ms[0], e->walk_phase_ms[1], e->walk_phase_ms[5], e->walk_phase_ms[6],
-                     e->walk_faults[0], e->walk_faults[1], e->walk_faults[5], e->walk_faults[6]);
+                     e->walk_faults[0], e->walk_faults[1], e->walk_faults[5], e->walk_faults[6],
+                     (unsigned long)g_hostvec_allocs.load(), (unsigned long)g_hostvec_unpinned.load());
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
