@@ -177,3 +177,53 @@ def test_bridge_leaves_other_flows_on_device():
     d = flowcmp.diff(got, want)
     assert not d, d
     assert sum(pl.calls.values()) == 0
+
+
+class PrefixMarker(plugins_py.PyPlugin):
+    """Claims a flow (ext bit) on a packet whose payload starts with its rule's prefixes: 7x under
+    the mask F0 (the fuzz corpus' TCP 'x...' and UDP 'y...' payloads), or 'yy' -- exactly the
+    packets the pre-classifier must route to the host walk.  Any packet the device misses leaves
+    the engine's ext different from the oracle's."""
+    proto_mask = 3
+    prefixes = (b"\x70", b"yy")
+
+    def __init__(self):
+        super().__init__()
+        s = self.struct
+        s.masked = 1
+        s.prefix_mask[0][0] = 0xF0
+        self.seen = 0
+
+    def _mark(self, rec, p, data):
+        if int(p["ip_proto"]) not in (6, 17) or int(p["frag_off"]):  # outside the rule: no-op
+            return 0
+        if (data[:1] and (data[0] & 0xF0) == 0x70) or data[:2] == b"yy":
+            self.seen += 1
+            rec["ext"] = int(rec["ext"]) | 1
+        return 0
+
+    def post_create(self, rec, p, data):
+        return self._mark(rec, p, data)
+
+    def post_update(self, rec, p, data):
+        return self._mark(rec, p, data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [None, 4096])
+def test_classifier_payload_offsets_on_fuzz_corpus(batch):
+    """The pre-classifier parses the register-walk shapes (VLAN/QinQ, MPLS, PPPoE, IPv4-in-GRE,
+    IPv6 with extension headers, TCP timestamps) from registers and computes their payload offset
+    and length itself (parse_medium<PAY>, parser.cpp:780-797): on the fuzz corpus -- every such
+    shape, truncated at every length -- the flows it routes to the hooks must be exactly those
+    with a rule packet, i.e. the engine's records (ext included) equal the oracle's, whose hooks
+    see every packet."""
+    from ipfixprobe_amd import run_capture
+    arena, desc = synth.to_batch(synth.fuzz_corpus(20000, seed=71))
+    eng, orc = PrefixMarker(), PrefixMarker()
+    got, _ = run_capture(arena, desc, params="s=18", batch=batch, plugins=[eng.struct])
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20, plugins=[orc.struct])
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+    assert (want["ext"] != 0).sum() > 100
+    assert eng.seen == orc.seen
