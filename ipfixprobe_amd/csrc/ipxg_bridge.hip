@@ -308,24 +308,39 @@ __global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginF
 }
 
 __global__ __launch_bounds__(256) void k_plugin_apply_recs(TableView t, const PluginFlow* flows, uint32_t nf,
-                                                           const uint32_t* idx, const ipxg_flow_record* recs,
-                                                           uint32_t n, BatchCtl* ctl) {
+                                                           const ipxg_flow_record* recs, uint32_t n, BatchCtl* ctl) {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
-    const uint32_t k = idx[j];
+    ipxg_flow_record r = recs[j];
+    uint32_t k;
+    memcpy(&k, r.reserved2, 4);  // the flow's index, carried in the record's spare bytes
+    memset(r.reserved2, 0, sizeof(r.reserved2));
     if (k >= nf || flows[k].slot > t.mask) {  // (guard: the host handed back a bad index)
         atomicOr(&ctl->guard, 4u);
         return;
     }
-    t.cold[flows[k].slot] = recs[j];
+    t.cold[flows[k].slot] = r;
 }
 
 void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* flows, const uint32_t* state, uint32_t nf,
-                         const uint32_t* idx, const ipxg_flow_record* recs, uint32_t nrec, BatchCtl* ctl) {
+                         const ipxg_flow_record* recs, uint32_t nrec, BatchCtl* ctl) {
     if (nrec)
-        hipLaunchKernelGGL(k_plugin_apply_recs, dim3((nrec + 255) / 256), dim3(256), 0, st, t, flows, nf, idx, recs, nrec,
-                           ctl);
+        hipLaunchKernelGGL(k_plugin_apply_recs, dim3((nrec + 255) / 256), dim3(256), 0, st, t, flows, nf, recs, nrec, ctl);
     hipLaunchKernelGGL(k_plugin_apply, dim3((nf + 255) / 256), dim3(256), 0, st, t, flows, state, nf, ctl);
+}
+
+// chunk blockIdx.y, 16-byte word (blockIdx.x * 256 + threadIdx.x) of its records
+__global__ __launch_bounds__(256) void k_host_gather(HostChunks c, uint4* dst) {
+    const uint32_t ch = blockIdx.y;
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= c.n[ch] * 8u) return;
+    dst[(size_t)c.at[ch] * 8u + w] = c.src[ch][w];
+}
+
+void launch_host_gather(hipStream_t st, const HostChunks& c, ipxg_flow_record* dst) {
+    if (!c.count || !c.max_n) return;
+    hipLaunchKernelGGL(k_host_gather, dim3((c.max_n * 8u + 255) / 256, c.count), dim3(256), 0, st, c,
+                       reinterpret_cast<uint4*>(dst));
 }
 
 }  // namespace ipxg

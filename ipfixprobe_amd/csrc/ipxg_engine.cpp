@@ -48,6 +48,7 @@ static std::atomic<uint64_t> g_hostvec_allocs{0}, g_hostvec_unpinned{0};  // (IP
 template <class T>
 struct HostVec {
     T* p = nullptr;
+    T* dev = nullptr;  // its device-visible address when page-locked (kernels read it over PCIe)
     size_t n = 0, cap = 0;
     bool reg = false;
     HostVec() = default;
@@ -59,7 +60,7 @@ struct HostVec {
             if (reg) (void)hipHostUnregister(p);
             std::free(p);
         }
-        p = nullptr;
+        p = dev = nullptr;
         n = cap = 0;
         reg = false;
     }
@@ -76,7 +77,8 @@ struct HostVec {
         p = static_cast<T*>(q);
         cap = bytes / sizeof(T);
         n = kept;
-        reg = pin && hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
+        reg = pin && hipHostRegister(p, bytes, hipHostRegisterMapped) == hipSuccess;
+        if (reg && hipHostGetDevicePointer((void**)&dev, p, 0) != hipSuccess) dev = nullptr;
         g_hostvec_allocs++;
         if (pin && !reg) g_hostvec_unpinned++;
         return true;
@@ -101,8 +103,8 @@ struct HostVec {
 struct alignas(128) ExportVec {
     HostVec<ipxg_flow_record> v;              // page-locked, sized by the engine's thread before the walk
     std::vector<ipxg_flow_record> spill;      // what did not fit (the walk threads make no HIP call)
-    HostVec<uint32_t> oidx;                   // the flows of its range live after the walk ...
-    HostVec<ipxg_flow_record> orec;           // ... and their records (one per flow at most)
+    HostVec<ipxg_flow_record> orec;           // the records of its range's flows live after the walk
+                                              // (one per flow at most; the flow's index in reserved2)
 };
 
 // The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
@@ -1137,7 +1139,8 @@ static void free_walk_copies(ipxg_engine* e) {
 static unsigned walk_want(const ipxg_engine* e) {
     for (const ipxg_plugin& q : e->plugins)
         if (!q.copy_ctx || !q.free_ctx) return 1;
-    return e->walk_threads ? e->walk_threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return std::min<unsigned>(HOST_CHUNKS, e->walk_threads ? e->walk_threads
+                                                           : std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
 }
 
 // Every registered plugin copied for walk threads 1 .. want-1 (walk_pl[t-1][k]: thread t's copy
@@ -1331,11 +1334,10 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         ExportVec& xv = *e->hw_ex[t];
         xv.v.clear();
         xv.spill.clear();
-        xv.oidx.clear();
         xv.orec.clear();
         const size_t nft = fr[t + 1] - fr[t];
         if (!xv.v.reserve(2 * (size_t)(first[fr[t + 1]] - first[fr[t]]) + 16, e->walk_pin) ||
-            !xv.oidx.reserve(nft + 1, e->walk_pin) || !xv.orec.reserve(nft + 1, e->walk_pin))
+            !xv.orec.reserve(nft + 1, e->walk_pin))
             return set_err(e, IPXG_ENOMEM, "host walk export buffers");
         wos.push_back(WalkOut{xv.v, xv.spill});
     }
@@ -1379,8 +1381,9 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
                 w.live && w.rec.ext && (uint64_t)w.rec.src_packets + w.rec.dst_packets < e->follow_max;
             fstate[f] = w.live ? (SLOT_LIVE | (follow ? SLOT_FOLLOW : 0u)) : 0u;
             if (w.live) {  // (capacity: one record per flow of the range)
-                xv.oidx.push_back(f);
-                xv.orec.push_back(w.rec);
+                ipxg_flow_record o2 = w.rec;
+                std::memcpy(o2.reserved2, &f, 4);
+                xv.orec.push_back(o2);
             }
             dl += (w.live ? 1 : 0) - (was_live ? 1 : 0);
             const uint32_t flen = first[f + 1] - first[f];
@@ -1418,33 +1421,49 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     WALK_MARK(5);
     // back to the device: the slot states, the live flows' records, then the exports after the
     // batch's own
+    // (the threads' records and exports are read by one kernel straight from their page-locked
+    // buffers -- one launch instead of a copy command per thread and array, ~10 us each)
     HIPCHK(e, hipMemcpyAsync(o.hstate, fstate, (size_t)nf * 4, hipMemcpyHostToDevice, e->st));
-    uint32_t nout = 0;
-    {
-        uint32_t* oidx_d = o.lflag;  // (free now: nf + 1 words)
-        ipxg_flow_record* orec_d = o.recs;
+    auto gather = [&](auto pick, ipxg_flow_record* dst, uint32_t at0, uint32_t& moved) -> int {
+        HostChunks c;
+        c.count = c.max_n = 0;
+        uint32_t at = at0;
         for (unsigned t = 0; t < T; ++t) {
-            const ExportVec& xv = *e->hw_ex[t];
-            const size_t k = xv.oidx.size();
+            const HostVec<ipxg_flow_record>& x = pick(t);
+            const uint32_t k = (uint32_t)x.size();
             if (!k) continue;
-            HIPCHK(e, hipMemcpyAsync(oidx_d + nout, xv.oidx.data(), k * 4, hipMemcpyHostToDevice, e->st));
-            HIPCHK(e, hipMemcpyAsync(orec_d + nout, xv.orec.data(), k * sizeof(ipxg_flow_record), hipMemcpyHostToDevice,
-                                     e->st));
-            nout += (uint32_t)k;
+            if (x.dev) {
+                c.src[c.count] = reinterpret_cast<const uint4*>(x.dev);
+                c.n[c.count] = k;
+                c.at[c.count] = at;
+                c.max_n = std::max(c.max_n, k);
+                c.count++;
+            } else {  // (not page-locked: a copy command)
+                HIPCHK(e, hipMemcpyAsync(dst + at, x.data(), (size_t)k * sizeof(ipxg_flow_record),
+                                         hipMemcpyHostToDevice, e->st));
+            }
+            at += k;
         }
-        launch_plugin_apply(e->st, table_view(e), o.flows, o.hstate, nf, oidx_d, orec_d, nout, e->ctl_d);
-    }
+        launch_host_gather(e->st, c, dst);
+        HIPCHK(e, hipGetLastError());
+        moved = at - at0;
+        return IPXG_OK;
+    };
+    uint32_t nout = 0;
+    if ((rc = gather([&](unsigned t) -> const HostVec<ipxg_flow_record>& { return e->hw_ex[t]->orec; }, o.recs, 0,
+                     nout)))
+        return rc;
+    launch_plugin_apply(e->st, table_view(e), o.flows, o.hstate, nf, o.recs, nout, e->ctl_d);
     HIPCHK(e, hipGetLastError());
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;
-        size_t at = e->ex_count;
-        for (unsigned t = 0; t < T; ++t) {
-            const HostVec<ipxg_flow_record>& x = wos[t].ex;
+        uint32_t moved = 0;
+        if ((rc = gather([&](unsigned t) -> const HostVec<ipxg_flow_record>& { return wos[t].ex; }, e->ex, e->ex_count,
+                         moved)))
+            return rc;
+        size_t at = e->ex_count + moved;
+        for (unsigned t = 0; t < T; ++t) {  // what overflowed the threads' buffers (REINSERT chains)
             const std::vector<ipxg_flow_record>& y = wos[t].spill;
-            if (!x.empty())
-                HIPCHK(e, hipMemcpyAsync(e->ex + at, x.data(), x.size() * sizeof(ipxg_flow_record),
-                                         hipMemcpyHostToDevice, e->st));
-            at += x.size();
             if (!y.empty())
                 HIPCHK(e, hipMemcpyAsync(e->ex + at, y.data(), y.size() * sizeof(ipxg_flow_record),
                                          hipMemcpyHostToDevice, e->st));

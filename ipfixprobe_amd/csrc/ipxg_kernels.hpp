@@ -286,8 +286,21 @@ void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, Fra
                         uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout);
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
                          uint8_t* out);
+// The host walk's results, read by one kernel straight from page-locked host memory (one launch
+// instead of a copy command per walk thread and array): chunk c = n[c] records at src[c] (a
+// device-visible address) to dst + at[c].
+constexpr int HOST_CHUNKS = 64;
+struct HostChunks {
+    const uint4* src[HOST_CHUNKS];
+    uint32_t n[HOST_CHUNKS];
+    uint32_t at[HOST_CHUNKS];
+    uint32_t count, max_n;
+};
+void launch_host_gather(hipStream_t st, const HostChunks& c, ipxg_flow_record* dst);
+// the write-back: slot states of the nf flows, then the records recs[0..nrec) of the flows live
+// after the walk (each carrying its flow's index in reserved2)
 void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* flows, const uint32_t* state, uint32_t nf,
-                         const uint32_t* idx, const ipxg_flow_record* recs, uint32_t nrec, BatchCtl* ctl);
+                         const ipxg_flow_record* recs, uint32_t nrec, BatchCtl* ctl);
 void launch_pstats(hipStream_t st, const BatchView& b, const Params& p, unsigned long long* pstat);
 void launch_ingest(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                    BatchCtl* ctl, uint32_t* deferred_list, unsigned long long* stats);
