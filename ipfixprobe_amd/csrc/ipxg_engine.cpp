@@ -683,6 +683,7 @@ int ipxg_destroy(ipxg_engine* e) {
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->stage_arena[0], &e->stage_arena[1], &e->stage_desc[0], &e->stage_desc[1], &e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_parsed, &e->pf_desc, &e->pf_off, &e->pf_bytes,
+                      &e->pf_keys, &e->pf_flen, &e->pf_tmp, &e->pf_live, &e->pf_recs,
                       &e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
                       &e->frag_sorted,
                       &e->frag_ports, &e->sort_tmp, &e->cx_list, &e->cx_sorted, &e->cx_rank, &e->bin_rec,
