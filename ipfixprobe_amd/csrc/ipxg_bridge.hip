@@ -343,41 +343,4 @@ void launch_host_gather(hipStream_t st, const HostChunks& c, ipxg_flow_record* d
                        reinterpret_cast<uint4*>(dst));
 }
 
-// A walk thread's share to the host (WalkShare): grid-stride over the four spans' words.  The
-// flag is raised by a second, one-thread kernel behind it on the stream: the stores of the first
-// reach host memory at its end (the kernel boundary's system-scope release writes the L2 back; a
-// flag raised by the share kernel's own last workgroup came before its data in tests).
-__global__ __launch_bounds__(256) void k_walk_share(WalkShare s, uint64_t words) {
-    const uint64_t n0 = s.w1[0] - s.w0[0], n1 = s.w1[1] - s.w0[1], n2 = s.w1[2] - s.w0[2];
-    for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < words; w += (uint64_t)gridDim.x * 256) {
-        uint64_t x = w;
-        int a = 0;
-        if (x >= n0) {
-            x -= n0;
-            a = 1;
-            if (x >= n1) {
-                x -= n1;
-                a = 2;
-                if (x >= n2) {
-                    x -= n2;
-                    a = 3;
-                }
-            }
-        }
-        const uint64_t at = s.w0[a] + x;
-        s.dst[a][at] = s.src[a][at];
-    }
-}
-
-__global__ void k_raise_flag(volatile uint32_t* flag) {
-    __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-void launch_walk_share(hipStream_t st, const WalkShare& s, uint64_t words) {
-    uint64_t g = (words + 255) / 256;
-    if (g > 1024) g = 1024;
-    if (words) hipLaunchKernelGGL(k_walk_share, dim3(g ? (uint32_t)g : 1u), dim3(256), 0, st, s, words);
-    hipLaunchKernelGGL(k_raise_flag, dim3(1), dim3(1), 0, st, s.flag);
-}
-
 }  // namespace ipxg

@@ -221,8 +221,6 @@ struct ipxg_engine {
     bool walked = false;  // a plugin walk has called hooks (plugin instances no longer pristine)
     WalkPool* pool = nullptr;
     std::vector<std::unique_ptr<ExportVec>> hw_ex;       // [t]
-    uint32_t* walk_flags = nullptr;                      // [HOST_CHUNKS] host-mapped: thread t's share landed
-    uint32_t* walk_flags_d = nullptr;                    // ... its device address
     std::vector<std::vector<uint64_t>> host_ports;      // [t]
     std::vector<std::vector<ipxg_plugin>> walk_pl;      // [t - 1]: thread t's plugin instances
     // staging for host batches
@@ -660,7 +658,6 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
     free_walk_copies(e);
-    if (e->walk_flags) hipHostFree(e->walk_flags);
     hipFree(e->hot);
     hipFree(e->cold);
     hipFree(e->slot_rank);
@@ -1293,41 +1290,22 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const ipxg_pkt_desc* de = e->hw_desc.data();
     const uint64_t* off = e->hw_off.data();
     const uint8_t* bytes = e->hw_bytes.data();
-    // What the walk reads reaches the host in two rounds.  First, in one round of copies: the
-    // flows' first packet positions and the byte offsets (they split the walk), the slot states
-    // and the records of the live flows only (the 160-byte flow images stay on the device for the
-    // write-back).  Then each walk thread's share -- the packet list, parsed packets, descriptors
-    // and frame bytes of its flow range -- is written by a kernel straight into the page-locked
-    // host buffers, which raises the thread's flag when the share has landed: the walk of the
-    // first ranges overlaps the transfer of the later ones, and the walk threads make no HIP call
-    // (they poll the flag).  Without device-visible host buffers: one round of copies.
+    // everything the walk reads, in one round of copies (page-locked host buffers); the walk
+    // threads make no HIP call (per-range copies behind events, waited on by each thread, gained
+    // nothing measurable: the copies of the first range hold up the last one anyway)
     HIPCHK(e, hipMemcpyAsync(e->hw_first.data(), o.first, ((size_t)nf + 1) * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(e->hw_off.data(), o.off, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost, e->st));
+    // (the flows' slot states, and the records of the live ones only: the 160-byte flow images
+    // stay on the device for the write-back)
     HIPCHK(e, hipMemcpyAsync(fstate, o.hstate, (size_t)nf * 4, hipMemcpyDeviceToHost, e->st));
     if (nlive)
         HIPCHK(e, hipMemcpyAsync(e->hw_recs.data(), o.recs, (size_t)nlive * sizeof(ipxg_flow_record),
                                  hipMemcpyDeviceToHost, e->st));
-    if (!e->walk_flags && e->walk_pin) {  // the shares' flags (host-mapped) and completion counters
-        void* fp = nullptr;
-        if (hipHostMalloc(&fp, HOST_CHUNKS * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-            void* fd = nullptr;
-            if (hipHostGetDevicePointer(&fd, fp, 0) == hipSuccess) {
-                e->walk_flags = static_cast<uint32_t*>(fp);
-                e->walk_flags_d = static_cast<uint32_t*>(fd);
-            } else {
-                (void)hipHostFree(fp);
-            }
-        }
-    }
-    const bool share = e->walk_flags && e->hw_idx.dev && e->hw_parsed.dev && e->hw_desc.dev && e->hw_bytes.dev &&
-                       !std::getenv("IPXG_WALK_NOSHARE");
-    if (!share) {
-        HIPCHK(e, hipMemcpyAsync(e->hw_idx.data(), o.idx, (size_t)m * 4, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
-        HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc),
-                                 hipMemcpyDeviceToHost, e->st));
-        HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, nbytes, hipMemcpyDeviceToHost, e->st));
-    }
+    HIPCHK(e, hipMemcpyAsync(e->hw_idx.data(), o.idx, (size_t)m * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(pk, e->pf_parsed.p, (size_t)m * sizeof(ipxg_parsed_pkt), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_desc.data(), e->pf_desc.p, (size_t)m * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost,
+                             e->st));
+    HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data(), e->pf_bytes.p, nbytes, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->tm.plugin_flows += nf;
     e->tm.plugin_packets += m;
@@ -1338,45 +1316,16 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     }
     lpos[0] = 0;  // flow f's record in recs_in, when it is live
     for (uint32_t f = 0; f < nf; ++f) lpos[f + 1] = lpos[f] + ((fstate[f] & SLOT_LIVE) ? 1u : 0u);
+    WALK_MARK(1);
     // the walk threads: contiguous flow ranges of about equal packet counts (flows in order of
-    // their first packet)
+    // their first packet); each thread's export buffer sized here for two exports per packet
+    // (more -- REINSERT chains -- go to its overflow vector)
     const unsigned T = walk_pool(e, nf, m);
     e->walked = true;
     std::vector<uint32_t> fr(T + 1);
     for (unsigned t = 0; t <= T; ++t)
         fr[t] = t == 0 ? 0 : t == T ? nf
                        : (uint32_t)(std::lower_bound(first, first + nf, (uint32_t)((uint64_t)m * t / T)) - first);
-    if (share) {
-        for (unsigned t = 0; t < T; ++t) e->walk_flags[t] = 0;
-        for (unsigned t = 0; t < T; ++t) {
-            const uint64_t a = first[fr[t]], b = first[fr[t + 1]];
-            WalkShare ws;
-            ws.src[0] = (const uint4*)o.idx;
-            ws.dst[0] = (uint4*)e->hw_idx.dev;
-            ws.w0[0] = a * 4 / 16;
-            ws.w1[0] = b > a ? (b * 4 + 15) / 16 : ws.w0[0];
-            ws.src[1] = (const uint4*)e->pf_parsed.p;
-            ws.dst[1] = (uint4*)e->hw_parsed.dev;
-            ws.w0[1] = a * sizeof(ipxg_parsed_pkt) / 16;
-            ws.w1[1] = b * sizeof(ipxg_parsed_pkt) / 16;
-            ws.src[2] = (const uint4*)e->pf_desc.p;
-            ws.dst[2] = (uint4*)e->hw_desc.dev;
-            ws.w0[2] = a;
-            ws.w1[2] = b;
-            ws.src[3] = (const uint4*)e->pf_bytes.p;
-            ws.dst[3] = (uint4*)e->hw_bytes.dev;
-            ws.w0[3] = off[a] / 16;
-            ws.w1[3] = off[b] > off[a] ? (off[b] + 15) / 16 : ws.w0[3];
-            ws.flag = e->walk_flags_d + t;
-            uint64_t words = 0;
-            for (int q = 0; q < 4; ++q) words += ws.w1[q] - ws.w0[q];
-            launch_walk_share(e->st, ws, words);
-        }
-        HIPCHK(e, hipGetLastError());
-    }
-    WALK_MARK(1);
-    // each thread's export buffer sized here for two exports per packet (more -- REINSERT chains --
-    // go to its overflow vector)
     while (e->hw_ex.size() < T) e->hw_ex.emplace_back(new ExportVec);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.size() < T) e->host_ports.resize(T);
@@ -1394,21 +1343,11 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         wos.push_back(WalkOut{xv.v, xv.spill});
     }
     std::vector<int64_t> dlive(T, 0);
-    std::vector<int> wfail(T, 0);  // 1: its share never landed, 2: out of host memory
+    std::vector<int> wfail(T, 0);  // a walk thread ran out of host memory
     auto walk_range = [&](unsigned t) {
         if (t >= T) return;  // (the pool may hold more threads than this walk uses)
         const uint32_t f0 = fr[t], f1 = fr[t + 1];
         WalkOut& wo = wos[t];
-        if (share) {  // the share has landed (the flag a kernel raises); bounded: a dead device
-            const auto t0w = std::chrono::steady_clock::now();
-            for (uint64_t spin = 0; __atomic_load_n(&e->walk_flags[t], __ATOMIC_ACQUIRE) == 0; ++spin) {
-                __builtin_ia32_pause();
-                if ((spin & 0xFFFF) == 0 && std::chrono::steady_clock::now() - t0w > std::chrono::seconds(60)) {
-                    wfail[t] = 1;
-                    return;
-                }
-            }
-        }
         try {
         const std::vector<ipxg_plugin>& pl = t ? e->walk_pl[t - 1] : e->plugins;
         uint64_t* pa = nullptr;
@@ -1467,9 +1406,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     for (unsigned t = 0; t < T; ++t)
         if (wfail[t]) {
             (void)hipStreamSynchronize(e->st);
-            return set_err(e, wfail[t] == 1 ? IPXG_EDEVICE : IPXG_ENOMEM,
-                           wfail[t] == 1 ? "plugin walk: a share of the packets never landed (60 s)"
-                                         : "plugin walk: host memory for the exports");
+            return set_err(e, IPXG_ENOMEM, "plugin walk: host memory for the exports");
         }
     // the threads' exports follow each other in thread order (copied to the device below)
     size_t nx = 0;

@@ -297,17 +297,6 @@ struct HostChunks {
     uint32_t count, max_n;
 };
 void launch_host_gather(hipStream_t st, const HostChunks& c, ipxg_flow_record* dst);
-// One walk thread's share of the walked packets out to page-locked host memory (device-visible
-// addresses), then its ready flag (a host-mapped word) raised by a kernel behind it: spans of
-// 16-byte words [w0, w1) of each array (the same offsets in the device and host arrays; the
-// shares' boundary words are written by both, with the same bytes).
-struct WalkShare {
-    const uint4* src[4];
-    uint4* dst[4];
-    uint64_t w0[4], w1[4];
-    volatile uint32_t* flag;   // host-mapped flag, set to 1 when the share has landed
-};
-void launch_walk_share(hipStream_t st, const WalkShare& s, uint64_t words);
 // the write-back: slot states of the nf flows, then the records recs[0..nrec) of the flows live
 // after the walk (each carrying its flow's index in reserved2)
 void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* flows, const uint32_t* state, uint32_t nf,
