@@ -1396,6 +1396,9 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
     __syncthreads();
     const bool force_cx = p.force_complex || ctl->nonmono;
     const bool slot_clean = ctl->spilled == 0;  // no packet was folded into a slot directly (k_bin / k_reduce)
+    // the batch's latest second: its last packet's, when no timestamp went backwards (else every
+    // flow is complex anyway, force_cx)
+    const uint32_t tmax = force_cx || b.n == 0 ? TMAX_UNKNOWN : b.desc[b.n - 1].ts_sec;
     uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0, n_keys = 0, n_def = 0;
     for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
         const uint32_t k = base + tid;
@@ -1438,7 +1441,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
             }
         }
         if (go) {
-            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean);
+            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean, tmax);
             if (fr.status == FIN_COMPLEX) n_cx++;
             else if (!fused && fr.created) n_live++;
             do_export = fr.do_export || fr.fin_export;

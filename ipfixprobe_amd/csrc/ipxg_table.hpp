@@ -1013,17 +1013,28 @@ struct FinResult {
 // the creating packet's forward hash, cache.cpp:84-92: it is the slot's canonical key iff the
 // creator went in canonical direction 0 -- the rule rec_create_w / the host walk store in
 // reserved[0]), so the second half is read only for an export.
+// tmax: the batch's latest second when its timestamps are known not to decrease (the caller's
+// batch was not flagged non-monotonic), else TMAX_UNKNOWN.  A continuing flow then reads its first
+// packet's descriptor only when the batch reaches an inactive or active boundary of its record
+// (the checks below cannot fire otherwise): one random 128-byte line less per flow on the 1M-flow
+// mixes, where most flows continue.
+constexpr uint32_t TMAX_UNKNOWN = 0xFFFFFFFFu;
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
                                                    bool force_cx, uint32_t* col, RecW& er, bool fuse = false,
-                                                   bool slot_clean = false) {
+                                                   bool slot_clean = false, uint32_t tmax = TMAX_UNKNOWN) {
     FinResult res = {FIN_DONE, false, false, false, 0};
     const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
     RecW rec;
     if (live) rec_load_head_w(&t.cold[s], rec);
-    const ipxg_pkt_desc df = b.desc[first];
+    ipxg_pkt_desc df;
+    bool have_df = false;
+    if (!live || tmax == TMAX_UNKNOWN) {
+        df = b.desc[first];
+        have_df = true;
+    }
     const ipxg_pkt_desc dl = b.desc[last];
     const uint32_t cdf = p.split_biflow ? 0u : first_dir(h.first_n);
     const uint32_t I = p.inactive_s, A = p.active_s;
@@ -1032,11 +1043,25 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     if (live) {
         const bool dsrc = p.split_biflow || cdf == creator;
         const uint32_t flw = dsrc ? rw_sflags(rec) : rw_dflags(rec);
-        if (first_syn(h.first_n) && (flw & 0x05)) bsplit = IPXG_FLOW_END_EOF;
-        else if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TLS] >= (int64_t)I) bsplit = export_reason_w(rec);
-        else if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TFS] >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
+        if (first_syn(h.first_n) && (flw & 0x05)) {
+            bsplit = IPXG_FLOW_END_EOF;
+        } else {
+            if (!have_df && ((int64_t)tmax - (int64_t)rec.w[RW_TLS] >= (int64_t)I ||
+                             (int64_t)tmax - (int64_t)rec.w[RW_TFS] >= (int64_t)A)) {
+                df = b.desc[first];
+                have_df = true;
+            }
+            if (have_df) {
+                if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TLS] >= (int64_t)I) bsplit = export_reason_w(rec);
+                else if ((int64_t)df.ts_sec - (int64_t)rec.w[RW_TFS] >= (int64_t)A) bsplit = IPXG_FLOW_END_ACTIVE;
+            }
+        }
     }
     const bool cont = live && !bsplit;
+    if (!cont && !have_df) {  // (a SYN-after-FIN split: the new record starts at the first packet)
+        df = b.desc[first];
+        have_df = true;
+    }
     bool cx = force_cx || (h.state & SLOT_HOST);  // a process plugin's flow: the host walks it
     const uint32_t tb = h.tbits;
     if (tb >> 31) cx = true;
