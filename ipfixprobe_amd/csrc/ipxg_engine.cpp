@@ -39,11 +39,12 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
-// Host memory for the walk's device-to-host copies: page-aligned malloc memory, page-locked with
-// hipHostRegister (so the DMA engine writes it directly, without the runtime's pageable staging)
-// and read by the CPU through its caches (hipHostMalloc'd memory read slower in the walk,
-// DESIGN 4.4).  Contents are not kept when it grows (each batch overwrites it).
-// IPXG_WALK_PAGEABLE=1 leaves it pageable (A/B).
+// Host memory for the walk's copies and for the write-back kernel: pinned allocations from the
+// HIP runtime (hipHostMalloc, mapped: a device-visible address in `dev`), growth only -- each
+// engine allocates a few and frees them at destroy.  (Earlier: malloc memory registered with
+// hipHostRegister and unregistered on growth; full GPU test runs then failed intermittently with
+// faults surfacing at later pageable copies -- the runtime-managed pinned path replaced it.)
+// IPXG_WALK_PAGEABLE=1: plain malloc memory, copies through the runtime's staging (A/B).
 static std::atomic<uint64_t> g_hostvec_allocs{0}, g_hostvec_unpinned{0};  // (IPXG_WALK_TRACE)
 template <class T>
 struct HostVec {
@@ -57,8 +58,8 @@ struct HostVec {
     ~HostVec() { release(); }
     void release() {
         if (p) {
-            if (reg) (void)hipHostUnregister(p);
-            std::free(p);
+            if (reg) (void)hipHostFree(p);
+            else std::free(p);
         }
         p = dev = nullptr;
         n = cap = 0;
@@ -70,14 +71,15 @@ struct HostVec {
         const size_t want = std::max(k, cap + cap / 2 + 1024);
         const size_t bytes = (want * sizeof(T) + 4095) & ~(size_t)4095;
         void* q = nullptr;
-        if (posix_memalign(&q, 4096, bytes)) return false;
+        bool pinned = pin && hipHostMalloc(&q, bytes, hipHostMallocMapped) == hipSuccess;
+        if (!pinned && posix_memalign(&q, 4096, bytes)) return false;
         const size_t kept = keep ? n : 0;
         if (kept) std::memcpy(q, p, kept * sizeof(T));
         release();
         p = static_cast<T*>(q);
         cap = bytes / sizeof(T);
         n = kept;
-        reg = pin && hipHostRegister(p, bytes, hipHostRegisterMapped) == hipSuccess;
+        reg = pinned;
         if (reg && hipHostGetDevicePointer((void**)&dev, p, 0) != hipSuccess) dev = nullptr;
         g_hostvec_allocs++;
         if (pin && !reg) g_hostvec_unpinned++;
