@@ -73,8 +73,11 @@ inline void fill_packet(ipxp::Packet& k, const ipxg_packet_view& v) {
     k.packet_len = (uint16_t)v.caplen;
     k.packet_len_wire = (uint16_t)v.wirelen;
     k.payload = v.data + p.payload_off;
-    k.payload_len = p.payload_len;
-    k.payload_len_wire = p.payload_len;
+    // (payload_len can run past the captured bytes on malformed lengths -- parser.cpp:780-797 in
+    // uint16_t; the reference's plugins then read past the frame: here the view ends at caplen)
+    const uint32_t cap_left = p.payload_off < v.caplen ? v.caplen - p.payload_off : 0u;
+    k.payload_len = (uint16_t)(p.payload_len < cap_left ? p.payload_len : cap_left);
+    k.payload_len_wire = k.payload_len;
     k.source_pkt = v.source_pkt != 0;
 }
 

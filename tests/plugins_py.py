@@ -33,7 +33,11 @@ def _pkt(view):
     p = np.frombuffer((ctypes.c_uint8 * pcaputil.PARSED_DTYPE.itemsize).from_address(v.pkt),
                       dtype=pcaputil.PARSED_DTYPE)[0]
     off, n = int(p["payload_off"]), int(p["payload_len"])
-    data = bytes(v.data[off:off + n]) if n else b""
+    # Packet::payload_len can run past the captured bytes (uint16_t wraps of malformed lengths,
+    # parser.cpp:780-797; the reference reads whatever follows): bytes at or past caplen read as 0
+    cap = int(v.caplen)
+    end = min(off + n, cap)
+    data = (bytes(v.data[off:end]) if end > off else b"") + bytes(max(0, off + n - max(end, off))) if n else b""
     return p, data
 
 
