@@ -267,6 +267,9 @@ struct ipxg_engine {
     uint64_t strict_q = 0;  // sweep steps taken (keyed packets + expire calls): the cursor
     DevBuf st_pkt, st_crec, st_keyed, st_qx, st_keys, st_vals, st_keys2, st_vals2, st_succ, st_pred, st_indeg, st_queue;
     // host-side counters
+    BinView bins_last = {};   // the last binned batch's partition records (k_complex_gather_rec)
+    bool bins_valid = false;
+    uint64_t gather_fallbacks = 0;  // complex gathers redone by re-parse (a complex flow in a tile aggregate)
     uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0, walked_pkts = 0;
     bool prev_valid = false;
     uint32_t prev_sec = 0, prev_usec = 0;
@@ -652,10 +655,12 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e && e->walk_trace && e->tm.plugin_flows)
         std::fprintf(stderr,
                      "ipxg plugin walk ms: order %.1f copies %.1f walk %.1f back %.1f"
-                     " | minor faults: %ld %ld %ld %ld | host buffers allocated %lu, not page-locked %lu\n",
+                     " | minor faults: %ld %ld %ld %ld | host buffers allocated %lu, not page-locked %lu"
+                     " | complex gathers re-parsed %lu\n",
                      e->walk_phase_ms[0], e->walk_phase_ms[1], e->walk_phase_ms[5], e->walk_phase_ms[6],
                      e->walk_faults[0], e->walk_faults[1], e->walk_faults[5], e->walk_faults[6],
-                     (unsigned long)g_hostvec_allocs.load(), (unsigned long)g_hostvec_unpinned.load());
+                     (unsigned long)g_hostvec_allocs.load(), (unsigned long)g_hostvec_unpinned.load(),
+                     (unsigned long)e->gather_fallbacks);
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
@@ -912,8 +917,11 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     Params p = params(e);
     FragView fv = frag_view(e);
     BinView bins = {};
+    e->bins_valid = false;
     if (binned) {
         if ((rc = setup_bins(e, n, bins))) return rc;
+        e->bins_last = bins;
+        e->bins_valid = true;
         if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
     }
     if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
@@ -1639,7 +1647,23 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         if ((rc = ensure(e, e->cx_sorted, (size_t)npk * 8 + 8))) return rc;
         cx.list = (uint64_t*)e->cx_list.p;
         cx.sorted = (uint64_t*)e->cx_sorted.p;
-        launch_complex_gather(e->st, bv, p, table_view(e), frag_view(e), cx, e->ctl_d);
+        // the complex flows' packets: from the batch's partition records when every packet left
+        // one (no spills, deferrals or fragments), else -- or when a complex flow was folded into a
+        // tile aggregate -- by re-parsing the frames
+        bool by_rec = binned && e->bins_valid && !c1.spilled && !c1.deferred && !c1.a_deferred && !c1.agg_deferred &&
+                      !c1.frag_count && !std::getenv("IPXG_GATHER_PARSE");
+        if (by_rec) {
+            HIPCHK(e, hipMemsetAsync(&e->ctl_d->cx_agg, 0, sizeof(uint32_t), e->st));
+            launch_complex_gather_rec(e->st, e->bins_last, cx, e->ctl_d);
+            HIPCHK(e, hipGetLastError());
+            if ((rc = sync_ctl(e))) return rc;
+            if (e->ctl_h->cx_agg) {  // start over: cursors back to 0
+                by_rec = false;
+                e->gather_fallbacks++;
+                HIPCHK(e, hipMemsetAsync(cx.cursor, 0, (size_t)ncx * sizeof(uint32_t), e->st));
+            }
+        }
+        if (!by_rec) launch_complex_gather(e->st, bv, p, table_view(e), frag_view(e), cx, e->ctl_d);
         HIPCHK(e, hipGetLastError());
         int bits = 24;
         while ((1ull << (bits - 24)) < ncx) bits++;

@@ -1553,4 +1553,40 @@ void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, 
     hipLaunchKernelGGL(k_complex_gather, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, f, cx, ctl);
 }
 
+// The complex flows' packets from the batch's partition records instead of the frames: 16 bytes
+// per packet read, no parse (the re-parse gather reads every frame head and parses it).  A thread
+// per segment (a k_bin / k_bin_slow workgroup's records of one partition: a few records each on
+// the 1M-flow mixes).  A complex flow with packets folded into a tile aggregate (no per-packet
+// index left) flags the batch for the re-parse gather.
+__global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexView cx, BatchCtl* ctl, uint32_t nseg) {
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nseg; s += gridDim.x * 256) {
+        const uint32_t c = s % bv.cols;
+        if (c >= bv.bin_grid && !bv.slow_cnt[c - bv.bin_grid]) continue;  // (a k_bin_slow column left unwritten)
+        const uint32_t n = bv.count[s];
+        const uint4* seg = bv.rec + (size_t)s * bv.seg_cap;
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint4 r = seg[j];
+            if (r.z == NO_REC) continue;
+            if (rec_is_agg(r)) {
+                if (rec_agg_slot(r) == 0 && complex_rank_of(cx, ((uint64_t)r.y << 32) | r.x) >= 0)
+                    atomicOr(&ctl->cx_agg, 1u);
+                continue;
+            }
+            const int64_t rr = complex_rank_of(cx, ((uint64_t)r.y << 32) | r.x);
+            if (rr < 0) continue;
+            const uint32_t rk = (uint32_t)rr;
+            const uint32_t pos = atomicAdd(&cx.cursor[rk], 1u);
+            if (pos < cx.len[rk]) cx.list[cx.seg[rk] + pos] = ((uint64_t)rk << 24) | (r.z & 0xFFFFFFu);
+            else atomicOr(&ctl->guard, 2u);
+        }
+    }
+}
+
+void launch_complex_gather_rec(hipStream_t st, const BinView& bv, ComplexView cx, BatchCtl* ctl) {
+    const uint32_t nseg = (1u << bv.part_bits) * bv.cols;
+    uint32_t g = (nseg + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_complex_gather_rec, dim3(g ? g : 1), dim3(256), 0, st, bv, cx, ctl, nseg);
+}
+
 }  // namespace ipxg

@@ -66,6 +66,7 @@ struct BatchCtl {
     uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
     uint32_t tb_any;         // OR of the time buckets of k_bin / k_bin_slow's records (0: all in bucket 0)
     uint32_t fin_deferred;   // finalise-list aggregates whose table probe failed (k_fin_list: table full)
+    uint32_t cx_agg;         // k_complex_gather_rec: a complex flow's packets were folded into a tile aggregate
     uint32_t guard;          // bounds guards that fired (engine bug, reported as IPXG_EDEVICE): 1 more complex
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
                              // past the table
@@ -317,6 +318,9 @@ void launch_finalize(hipStream_t st, const BatchView& b, const Params& p, TableV
 void launch_complex_rank(hipStream_t st, TableView t, ComplexView cx, BatchCtl* ctl, uint32_t cap, uint32_t ncx);
 void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                            ComplexView cx, BatchCtl* ctl);
+// the same from the batch's partition records (k_bin / k_bin_slow), when every packet of the batch
+// left one (no spills, deferrals or fragments); ctl->cx_agg set: redo with the re-parse above
+void launch_complex_gather_rec(hipStream_t st, const BinView& bv, ComplexView cx, BatchCtl* ctl);
 void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                          ComplexView cx, uint32_t nranks, ExportView ex, BatchCtl* ctl,
                          unsigned long long* stats);
