@@ -250,6 +250,10 @@ struct ipxg_engine {
     DevBuf stage_arena[2], stage_desc[2];
     hipStream_t cst = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr};
+    // k_classify runs beside k_bin / k_bin_slow (neither reads the flow table) on its own
+    // stream; k_reduce waits for it
+    hipStream_t cls_st = nullptr;
+    hipEvent_t cls_fork = nullptr, cls_join = nullptr;
     int stage_next = 0;
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     DevBuf ipf_msg, ipf_plan;                   // IPFIX messages: output, plan (sets + messages)
@@ -676,6 +680,9 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->cst) (void)hipStreamDestroy(e->cst);
     for (hipEvent_t ev : e->copied)
         if (ev) (void)hipEventDestroy(ev);
+    if (e->cls_st) (void)hipStreamDestroy(e->cls_st);
+    for (hipEvent_t ev : {e->cls_fork, e->cls_join})
+        if (ev) (void)hipEventDestroy(ev);
     if (e->pstat_d) hipFree(e->pstat_d);
     hipFree(e->sv.rec);
     hipFree(e->sv.hash);
@@ -925,9 +932,21 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
     }
     if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
-    if (!e->plugins.empty() && binned)  // the process plugins' flows: SLOT_PLUGIN, before the ingest
-        launch_classify(e->st, bv, p, table_view(e), (const DevRule*)e->rules_d.p, (uint32_t)e->plugins.size(),
+    // the process plugins' flows: SLOT_PLUGIN in the table before k_reduce folds the batch;
+    // k_bin and k_bin_slow only write partition records, so k_classify runs beside them
+    const bool classify = !e->plugins.empty() && binned;
+    if (classify) {
+        if (!e->cls_st) {
+            HIPCHK(e, hipStreamCreateWithFlags(&e->cls_st, hipStreamNonBlocking));
+            HIPCHK(e, hipEventCreateWithFlags(&e->cls_fork, hipEventDisableTiming));
+            HIPCHK(e, hipEventCreateWithFlags(&e->cls_join, hipEventDisableTiming));
+        }
+        HIPCHK(e, hipEventRecord(e->cls_fork, e->st));
+        HIPCHK(e, hipStreamWaitEvent(e->cls_st, e->cls_fork, 0));
+        launch_classify(e->cls_st, bv, p, table_view(e), (const DevRule*)e->rules_d.p, (uint32_t)e->plugins.size(),
                         e->ctl_d);
+        HIPCHK(e, hipEventRecord(e->cls_join, e->cls_st));
+    }
     ev_rec(e, 0);
     if (binned) {
         uint32_t* dl = (uint32_t*)e->defer_a.p;
@@ -938,6 +957,7 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
         ev_rec(e, 1);
         launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 2);
+        if (classify) HIPCHK(e, hipStreamWaitEvent(e->st, e->cls_join, 0));
         launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
         if (!async) {
             ev_rec(e, 3);
