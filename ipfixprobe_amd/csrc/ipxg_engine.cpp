@@ -261,6 +261,7 @@ struct ipxg_engine {
     size_t plan_h_bytes = 0;
     hipEvent_t plan_ev = nullptr;               // the last plan upload
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
+    uint32_t last_n = 0;                 // its packets
     double skew = 1.0;                   // previous batch: most loaded partition / mean partition
     uint32_t part_bits_last = 0;         // partitions of the last binned batch (log2)
     FragEntry* frag_ent = nullptr;
@@ -339,7 +340,7 @@ static ExportView export_view(ipxg_engine* e) {
 }
 
 // Partitions for k_bin/k_reduce: enough that a partition's flows fit k_reduce's LDS table
-// (RED_TARGET_FLOWS each), estimated from the previous batch / the live table, never more
+// (RED_TARGET_FLOWS each), estimated from the previous batch's touched flows, never more
 // than the batch's packets.  k_bin runs bin_grid persistent workgroups over tiles of
 // BIN_TILE_PKTS packets; each owns one segment per partition, sized for its mean share of the
 // packets times max(3 when aggregating else 1.5, 1.25 x the previous batch's most loaded
@@ -354,10 +355,15 @@ static bool wide_walk(const ipxg_engine* e) {
 }
 
 static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
-    uint64_t est = std::max<uint64_t>(e->live, e->last_touched);
+    // the flows this batch touches: the previous batch's (scaled up to a larger batch), else the
+    // live table's, else one per packet
+    uint64_t est = e->last_touched ? e->last_touched : e->live;
+    if (e->last_touched && e->last_n && n > e->last_n) est = est * n / e->last_n;
     if (est == 0 || est > n) est = n;
     uint32_t bits = 0;
     while (bits < BIN_MAX_PART_BITS && ((uint64_t)RED_TARGET_FLOWS << bits) < est) bits++;
+    // at least a workgroup per CU (256) while partitions keep >= RED_MIN_FLOWS flows each
+    while (bits < 8 && ((uint64_t)RED_MIN_FLOWS << bits) < est) bits++;
     if (const char* pb = std::getenv("IPXG_PART_BITS"))  // tuning knob (experiments only)
         bits = std::min<uint32_t>((uint32_t)std::atoi(pb), BIN_MAX_PART_BITS);
     const uint32_t P = 1u << bits;
@@ -1722,6 +1728,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     e->live += c2.cx_new_live;
     e->live = (uint32_t)((int64_t)e->live + plugin_live);
     e->last_touched = c2.touched;
+    e->last_n = n;
     if (binned && c2.total_slots) {  // the next batch's segment sizing
         const uint32_t P = 1u << e->part_bits_last;
         e->skew = (double)c2.max_part * P / c2.total_slots;

@@ -203,7 +203,11 @@ constexpr uint32_t RED_THREADS = 1024;      // k_reduce workgroup
 #define IPXG_RED_ENTRIES 2048
 #endif
 constexpr uint32_t RED_ENTRIES = IPXG_RED_ENTRIES;  // k_reduce LDS flow table (56 B entries)
-constexpr uint32_t RED_TARGET_FLOWS = 600;  // flows per partition the host sizes for
+// flows per partition the host sizes for: <= 0.6 of the LDS table's entries (linear probing).
+// (600 until round 3: on the 1M-flow mixes twice the k_reduce workgroups, each zeroing and
+// scanning its LDS table for half the flows -- k_reduce -30 % quic, -50 % imix at 1200)
+constexpr uint32_t RED_TARGET_FLOWS = 1200;
+constexpr uint32_t RED_MIN_FLOWS = 256;  // below 256 partitions (one per CU), flows per partition at least
 
 struct ComplexView {
     uint64_t* list;      // (rank << 24) | packet index

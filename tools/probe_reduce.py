@@ -30,7 +30,7 @@ def main(name):
     st = eng.stats()
     flows = st["flows_in_cache"]
     bits = 0
-    while (600 << bits) < flows and bits < 12:
+    while (1200 << bits) < flows and bits < 11:
         bits += 1
     P = 1 << bits
     print("%s: %d packets per batch, %d flows in cache, ~%d partitions (k_reduce workgroups)" % (name, n, flows, P))
