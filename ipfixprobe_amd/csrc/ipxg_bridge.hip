@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_plugin_keys(TableView t, ComplexView cx
                                                      uint32_t* count) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= ncx) return;
-    const bool host = (t.hot[cx.slot_of[r]].state & SLOT_HOST) != 0;
+    const bool host = (t.hot(cx.slot_of[r]).state & SLOT_HOST) != 0;
     keys[r] = host ? ((cx.sorted[cx.seg[r]] & 0xFFFFFFull) << 32) | r : PF_NONE;
     // one atomic per wave
     const uint64_t m = __ballot(host);
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx
     }
     const uint32_t r = (uint32_t)skeys[k];
     const uint32_t s = cx.slot_of[r];
-    const HotSlot h = t.hot[s];
+    const HotSlot h = t.hot(s);
     PluginFlow f;
     f.slot = s;
     f.seg = cx.seg[r];
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void k_plugin_pack(TableView t, ComplexView cx
     f.state = h.state;
     f.key = h.key;
     f.pad = 0;
-    f.rec = t.cold[s];
+    f.rec = tbl_rec(t, s);
     out[k] = f;
     flen[k] = f.len;
     hstate[k] = f.state;
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void k_plugin_apply(TableView t, const PluginF
         atomicOr(&ctl->guard, 4u);
         return;
     }
-    clear_slot(&t.hot[slot], flows[k].key, state[k] & (SLOT_LIVE | SLOT_FOLLOW));
+    clear_slot(&t.hot(slot), flows[k].key, state[k] & (SLOT_LIVE | SLOT_FOLLOW));
 }
 
 __global__ __launch_bounds__(256) void k_plugin_apply_recs(TableView t, const PluginFlow* flows, uint32_t nf,
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void k_plugin_apply_recs(TableView t, const Pl
         atomicOr(&ctl->guard, 4u);
         return;
     }
-    t.cold[flows[k].slot] = r;
+    tbl_put_rec(t, flows[k].slot, r);
 }
 
 void launch_plugin_apply(hipStream_t st, TableView t, const PluginFlow* flows, const uint32_t* state, uint32_t nf,

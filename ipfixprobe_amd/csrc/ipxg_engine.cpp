@@ -171,8 +171,8 @@ struct ipxg_engine {
     std::string err;
     // flow table
     uint32_t cap = 0;
-    HotSlot* hot = nullptr;
-    ipxg_flow_record* cold = nullptr;
+    SlotLine* line = nullptr;  // hot slot + record head per slot (TableView)
+    uint32_t* tail = nullptr;  // record tails
     uint32_t* slot_rank = nullptr;
     uint32_t keys = 0, live = 0;
     // export buffer: records [ex_head, ex_count) are pending
@@ -328,7 +328,7 @@ static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
 }
 
 static TableView table_view(ipxg_engine* e) {
-    return TableView{e->hot, e->cold, e->slot_rank, e->cap - 1, e->pstat_d};  // pstat_d starts with the ports
+    return TableView{e->line, e->tail, e->slot_rank, e->cap - 1, e->pstat_d};  // pstat_d starts with the ports
 }
 
 static ExportView export_view(ipxg_engine* e) {
@@ -430,18 +430,18 @@ static Params params(ipxg_engine* e) {
     return p;
 }
 
-static int alloc_table(ipxg_engine* e, uint32_t cap, HotSlot** hot, ipxg_flow_record** cold, uint32_t** rank) {
-    if (hipMalloc((void**)hot, sizeof(HotSlot) * (size_t)cap) != hipSuccess) return IPXG_ENOMEM;
-    if (hipMalloc((void**)cold, sizeof(ipxg_flow_record) * (size_t)cap) != hipSuccess) {
-        hipFree(*hot);
+static int alloc_table(ipxg_engine* e, uint32_t cap, SlotLine** line, uint32_t** tail, uint32_t** rank) {
+    if (hipMalloc((void**)line, sizeof(SlotLine) * (size_t)cap) != hipSuccess) return IPXG_ENOMEM;
+    if (hipMalloc((void**)tail, sizeof(uint32_t) * REC_TAIL_WORDS * (size_t)cap) != hipSuccess) {
+        hipFree(*line);
         return IPXG_ENOMEM;
     }
     if (hipMalloc((void**)rank, sizeof(uint32_t) * (size_t)cap) != hipSuccess) {
-        hipFree(*hot);
-        hipFree(*cold);
+        hipFree(*line);
+        hipFree(*tail);
         return IPXG_ENOMEM;
     }
-    HIPCHK(e, hipMemsetAsync(*hot, 0, sizeof(HotSlot) * (size_t)cap, e->st));
+    HIPCHK(e, hipMemsetAsync(*line, 0, sizeof(SlotLine) * (size_t)cap, e->st));
     return IPXG_OK;
 }
 
@@ -486,8 +486,8 @@ static int sync_ctl(ipxg_engine* e) {
 
 // Rebuild the table at new_cap, dropping dead slots (no live record, untouched).
 static int rehash(ipxg_engine* e, uint32_t new_cap) {
-    HotSlot* nh;
-    ipxg_flow_record* nc;
+    SlotLine* nh;
+    uint32_t* nc;
     uint32_t* nr;
     int rc = alloc_table(e, new_cap, &nh, &nc, &nr);
     if (rc) return set_err(e, rc, "table allocation failed (capacity " + std::to_string(new_cap) + ")");
@@ -498,11 +498,11 @@ static int rehash(ipxg_engine* e, uint32_t new_cap) {
     uint32_t fail = 0;
     HIPCHK(e, hipMemcpyAsync(&fail, e->misc_d, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
-    HIPCHK(e, hipFree(e->hot));
-    HIPCHK(e, hipFree(e->cold));
+    HIPCHK(e, hipFree(e->line));
+    HIPCHK(e, hipFree(e->tail));
     HIPCHK(e, hipFree(e->slot_rank));
-    e->hot = nh;
-    e->cold = nc;
+    e->line = nh;
+    e->tail = nc;
     e->slot_rank = nr;
     e->cap = new_cap;
     e->rehashes++;
@@ -609,7 +609,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     // the reference sizes its table 2^s with 16-way lines; ours is open-addressed and grows,
     // so start at 2^s but never below 2^16
     uint32_t cap = 1u << std::max<uint32_t>(cfg->cache_exp, 16);
-    if ((rc = alloc_table(e, cap, &e->hot, &e->cold, &e->slot_rank))) return fail(rc);
+    if ((rc = alloc_table(e, cap, &e->line, &e->tail, &e->slot_rank))) return fail(rc);
     e->cap = cap;
     e->ex_cap = 1u << 16;
     if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
@@ -675,8 +675,8 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->st) hipStreamSynchronize(e->st);
     delete e->pool;
     free_walk_copies(e);
-    hipFree(e->hot);
-    hipFree(e->cold);
+    hipFree(e->line);
+    hipFree(e->tail);
     hipFree(e->slot_rank);
     hipFree(e->ex);
     hipFree(e->ctl_d);
@@ -1877,7 +1877,7 @@ int ipxg_reset(ipxg_engine* e) {
         if (rc0) return rc0;
     }
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
-    HIPCHK(e, hipMemsetAsync(e->hot, 0, sizeof(HotSlot) * (size_t)e->cap, e->st));
+    HIPCHK(e, hipMemsetAsync(e->line, 0, sizeof(SlotLine) * (size_t)e->cap, e->st));
     if (e->strict) {
         launch_strict_clear(e->st, e->sv);
         HIPCHK(e, hipGetLastError());

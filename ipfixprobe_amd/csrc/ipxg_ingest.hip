@@ -1260,13 +1260,13 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q) {
         hkey[q] = ht[tid + q * RED_THREADS].key;
-        if (hkey[q] && !unresolved) img[q] = t.hot[(uint32_t)hkey[q] & t.mask];
+        if (hkey[q] && !unresolved) img[q] = t.hot((uint32_t)hkey[q] & t.mask);
     }
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q) {
         old[q] = ~0ull;
         if (hkey[q] && !unresolved && img[q].key == 0)
-            old[q] = atomicCAS((unsigned long long*)&t.hot[(uint32_t)hkey[q] & t.mask].key, 0ull,
+            old[q] = atomicCAS((unsigned long long*)&t.hot((uint32_t)hkey[q] & t.mask).key, 0ull,
                                (unsigned long long)hkey[q]);
     }
 #pragma unroll
@@ -1287,7 +1287,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         } else if (a.key) {
             n_touch++;
             bool claimed = false;
-            HotSlot* hp = &t.hot[(uint32_t)a.key & t.mask];  // this workgroup is the slot's only writer here
+            HotSlot* hp = &t.hot((uint32_t)a.key & t.mask);  // this workgroup is the slot's only writer here
             if (img[q].key == a.key) {
                 // found at home
             } else if (img[q].key == 0 && old[q] == 0) {
@@ -1306,7 +1306,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
             } else {
                 agg_fold(img[q], a);
                 if (fuse) {  // the merged image goes to k_fin_list, which writes the slot back
-                    img[q].pad = (uint32_t)(hp - t.hot);
+                    img[q].pad = t.slot_index(hp);
                     listed[q] = true;
                     n_list++;
                 } else {
@@ -1435,7 +1435,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
             } else {
                 n_keys += claimed ? 1u : 0u;
                 agg_fold(img, a);
-                img.pad = (uint32_t)(hp - t.hot);
+                img.pad = t.slot_index(hp);
                 h = img;
                 if (deferred_only) fin_list[k].pad = FIN_UNRESOLVED;  // done: later re-runs skip it
             }

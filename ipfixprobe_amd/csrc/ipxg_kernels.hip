@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
     __syncthreads();
     uint32_t keys = 0, live_n = 0, cx_n = 0, ex_n = 0;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const HotSlot h = t.hot[s];
+        const HotSlot h = t.hot(s);
         bool do_export = false;
         uint8_t reason = 0;
         RecW er;
@@ -345,10 +345,10 @@ __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView c
     __syncthreads();
     const uint32_t s0 = blockIdx.x * span, s1 = min(cap, s0 + span);
     for (uint32_t s = s0 + tid; s < s1; s += 256) {
-        const uint64_t key = t.hot[s].key;
-        const uint32_t st = t.hot[s].state;
+        const uint64_t key = t.hot(s).key;
+        const uint32_t st = t.hot(s).state;
         if (key == 0 || !(st & SLOT_COMPLEX)) continue;
-        const uint64_t a0 = t.hot[s].acc[0], a1 = t.hot[s].acc[1];
+        const uint64_t a0 = t.hot(s).acc[0], a1 = t.hot(s).acc[1];
         const uint32_t k = atomicAdd(&l_n, 1u);
         l_slot[k] = s;
         l_npk[k] = (uint32_t)(a0 >> 40) + (uint32_t)(a1 >> 40);
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView c
         cx.len[r] = npk;
         cx.cursor[r] = 0;
         off += npk;
-        const uint64_t key = t.hot[sl].key;
+        const uint64_t key = t.hot(sl).key;
         uint32_t e = (uint32_t)key & cx.kmask;  // >= 2 entries per complex flow: terminates
         while (atomicCAS(&cx.keys[e], 0ull, (unsigned long long)key) != 0ull) e = (e + 1) & cx.kmask;
         cx.key_rank[e] = r;
@@ -398,12 +398,12 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nranks) return;
     const uint32_t s = cx.slot_of[r];
-    const HotSlot h = t.hot[s];
+    const HotSlot h = t.hot(s);
     if (h.state & SLOT_HOST) return;  // a process plugin's flow: the host walks it (plugin_walk)
     bool live = h.state & SLOT_LIVE;
     if (!live) atomicAdd(&ctl->cx_new_live, 1u);  // the slot ends the walk live
     ipxg_flow_record rec;
-    if (live) rec = t.cold[s];
+    if (live) rec = tbl_rec(t, s);
     const uint32_t seg = cx.seg[r], len = cx.len[r];
     const uint32_t I = p.inactive_s, A = p.active_s;
     uint32_t n_ex = 0;
@@ -453,8 +453,8 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
             }
         }
     }
-    t.cold[s] = rec;
-    clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+    tbl_put_rec(t, s, rec);
+    clear_slot(&t.hot(s), h.key, SLOT_LIVE);
     count_flow_ports(t, rec, len);  // every packet of the walk: the flow's ports
     if (n_ex) atomicAdd(&ctl->exported, n_ex);
 }
@@ -491,11 +491,11 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const uint32_t s = base + j * 256 + threadIdx.x;
         if (s >= cap) continue;
-        const uint64_t key = t.hot[s].key;
-        const uint32_t state = t.hot[s].state;
+        const uint64_t key = t.hot(s).key;
+        const uint32_t state = t.hot(s).state;
         if (key != 0 && (state & SLOT_LIVE) &&
-            now - (int64_t)t.cold[s].time_last_sec >= (int64_t)p.inactive_s) {
-            t.hot[s].state = state & ~SLOT_LIVE;
+            now - (int64_t)t.line[s].head[RW_TLS] >= (int64_t)p.inactive_s) {
+            t.hot(s).state = state & ~SLOT_LIVE;
             mask |= 1u << j;
             c++;
         }
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
         const bool mine = mask >> j & 1;
         RecW rec;
         if (mine) {
-            rec = rec_load_w(&t.cold[base + j * 256 + threadIdx.x]);
+            rec = tbl_load_rec(t, base + j * 256 + threadIdx.x);
             const uint8_t reason = export_reason_w(rec);
             store_export_w(ex, pos++, rec, reason);
             count_export_w(sc, rec, reason);
@@ -552,12 +552,12 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const uint32_t s = base + j * 256 + threadIdx.x;
         if (s >= cap) continue;
-        if (t.hot[s].key == 0) continue;  // an empty slot is all zero already
-        if (t.hot[s].state & SLOT_LIVE) {
+        if (t.hot(s).key == 0) continue;  // an empty slot is all zero already
+        if (t.hot(s).state & SLOT_LIVE) {
             mask |= 1u << j;
             c++;
         }
-        uint4* z = reinterpret_cast<uint4*>(&t.hot[s]);
+        uint4* z = reinterpret_cast<uint4*>(&t.hot(s));
         z[0] = z[1] = z[2] = z[3] = make_uint4(0, 0, 0, 0);
     }
     uint32_t total;
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         const bool mine = mask >> j & 1;
         RecW rec;
         if (mine) {
-            rec = rec_load_w(&t.cold[base + j * 256 + threadIdx.x]);
+            rec = tbl_load_rec(t, base + j * 256 + threadIdx.x);
             store_export_w(ex, pos++, rec, IPXG_FLOW_END_FORCED);
             atomicAdd(&pb[pkts_bucket((uint64_t)rec.w[RW_SPK] + rec.w[RW_DPK])], 1u);
         }
@@ -602,13 +602,13 @@ void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, uns
 __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_cap, TableView to,
                                                 uint32_t* fail) {
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < from_cap; s += gridDim.x * blockDim.x) {
-        const HotSlot h = from.hot[s];
+        const HotSlot h = from.hot(s);
         if (h.key == 0) continue;
         if (!(h.state & (SLOT_LIVE | SLOT_COMPLEX | SLOT_HOST)) && h.last1 == 0) continue;  // dead slot
         uint32_t ns = (uint32_t)h.key & to.mask;
         bool ok = false;
         for (uint32_t probe = 0; probe <= to.mask; ++probe) {
-            unsigned long long old = atomicCAS((unsigned long long*)&to.hot[ns].key, 0ull,
+            unsigned long long old = atomicCAS((unsigned long long*)&to.hot(ns).key, 0ull,
                                                (unsigned long long)h.key);
             if (old == 0) {
                 ok = true;
@@ -621,10 +621,10 @@ __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_ca
             continue;
         }
         HotSlot c = h;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&to.hot[ns]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&to.hot(ns));
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&c);
         for (int k = 2; k < 16; ++k) dst[k] = src[k];  // key already claimed
-        to.cold[ns] = from.cold[s];
+        tbl_store_rec(to, ns, tbl_load_rec(from, s));
     }
 }
 
@@ -635,7 +635,7 @@ void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView 
 __global__ __launch_bounds__(256) void k_count(TableView t, uint32_t cap, BatchCtl* ctl) {
     uint32_t keys = 0, live = 0;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const HotSlot& h = t.hot[s];
+        const HotSlot& h = t.hot(s);
         if (h.key) {
             keys++;
             if (h.state & SLOT_LIVE) live++;

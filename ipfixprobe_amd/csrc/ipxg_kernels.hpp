@@ -99,12 +99,27 @@ __host__ __device__ inline uint32_t pkts_bucket(uint64_t n) {
 }
 
 // Everything a kernel needs about the engine, passed by value.
+// A slot's 128-byte line: its hot half and the first half of its flow record (the words a
+// continuing flow's batch reads and updates: times, counters, TCP flags), so the finalise of a
+// continuing flow touches one line; the record's second half (addresses, MACs, VLAN, extension),
+// written at creation and read at export, lives in a table of its own (`tail`).
+struct alignas(128) SlotLine {
+    HotSlot hot;
+    uint32_t head[16];  // ipxg_flow_record bytes 0-63
+};
+static_assert(sizeof(SlotLine) == 128, "slot line");
+constexpr uint32_t REC_TAIL_WORDS = 16;  // ipxg_flow_record bytes 64-127 per slot
+
 struct TableView {
-    HotSlot* hot;
-    ipxg_flow_record* cold;
+    SlotLine* line;
+    uint32_t* tail;  // REC_TAIL_WORDS per slot
     uint32_t* slot_rank;
     uint32_t mask;  // capacity - 1
     unsigned long long* port_cnt;  // ps=true: TopPorts' TCP then UDP frequencies (2 x 65536), else null
+    __host__ __device__ HotSlot& hot(uint32_t s) const { return line[s].hot; }
+    __host__ __device__ uint32_t slot_index(const HotSlot* h) const {
+        return (uint32_t)(reinterpret_cast<const SlotLine*>(h) - line);
+    }
 };
 
 struct ExportView {

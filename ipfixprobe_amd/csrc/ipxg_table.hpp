@@ -153,7 +153,7 @@ __device__ __forceinline__ HotSlot* probe_insert(const TableView& t, uint64_t lo
     uint32_t s = (uint32_t)lo & t.mask;
     claimed = false;
     for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
-        HotSlot* h = &t.hot[s];
+        HotSlot* h = &t.hot(s);
         head = *reinterpret_cast<const uint4*>(h);
         uint64_t k = ((uint64_t)head.y << 32) | head.x;
         if (k == 0) {
@@ -180,7 +180,7 @@ __device__ __forceinline__ HotSlot* probe_insert_full(const TableView& t, uint64
     uint32_t s = (uint32_t)lo & t.mask;
     claimed = false;
     for (uint32_t probe = 0; probe < MAX_PROBE; ++probe) {
-        HotSlot* p = &t.hot[s];
+        HotSlot* p = &t.hot(s);
         h = *p;
         if (h.key == 0) {
             const unsigned long long old = atomicCAS((unsigned long long*)&p->key, 0ull, (unsigned long long)lo);
@@ -205,7 +205,7 @@ __device__ __forceinline__ HotSlot* probe_insert_full(const TableView& t, uint64
 __device__ __forceinline__ int64_t probe_find(const TableView& t, uint64_t lo) {
     uint32_t s = (uint32_t)lo & t.mask;
     for (uint32_t probe = 0; probe <= t.mask; ++probe) {
-        uint64_t k = t.hot[s].key;
+        uint64_t k = t.hot(s).key;
         if (k == lo) return s;
         if (k == 0) return -1;
         s = (s + 1) & t.mask;
@@ -482,6 +482,48 @@ __device__ __forceinline__ void rec_store_w(ipxg_flow_record* p, const RecW& r) 
     uint4* q = reinterpret_cast<uint4*>(p);
 #pragma unroll
     for (int i = 0; i < 8; ++i) q[i] = make_uint4(r.w[4 * i], r.w[4 * i + 1], r.w[4 * i + 2], r.w[4 * i + 3]);
+}
+// the record of slot s in the table: its first half in the slot's line, its second in `tail`
+__device__ __forceinline__ void tbl_load_head(const TableView& t, uint32_t s, RecW& r) {
+    rec_load_head_w(reinterpret_cast<const ipxg_flow_record*>(t.line[s].head), r);
+}
+__device__ __forceinline__ void tbl_load_tail(const TableView& t, uint32_t s, RecW& r) {
+    const uint4* q = reinterpret_cast<const uint4*>(t.tail + (size_t)s * REC_TAIL_WORDS);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = q[i];
+        r.w[16 + 4 * i] = v.x;
+        r.w[16 + 4 * i + 1] = v.y;
+        r.w[16 + 4 * i + 2] = v.z;
+        r.w[16 + 4 * i + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void tbl_store_head(const TableView& t, uint32_t s, const RecW& r) {
+    rec_store_head_w(reinterpret_cast<ipxg_flow_record*>(t.line[s].head), r);
+}
+__device__ __forceinline__ void tbl_store_rec(const TableView& t, uint32_t s, const RecW& r) {
+    tbl_store_head(t, s, r);
+    uint4* q = reinterpret_cast<uint4*>(t.tail + (size_t)s * REC_TAIL_WORDS);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        q[i] = make_uint4(r.w[16 + 4 * i], r.w[16 + 4 * i + 1], r.w[16 + 4 * i + 2], r.w[16 + 4 * i + 3]);
+}
+__device__ __forceinline__ RecW tbl_load_rec(const TableView& t, uint32_t s) {
+    RecW r;
+    tbl_load_head(t, s, r);
+    tbl_load_tail(t, s, r);
+    return r;
+}
+__device__ __forceinline__ ipxg_flow_record tbl_rec(const TableView& t, uint32_t s) {
+    const RecW w = tbl_load_rec(t, s);
+    ipxg_flow_record r;
+    memcpy(&r, &w, sizeof(r));
+    return r;
+}
+__device__ __forceinline__ void tbl_put_rec(const TableView& t, uint32_t s, const ipxg_flow_record& r) {
+    RecW w;
+    memcpy(&w, &r, sizeof(w));
+    tbl_store_rec(t, s, w);
 }
 __device__ __forceinline__ uint8_t export_reason_w(const RecW& r) {
     return ((rw_sflags(r) | rw_dflags(r)) & 0x05) ? IPXG_FLOW_END_EOF : IPXG_FLOW_END_INACTIVE;
@@ -1028,7 +1070,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     const uint32_t first = first_idx(h.first_n), last = h.last1 - 1;
     const bool live = h.state & SLOT_LIVE;
     RecW rec;
-    if (live) rec_load_head_w(&t.cold[s], rec);
+    if (live) tbl_load_head(t, s, rec);
     ipxg_pkt_desc df;
     bool have_df = false;
     if (!live || tmax == TMAX_UNKNOWN) {
@@ -1084,12 +1126,12 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         HotSlot c = h;
         c.state = h.state | SLOT_COMPLEX;
         c.pad = 0;
-        t.hot[s] = c;
+        t.hot(s) = c;
         res.status = FIN_COMPLEX;
         return res;
     }
     if (bsplit) {
-        rec_load_tail_w(&t.cold[s], rec);
+        tbl_load_tail(t, s, rec);
         res.do_export = true;
         res.reason = bsplit;
         er = rec;
@@ -1116,19 +1158,19 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     res.created = !live;
     count_flow_ports_w(t, rec, (uint32_t)(as >> 40) + (uint32_t)(ad >> 40));
     if (fuse && !res.do_export) {
-        if (cont) rec_load_tail_w(&t.cold[s], rec);  // (fused finishes follow an empty table: none)
+        if (cont) tbl_load_tail(t, s, rec);  // (fused finishes follow an empty table: none)
         er = rec;
         res.fin_export = true;
-        clear_slot(&t.hot[s], 0, 0);  // empty (every slot empties at the finish)
+        clear_slot(&t.hot(s), 0, 0);  // empty (every slot empties at the finish)
         return res;
     }
     if (cont) {
-        rec_store_head_w(&t.cold[s], rec);
-        if (!(slot_clean && h.state == SLOT_LIVE)) clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+        tbl_store_head(t, s, rec);
+        if (!(slot_clean && h.state == SLOT_LIVE)) clear_slot(&t.hot(s), h.key, SLOT_LIVE);
         return res;
     }
-    rec_store_w(&t.cold[s], rec);
-    clear_slot(&t.hot[s], h.key, SLOT_LIVE);
+    tbl_store_rec(t, s, rec);
+    clear_slot(&t.hot(s), h.key, SLOT_LIVE);
     return res;
 }
 
