@@ -989,6 +989,35 @@ __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p,
             apply_frag_ports(p, f, idx, pk);
             return true;
         }
+        // the wide register walk (k_bin's: tags, MPLS, PPPoE, IPv6, GRE, TCP timestamps) on the
+        // 80-byte head -- the creators of the configs[2]/[4] mixes' flows, before the LDS walk
+        if ((uint64_t)d.offset + 16u * 5 <= b.arena_lim) {
+            const uint4 z = make_uint4(0, 0, 0, 0);  // (chunks past caplen read as 0, as k_bin's loads)
+            const uint4 c3 = 48u < d.caplen ? fr[3] : z, c4 = 64u < d.caplen ? fr[4] : z;
+            const uint4 cc[5] = {c0, c1, c2, c3, c4};
+            uint32_t w[WIDE_DW];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                w[4 * k] = cc[k].x;
+                w[4 * k + 1] = cc[k].y;
+                w[4 * k + 2] = cc[k].z;
+                w[4 * k + 3] = cc[k].w;
+            }
+            bool ext = false;
+            if (parse_medium(w, d.caplen, p.frag_enable, pk, dummy, ext)) {
+                if (FULL) {
+                    pk.mac_lo = c0.x;
+                    pk.mac_mid = c0.y;
+                    pk.mac_hi = c0.z;
+                    pk.mpls_top = pk.tcp_seq = pk.tcp_ack = pk.tcp_mss = 0;
+                    pk.tcp_options = 0;
+                    pk.tcp_window = 0;
+                    pk.ip_ttl = pk.ip_tos = pk.ip_flags = 0;
+                }
+                apply_frag_ports(p, f, idx, pk);
+                return true;
+            }
+        }
     }
     stage_frame(col, b.arena, d.offset, d.caplen);
     LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};

@@ -304,18 +304,34 @@ class Generator:
         alen = torch.empty(n, dtype=torch.int64, device=self.device)
         if lib().synth_plan(ctypes.byref(p), plan.data_ptr(), alen.data_ptr(), stream):
             raise RuntimeError("synth_plan failed")
-        ends = torch.cumsum(alen, 0)
-        total = int(ends[-1].item()) if n else 0
+        off, total = place(alen, torch)
         if total + 64 >= 1 << 32:
             raise ValueError("batch arena %d B exceeds the 4 GiB descriptor offset range" % total)
-        off = ends - alen
         arena = torch.zeros(total + 64, dtype=torch.uint8, device=self.device)
         desc = torch.empty(n * 16, dtype=torch.uint8, device=self.device)
         if lib().synth_write(ctypes.byref(p), plan.data_ptr(), off.data_ptr(), arena.data_ptr(), desc.data_ptr(),
                              stream):
             raise RuntimeError("synth_write failed")
-        del plan, alen, ends, off
+        del plan, alen, off
         return arena, desc
+
+
+def place(alen, xp):
+    """Frame placement in the arena (the producer's choice: the batch format takes any offsets).
+    Frames longer than 64 bytes start on a 128-byte line (the region they share is laid out in
+    128-byte multiples), so a header walk's head (<= 128 bytes) is one line, not two; frames of
+    <= 64 bytes pack two to a line in a region of their own after it -- as NIC DMA into
+    line-aligned receive buffers from two pools by size would place them.  alen = the frames'
+    64-byte-rounded lengths in packet order (numpy or torch); returns (offsets, arena bytes)."""
+    big = alen > 64
+    abig = xp.where(big, (alen + 127) // 128 * 128, xp.zeros_like(alen))
+    asmall = xp.where(big, xp.zeros_like(alen), xp.full_like(alen, 64))
+    ebig = xp.cumsum(abig, 0) if xp is not np else np.cumsum(abig)
+    esmall = xp.cumsum(asmall, 0) if xp is not np else np.cumsum(asmall)
+    nbig = ebig[-1] if alen.shape[0] else 0
+    off = xp.where(big, ebig - abig, nbig + esmall - asmall)
+    total = (int(nbig) + int(esmall[-1])) if alen.shape[0] else 0
+    return off, total
 
 
 def alg_bytes(desc_np):
@@ -373,8 +389,9 @@ def host_batch(gen, first, n):
     L = mix.layouts[mix.flows["layout"][f].astype(np.int64)]
     g = np.arange(first, first + n, dtype=np.uint64)
     alen = (ln + 63) & ~63
-    off = np.concatenate([[0], np.cumsum(alen)[:-1]]).astype(np.int64)
-    arena = np.zeros(int(alen.sum()) + 64, dtype=np.uint8)
+    off, total = place(alen, np)
+    off = off.astype(np.int64)
+    arena = np.zeros(total + 64, dtype=np.uint8)
     import pcaputil
     desc = np.zeros(n, dtype=pcaputil.DESC_DTYPE)
     t = np.uint64(gen.t0_ns) + g * np.uint64(gen.dt_ns)
