@@ -1483,8 +1483,19 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, 
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
                      bool finishing, bool deferred_only) {
+    // at most one wave of resident workgroups (3 per CU): a grid past it ran its last blocks'
+    // several passes over the list in a second wave on a third of the chip
+    static uint32_t resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fin_list, IPXG_BLOCK, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        resident = (uint32_t)std::max(1, cus * per_cu);
+    }
     uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
-    if (grid > 1024) grid = 1024;
+    if (grid > resident) grid = resident;
     hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, ex, ctl, fin_list,
                        stats, finishing ? 1u : 0u, deferred_only ? 1u : 0u);
 }
