@@ -1377,7 +1377,10 @@ void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSl
 // full near the slot) marks the entry FIN_DEFERRED and counts it in ctl->fin_deferred -- the host
 // grows the table and runs this kernel again over those entries only (deferred_only), not
 // finishing.
-__global__ __launch_bounds__(IPXG_BLOCK) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
+#ifndef IPXG_FIN_WAVES  // tuning knob: k_fin_list's waves per SIMD (register budget)
+#define IPXG_FIN_WAVES 3
+#endif
+__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_FIN_WAVES))) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
                                                          ExportView ex, BatchCtl* ctl, HotSlot* fin_list,
                                                          unsigned long long* stats, uint32_t finishing,
                                                          uint32_t deferred_only) {

@@ -994,15 +994,8 @@ __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p,
         if ((uint64_t)d.offset + 16u * 5 <= b.arena_lim) {
             const uint4 z = make_uint4(0, 0, 0, 0);  // (chunks past caplen read as 0, as k_bin's loads)
             const uint4 c3 = 48u < d.caplen ? fr[3] : z, c4 = 64u < d.caplen ? fr[4] : z;
-            const uint4 cc[5] = {c0, c1, c2, c3, c4};
-            uint32_t w[WIDE_DW];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                w[4 * k] = cc[k].x;
-                w[4 * k + 1] = cc[k].y;
-                w[4 * k + 2] = cc[k].z;
-                w[4 * k + 3] = cc[k].w;
-            }
+            const uint32_t w[WIDE_DW] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y,
+                                         c2.z, c2.w, c3.x, c3.y, c3.z, c3.w, c4.x, c4.y, c4.z, c4.w};
             bool ext = false;
             if (parse_medium(w, d.caplen, p.frag_enable, pk, dummy, ext)) {
                 if (FULL) {
