@@ -610,6 +610,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     // so start at 2^s but never below 2^16
     uint32_t cap = 1u << std::max<uint32_t>(cfg->cache_exp, 16);
     if ((rc = alloc_table(e, cap, &e->line, &e->tail, &e->slot_rank))) return fail(rc);
+    if (const char* a = std::getenv("IPXG_TILE_AGG")) e->tile_agg = std::atoi(a) != 0;  // tests / experiments
     e->cap = cap;
     e->ex_cap = 1u << 16;
     if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);

@@ -531,7 +531,10 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     ParseCounts c = {};
     uint32_t spilled = 0, walked = 0, tb_or = 0;
     constexpr bool XP = IPXG_BIN_XPOSE && !WIDE;
-    constexpr int NC = WIDE ? WIDE_DW / 4 : (XP ? 4 : 3);
+    // the wide walk's window: 96 bytes (WIDE2_DW) without tile aggregation, 80 with it (its
+    // registers: 245 VGPRs at 80 bytes)
+    constexpr int WD = AGG ? WIDE_DW : WIDE2_DW;
+    constexpr int NC = WIDE ? WD / 4 : (XP ? 4 : 3);
     // the wave's transpose area (XP): the stage array is free during the packet loop
     uint4* const xs = reinterpret_cast<uint4*>(stage) + (tid >> 6) * 320u;
     static_assert(IPXG_BLOCK / 64 * 320 <= BIN_TILE, "transpose areas fit the stage array");
@@ -649,7 +652,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             if (act) {
 #endif
                 if constexpr (WIDE) {
-                    uint32_t w[WIDE_DW];
+                    uint32_t w[WD];
 #pragma unroll
                     for (int k = 0; k < NC; ++k) {
                         w[4 * k] = hc.c[k].x;
@@ -658,7 +661,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         w[4 * k + 3] = hc.c[k].w;
                     }
                     bool ext = false;
-                    if (fast_ok && fast_shape(dc) && parse_medium(w, dc.caplen, p.frag_enable, pk, c, ext)) {
+                    if (fast_ok && fast_shape(dc) && parse_medium<false, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
                         have = true;
                         walked += ext ? 1 : 0;
                     } else {

@@ -671,6 +671,9 @@ __device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.o
 // or any read the caplen checks would not cover, returns false and the frame takes the general
 // parser (k_bin_slow).  *ext: the frame is not the plain shape parse_fast takes.
 constexpr int WIDE_DW = 20;  // 80 bytes
+constexpr int WIDE2_DW = 24; // 96 bytes: k_bin's wide walk without tile aggregation (its registers allow
+                             // a sixth chunk): also IPv6 with three 8-byte extension headers (UDP) and
+                             // IPv6 TCP behind one or two, timestamp options included
 
 template <int O>
 __device__ __forceinline__ uint32_t wle32(const uint32_t* w) {
@@ -684,9 +687,11 @@ __device__ __forceinline__ uint32_t wbe16(const uint32_t* w) { return bswap16(wl
 
 // PAY: also Packet::payload / payload_len as parse_frame<true> gives them (parser.cpp:780-797;
 // the pre-classifier of the plugin bridge compares payload prefixes)
-template <bool PAY = false>
-__device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint32_t caplen, bool frag_enable,
+template <bool PAY = false, int WD = WIDE_DW>
+__device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WD], uint32_t caplen, bool frag_enable,
                                              DevPkt& p, ParseCounts& c, bool& ext) {
+    static_assert(WD == WIDE_DW || WD == WIDE2_DW, "window");
+    constexpr bool W2 = WD >= WIDE2_DW;
     // Ethernet + tags (parse_eth_hdr): only the outermost tag's VLAN id is kept
     uint32_t et = wbe16<12>(w), vlan = 0, S = 0;
     if (et == ETH_P_8021AD || et == ETH_P_8021Q) {
@@ -721,14 +726,14 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     }
     if (l3 != ETH_P_IP && l3 != ETH_P_IPV6) return false;
     // the window re-based so that the L3 header starts at byte 14 of v
-    constexpr int VD = WIDE_DW - 2;
+    constexpr int VD = WD - 2;
     uint32_t v[VD];
     // masks rather than a select the compiler could fold into a dynamic index of w (which
     // would put w on the stack)
     const uint32_t m0 = 0u - (S == 0), m1 = 0u - (S == 1), m2 = 0u - (S == 2), m3 = 0u - (S == 3);
 #pragma unroll
     for (int k = 3; k < VD; ++k)
-        v[k] = (w[k] & m0) | (w[k + 1] & m1) | (w[k + 2] & m2) | (k + 3 < WIDE_DW ? w[k + 3] & m3 : 0u);
+        v[k] = (w[k] & m0) | (w[k + 1] & m1) | (w[k + 2] & m2) | (k + 3 < WD ? w[k + 3] & m3 : 0u);
     v[0] = v[1] = v[2] = 0;
     // untagged IPv4 (IHL 5) -> GRE -> IPv4 (parse_ipv4_hdr :320-326, parse_gre :256-302): the
     // outer header sets no field; the inner one starts 6 dwords later plus one per optional
@@ -742,8 +747,8 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
         const uint32_t g0 = 0u - (gopt == 0), g1 = 0u - (gopt == 1), g2 = 0u - (gopt == 2), g3 = 0u - (gopt == 3);
 #pragma unroll
         for (int k = 3; k < VD; ++k)
-            v[k] = (k + 6 < WIDE_DW ? w[k + 6] & g0 : 0u) | (k + 7 < WIDE_DW ? w[k + 7] & g1 : 0u) |
-                   (k + 8 < WIDE_DW ? w[k + 8] & g2 : 0u) | (k + 9 < WIDE_DW ? w[k + 9] & g3 : 0u);
+            v[k] = (k + 6 < WD ? w[k + 6] & g0 : 0u) | (k + 7 < WD ? w[k + 7] & g1 : 0u) |
+                   (k + 8 < WD ? w[k + 8] & g2 : 0u) | (k + 9 < WD ? w[k + 9] & g3 : 0u);
         gre = true;
     }
     const uint32_t o3 = 14 + 4 * S + (gre ? 24u + 4u * gopt : 0u);  // the L3 offset in the frame
@@ -779,13 +784,20 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
                 if (wb8<63>(w) != 0) return false;
                 proto = wb8<62>(w);
                 xh = 2;
+                if constexpr (W2) {  // a third (the 96-byte window)
+                    if (proto == 0 || proto == 43 || proto == 60) {
+                        if (wb8<71>(w) != 0) return false;
+                        proto = wb8<70>(w);
+                        xh = 3;
+                    }
+                }
             } else {
                 proto = p1;
                 xh = 1;
             }
         }
         if (proto != 6 && proto != 17) return false;   // other extension headers (or another L4)
-        if (xh == 2 && proto == 6) return false;        // its TCP header would end past the window
+        if (xh == (W2 ? 3u : 2u) && proto == 6) return false;  // its TCP header would end past the window
         if (S == 3 && proto == 6) return false;         // under 3 MPLS labels: UDP fits, TCP does not
         p.ip_version = 6;
         p.ip_len = (uint16_t)(wbe16<18>(v) + 40);
@@ -807,20 +819,23 @@ __device__ __forceinline__ bool parse_medium(const uint32_t (&w)[WIDE_DW], uint3
     bool tcp_opt = false;
     if (frag_off == 0 && proto == 6) {
         if (caplen < o4 + 20 || gopt > 1) return false;  // (past the window)
-        const uint32_t w3 = v6 ? (xh ? wle32<74>(w) : wle32<66>(v)) : wle32<46>(v);  // L4 bytes 12..15
+        uint32_t w3 = v6 ? (xh ? wle32<74>(w) : wle32<66>(v)) : wle32<46>(v);  // L4 bytes 12..15
+        if constexpr (W2) w3 = xh == 2 ? wle32<82>(w) : w3;
         const uint32_t doff = (w3 & 0xFF) >> 4;
         l4h = 4 * doff;
         if (doff > 5) {
-            if (gre || (v6 && (S != 0 || xh))) return false;  // the options would end past the window
-            const uint32_t opt = v6 ? wle32<74>(w) : wle32<54>(v);  // L4 bytes 20..23
+            if (gre || (v6 && (S != 0 || (!W2 && xh)))) return false;  // the options would end past the window
+            uint32_t opt = v6 ? wle32<74>(w) : wle32<54>(v);  // L4 bytes 20..23
+            if constexpr (W2) opt = v6 ? (xh == 2 ? wle32<90>(w) : (xh ? wle32<82>(w) : opt)) : opt;
             if (doff != 8 || opt != 0x0A080101u || caplen < o4 + 32) return false;
             tcp_opt = true;
         }
         flags = (w3 >> 8) & 0xFF;
-        ports = v6 ? (xh ? wle32<62>(w) : wle32<54>(v)) : wle32<34>(v);
+        ports = v6 ? (xh == 2 ? wle32<70>(w) : (xh ? wle32<62>(w) : wle32<54>(v))) : wle32<34>(v);
     } else if (frag_off == 0 && proto == 17) {
         if (caplen < o4 + 8) return false;
         ports = v6 ? (xh == 2 ? wle32<70>(w) : (xh ? wle32<62>(w) : wle32<54>(v))) : wle32<34>(v);
+        if constexpr (W2) ports = xh == 3 ? wle32<78>(w) : ports;
         l4h = 8;
     }
     if constexpr (PAY) {  // parser.cpp:780-797 in its uint16_t arithmetic (l4 offset o4 != l3 offset)

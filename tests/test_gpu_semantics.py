@@ -452,11 +452,14 @@ def _edge_frames():
 
 @pytest.mark.parametrize("walk", ["", "walk=wide"])
 @pytest.mark.parametrize("frag", [True, False])
-def test_wide_walk_ext_and_gre_edges(walk, frag):
+@pytest.mark.parametrize("agg", ["1", "0"])
+def test_wide_walk_ext_and_gre_edges(walk, frag, agg, monkeypatch):
     """IPv6 extension headers and IPv4-in-GRE at the border of k_bin's register walk (untagged
-    IPv6 + one or two 8-byte extension headers, IPv4 + GRE + IPv4): flow records
-    and parser counters equal the oracle's, truncated copies included."""
+    IPv6 + one to three 8-byte extension headers, IPv4 + GRE + IPv4): flow records
+    and parser counters equal the oracle's, truncated copies included.  agg=0: k_bin without
+    tile aggregation from the first batch on, whose wide walk reads the 96-byte window."""
     from ipfixprobe_amd import run_capture
+    monkeypatch.setenv("IPXG_TILE_AGG", agg)
     arena, desc = synth.to_batch(_edge_frames())
     want, wst = oracle_py.run_capture(arena, desc, 1, cache_exp=20, frag_enable=frag)
     got, gst = run_capture(arena, desc, params=";".join(x for x in (walk, "" if frag else "fe=false") if x))
