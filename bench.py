@@ -419,20 +419,35 @@ def make_workload(args, rank, world, device, local):
     return Workload(args.workload, batches, len(mix.flows), args.batches, True, desc)
 
 
-def rank_flows(mix, rank, world, local):
-    """Indices of the mix's flows whose canonical hash this rank owns."""
+def flow_owners(mix, world, local=0, hasher=None):
+    """The rank (of world) owning each flow of the mix by its canonical hash (shard.owner).
+    hasher(keys, keylen) -> XXH64 per key: the engine's (ipxg_xxh64_batch on GPU `local`) by
+    default; the CPU tests pass the oracle's."""
     from ipfixprobe_amd import Engine, shard
     F = len(mix.flows)
     owner = np.zeros(F, dtype=np.int64)
-    with Engine(device_id=local) as e:
+    e = None
+    if hasher is None:
+        e = Engine(device_id=local)
+        hasher = e.xxh64
+    try:
         for s in range(0, F, 1 << 20):
             sub = mix.flows[s:s + (1 << 20)]
-            owner[s:s + len(sub)] = shard.owner(flow_canon(e, mix, sub), world)
-    return np.nonzero(owner == rank)[0]
+            owner[s:s + len(sub)] = shard.owner(flow_canon(hasher, mix, sub), world)
+    finally:
+        if e is not None:
+            e.close()
+    return owner
 
 
-def flow_canon(e, mix, fl):
-    """Canonical hash of each flow of a synthetic mix from its packed keys (cache.hpp:29-46)."""
+def rank_flows(mix, rank, world, local, hasher=None):
+    """Indices of the mix's flows whose canonical hash this rank owns."""
+    return np.nonzero(flow_owners(mix, world, local, hasher) == rank)[0]
+
+
+def flow_canon(hasher, mix, fl):
+    """Canonical hash of each flow of a synthetic mix from its packed keys (cache.hpp:29-46);
+    hasher(keys, keylen) -> XXH64 per key (Engine.xxh64, or the oracle's on the CPU)."""
     from ipfixprobe_amd import shard
     lay = mix.layouts[fl["layout"].astype(np.int64)]
     v6 = lay["addr_len"] == 16
@@ -456,7 +471,7 @@ def flow_canon(e, mix, fl):
             k[:, 6:6 + al] = a[:, :al]
             k[:, 6 + al:6 + 2 * al] = b[:, :al]
             k[:, 6 + 2 * al:8 + 2 * al] = vl.view(np.uint8).reshape(-1, 2)
-        out[sel] = shard.canonical(e.xxh64(kf.reshape(-1), klen), e.xxh64(ki.reshape(-1), klen))
+        out[sel] = shard.canonical(hasher(kf.reshape(-1), klen), hasher(ki.reshape(-1), klen))
     return out
 
 

@@ -28,8 +28,9 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 3 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
-                              3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk) */
+#define IPXG_ABI_VERSION 4 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+                              3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
+                              4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error) */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -40,6 +41,11 @@ extern "C" {
 #define IPXG_ETOOBIG (-5)  /* batch larger than IPXG_MAX_BATCH or arena > 4 GiB          */
 #define IPXG_EIO (-6)      /* file could not be read / unsupported capture format        */
 #define IPXG_ESTATE (-7)   /* call not valid in the engine's current state               */
+#define IPXG_EPLUGIN (-8)  /* a process plugin's hook failed -- the reference's PluginError
+                              (plugin.hpp:81-91), which its input worker catches and reports
+                              through WorkerResult (workers.cpp:107-112): the message is in
+                              ipxg_last_error, the batch is lost, and the engine accepts only
+                              ipxg_reset / ipxg_destroy / ipxg_last_error until reset        */
 
 #define IPXG_MAX_BATCH (16u * 1024u * 1024u - 1u) /* per-batch counters are 24-bit     */
 
@@ -349,7 +355,10 @@ typedef struct ipxg_packet_view {
  * in order on the host, through these hooks at put_pkt_recursive's call sites.  The record's
  * ext field (a 64-bit handle) is the plugins' per-flow state -- Flow::m_exts: zero on a new
  * record, cleared by erase/reuse, carried by the exported record.  Hooks return 0 or
- * IPXG_FLOW_FLUSH / IPXG_FLOW_FLUSH_WITH_REINSERT. */
+ * IPXG_FLOW_FLUSH / IPXG_FLOW_FLUSH_WITH_REINSERT, or a negative value (IPXG_PLUGIN_ERROR) where
+ * the reference plugin throws PluginError: the walk stops and the call that ran it fails with
+ * IPXG_EPLUGIN.  No C++ exception may leave a hook (the adapter of INTEGRATION.md catches them). */
+#define IPXG_PLUGIN_ERROR (-1)
 typedef struct ipxg_plugin {
     void* ctx;
     uint32_t proto_mask;
@@ -378,6 +387,11 @@ typedef struct ipxg_plugin {
      * engine.  A NULL copy_ctx on any registered plugin keeps the walk on one thread. */
     void* (*copy_ctx)(void* ctx);
     void (*free_ctx)(void* ctx);
+    /* ABI 4: the message of a failure of this instance since the previous call, or NULL
+     * (optional; the string stays valid until the instance fails again).  The engine calls it
+     * after a hook returned IPXG_PLUGIN_ERROR, and after every walk of a batch -- pre_export
+     * returns nothing, so a failure there is reported only here. */
+    const char* (*error)(void* ctx);
 } ipxg_plugin;
 
 /* Register a plugin (the order of registration is the order of the hook calls). */

@@ -126,6 +126,9 @@ public:
         for (std::thread& t : th_) t.join();
     }
     unsigned size() const { return (unsigned)th_.size() + 1; }
+    // true when a job raised out of a worker thread since the last call (then: an engine bug or a
+    // plugin that throws past the C ABI; plugin_walk fails the batch with IPXG_EPLUGIN)
+    bool take_escaped() { return escaped_.exchange(false); }
     void run(const std::function<void(unsigned)>& f) {
         {
             std::lock_guard<std::mutex> g(m_);
@@ -152,7 +155,14 @@ private:
                 seen = gen_;
                 f = job_;
             }
-            (*f)(t);
+            // the job catches what its hooks raise (plugin_walk's walk_range); nothing may unwind
+            // out of a worker thread (std::terminate) -- whatever still does is recorded and
+            // reported by the caller's run() like a failed range
+            try {
+                (*f)(t);
+            } catch (...) {
+                escaped_.store(true);
+            }
             std::lock_guard<std::mutex> g(m_);
             if (--left_ == 0) done_.notify_one();
         }
@@ -164,6 +174,7 @@ private:
     unsigned left_ = 0;
     uint64_t gen_ = 0;
     bool quit_ = false;
+    std::atomic<bool> escaped_{false};
 };
 struct ipxg_engine {
     ipxg_config cfg;
@@ -221,6 +232,9 @@ struct ipxg_engine {
     // summed when read) and, for t >= 1, its copies of the plugins (ipxg_plugin.copy_ctx)
     uint32_t walk_threads = 0;
     bool walked = false;  // a plugin walk has called hooks (plugin instances no longer pristine)
+    // a process plugin failed (IPXG_EPLUGIN): only ipxg_reset / ipxg_destroy until reset; its message
+    bool failed = false;
+    std::string fail_msg;
     WalkPool* pool = nullptr;
     std::vector<std::unique_ptr<ExportVec>> hw_ex;       // [t]
     std::vector<std::vector<uint64_t>> host_ports;      // [t]
@@ -250,8 +264,11 @@ struct ipxg_engine {
     DevBuf stage_arena[2], stage_desc[2];
     hipStream_t cst = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr};
-    // k_classify runs beside k_bin / k_bin_slow (neither reads the flow table) on its own
-    // stream; k_reduce waits for it
+    // k_classify runs beside k_bin / k_bin_slow on its own stream; k_reduce waits for it.  Both
+    // sides may touch the same slots -- k_classify claims slots and ORs SLOT_PLUGIN, k_bin's spills
+    // (a full segment: tile_emit) claim and accumulate into slots -- which is safe only because every
+    // slot write on either side is an atomic CAS or RMW: a plain slot store added to either path
+    // would race
     hipStream_t cls_st = nullptr;
     hipEvent_t cls_fork = nullptr, cls_join = nullptr;
     int stage_next = 0;
@@ -739,7 +756,24 @@ static int launch_tail(ipxg_engine* e, bool finishing) {
     return IPXG_OK;
 }
 
+static int complete_batch_impl(ipxg_engine* e);
+// (every entry point completes the batch in flight first: no C++ exception leaves it, and a
+// failed engine completes nothing)
 static int complete_batch(ipxg_engine* e) {
+    if (e->failed)
+        return set_err(e, IPXG_ESTATE, "engine stopped by a process plugin error (ipxg_reset or ipxg_destroy): " +
+                                           e->fail_msg);
+    if (!e->inflight.on) return IPXG_OK;
+    try {
+        return complete_batch_impl(e);
+    } catch (const std::bad_alloc&) {
+        return set_err(e, IPXG_ENOMEM, "host allocation failed");
+    } catch (...) {
+        return set_err(e, IPXG_EDEVICE, "internal error: exception while completing a batch");
+    }
+}
+
+static int complete_batch_impl(ipxg_engine* e) {
     if (!e->inflight.on) return IPXG_OK;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     int rc;
@@ -851,7 +885,7 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     return IPXG_OK;
 }
 
-int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
+static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
     if (!e || !batch) return IPXG_EINVAL;
     const uint32_t n = batch->n;
     if (n == 0) return IPXG_OK;
@@ -940,7 +974,8 @@ int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) {
     }
     if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
     // the process plugins' flows: SLOT_PLUGIN in the table before k_reduce folds the batch;
-    // k_bin and k_bin_slow only write partition records, so k_classify runs beside them
+    // k_bin and k_bin_slow write partition records and, on a full segment, atomic slot updates
+    // (tile_emit's spill); k_classify's slot updates are atomic too, so it runs beside them
     const bool classify = !e->plugins.empty() && binned;
     if (classify) {
         if (!e->cls_st) {
@@ -1008,6 +1043,14 @@ struct alignas(128) WalkOut {  // one per walk thread, on cache lines of its own
     uint64_t v6 = 0;          // IPv6 records among ex
 };
 
+// A hook returned IPXG_PLUGIN_ERROR (the reference plugin threw PluginError): raised inside the
+// walk's own code and caught by the walk thread (walk_range), which stops its range -- as the
+// reference's input worker leaves its loop at the first PluginError (workers.cpp:107-112).
+struct HookFail {
+    size_t plugin;
+    const char* hook;
+};
+
 struct FlowWalk {
     const std::vector<ipxg_plugin>& pl;
     const Params& p;
@@ -1015,28 +1058,32 @@ struct FlowWalk {
     ipxg_flow_record rec;
     bool live;
 
+    static int ret(int r, size_t k, const char* hook) {
+        if (r < 0) throw HookFail{k, hook};
+        return r;
+    }
     int pre_create(ipxg_packet_view* v) {
         int r = 0;
-        for (const ipxg_plugin& q : pl)
-            if (q.pre_create) r |= q.pre_create(q.ctx, v);
+        for (size_t k = 0; k < pl.size(); ++k)
+            if (pl[k].pre_create) r |= ret(pl[k].pre_create(pl[k].ctx, v), k, "pre_create");
         return r;
     }
     int post_create(const ipxg_packet_view* v) {
         int r = 0;
-        for (const ipxg_plugin& q : pl)
-            if (q.post_create) r |= q.post_create(q.ctx, &rec, v);
+        for (size_t k = 0; k < pl.size(); ++k)
+            if (pl[k].post_create) r |= ret(pl[k].post_create(pl[k].ctx, &rec, v), k, "post_create");
         return r;
     }
     int pre_update(ipxg_packet_view* v) {
         int r = 0;
-        for (const ipxg_plugin& q : pl)
-            if (q.pre_update) r |= q.pre_update(q.ctx, &rec, v);
+        for (size_t k = 0; k < pl.size(); ++k)
+            if (pl[k].pre_update) r |= ret(pl[k].pre_update(pl[k].ctx, &rec, v), k, "pre_update");
         return r;
     }
     int post_update(const ipxg_packet_view* v) {
         int r = 0;
-        for (const ipxg_plugin& q : pl)
-            if (q.post_update) r |= q.post_update(q.ctx, &rec, v);
+        for (size_t k = 0; k < pl.size(); ++k)
+            if (pl[k].post_update) r |= ret(pl[k].post_update(pl[k].ctx, &rec, v), k, "post_update");
         return r;
     }
     void pre_export() {
@@ -1219,7 +1266,7 @@ static unsigned walk_pool(ipxg_engine* e, uint32_t nf, uint32_t m) {
     return T;
 }
 
-int ipxg_set_walk_threads(ipxg_engine* e, uint32_t threads) {
+static int set_walk_threads_impl(ipxg_engine* e, uint32_t threads) {
     if (!e || threads > 256) return IPXG_EINVAL;
     const uint32_t old = e->walk_threads;
     e->walk_threads = threads;
@@ -1380,7 +1427,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         wos.push_back(WalkOut{xv.v, xv.spill});
     }
     std::vector<int64_t> dlive(T, 0);
-    std::vector<int> wfail(T, 0);  // a walk thread ran out of host memory
+    std::vector<int> wfail(T, 0);  // a walk thread: 2 out of host memory, 3 a plugin failed
+    std::vector<std::string> wmsg(T);
     auto walk_range = [&](unsigned t) {
         if (t >= T) return;  // (the pool may hold more threads than this walk uses)
         const uint32_t f0 = fr[t], f1 = fr[t + 1];
@@ -1434,16 +1482,49 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             }
         }
         dlive[t] = dl;
+        } catch (const HookFail& h) {
+            wfail[t] = 3;
+            const ipxg_plugin& q = (t ? e->walk_pl[t - 1] : e->plugins)[h.plugin];
+            const char* m = q.error ? q.error(q.ctx) : nullptr;
+            wmsg[t] = "process plugin " + std::to_string(h.plugin) + " " + h.hook + ": " +
+                      (m ? m : "returned IPXG_PLUGIN_ERROR");
         } catch (const std::bad_alloc&) {
             wfail[t] = 2;
+        } catch (const std::exception& x) {  // (a hook that threw past the C ABI)
+            wfail[t] = 3;
+            wmsg[t] = std::string("process plugin walk: ") + x.what();
+        } catch (...) {
+            wfail[t] = 3;
+            wmsg[t] = "process plugin walk: a hook raised a non-standard exception";
         }
     };
     if (T > 1) e->pool->run(walk_range);
     else walk_range(0);
+    if (T > 1 && e->pool->take_escaped()) {  // (walk_range catches everything: not expected)
+        wfail[0] = 3;
+        wmsg[0] = "process plugin walk: an exception left a walk thread";
+    }
+    // failures a hook could not return (pre_export returns nothing): each instance's error()
+    for (unsigned t = 0; t < T; ++t) {
+        if (wfail[t]) continue;
+        const std::vector<ipxg_plugin>& pl = t ? e->walk_pl[t - 1] : e->plugins;
+        for (size_t k = 0; k < pl.size() && !wfail[t]; ++k)
+            if (const char* m = pl[k].error ? pl[k].error(pl[k].ctx) : nullptr) {
+                wfail[t] = 3;
+                wmsg[t] = "process plugin " + std::to_string(k) + ": " + m;
+            }
+    }
     for (unsigned t = 0; t < T; ++t)
-        if (wfail[t]) {
+        if (wfail[t] == 2) {
             (void)hipStreamSynchronize(e->st);
             return set_err(e, IPXG_ENOMEM, "plugin walk: host memory for the exports");
+        }
+    for (unsigned t = 0; t < T; ++t)
+        if (wfail[t] == 3) {  // the batch is lost; the engine stops until ipxg_reset
+            (void)hipStreamSynchronize(e->st);
+            e->failed = true;
+            e->fail_msg = wmsg[t];
+            return set_err(e, IPXG_EPLUGIN, wmsg[t]);
         }
     // the threads' exports follow each other in thread order (copied to the device below)
     size_t nx = 0;
@@ -1522,7 +1603,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     return IPXG_OK;
 }
 
-int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
+static int add_plugin_impl(ipxg_engine* e, const ipxg_plugin* pl) {
     if (!e || !pl) return IPXG_EINVAL;
     if (pl->n_ports > IPXG_PLUGIN_MAX_PORTS || pl->n_prefixes > IPXG_PLUGIN_MAX_PREFIXES)
         return set_err(e, IPXG_EINVAL, "plugin rule: too many ports or prefixes");
@@ -1537,6 +1618,15 @@ int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) {
     e->plugins.push_back(*pl);
     if (const int rc1 = make_walk_copies(e)) {  // the walk threads' copies of the new plugin
         e->plugins.pop_back();
+        // a copy failed on some thread: the threads before it already hold a copy of the new
+        // plugin -- free those, so every thread's instances line up with e->plugins again
+        // (else a later registration would skip them and those threads would call the failed
+        // plugin's copy in the next one's place)
+        for (std::vector<ipxg_plugin>& v : e->walk_pl)
+            while (v.size() > e->plugins.size()) {
+                if (v.back().free_ctx && v.back().ctx) v.back().free_ctx(v.back().ctx);
+                v.pop_back();
+            }
         return rc1;
     }
     e->follow_max = std::max<uint64_t>(e->follow_max, pl->follow_packets);
@@ -1765,7 +1855,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     return IPXG_OK;
 }
 
-int ipxg_expire(ipxg_engine* e, int64_t now_sec) {
+static int expire_impl(ipxg_engine* e, int64_t now_sec) {
     if (!e) return IPXG_EINVAL;
     {
         const int rc0 = complete_batch(e);
@@ -1796,7 +1886,7 @@ int ipxg_expire(ipxg_engine* e, int64_t now_sec) {
     return IPXG_OK;
 }
 
-int ipxg_finish(ipxg_engine* e) {
+static int finish_impl(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
@@ -1873,6 +1963,11 @@ int ipxg_finish(ipxg_engine* e) {
 
 int ipxg_reset(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
+    if (e->failed) {  // a process plugin's failure: the lost batch's host state is dropped too
+        e->failed = false;
+        e->fail_msg.clear();
+        e->inflight.on = e->inflight.tail = false;
+    }
     {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
@@ -1898,7 +1993,7 @@ int ipxg_reset(ipxg_engine* e) {
     return IPXG_OK;
 }
 
-int ipxg_pending_exports(ipxg_engine* e, size_t* n) {
+static int pending_exports_impl(ipxg_engine* e, size_t* n) {
     if (!e || !n) return IPXG_EINVAL;
     {
         const int rc0 = complete_batch(e);
@@ -1908,7 +2003,7 @@ int ipxg_pending_exports(ipxg_engine* e, size_t* n) {
     return IPXG_OK;
 }
 
-int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t* n) {
+static int poll_exports_impl(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t* n) {
     if (!e || !n || (cap && !out)) return IPXG_EINVAL;
     {
         const int rc0 = complete_batch(e);
@@ -2273,7 +2368,7 @@ int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n
     return IPXG_OK;
 }
 
-int ipxg_clear_exports(ipxg_engine* e) {
+static int clear_exports_impl(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     {
         const int rc0 = complete_batch(e);
@@ -2492,5 +2587,39 @@ int ipxg_xxh64_batch(ipxg_engine* e, const uint8_t* keys, uint32_t keylen, uint3
     if (le != hipSuccess) return set_err(e, IPXG_EDEVICE, hipGetErrorString(le));
     return IPXG_OK;
 }
+
+// The calls that run the engine's C++ host code (containers, the process-plugin walk): no C++
+// exception crosses the C ABI (include/ipxg.h: int codes only), and after a process plugin's
+// failure (IPXG_EPLUGIN) the engine refuses them until ipxg_reset, as the reference's pipeline
+// stops at its first PluginError (workers.cpp:107-112).
+extern "C++" template <class F>
+static int guarded(ipxg_engine* e, F&& f) {
+    if (!e) return IPXG_EINVAL;
+    if (e->failed)
+        return set_err(e, IPXG_ESTATE, "engine stopped by a process plugin error (ipxg_reset or ipxg_destroy): " +
+                                           e->fail_msg);
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return set_err(e, IPXG_ENOMEM, "host allocation failed");
+    } catch (const std::exception& x) {
+        return set_err(e, IPXG_EDEVICE, std::string("internal error: ") + x.what());
+    } catch (...) {
+        return set_err(e, IPXG_EDEVICE, "internal error: unknown exception");
+    }
+}
+
+int ipxg_submit(ipxg_engine* e, const ipxg_batch* batch) { return guarded(e, [&] { return submit_impl(e, batch); }); }
+int ipxg_set_walk_threads(ipxg_engine* e, uint32_t threads) {
+    return guarded(e, [&] { return set_walk_threads_impl(e, threads); });
+}
+int ipxg_add_plugin(ipxg_engine* e, const ipxg_plugin* pl) { return guarded(e, [&] { return add_plugin_impl(e, pl); }); }
+int ipxg_expire(ipxg_engine* e, int64_t now_sec) { return guarded(e, [&] { return expire_impl(e, now_sec); }); }
+int ipxg_finish(ipxg_engine* e) { return guarded(e, [&] { return finish_impl(e); }); }
+int ipxg_pending_exports(ipxg_engine* e, size_t* n) { return guarded(e, [&] { return pending_exports_impl(e, n); }); }
+int ipxg_poll_exports(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t* n) {
+    return guarded(e, [&] { return poll_exports_impl(e, out, cap, n); });
+}
+int ipxg_clear_exports(ipxg_engine* e) { return guarded(e, [&] { return clear_exports_impl(e); }); }
 
 }  // extern "C"

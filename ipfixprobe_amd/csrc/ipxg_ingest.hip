@@ -27,6 +27,8 @@
 // accumulation (merge_packet_atomic); the engine then runs the k_finalize scan for the
 // batch (ctl->pending).  Both paths are order-independent reductions keyed by packet index,
 // so the result does not depend on which lane or workgroup runs first.
+#include <atomic>
+
 #include "ipxg_table.hpp"
 
 namespace ipxg {
@@ -1080,6 +1082,24 @@ __device__ __noinline__ void red_spill(const TableView& t, BatchCtl* ctl, uint32
         defer_packet(ctl, deferred_list, r.z, false);
 }
 
+// lds_slot's continuation after a first read k of entry e that was not the key: insert into an
+// empty entry, or probe on.  Inline: at the udp64 partitions' ~0.2 load of the LDS table one
+// record in five finds another flow in its home entry, so nearly every wave-group has a lane
+// here, and as a call (scratch saves of the caller's registers, a full vmcnt drain) it stalled
+// the group's prefetched record loads.
+__device__ __forceinline__ int red_probe(FlowAgg* ht, uint64_t lo, uint32_t e, unsigned long long k) {
+    for (uint32_t probe = 0; probe < RED_MAX_PROBE; ++probe) {
+        if (k == 0) {
+            k = atomicCAS(&ht[e].key, 0ull, (unsigned long long)lo);
+            if (k == 0) return (int)e;
+        }
+        if (k == lo) return (int)e;
+        e = (e + 1) & (RED_ENTRIES - 1);
+        k = ht[e].key;
+    }
+    return -1;
+}
+
 __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
                                            uint4* agg_list, uint32_t* cnt, const uint4& r, const uint4* rp, bool ok,
                                            bool one_tb) {
@@ -1171,73 +1191,90 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                 red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], rp[u], k0 + u * RED_THREADS + tid < total, one_tb);
         }
     } else {
-        // Each wave takes whole segments, RED_U at a time (lane = record of the segment: coalesced
-        // loads, no search); a segment longer than a wave loops (wave-uniform).  The segments'
-        // positions are wave-uniform (scalar), read before the loads are issued, so no branch
-        // separates a load from its use.  Two register sets (A, B): the next group's loads are
-        // in flight while this group's records are folded into the LDS table.
+        // Chunks of 64 records: a non-empty segment of len records gives ceil(len / 64) chunks,
+        // listed in LDS as {column << 20 | chunk << 6 | records - 1} (ne[], in windows of
+        // RED_MAX_COLS entries).  Waves take chunks wv, wv + NW, ... (lane = record of the chunk:
+        // coalesced loads, no search).  A wave reads the descriptors of its next 64 chunks with
+        // ONE LDS read (lane j: its j-th chunk) and walks them by v_readlane into SGPRs, so no
+        // LDS round trip stands between a chunk and its loads; RED_U chunks per group, two groups
+        // in flight (A/B) while the previous one is folded.  (Round 3 took whole segments: a
+        // segment's records past the first 64 were loaded synchronously inside the fold, and the
+        // segment's position came from two dependent LDS reads per group behind the other waves'
+        // atomics -- with the udp64 partitions' ~76-record segments k_reduce waited on memory once
+        // per segment.)
         const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-        constexpr uint32_t STEP = NW * RED_U;
-        uint4 ra[RED_U], rb[RED_U];
-        uint32_t sca[RED_U], sla[RED_U], scb[RED_U], slb[RED_U];
-        auto issue = [&](uint32_t s0, uint4(&r)[RED_U], uint32_t(&sc)[RED_U], uint32_t(&sl)[RED_U]) {
+        uint32_t nch = 0;
 #pragma unroll
-            for (uint32_t u = 0; u < RED_U; ++u) {
-                const uint32_t si = s0 + u * NW;
-                const uint32_t c = ne[si < nseg ? si : 0];
-                sc[u] = __builtin_amdgcn_readfirstlane(c);
-                sl[u] = __builtin_amdgcn_readfirstlane(si < nseg ? pre[c + 1] - pre[c] : 0u);
+        for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) nch += (v[q] + 63) >> 6;
+        uint32_t total_ch;
+        const uint32_t cb0 = block_exclusive_scan<RED_THREADS>(nch, scan_s, &total_ch);
+        for (uint32_t w0 = 0; w0 < total_ch; w0 += RED_MAX_COLS) {  // uniform
+            __syncthreads();  // ne[] is free (the non-empty list above / the previous window)
+            uint32_t at = cb0;
+#pragma unroll
+            for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
+                const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
+                for (uint32_t j = 0; j * 64 < v[q]; ++j, ++at)
+                    if (at - w0 < RED_MAX_COLS) ne[at - w0] = (c << 20) | (j << 6) | (min(64u, v[q] - j * 64) - 1);
             }
+            __syncthreads();
+            const uint32_t nw = min(RED_MAX_COLS, total_ch - w0);
+            for (uint32_t g = wv; g < nw; g += 64 * NW) {  // uniform over the wave
+                const uint32_t mine = g + lane * NW;
+                const uint32_t cd = mine < nw ? ne[mine] : 0u;
+                const uint32_t left = (nw - g + NW - 1) / NW;
+                const uint32_t ng = left < 64 ? left : 64;  // the wave's chunks in this group
+                uint4 ra[RED_U], rb[RED_U];
+                uint32_t ca[RED_U], cbk[RED_U];
+                auto issue = [&](uint32_t j0, uint4(&r)[RED_U], uint32_t(&cs)[RED_U]) {
 #pragma unroll
-            for (uint32_t u = 0; u < RED_U; ++u) {
-#ifdef IPXG_RED_NT  // tuning knob: streaming loads of the records (read once)
-                r[u] = u4(__builtin_nontemporal_load(
-                    reinterpret_cast<const u32x4*>(&segs[(size_t)sc[u] * bv.seg_cap + (lane < sl[u] ? lane : 0)])));
-#else
-                r[u] = segs[(size_t)sc[u] * bv.seg_cap + (lane < sl[u] ? lane : 0)];  // unconditional load
-#endif
-            }
-        };
-        auto fold = [&](const uint4(&r)[RED_U], const uint32_t(&sc)[RED_U], const uint32_t(&sl)[RED_U]) {
+                    for (uint32_t u = 0; u < RED_U; ++u) {
+                        const uint32_t j = j0 + u < ng ? j0 + u : 0;
+                        cs[u] = __builtin_amdgcn_readlane(cd, j);
+                    }
 #pragma unroll
-            for (uint32_t u = 0; u < RED_U; ++u) {
-                const uint4* sg = segs + (size_t)sc[u] * bv.seg_cap;
-                red_record(ht, t, ctl, deferred_list, agg_list, cnt, r[u], sg + lane, lane < sl[u], one_tb);
-                for (uint32_t off = 64; off < sl[u]; off += 64) {  // long segment (uniform over the wave)
-                    const uint4 x = sg[off + lane < sl[u] ? off + lane : 0];
-                    red_record(ht, t, ctl, deferred_list, agg_list, cnt, x, sg + off + lane, off + lane < sl[u], one_tb);
+                    for (uint32_t u = 0; u < RED_U; ++u) {
+                        const uint32_t n = (cs[u] & 63) + 1;
+                        r[u] = segs[(size_t)(cs[u] >> 20) * bv.seg_cap + ((cs[u] >> 6) & 0x3FFF) * 64 +
+                                    (lane < n ? lane : 0)];  // unconditional load
+                    }
+                };
+                auto fold = [&](const uint4(&r)[RED_U], const uint32_t(&cs)[RED_U], uint32_t j0) {
+                    bool ok[RED_U];
+                    uint32_t e[RED_U];
+                    unsigned long long k[RED_U];
+#pragma unroll
+                    for (uint32_t u = 0; u < RED_U; ++u) {
+                        ok[u] = j0 + u < ng && lane <= (cs[u] & 63) && r[u].z != NO_REC;
+                        e[u] = r[u].x & (RED_ENTRIES - 1);
+                    }
+                    // the probes' first reads, issued together (no atomic of this group before them)
+#pragma unroll
+                    for (uint32_t u = 0; u < RED_U; ++u) k[u] = ok[u] && !rec_is_agg(r[u]) ? ht[e[u]].key : 0ull;
+#pragma unroll
+                    for (uint32_t u = 0; u < RED_U; ++u) {
+                        if (!ok[u]) continue;
+                        const uint4* rp = segs + (size_t)(cs[u] >> 20) * bv.seg_cap + ((cs[u] >> 6) & 0x3FFF) * 64 + lane;
+                        if (rec_is_agg(r[u])) {
+                            red_agg(ht, t, ctl, agg_list, cnt, r[u], rp);
+                            continue;
+                        }
+                        const uint64_t lo = ((uint64_t)r[u].y << 32) | r[u].x;
+                        const int slot = k[u] == lo ? (int)e[u] : red_probe(ht, lo, e[u], k[u]);
+                        if (slot >= 0) lds_fold(ht[slot], r[u].z, r[u].w, one_tb);
+                        else red_spill(t, ctl, deferred_list, cnt, r[u]);
+                    }
+                };
+                issue(0, ra, ca);
+                for (uint32_t j0 = 0; j0 < ng; j0 += 2 * RED_U) {  // uniform
+                    issue(j0 + RED_U, rb, cbk);
+                    fold(ra, ca, j0);
+                    if (j0 + RED_U >= ng) break;
+                    issue(j0 + 2 * RED_U, ra, ca);
+                    fold(rb, cbk, j0 + RED_U);
                 }
             }
-        };
-#ifdef IPXG_PROBE  // [12] waits for a group's records (the next group's loads in flight), [13] folds
-        uint64_t pw = 0, pf = 0;
-#define RED_PROBE_FOLD(R, SC, SL)                                                              \
-    do {                                                                                        \
-        const uint64_t a_ = __builtin_readcyclecounter();                                      \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RED_U) : "memory");                           \
-        const uint64_t b_ = __builtin_readcyclecounter();                                      \
-        fold(R, SC, SL);                                                                        \
-        pw += b_ - a_;                                                                          \
-        pf += __builtin_readcyclecounter() - b_;                                                \
-    } while (0)
-#else
-#define RED_PROBE_FOLD(R, SC, SL) fold(R, SC, SL)
-#endif
-        issue(wv, ra, sca, sla);
-        for (uint32_t s0 = wv; s0 < nseg; s0 += 2 * STEP) {
-            issue(s0 + STEP, rb, scb, slb);
-            RED_PROBE_FOLD(ra, sca, sla);
-            if (s0 + STEP >= nseg) break;  // uniform
-            issue(s0 + 2 * STEP, ra, sca, sla);
-            RED_PROBE_FOLD(rb, scb, slb);
         }
-#undef RED_PROBE_FOLD
-#ifdef IPXG_PROBE
-        if (lane == 0) {
-            atomicAdd((unsigned long long*)&ctl->probe[12], (unsigned long long)pw);
-            atomicAdd((unsigned long long*)&ctl->probe[13], (unsigned long long)pf);
-        }
-#endif
     }
     __syncthreads();
     PROBE_T(q2t);
@@ -1491,14 +1528,20 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
                      bool finishing, bool deferred_only) {
     // at most one wave of resident workgroups (3 per CU): a grid past it ran its last blocks'
     // several passes over the list in a second wave on a third of the chip
-    static uint32_t resident = 0;
+    // (per device, computed once; engines on several devices or threads share the cache: relaxed
+    // atomics, every writer stores the same value for its device)
+    static std::atomic<uint32_t> resident_of[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::atomic<uint32_t>& slot = resident_of[dev & 63];
+    uint32_t resident = slot.load(std::memory_order_relaxed);
     if (!resident) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
+        int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fin_list, IPXG_BLOCK, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         resident = (uint32_t)std::max(1, cus * per_cu);
+        slot.store(resident, std::memory_order_relaxed);
     }
     uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
     if (grid > resident) grid = resident;

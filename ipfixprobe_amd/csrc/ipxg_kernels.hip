@@ -495,7 +495,10 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
         const uint32_t state = t.hot(s).state;
         if (key != 0 && (state & SLOT_LIVE) &&
             now - (int64_t)t.line[s].head[RW_TLS] >= (int64_t)p.inactive_s) {
-            t.hot(s).state = state & ~SLOT_LIVE;
+            // the record leaves with its plugin extensions: nothing is followed any more (a
+            // FOLLOW bit left behind kept the dead slot through every rehash and sent the key's
+            // next packets to the host walk)
+            t.hot(s).state = state & ~(SLOT_LIVE | SLOT_FOLLOW);
             mask |= 1u << j;
             c++;
         }

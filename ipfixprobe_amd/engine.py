@@ -119,6 +119,8 @@ class PacketView(ctypes.Structure):
 PRE_CREATE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(PacketView))
 FLOW_HOOK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(PacketView))
 PRE_EXPORT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+ERROR_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p)  # const char* (a C string the plugin keeps)
+PLUGIN_ERROR = -1  # IPXG_PLUGIN_ERROR: a hook's PluginError
 
 
 class Plugin(ctypes.Structure):
@@ -130,7 +132,8 @@ class Plugin(ctypes.Structure):
                 ("post_update", FLOW_HOOK_FN), ("pre_export", PRE_EXPORT_FN),
                 ("masked", ctypes.c_uint32), ("follow_packets", ctypes.c_uint32),
                 ("prefix_mask", (ctypes.c_uint8 * 16) * 16),
-                ("copy_ctx", ctypes.c_void_p), ("free_ctx", ctypes.c_void_p)]  # ABI 3 (C function pointers)
+                ("copy_ctx", ctypes.c_void_p), ("free_ctx", ctypes.c_void_p),  # ABI 3 (C function pointers)
+                ("error", ERROR_FN)]  # ABI 4
 
 # ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),
@@ -323,7 +326,9 @@ class Engine:
     def _check(self, rc, what):
         if rc:
             msg = lib().ipxg_last_error(self._h).decode(errors="replace")
-            raise IpxgError("%s failed (rc %d): %s" % (what, rc, msg))
+            err = IpxgError("%s failed (rc %d): %s" % (what, rc, msg))
+            err.rc = rc
+            raise err
 
     @property
     def handle(self):

@@ -273,15 +273,47 @@ static int http_pre_update(void* ctx, ipxg_flow_record* f, ipxg_packet_view* v) 
     return count(ctx, C_PRE_UPDATE, r);
 }
 
-/* ---- TLS (tls.cpp:101-122, add_tls_record :410-425; TLSParser::parse tls_parser.cpp:72-150) ---
- * A handshake record (type 22, version 3.0-3.3) holding a ClientHello / ServerHello of version
- * 3.1-3.3 attaches the extension; nothing ends a flow. */
+/* ---- TLS (tls.cpp:101-122, add_tls_record :410-425; TLSParser::parse tls_parser.cpp:72-100) ---
+ * The extension is attached when TLSPlugin::parse_tls accepts a ClientHello (a ServerHello never
+ * attaches one: parse_tls returns false after it, tls.cpp:392-401): the record header (type 22,
+ * version 3.0-3.3, :102-124), the handshake (ClientHello / ServerHello, version 3.1-3.3,
+ * :126-154), then every length check of the session id (:156-170), cipher suites (:172-203),
+ * compression methods (:205-223) and the extensions section (has_valid_extension_length,
+ * :413-427) -- a hello cut short by the capture (the configs[2] mix's 64-byte-class frames hold
+ * 43 bytes of it) attaches nothing.  Bytes at or past the payload's end read as 0 (the reference
+ * reads whatever follows; DESIGN.md section 2 rule 1).  Nothing ends a flow. */
+static uint32_t tls_b(const uint8_t* d, uint32_t n, uint32_t i) { return i < n ? d[i] : 0u; }
 static int tls_hello(const uint8_t* d, uint32_t n) {
-    if (n < 5 + 6) return 0;
-    if (d[0] != 22 || d[1] != 3 || d[2] > 3) return 0;
+    if (n < 5 || d[0] != 22 || d[1] != 3 || d[2] > 3) return 0;  /* parse_tls_header */
+    if (5 + 6 > n) return 0;                                       /* parse_tls_handshake */
     const uint8_t t = d[5];
     if (t != 1 && t != 2) return 0;
-    return d[9] == 3 && d[10] >= 1 && d[10] <= 3;
+    if (!(d[9] == 3 && d[10] >= 1 && d[10] <= 3)) return 0;
+    const uint32_t sid_off = 5 + 6 + 32;                           /* parse_session_id */
+    if (sid_off > n) return 0;
+    const uint32_t sid_sec = 1 + tls_b(d, n, sid_off);
+    if (sid_off + sid_sec > n) return 0;
+    const uint32_t cs_off = sid_off + sid_sec;                     /* parse_cipher_suites */
+    if (cs_off + 2 > n) return 0;
+    uint32_t cs_sec = 2;
+    if (t == 1) {
+        const uint32_t cl = (tls_b(d, n, cs_off) << 8) | tls_b(d, n, cs_off + 1);
+        if (cs_off + 2 + cl > n) return 0;
+        cs_sec = 2 + cl;
+    }
+    const uint32_t cm_off = cs_off + cs_sec;                       /* parse_compression_methods */
+    if (cm_off > n) return 0;
+    uint32_t cm_sec = 1;
+    if (t == 1) {
+        const uint32_t cm = tls_b(d, n, cm_off);
+        if (1 + cm > n) return 0;  /* (the reference compares with the whole length) */
+        cm_sec = 1 + cm;
+    }
+    if (t != 1) return 0;                                          /* only a ClientHello attaches */
+    const uint32_t ext_off = cm_off + cm_sec;                      /* has_valid_extension_length */
+    if (ext_off > n) return 0;
+    const uint32_t el = (tls_b(d, n, ext_off) << 8) | tls_b(d, n, ext_off + 1);
+    return ext_off + el <= n;
 }
 static int tls_post_create(void* ctx, ipxg_flow_record* f, const ipxg_packet_view* v) {
     uint32_t n;

@@ -155,11 +155,17 @@ public:
         std::memset(&q, 0, sizeof(q));
         if (!rule_for(kind, q)) return false;
         q.ctx = this;
+        // Every virtual is called inside guard(): a PluginError (plugin.hpp:81-91) -- or any other
+        // exception -- must not cross the engine's C ABI; it becomes IPXG_PLUGIN_ERROR with the
+        // message kept for q.error, and the engine fails the call with IPXG_EPLUGIN as the
+        // reference's input worker reports it (workers.cpp:107-112).
         q.pre_create = [](void* c, ipxg_packet_view* v) -> int {
             Adapter* a = static_cast<Adapter*>(c);
-            ipxp::Packet k;
-            fill_packet(k, *v);
-            return a->m_p->pre_create(k);
+            return a->guard([&] {
+                ipxp::Packet k;
+                fill_packet(k, *v);
+                return a->m_p->pre_create(k);
+            });
         };
         q.post_create = [](void* c, ipxg_flow_record* r, const ipxg_packet_view* v) -> int {
             return static_cast<Adapter*>(c)->call(r, v, [](ipxp::ProcessPlugin* p, ipxp::Flow& f, ipxp::Packet& k) {
@@ -178,9 +184,18 @@ public:
         };
         q.pre_export = [](void* c, ipxg_flow_record* r) {
             Adapter* a = static_cast<Adapter*>(c);
-            ipxp::Flow& f = a->flow(*r);
-            a->m_p->pre_export(f);
-            a->adopt(*r, f);
+            (void)a->guard([&] {
+                ipxp::Flow& f = a->flow(*r);
+                a->m_p->pre_export(f);
+                a->adopt(*r, f);
+                return 0;
+            });
+        };
+        q.error = [](void* c) -> const char* {  // a failure since the last call, taken
+            Adapter* a = static_cast<Adapter*>(c);
+            if (!a->m_fresh) return nullptr;
+            a->m_fresh = false;
+            return a->m_err.c_str();  // (valid until this instance fails again)
         };
         // a walk thread's own instance: ProcessPlugin::copy() (processPlugin.hpp:50), as the
         // reference copies every process plugin per storage pipeline (ipfixprobe.cpp:430-436)
@@ -212,16 +227,38 @@ private:
     }
     template <class F>
     int call(ipxg_flow_record* r, const ipxg_packet_view* v, F hook) {
-        ipxp::Packet k;
-        fill_packet(k, *v);
-        ipxp::Flow& f = flow(*r);
-        const int ret = hook(m_p, f, k);
-        adopt(*r, f);
-        return ret;
+        return guard([&] {
+            ipxp::Packet k;
+            fill_packet(k, *v);
+            ipxp::Flow& f = flow(*r);
+            const int ret = hook(m_p, f, k);
+            adopt(*r, f);
+            return ret;
+        });
+    }
+    template <class F>
+    int guard(F&& body) {
+        std::string msg;
+        try {
+            return body();
+        } catch (const ipxp::PluginError& x) {
+            msg = std::string("PluginError: ") + x.what();
+        } catch (const std::exception& x) {
+            msg = x.what();
+        } catch (...) {
+            msg = "unknown exception";
+        }
+        if (!m_fresh) {  // the first failure since error() last took one
+            m_err = msg;
+            m_fresh = true;
+        }
+        return IPXG_PLUGIN_ERROR;
     }
 
     ipxp::ProcessPlugin* m_p;
     bool m_owns;
+    std::string m_err;     // the first failure since q.error last took one
+    bool m_fresh = false;  // m_err not taken yet
     ipxp::Flow m_scratch{};  // the hooks' Flow for a record without extensions
 };
 

@@ -98,6 +98,13 @@ uint64_t oracle_xxh64(const void* data, size_t len, uint64_t seed)
     return xx_aval(h);
 }
 
+/* n keys of keylen bytes, back to back -> XXH64 of each (test helper: flow-hash shards of a
+ * synthetic mix on the CPU) */
+void oracle_xxh64_batch(const uint8_t* keys, size_t keylen, size_t n, uint64_t seed, uint64_t* out)
+{
+    for (size_t i = 0; i < n; ++i) out[i] = oracle_xxh64(keys + i * keylen, keylen, seed);
+}
+
 /* ===================================================================================== */
 /* Parser -- src/plugins/input/parser/parser.cpp                                         */
 /* Offsets are absolute byte offsets into the frame; "data_len" values are uint16_t     */

@@ -38,6 +38,7 @@ extern "C" {
 #endif
 
 uint64_t oracle_xxh64(const void* data, size_t len, uint64_t seed);
+void oracle_xxh64_batch(const uint8_t* keys, size_t keylen, size_t n, uint64_t seed, uint64_t* out);
 
 /* Parse one frame; returns 1 if parse_packet would append it to the block (valid). */
 int oracle_parse(const uint8_t* data, uint16_t caplen, uint16_t wirelen, uint32_t ts_sec,

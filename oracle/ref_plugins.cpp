@@ -27,9 +27,42 @@ std::map<void*, Held*>& held() {
     return m;
 }
 
+// A process plugin that throws the reference's PluginError (plugin.hpp:81-91) on its nth
+// post_create / post_update call -- each instance counts its own calls, so every walk thread's
+// copy fails on its nth -- behind the same adapter, with dns's rule (port 53): the failure path
+// of the bridge, where the reference's input worker catches the error and
+// reports it through WorkerResult (workers.cpp:107-112).
+class FailingPlugin : public ipxp::ProcessPlugin {
+public:
+    FailingPlugin(int id, int nth) : ipxp::ProcessPlugin(id), m_nth(nth) {}
+    ipxp::ProcessPlugin* copy() override { return new FailingPlugin(*this); }
+    ipxp::OptionsParser* get_parser() const override { return nullptr; }
+    std::string get_name() const override { return "failing"; }
+    int post_create(ipxp::Flow&, const ipxp::Packet&) override { return step(); }
+    int post_update(ipxp::Flow&, const ipxp::Packet&) override { return step(); }
+
+private:
+    int step() {
+        if (++m_calls == m_nth) throw ipxp::PluginError("failing plugin: hook call " + std::to_string(m_nth));
+        return 0;
+    }
+    int m_nth, m_calls = 0;
+};
+
 }  // namespace
 
 extern "C" {
+
+// FailingPlugin(nth) behind an adapter with dns's rule: *out is its ipxg_plugin (release it with
+// ref_plugin_destroy).  0, or -1.
+int ref_failing_plugin_create(int nth, ipxg_plugin* out) {
+    auto h = std::make_unique<Held>();
+    h->plugin = std::make_unique<FailingPlugin>(0, nth);
+    h->adapter = std::make_unique<ipxg_ref::Adapter>(h->plugin.get());
+    if (!h->adapter->make("dns", *out)) return -1;
+    held()[out->ctx] = h.release();
+    return 0;
+}
 
 // A fresh instance of the reference plugin `name` (its registrar's factory entry, as ipfixprobe's
 // process_plugin_args creates it, ipfixprobe.cpp:300-308) behind an adapter: *out is its

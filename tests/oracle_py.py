@@ -23,6 +23,7 @@ def lib():
         vp, u8p = ctypes.c_void_p, ctypes.c_void_p
         L.oracle_xxh64.restype = ctypes.c_uint64
         L.oracle_xxh64.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint64]
+        L.oracle_xxh64_batch.argtypes = [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, vp]
         L.oracle_parse.restype = ctypes.c_int
         L.oracle_parse.argtypes = [u8p, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint32,
                                    ctypes.c_uint32, ctypes.c_uint32, vp,
@@ -54,6 +55,15 @@ def lib():
 def xxh64(data: bytes, seed=0):
     buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
     return lib().oracle_xxh64(buf, len(data), seed)
+
+
+def xxh64_batch(keys: np.ndarray, keylen: int, seed=0):
+    """XXH64 of each keylen-byte key of the flat uint8 array keys (as Engine.xxh64, on the CPU)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    n = len(keys) // keylen
+    out = np.empty(n, dtype=np.uint64)
+    lib().oracle_xxh64_batch(keys.ctypes.data, keylen, n, seed, out.ctypes.data)
+    return out
 
 
 def parse(frame: bytes, caplen=None, wirelen=None, datalink=1, sec=0, usec=0):

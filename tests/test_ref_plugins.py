@@ -171,3 +171,45 @@ def test_bridge_with_reference_plugins_on_workload(mix, names, threads):
     tg, tw = take_texts(got), take_texts(want)
     assert sum(1 for t in tw if t) > 50
     assert keyed(got, tg) == keyed(want, tw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 16])
+def test_plugin_error_fails_the_call_cleanly(threads):
+    """A process plugin that throws PluginError on its 50th hook call: the
+    adapter turns it into IPXG_PLUGIN_ERROR, the walk thread stops, and ipxg_submit fails with
+    IPXG_EPLUGIN and the plugin's message -- on 1 and on 16 walk threads (every thread's copy
+    throws) -- as the reference's input worker reports a PluginError (workers.cpp:107-112).  The
+    engine then refuses work (IPXG_ESTATE) until ipxg_reset, runs again after it, and destroys."""
+    import synth
+    from ipfixprobe_amd import Engine
+    from ipfixprobe_amd.engine import IpxgError, Plugin
+    lib().ref_failing_plugin_create.argtypes = [ctypes.c_int, ctypes.POINTER(Plugin)]
+    nfl, per = 12000, 4
+    frames = []
+    for i in range(nfl * per):
+        f = i % nfl
+        ip = synth.ipv4(synth.ip4(0x0A000000 + f), synth.ip4(0xC0A80001), 17, synth.udp(1024 + f % 60000, 53, b"\x00" * 12))
+        frames.append(synth.pad(synth.eth(synth.mac(1), synth.mac(2), 0x0800) + ip))
+    arena, desc = synth.to_batch([(fr, len(fr), len(fr)) for fr in frames])
+    pl = Plugin()
+    assert lib().ref_failing_plugin_create(50, ctypes.byref(pl)) == 0
+    e = Engine("s=17")
+    try:
+        e.set_walk_threads(threads)
+        e.add_plugin(pl)
+        with pytest.raises(IpxgError) as ex:
+            e.submit(arena, desc)
+        assert ex.value.rc == -8, str(ex.value)  # IPXG_EPLUGIN
+        assert "PluginError: failing plugin: hook call 50" in str(ex.value)
+        with pytest.raises(IpxgError) as ex2:
+            e.submit(arena, desc)
+        assert ex2.value.rc == -7  # IPXG_ESTATE until reset
+        e.reset()
+        e.submit(arena, desc)  # (every instance is past its 50th call: no failure now)
+        e.finish()
+        got = e.poll()
+        assert len(got) == nfl and int(got["src_packets"].sum() + got["dst_packets"].sum()) == nfl * per
+    finally:
+        e.close()  # destroyable after the failure
+        lib().ref_plugin_destroy(ctypes.byref(pl))

@@ -188,3 +188,36 @@ def test_follow_packets_keeps_claimed_flows_on_host(batch):
     want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=16, plugins=[orc.struct])
     assert not flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
     assert eng.seen == orc.seen and len(orc.seen) == 4 * 4  # packets 2..5 of the 4 claimed flows
+
+
+@pytest.mark.gpu
+def test_expired_followed_flow_leaves_the_host_walk():
+    """ipxg_expire exports a followed flow's record with its extension: the slot must stop being
+    followed (k_expire cleared only SLOT_LIVE, so the dead slot kept SLOT_FOLLOW, survived
+    every rehash and sent the key's next packets to the host walk).  Packets of the same keys after
+    the expiry, outside the plugin's rule, stay on the device."""
+    import synth
+    from ipfixprobe_amd import Engine
+    cli, srv = synth.ip4(10), synth.ip4(200)
+    nfl = 3000
+
+    def batch(payload, t0):
+        fr = [synth.pad(synth.eth(synth.mac(1), synth.mac(2), 0x0800) +
+                        synth.ipv4(cli, srv, 17, synth.udp(1024 + f, 443, payload))) for f in range(nfl)]
+        return synth.to_batch([(f, len(f), len(f)) for f in fr], t0=t0)
+
+    probe = FollowProbe()
+    with Engine("s=16") as e:
+        e.add_plugin(probe.struct)
+        arena, desc = batch(b"\xc0" + b"\x00" * 20, 1000)  # claimed: one long-header packet each
+        e.submit(arena, desc)
+        t1 = e.timing()["plugin_packets"]
+        assert t1 == nfl
+        e.expire(1000 + 60)  # every record idle past the inactive timeout (30 s)
+        assert e.stats()["flows_in_cache"] == 0
+        assert len(e.poll()) == nfl
+        arena, desc = batch(b"\x40" + b"\x01" * 20, 1100)  # the same keys, short headers (no rule)
+        e.submit(arena, desc)
+        assert e.timing()["plugin_packets"] == t1, "an expired flow's slot still sent packets to the host walk"
+        e.expire(1100 + 60)
+        assert len(e.poll()) == nfl and e.stats()["flows_in_cache"] == 0
