@@ -977,6 +977,7 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
     // k_bin and k_bin_slow write partition records and, on a full segment, atomic slot updates
     // (tile_emit's spill); k_classify's slot updates are atomic too, so it runs beside them
     const bool classify = !e->plugins.empty() && binned;
+    p.classify = classify ? 1u : 0u;
     if (classify) {
         if (!e->cls_st) {
             HIPCHK(e, hipStreamCreateWithFlags(&e->cls_st, hipStreamNonBlocking));

@@ -1455,7 +1455,12 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
             if (deferred_only) go = h.pad == FIN_DEFERRED;
             else if (h.pad == FIN_DEFERRED) go = false;  // (not from this batch's k_reduce)
         }
-        if (go && h.pad >= FIN_DEFERRED) {
+        // fused finish into a table that was empty before the batch: a new flow is created and
+        // exported here, so it needs no slot -- no probe, no claim (two dependent round trips
+        // per flow), unless it turns out complex (claimed below)
+        const bool no_slot = go && fused && !deferred_only && !p.classify && h.pad >= FIN_DEFERRED;
+        if (no_slot) h.pad = FIN_NO_SLOT;
+        if (go && !no_slot && h.pad >= FIN_DEFERRED) {
             FlowAgg a;
             a.key = h.key;
             a.acc[0] = h.acc[0];
@@ -1485,7 +1490,22 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
         }
         if (go) {
             const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean, tmax);
-            if (fr.status == FIN_COMPLEX) n_cx++;
+            if (fr.status == FIN_COMPLEX && no_slot) {  // a complex flow: its slot now, for the sequential path
+                HotSlot img;
+                bool claimed;
+                HotSlot* hp = probe_insert_full(t, h.key, img, claimed);
+                if (!hp) {  // (the host grows the table and runs the list again: deferred_only)
+                    fin_list[k].pad = FIN_DEFERRED;
+                    n_def++;
+                } else {
+                    n_keys += claimed ? 1u : 0u;
+                    HotSlot c = h;  // (a slot empty before the batch: the image is the whole slot)
+                    c.state = h.state | SLOT_COMPLEX;
+                    c.pad = 0;
+                    *hp = c;
+                    n_cx++;
+                }
+            } else if (fr.status == FIN_COMPLEX) n_cx++;
             else if (!fused && fr.created) n_live++;
             do_export = fr.do_export || fr.fin_export;
             reason = fr.fin_export ? (uint8_t)IPXG_FLOW_END_FORCED : fr.reason;

@@ -143,6 +143,8 @@ struct Params {
     uint32_t tile_agg;       // k_bin / k_bin_slow aggregate frequent flows per tile (skewed traffic)
     uint32_t wide;           // k_bin's wide walk (96-byte loads, parse_medium)
     uint32_t spin_max;       // strict replay: polling rounds without progress before giving up
+    uint32_t classify;       // k_classify ran for the batch (process plugins): slots were claimed and
+                             // marked before k_reduce, so every listed flow must find its slot
 };
 
 // ---- strict mode (ipxg_strict.hip): the reference's line table -------------------------------

@@ -1098,6 +1098,10 @@ struct FinResult {
 // (the checks below cannot fire otherwise): one random 128-byte line less per flow on the 1M-flow
 // mixes, where most flows continue.
 constexpr uint32_t TMAX_UNKNOWN = 0xFFFFFFFFu;
+// s = FIN_NO_SLOT: a new flow finalised without a table slot (k_fin_list's fused finish into a
+// table empty before the batch: the record leaves at once); a flow that turns out complex is
+// returned with FIN_COMPLEX and nothing written -- the caller claims its slot then.
+constexpr uint32_t FIN_NO_SLOT = 0xFFFFFFFFu;
 template <bool LDSW>
 __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Params& p, const TableView& t,
                                                    const FragView& f, uint32_t s, const HotSlot& h,
@@ -1160,10 +1164,12 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         if (h.fin_n[dd] && sidx > ~h.fin_n[dd]) cx = true;
     }
     if (cx) {
-        HotSlot c = h;
-        c.state = h.state | SLOT_COMPLEX;
-        c.pad = 0;
-        t.hot(s) = c;
+        if (s != FIN_NO_SLOT) {
+            HotSlot c = h;
+            c.state = h.state | SLOT_COMPLEX;
+            c.pad = 0;
+            t.hot(s) = c;
+        }
         res.status = FIN_COMPLEX;
         return res;
     }
@@ -1198,7 +1204,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         if (cont) tbl_load_tail(t, s, rec);  // (fused finishes follow an empty table: none)
         er = rec;
         res.fin_export = true;
-        clear_slot(&t.hot(s), 0, 0);  // empty (every slot empties at the finish)
+        if (s != FIN_NO_SLOT) clear_slot(&t.hot(s), 0, 0);  // empty (every slot empties at the finish)
         return res;
     }
     if (cont) {

@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
 REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libref_plugins.so")
 
-PLUGINS = {"imix": ("dns", "http", "tls")}  # bench.py --plugins config (configs[4]: quic, below)
+PLUGINS = {"imix": ("dns", "http", "tls"), "quic": ("quic",)}  # bench.py --plugins config
 
 
 class _G:

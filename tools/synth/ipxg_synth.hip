@@ -34,7 +34,9 @@ struct SynthLayout {              // 256 bytes
     uint16_t min_len;             // shortest frame (>= hdr_len)
     uint16_t alt_len;             // bytes of alt[] written at l7_off in packets of established flows
     uint8_t alt[8];               //   (the protocol's later messages: TLS application data, HTTP body)
-    uint16_t pad[8];
+    uint16_t blob_len;            // QUIC: the opening flows' long-header packets carry the mix's blob
+                                  // (a complete client Initial datagram) at l7_off, blob_len bytes
+    uint16_t pad[7];
 };
 static_assert(sizeof(SynthLayout) == 256, "layout record");
 
@@ -59,6 +61,7 @@ struct SynthParams {
     uint32_t dt_ns;
     uint32_t fwd_q16;             // P(forward direction) * 65536
     uint32_t syn_q16, psh_q16;    // TCP: P(SYN), P(PSH|ACK) * 65536 (else ACK)
+    const uint8_t* blob;          // the layouts' blob (blob_len bytes), or null
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
@@ -98,7 +101,8 @@ __global__ __launch_bounds__(256) void k_synth_plan(SynthParams P, uint4* plan, 
     } else if (L.size_mode == 1) {  // QUIC: an opening flow's packets are long-header Initials
         lng = P.flows[f].opening ? 1u : 0u;  // (>= 1200 B datagrams), an established flow's short
                                              // header 1-RTT packets
-        len = lng ? L.l7_off + 1200u : (s12 < 6 ? 80u : 1350u);
+        const uint32_t ini = L.blob_len > 1200u ? L.blob_len : 1200u;
+        len = lng ? L.l7_off + ini : (s12 < 6 ? 80u : 1350u);
     } else {
         len = 64u;
     }
@@ -119,7 +123,7 @@ __device__ __forceinline__ void put16(uint8_t* h, uint32_t off, uint32_t v) {
 __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4* plan, const uint64_t* off,
                                                      uint8_t* arena, uint4* desc) {
     __shared__ uint4 hdr[64][SYNTH_TMPL / 16];
-    __shared__ uint32_t meta[64][3];  // offset, len, hdr_len
+    __shared__ uint32_t meta[64][5];  // offset, len, hdr_len, blob start (l7_off), blob bytes (0: none)
     const uint32_t tid = threadIdx.x;
     const uint32_t base = blockIdx.x * 64u;
     if (tid < 64 && base + tid < P.n) {
@@ -160,6 +164,8 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4*
         meta[tid][0] = (uint32_t)off[i];
         meta[tid][1] = len;
         meta[tid][2] = L.hdr_len;
+        meta[tid][3] = L.l7_off;
+        meta[tid][4] = lng && P.blob ? L.blob_len : 0u;  // (an opening QUIC flow's Initial)
         const uint64_t t = P.t0_ns + (P.first_idx + i) * (uint64_t)P.dt_ns;
         const uint64_t us = t / 1000u;
         desc[i] = make_uint4((uint32_t)off[i], len | (len << 16), (uint32_t)(us / 1000000u), (uint32_t)(us % 1000000u));
@@ -167,10 +173,17 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4*
     __syncthreads();
     const uint32_t np = min(64u, P.n - base);
     for (uint32_t q = 0; q < np; ++q) {
-        const uint32_t o = meta[q][0], len = meta[q][1], hl = meta[q][2];
+        const uint32_t o = meta[q][0], len = meta[q][1], hl = meta[q][2], b0 = meta[q][3], bl = meta[q][4];
         for (uint32_t c = tid; c * 16u < len; c += 256u) {
             uint4 v = make_uint4(0, 0, 0, 0);
             if (c * 16u < hl) v = hdr[q][c];
+            if (bl && c * 16u + 16u > b0 && c * 16u < b0 + bl) {  // the blob over the template
+                uint8_t* vb = reinterpret_cast<uint8_t*>(&v);
+                for (uint32_t k = 0; k < 16; ++k) {
+                    const uint32_t at = c * 16u + k;
+                    if (at >= b0 && at < b0 + bl) vb[k] = P.blob[at - b0];
+                }
+            }
             *reinterpret_cast<uint4*>(arena + o + c * 16u) = v;
         }
     }

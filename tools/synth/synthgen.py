@@ -28,7 +28,7 @@ LAYOUT_DTYPE = np.dtype([
     ("tmpl", "u1", (192,)), ("hdr_len", "<u2"), ("addr_len", "<u2"), ("sip_off", "<u2"), ("dip_off", "<u2"),
     ("sport_off", "<u2"), ("dport_off", "<u2"), ("tcp_flags_off", "<u2"), ("vlan_off", "<u2"),
     ("patch_off", "<u2", (4,)), ("patch_bias", "<u2", (4,)), ("size_mode", "<u2"), ("l7_off", "<u2"),
-    ("min_len", "<u2"), ("alt_len", "<u2"), ("alt", "u1", (8,)), ("pad", "<u2", (8,)),
+    ("min_len", "<u2"), ("alt_len", "<u2"), ("alt", "u1", (8,)), ("blob_len", "<u2"), ("pad", "<u2", (7,)),
 ])
 FLOW_DTYPE = np.dtype([("sip", "u1", (16,)), ("dip", "u1", (16,)), ("sport", "<u2"), ("dport", "<u2"),
                        ("layout", "<u2"), ("vlan", "<u2"), ("mac_id", "<u4"), ("opening", "<u4")])
@@ -157,6 +157,31 @@ MIXES = {
 }
 
 
+_INITIAL = []
+
+
+def quic_initial():
+    """A complete QUIC client Initial datagram (the UDP payload of the reference's own QUIC test
+    capture, tests/functional/inputs/quic_initial-sample.pcap, copied into tests/golden/reference:
+    draft-29, 1330 bytes, one CRYPTO frame holding a TLS ClientHello).  The configs[4] mix's opening
+    flows carry it as their long-header packets, so the reference's QUIC plugin decrypts a real
+    Initial (RFC 9001 initial secrets from its DCID) on every one of them, as on live traffic -- a
+    template with an undecryptable payload was never detected by it (quic_parser.cpp
+    quic_set_server_port needs the parsed ClientHello)."""
+    if not _INITIAL:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "tests"))
+        import pcaputil
+        dl, pk = pcaputil.read_capture(os.path.join(os.path.dirname(os.path.dirname(HERE)), "tests", "golden",
+                                                    "reference", "quic_initial-sample.pcap"))
+        fr = bytes(pk[0][4])
+        et = struct.unpack(">H", fr[12:14])[0]
+        assert et == 0x86DD and fr[14 + 6] == 17  # IPv6 / UDP
+        udp = fr[54:]
+        _INITIAL.append(udp[8:8 + struct.unpack(">H", udp[4:6])[0] - 8])
+    return _INITIAL[0]
+
+
 class Mix:
     """Layouts + flow table (+ Zipf CDF) of one mix, on the host.
 
@@ -175,6 +200,12 @@ class Mix:
         rng = np.random.default_rng(seed)
         recs = [build_layout(**kw) for _, kw in spec]
         self.layouts = np.array([r for r, _ in recs], dtype=LAYOUT_DTYPE)
+        # QUIC layouts: the opening flows' long headers are a real client Initial (quic_initial)
+        self.blob = None
+        quic = np.array([kw.get("l7") == QUIC_INITIAL and kw.get("size_mode") == SIZE_QUIC for _, kw in spec])
+        if quic.any():
+            self.blob = np.frombuffer(quic_initial(), dtype=np.uint8)
+            self.layouts["blob_len"][quic] = len(self.blob)
         shares = np.array([s for s, _ in spec], dtype=np.float64)
         shares /= shares.sum()
         F = int(n_flows)
@@ -249,7 +280,7 @@ class _Params(ctypes.Structure):
                 ("rank_flow", ctypes.c_void_p), ("seed", ctypes.c_uint64), ("first_idx", ctypes.c_uint64),
                 ("t0_ns", ctypes.c_uint64), ("nflows", ctypes.c_uint32), ("n", ctypes.c_uint32),
                 ("dt_ns", ctypes.c_uint32), ("fwd_q16", ctypes.c_uint32), ("syn_q16", ctypes.c_uint32),
-                ("psh_q16", ctypes.c_uint32)]
+                ("psh_q16", ctypes.c_uint32), ("blob", ctypes.c_void_p)]
 
 
 _LIB = None
@@ -282,6 +313,7 @@ class Generator:
         self.d_flows = up(mix.flows)
         self.d_cdf = up(mix.cdf) if mix.cdf is not None else None
         self.d_rank = up(mix.rank_flow) if mix.rank_flow is not None else None
+        self.d_blob = up(mix.blob) if mix.blob is not None else None
         self.q16 = [int(round(x * 65536)) for x in (fwd_share, syn_share, psh_share)]
 
     def _params(self, first, n):
@@ -293,6 +325,7 @@ class Generator:
         p.seed, p.first_idx, p.t0_ns = self.seed, first, self.t0_ns
         p.nflows, p.n, p.dt_ns = len(self.mix.flows), n, self.dt_ns
         p.fwd_q16, p.syn_q16, p.psh_q16 = self.q16
+        p.blob = self.d_blob.data_ptr() if self.d_blob is not None else None
         return p
 
     def batch(self, first, n):
@@ -373,7 +406,8 @@ def host_plan(gen, first, n):
     lng = mix.flows["opening"][f] != 0
     mode = L["size_mode"].astype(np.int64)
     imix = np.where(s12 < 7, 64, np.where(s12 < 11, 594, 1518))
-    quic = np.where(lng, L["l7_off"].astype(np.int64) + 1200, np.where(s12 < 6, 80, 1350))
+    ini = np.maximum(L["blob_len"].astype(np.int64), 1200)
+    quic = np.where(lng, L["l7_off"].astype(np.int64) + ini, np.where(s12 < 6, 80, 1350))
     ln = np.where(mode == 0, imix, np.where(mode == 1, quic, 64))
     lng = lng & (mode == 1)
     ln = np.maximum(ln, L["min_len"].astype(np.int64))
@@ -435,4 +469,7 @@ def host_batch(gen, first, n):
             h[o:o + int(lay["alt_len"])] = lay["alt"][:int(lay["alt_len"])].tobytes()
         hl = min(int(lay["hdr_len"]), int(ln[i]))
         arena[off[i]:off[i] + hl] = np.frombuffer(bytes(h[:hl]), dtype=np.uint8)
+        if lng[i] and int(lay["blob_len"]) and mix.blob is not None:  # the Initial over the template
+            o = off[i] + int(lay["l7_off"])
+            arena[o:o + len(mix.blob)] = mix.blob
     return arena, desc
