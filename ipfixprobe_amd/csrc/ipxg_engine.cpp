@@ -31,6 +31,7 @@
 
 #include "../../include/ipxg.h"
 #include "ipxg_kernels.hpp"
+#include "ipxg_walkpool.hpp"
 
 using namespace ipxg;
 
@@ -109,73 +110,6 @@ struct alignas(128) ExportVec {
                                               // (one per flow at most; the flow's index in reserved2)
 };
 
-// The host walk's worker threads: run(f) calls f(t) for every t in [0, size()) -- t = 0 on the
-// calling thread -- and returns when all have returned.  Persistent across batches (a batch of
-// configs[2] walks ~10^5 flows; spawning threads per batch would cost more than small walks).
-class WalkPool {
-public:
-    explicit WalkPool(unsigned n) {
-        for (unsigned t = 1; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
-    }
-    ~WalkPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            quit_ = true;
-        }
-        cv_.notify_all();
-        for (std::thread& t : th_) t.join();
-    }
-    unsigned size() const { return (unsigned)th_.size() + 1; }
-    // true when a job raised out of a worker thread since the last call (then: an engine bug or a
-    // plugin that throws past the C ABI; plugin_walk fails the batch with IPXG_EPLUGIN)
-    bool take_escaped() { return escaped_.exchange(false); }
-    void run(const std::function<void(unsigned)>& f) {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &f;
-            left_ = (unsigned)th_.size();
-            ++gen_;
-        }
-        cv_.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> g(m_);
-        done_.wait(g, [this] { return left_ == 0; });
-        job_ = nullptr;
-    }
-
-private:
-    void loop(unsigned t) {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(unsigned)>* f;
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return quit_ || gen_ != seen; });
-                if (quit_) return;
-                seen = gen_;
-                f = job_;
-            }
-            // the job catches what its hooks raise (plugin_walk's walk_range); nothing may unwind
-            // out of a worker thread (std::terminate) -- whatever still does is recorded and
-            // reported by the caller's run() like a failed range
-            try {
-                (*f)(t);
-            } catch (...) {
-                escaped_.store(true);
-            }
-            std::lock_guard<std::mutex> g(m_);
-            if (--left_ == 0) done_.notify_one();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(unsigned)>* job_ = nullptr;
-    unsigned left_ = 0;
-    uint64_t gen_ = 0;
-    bool quit_ = false;
-    std::atomic<bool> escaped_{false};
-};
 struct ipxg_engine {
     ipxg_config cfg;
     hipStream_t st = nullptr;
@@ -275,6 +209,7 @@ struct ipxg_engine {
     DevBuf ipf_rec, ipf_out, ipf_tot, ipf_off;  // IPFIX formatting scratch
     DevBuf ipf_msg, ipf_plan;                   // IPFIX messages: output, plan (sets + messages)
     uint8_t* plan_h = nullptr;                  // pinned staging of the plan (asynchronous upload)
+    const uint64_t* ipf_counts = nullptr;       // device: {bytes, records} of the last message call
     size_t plan_h_bytes = 0;
     hipEvent_t plan_ev = nullptr;               // the last plan upload
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
@@ -1431,7 +1366,6 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     std::vector<int> wfail(T, 0);  // a walk thread: 2 out of host memory, 3 a plugin failed
     std::vector<std::string> wmsg(T);
     auto walk_range = [&](unsigned t) {
-        if (t >= T) return;  // (the pool may hold more threads than this walk uses)
         const uint32_t f0 = fr[t], f1 = fr[t + 1];
         WalkOut& wo = wos[t];
         try {
@@ -1499,7 +1433,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             wmsg[t] = "process plugin walk: a hook raised a non-standard exception";
         }
     };
-    if (T > 1) e->pool->run(walk_range);
+    if (T > 1) e->pool->run(walk_range, T);  // (threads T.. of a larger pool sit this walk out)
     else walk_range(0);
     if (T > 1 && e->pool->take_escaped()) {  // (walk_range catches everything: not expected)
         wfail[0] = 3;
@@ -2228,7 +2162,8 @@ static int ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flo
     const IpfixPlan P = ipfix_plan(n - (uint64_t)n6, (uint64_t)n6, *x);
     const size_t ns4 = P.sets[0].size(), ns6 = P.sets[1].size(), nm = P.msgs.size();
     const size_t moff = (ns4 + ns6) * sizeof(IpfixSet), toff = moff + nm * sizeof(IpfixMsg);
-    const size_t pbytes = toff + IPFIX_TMPL_MSG;
+    const size_t coff = (toff + IPFIX_TMPL_MSG + 7) & ~(size_t)7;  // {stream bytes, records} (u64 each)
+    const size_t pbytes = coff + 2 * sizeof(uint64_t);
     // the pinned staging buffer may still feed the previous plan's upload
     if (e->plan_ev) HIPCHK(e, hipEventSynchronize(e->plan_ev));
     else HIPCHK(e, hipEventCreateWithFlags(&e->plan_ev, hipEventDisableTiming));
@@ -2244,10 +2179,13 @@ static int ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flo
     std::memcpy(plan + ns4 * sizeof(IpfixSet), P.sets[1].data(), ns6 * sizeof(IpfixSet));
     std::memcpy(plan + moff, P.msgs.data(), nm * sizeof(IpfixMsg));
     ipfix_template_msg(plan + toff, *x);
+    const uint64_t counts[2] = {P.bytes, n};
+    std::memcpy(plan + coff, counts, sizeof(counts));
     if ((rc = ensure(e, e->ipf_plan, pbytes))) return rc;
     if ((rc = ensure(e, e->ipf_msg, P.bytes + 16))) return rc;
     HIPCHK(e, hipMemcpyAsync(e->ipf_plan.p, plan, pbytes, hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipEventRecord(e->plan_ev, e->st));
+    e->ipf_counts = (const uint64_t*)((uint8_t*)e->ipf_plan.p + coff);
     uint8_t* out = (uint8_t*)e->ipf_msg.p;
     if (P.tmpl)
         HIPCHK(e, hipMemcpyAsync(out, (uint8_t*)e->ipf_plan.p + toff, IPFIX_TMPL_MSG, hipMemcpyDeviceToDevice, e->st));
@@ -2325,6 +2263,13 @@ int ipxg_device_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const uin
     e->ex6_valid = e->count6_on;
     HIPCHK(e, hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st));
     e->ex_zero_pending = false;
+    return IPXG_OK;
+}
+
+int ipxg_device_ipfix_counts(ipxg_engine* e, const uint64_t** dptr) {
+    if (!e || !dptr) return IPXG_EINVAL;
+    if (!e->ipf_counts) return set_err(e, IPXG_ESTATE, "no ipxg_device_ipfix_messages call yet");
+    *dptr = e->ipf_counts;
     return IPXG_OK;
 }
 
