@@ -7,8 +7,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <pthread.h>
+
 #include <openssl/evp.h>
-#include <openssl/hmac.h>
 
 enum { C_PRE_CREATE, C_POST_CREATE, C_PRE_UPDATE, C_POST_UPDATE, C_PRE_EXPORT, C_FLUSH, C_N };
 
@@ -21,7 +22,15 @@ typedef struct std_ctx {
     struct std_ctx* root;   /* NULL on the instance ipxg_std_plugin made */
     struct std_ctx* next;   /* root: first copy; copy: next copy of the same root */
     struct std_ctx* prev;
+    EVP_CIPHER_CTX* ecb;    /* QUIC: the instance's cipher contexts, made on first use and kept */
+    EVP_CIPHER_CTX* gcm;    /* (walk threads each hold their own copy) */
 } std_ctx;
+
+static void std_ctx_release(std_ctx* c) {
+    if (c->ecb) EVP_CIPHER_CTX_free(c->ecb);
+    if (c->gcm) EVP_CIPHER_CTX_free(c->gcm);
+    free(c);
+}
 
 static void* std_copy(void* ctx) {
     std_ctx* r = (std_ctx*)ctx;
@@ -42,7 +51,7 @@ static void std_free_copy(void* ctx) {
     for (int k = 0; k < C_N; ++k) c->root->calls[k] += c->calls[k];
     c->prev->next = c->next;
     if (c->next) c->next->prev = c->prev;
-    free(c);
+    std_ctx_release(c);
 }
 
 static const uint8_t* payload(const ipxg_packet_view* v, uint32_t* n) {
@@ -417,8 +426,100 @@ static const uint8_t* quic_salt(uint32_t v) {
     return NULL;
 }
 
+/* SHA-256 (FIPS 180-4) and HMAC-SHA256 (RFC 2104) for the Initial secrets (RFC 9001 §5.2): a
+ * few hundred bytes per flow, where OpenSSL 3's one-shot HMAC() fetches its algorithms on every
+ * call and serialises the walk threads on the provider's locks. */
+typedef struct {
+    uint32_t h[8];
+    uint8_t b[64];
+    uint64_t n;
+} sha256_t;
+
+static const uint32_t SHA_K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+#define ROR32(x, r) (((x) >> (r)) | ((x) << (32 - (r))))
+
+static void sha256_block(uint32_t h[8], const uint8_t* p) {
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i)
+        w[i] = ((uint32_t)p[4 * i] << 24) | ((uint32_t)p[4 * i + 1] << 16) | ((uint32_t)p[4 * i + 2] << 8) | p[4 * i + 3];
+    for (int i = 16; i < 64; ++i) {
+        const uint32_t s0 = ROR32(w[i - 15], 7) ^ ROR32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        const uint32_t s1 = ROR32(w[i - 2], 17) ^ ROR32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t t1 = k + (ROR32(e, 6) ^ ROR32(e, 11) ^ ROR32(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[i] + w[i];
+        const uint32_t t2 = (ROR32(a, 2) ^ ROR32(a, 13) ^ ROR32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+}
+
+static void sha256_init(sha256_t* s) {
+    static const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    memcpy(s->h, iv, sizeof(iv));
+    s->n = 0;
+}
+
+static void sha256_put(sha256_t* s, const uint8_t* p, size_t n) {
+    while (n) {
+        const size_t at = s->n & 63, k = 64 - at < n ? 64 - at : n;
+        memcpy(s->b + at, p, k);
+        s->n += k;
+        p += k;
+        n -= k;
+        if ((s->n & 63) == 0) sha256_block(s->h, s->b);
+    }
+}
+
+static void sha256_end(sha256_t* s, uint8_t out[32]) {
+    const uint64_t bits = s->n * 8;
+    static const uint8_t pad[64] = {0x80};
+    sha256_put(s, pad, 1 + ((119 - (s->n & 63)) & 63));
+    uint8_t l[8];
+    for (int i = 0; i < 8; ++i) l[i] = (uint8_t)(bits >> (56 - 8 * i));
+    sha256_put(s, l, 8);
+    for (int i = 0; i < 8; ++i) {
+        out[4 * i] = (uint8_t)(s->h[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(s->h[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(s->h[i] >> 8);
+        out[4 * i + 3] = (uint8_t)s->h[i];
+    }
+}
+
+/* HMAC-SHA256 with a key of at most 64 bytes (the salts and secrets here: 20 / 32) */
+static void hmac_sha256(const uint8_t* key, size_t kl, const uint8_t* msg, size_t ml, uint8_t out[32]) {
+    uint8_t ip[64], op[64], inner[32];
+    memset(ip, 0x36, 64);
+    memset(op, 0x5c, 64);
+    for (size_t i = 0; i < kl; ++i) {
+        ip[i] ^= key[i];
+        op[i] ^= key[i];
+    }
+    sha256_t s;
+    sha256_init(&s);
+    sha256_put(&s, ip, 64);
+    sha256_put(&s, msg, ml);
+    sha256_end(&s, inner);
+    sha256_init(&s);
+    sha256_put(&s, op, 64);
+    sha256_put(&s, inner, 32);
+    sha256_end(&s, out);
+}
+
 /* HKDF-Expand-Label(secret, "tls13 " + label, "", len) for len <= 32 (one HMAC-SHA256 block) */
-static int quic_expand(const uint8_t secret[32], const char* label, unsigned len, uint8_t* out) {
+static void quic_expand(const uint8_t secret[32], const char* label, unsigned len, uint8_t* out) {
     uint8_t info[64];
     const unsigned ll = (unsigned)strlen(label);
     info[0] = 0;
@@ -429,10 +530,18 @@ static int quic_expand(const uint8_t secret[32], const char* label, unsigned len
     info[9 + ll] = 0;     /* context length */
     info[10 + ll] = 1;    /* HKDF-Expand block counter */
     uint8_t t[32];
-    unsigned tl = 0;
-    if (!HMAC(EVP_sha256(), secret, 32, info, 11 + ll, t, &tl)) return 0;
+    hmac_sha256(secret, 32, info, 11 + ll, t);
     memcpy(out, t, len);
-    return 1;
+}
+
+/* The ciphers, fetched once per process (an implicit fetch per EVP_*Init_ex call is the other
+ * provider-lock hot spot of OpenSSL 3) */
+static EVP_CIPHER* g_aes_ecb;
+static EVP_CIPHER* g_aes_gcm;
+static pthread_once_t g_aes_once = PTHREAD_ONCE_INIT;
+static void aes_fetch(void) {
+    g_aes_ecb = EVP_CIPHER_fetch(NULL, "AES-128-ECB", NULL);
+    g_aes_gcm = EVP_CIPHER_fetch(NULL, "AES-128-GCM", NULL);
 }
 
 /* quic_get_variable_length (:206-251) over a buffer of at least QUIC_BUF + 8 bytes */
@@ -485,23 +594,24 @@ static int quic_tls(const uint8_t* d, uint32_t n) {
 
 /* quic_parse_initial (:1430-1470) of the Initial whose packet number starts at pkt[pn] with the
  * Length field's value plen: 0 failed, 1 the TLS handshake header parsed, 2 parsed_initial */
-static int quic_open_initial(const uint8_t* pkt, uint64_t pn, uint64_t plen, const uint8_t* salt, int v2,
-                             const uint8_t* dcid, unsigned dcl) {
+static int quic_open_initial(std_ctx* cx, const uint8_t* pkt, uint64_t pn, uint64_t plen, const uint8_t* salt,
+                             int v2, const uint8_t* dcid, unsigned dcl) {
     uint8_t sec[32], cis[32], key[16], iv[12], hp[16];
-    unsigned sl = 0;
-    if (!HMAC(EVP_sha256(), salt, 20, dcid, dcl, sec, &sl)) return 0;            /* HKDF-Extract */
-    if (!quic_expand(sec, "client in", 32, cis)) return 0;
-    if (!quic_expand(cis, v2 ? "quicv2 key" : "quic key", 16, key) || !quic_expand(cis, v2 ? "quicv2 iv" : "quic iv", 12, iv) ||
-        !quic_expand(cis, v2 ? "quicv2 hp" : "quic hp", 16, hp))
-        return 0;
+    hmac_sha256(salt, 20, dcid, dcl, sec);  /* HKDF-Extract */
+    quic_expand(sec, "client in", 32, cis);
+    quic_expand(cis, v2 ? "quicv2 key" : "quic key", 16, key);
+    quic_expand(cis, v2 ? "quicv2 iv" : "quic iv", 12, iv);
+    quic_expand(cis, v2 ? "quicv2 hp" : "quic hp", 16, hp);
+    pthread_once(&g_aes_once, aes_fetch);
+    if (!g_aes_ecb || !g_aes_gcm) return 0;
+    if (!cx->ecb && !(cx->ecb = EVP_CIPHER_CTX_new())) return 0;
+    if (!cx->gcm && !(cx->gcm = EVP_CIPHER_CTX_new())) return 0;
     /* header protection (quic_decrypt_initial_header :780-842): AES-128-ECB of the sample */
     uint8_t mask[16];
     int ol = 0, fl = 0;
-    EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
-    if (!c) return 0;
-    int ok = EVP_EncryptInit_ex(c, EVP_aes_128_ecb(), NULL, hp, NULL) && EVP_CIPHER_CTX_set_padding(c, 0) &&
+    EVP_CIPHER_CTX* c = cx->ecb;
+    int ok = EVP_EncryptInit_ex(c, g_aes_ecb, NULL, hp, NULL) && EVP_CIPHER_CTX_set_padding(c, 0) &&
              EVP_EncryptUpdate(c, mask, &ol, pkt + pn + 4, 16) && EVP_EncryptFinal_ex(c, mask + ol, &fl);
-    EVP_CIPHER_CTX_free(c);
     if (!ok) return 0;
     const uint8_t first = pkt[0] ^ (mask[0] & 0x0f);
     const unsigned pnl = (first & 3u) + 1;
@@ -521,14 +631,12 @@ static int quic_open_initial(const uint8_t* pkt, uint64_t pn, uint64_t plen, con
     len -= 16;
     uint8_t dec[QUIC_BUF + 16];
     memset(dec, 0, sizeof(dec));
-    c = EVP_CIPHER_CTX_new();
-    if (!c) return 0;
-    ok = EVP_DecryptInit_ex(c, EVP_aes_128_gcm(), NULL, NULL, NULL) &&
+    c = cx->gcm;
+    ok = EVP_DecryptInit_ex(c, g_aes_gcm, NULL, NULL, NULL) &&
          EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_SET_IVLEN, 12, NULL) && EVP_DecryptInit_ex(c, NULL, NULL, key, iv) &&
          EVP_DecryptUpdate(c, NULL, &ol, hdr, (int)body) && EVP_DecryptUpdate(c, dec, &ol, pkt + body, (int)len) &&
          EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_SET_TAG, 16, (void*)(pkt + body + len)) &&
          EVP_DecryptFinal_ex(c, dec + ol, &fl) > 0;
-    EVP_CIPHER_CTX_free(c);
     if (!ok) return 0;
     /* CRYPTO frames (quic_reassemble_frames :1009-1043) */
     uint8_t asm_[QUIC_BUF + 16];
@@ -583,7 +691,7 @@ static int quic_open_initial(const uint8_t* pkt, uint64_t pn, uint64_t plen, con
 }
 
 /* QUICParser::quic_check_quic_long_header_packet (:1409-1428) for a new flow (no stored DCID) */
-static int quic_detected(const uint8_t* d, uint32_t n) {
+static int quic_detected(std_ctx* cx, const uint8_t* d, uint32_t n) {
     if (n < 8 || !(d[0] & 0x80)) return 0;  /* quic_long_header_packet: long header, >= 8 bytes */
     int v2;
     const uint32_t ver0 = ((uint32_t)d[1] << 24) | ((uint32_t)d[2] << 16) | ((uint32_t)d[3] << 8) | d[4];
@@ -644,7 +752,7 @@ static int quic_detected(const uint8_t* d, uint32_t n) {
                 /* the first attempt with the flow's first DCID, then with this packet's: one DCID
                  * for a new flow (a flow whose later Initial only opens with the DCID of its first
                  * one -- after a Retry -- is decided on this packet's alone: not restated) */
-                const int r = quic_open_initial(pk + off, o - off, plen, salt ? salt : pk, v2, dcid, dcl);
+                const int r = quic_open_initial(cx, pk + off, o - off, plen, salt ? salt : pk, v2, dcid, dcl);
                 if (r >= 1) hs = 1;
                 if (r == 2) parsed = 1;
             }
@@ -668,7 +776,7 @@ static int quic_add(void* ctx, ipxg_flow_record* f, const ipxg_packet_view* v, i
     const uint8_t* d = payload(v, &n);
     /* add_quic: a flow without the extension gets it when QUIC is detected; with it, nothing
      * changes the flow (the packet types it records are enrichment) */
-    if (!(f->ext & IPXG_STD_EXT_QUIC) && v->pkt->ip_proto == 17 && quic_detected(d, n)) f->ext |= IPXG_STD_EXT_QUIC;
+    if (!(f->ext & IPXG_STD_EXT_QUIC) && v->pkt->ip_proto == 17 && quic_detected((std_ctx*)ctx, d, n)) f->ext |= IPXG_STD_EXT_QUIC;
     return count(ctx, idx, 0);
 }
 static int quic_post_create(void* ctx, ipxg_flow_record* f, const ipxg_packet_view* v) {
@@ -736,9 +844,9 @@ void ipxg_std_plugin_free(ipxg_plugin* pl) {
         while (r->next) { /* copies an engine still held (destroy the engine first) */
             std_ctx* c = r->next;
             r->next = c->next;
-            free(c);
+            std_ctx_release(c);
         }
-        free(r);
+        std_ctx_release(r);
         pl->ctx = NULL;
     }
 }

@@ -4,7 +4,7 @@ against the bench's native stand-ins, same workload, same engine: the host walk'
 with the real plugins -- their enrichment included (TLS/QUIC ClientHello parsing, QUIC's
 AES-GCM Initial decryption) -- which bench.py cannot time (it may load nothing under oracle/).
 
-  python3 tools/real_plugins_walk.py imix|quic [steps]   -> one JSON line per plugin set
+  python3 tools/real_plugins_walk.py imix|quic [steps] [stand-in|reference]   -> one JSON line per plugin set
 
 Test/measurement tooling only (loads oracle/_ref)."""
 import json
@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools", "synth"))
 
 
-def main(name, steps):
+def main(name, steps, kinds=("stand-in", "reference")):
     import torch
     import bench
     import synthgen
@@ -32,7 +32,7 @@ def main(name, steps):
     gen = synthgen.Generator(mix, dev, seed=1234)
     batches = [gen.batch(k * n, n) for k in range(nb)]
     torch.cuda.synchronize()
-    for kind in ("stand-in", "reference"):
+    for kind in kinds:
         pls = [StdPlugin(p) if kind == "stand-in" else test_ref_plugins.RefPlugin(p) for p in names]
         with Engine(bench.engine_params(1_000_000)) as e:
             for p in pls:
@@ -62,4 +62,5 @@ def main(name, steps):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "imix", int(sys.argv[2]) if len(sys.argv) > 2 else 2)
+    main(sys.argv[1] if len(sys.argv) > 1 else "imix", int(sys.argv[2]) if len(sys.argv) > 2 else 2,
+         tuple(sys.argv[3:]) or ("stand-in", "reference"))
