@@ -176,12 +176,13 @@ class ExportGather:
         import torch
         ptr, nb, nr, _ = self.eng.device_ipfix_messages(self.x)
         src = torch.as_tensor(_DevArray(ptr, max(nb, 1)), device=self.device)
+        counts = torch.as_tensor(_DevArray(self.eng.device_ipfix_counts(), 16), device=self.device).view(torch.int64)
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         copied = torch.cuda.Event()
         self.side.wait_stream(self.eng_stream)
         with torch.cuda.stream(self.side):
             t0.record()
-            self.g.push(src, nb, nr, copied=copied)
+            self.g.push(src, nb, nr, copied=copied, counts=counts)
             t1.record()
         self.eng_stream.wait_event(copied)
         self.events.append((t0, t1))
@@ -575,6 +576,9 @@ def main():
                          "dns,http,tls; configs[4]: quic)")
     ap.add_argument("--walk-threads", type=int, default=0,
                     help="threads of the plugin flows' host walk (0: the host's threads, at most 16)")
+    ap.add_argument("--gather", action="store_true",
+                    help="run the N > 1 step's export exchange (IPFIX streams to rank 0, shard.StreamGather) at any "
+                         "N, world size 1 included: its cost on one GPU")
     ap.add_argument("--cpu-selftest", action="store_true",
                     help="no GPU: the N-rank launcher and the export exchange over gloo with synthetic streams "
                          "(tests/test_launcher.py)")
@@ -634,7 +638,7 @@ def main():
             eng.add_plugin(pl.struct)
         wl.description += "; process plugins %s through the bridge (native stand-ins)" % ",".join(names)
     cursor = [0]
-    gather = ExportGather(eng, rank, world, device) if world > 1 else None
+    gather = ExportGather(eng, rank, world, device) if world > 1 or args.gather else None
 
     def step():
         if wl.finish:

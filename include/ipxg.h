@@ -492,6 +492,12 @@ int ipxg_poll_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, uint8_t* 
  * gathering the per-GPU message streams with RCCL. */
 int ipxg_device_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, const uint8_t** dptr, size_t* n_records,
                                size_t* bytes, size_t* msgs);
+/* The {stream bytes, records} of the last ipxg_device_ipfix_messages call as two uint64 in device
+ * memory, written in order on the engine's stream (ipxg_stream) with the messages: a consumer on
+ * another stream that waits for the engine's reads them without a host round trip (the header of
+ * the multi-GPU stream gather).  Valid until the next IPFIX message call (ipxg_ipfix_export,
+ * ipxg_poll_ipfix_messages, ipxg_device_ipfix_messages).  IPXG_ESTATE before the first. */
+int ipxg_device_ipfix_counts(ipxg_engine* eng, const uint64_t** dptr);
 
 /* ---- stateless device entry points (parity tests, tools) ---------------------------- */
 /* Run the device parser on a batch; out receives n records (host pointer). */

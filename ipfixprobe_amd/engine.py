@@ -101,6 +101,7 @@ EXPORTED_SYMBOLS = [
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
     "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
     "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
+    "ipxg_device_ipfix_counts",
     "ipxg_parser_stats", "ipxg_top_ports", "ipxg_add_plugin", "ipxg_set_walk_threads",
     "ipxg_demux", "ipxg_demux_arena_bytes", "ipxg_demux_split",
 ]
@@ -205,6 +206,7 @@ def lib():
         L.ipxg_top_ports.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
         L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                  ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.ipxg_device_ipfix_counts.argtypes = [vp, ctypes.POINTER(vp)]
         L.ipxg_demux.argtypes = [ctypes.POINTER(Batch), u32, u32, vp, vp]
         L.ipxg_demux_arena_bytes.argtypes = [ctypes.POINTER(Batch), vp, u32]
         L.ipxg_demux_arena_bytes.restype = ctypes.c_uint64
@@ -510,6 +512,13 @@ class Engine:
         self._check(lib().ipxg_device_ipfix_messages(self._h, ctypes.byref(x), ctypes.byref(p), ctypes.byref(nr),
                                                      ctypes.byref(nb), ctypes.byref(nm)), "ipxg_device_ipfix_messages")
         return p.value, nb.value, nr.value, nm.value
+
+    def device_ipfix_counts(self):
+        """Device pointer to the {bytes, records} (2 x uint64) of the last device_ipfix_messages
+        call, written on the engine's stream (no host round trip for the gather's header)."""
+        p = ctypes.c_void_p()
+        self._check(lib().ipxg_device_ipfix_counts(self._h, ctypes.byref(p)), "ipxg_device_ipfix_counts")
+        return p.value
 
     def parse(self, arena, desc):
         b = self._batch(arena, desc)

@@ -2,6 +2,7 @@
 canonical hash never share state, so the union of per-rank results equals one run over the
 whole capture; the export gather runs over torch.distributed (gloo on CPU here, RCCL on the
 GPUs in bench.py)."""
+import json
 import os
 import socket
 import sys
@@ -234,5 +235,26 @@ def test_bench_export_gather_single_rank():
         recs["end_reason"] = 0
         assert ipfixdec.basic_view(recs) == ipfixdec.basic_view(w)
         assert g.g.received_bytes == len(b0) + len(b1)
+        # the headers were device copies of the engine's own counts (ipxg_device_ipfix_counts)
+        assert sorted(tuple(int(v) for v in h[0]) for h in g.g.hdr_host) == sorted([(len(b0), n0), (len(b1), n1)])
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_bench_gather_flag_single_gpu():
+    """bench.py --gather: the N > 1 exchange at world size 1, no launcher --
+    every exported flow's IPFIX record reaches rank 0's stream, the stream bytes rank 0 holds
+    equal the bytes produced, and the line reports the side stream's per-step cost."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gather", "--steps", "20", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-e2e"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    g = line["gather"]
+    assert line["n_gpus"] == 1 and g is not None
+    assert g["device_ms_per_step"] > 0
+    assert g["rank0_receives_bytes_per_step"] == g["rank0_stream_bytes_per_step"] > 0
+    # 100k flows exported per udp64 step, 81 bytes each (IPv4 basic record) plus message headers
+    assert 81 * line["flows_exported_per_step"] < g["rank0_stream_bytes_per_step"] < 90 * line["flows_exported_per_step"]
