@@ -23,7 +23,7 @@ __device__ __forceinline__ bool flow_accumulate(const TableView& t, const Params
                                                 const DevPkt& pk, uint32_t idx, uint32_t sec, uint32_t* new_keys) {
     uint64_t lo, hf;
     uint32_t cdir;
-    canon(pk, p, lo, cdir, hf);
+    canon<false>(pk, p, lo, cdir, hf);
     return merge_packet_atomic(t, lo, idx, pack_misc(pk, cdir, time_bucket(sec, b.base_sec, p.bucket_w)),
                                new_keys);
 }
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, Ta
             if (is_frag) apply_frag_ports(p, f, i, pk);
             uint64_t lo, hf;
             uint32_t cdir;
-            canon(pk, p, lo, cdir, hf);
+            canon<false>(pk, p, lo, cdir, hf);
             const int64_t rr = complex_rank_of(cx, lo);
             if (rr >= 0) {
                 const uint32_t r = (uint32_t)rr;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
         canon(pk, p, lo, cdir, hf);
         bool dsrc = true;
         if (live) {  // cache.cpp:428-472
-            dsrc = p.split_biflow || cdir == rec.reserved[0];
+            dsrc = p.split_biflow || hf == rec.flow_hash;  // cache.cpp:428 (the record may be the host walk's)
             const uint8_t flw = dsrc ? rec.src_tcp_flags : rec.dst_tcp_flags;
             uint8_t reason = 0;
             if ((pk.tcp_flags & 0x02) && (flw & 0x05)) reason = IPXG_FLOW_END_EOF;

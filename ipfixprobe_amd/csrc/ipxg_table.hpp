@@ -99,19 +99,44 @@ __device__ __forceinline__ void flush_block_stats(uint32_t* sc, unsigned long lo
 // lo = min(XXH64(key), XXH64(key_inv)) identifies the biflow (the reference's identity is
 // the 64-bit hash too, cache.cpp:84-92, looked up forward then inverse, :341-373); cdir is
 // the packet's direction relative to lo; hf the forward hash (the record's flow_hash).
+// The canonical direction of a packet: 1 when its (source address, source port) endpoint orders
+// after its (destination address, destination port) one -- address words compared first (one for
+// IPv4, four for IPv6), then ports; equal endpoints give 0.  Both directions of a biflow see the
+// same canonical endpoint order, so the same canonical key.
+__device__ __forceinline__ uint32_t canon_dir(const DevPkt& pk) {
+    // (words compared most significant first as one 64-bit pair per step: no loop, no indexing)
+    const bool v6 = pk.ip_version == 6;
+    const uint64_t s0 = ((uint64_t)pk.sip[0] << 32) | (v6 ? pk.sip[1] : 0u);
+    const uint64_t d0 = ((uint64_t)pk.dip[0] << 32) | (v6 ? pk.dip[1] : 0u);
+    const uint64_t s1 = v6 ? ((uint64_t)pk.sip[2] << 32) | pk.sip[3] : 0ull;
+    const uint64_t d1 = v6 ? ((uint64_t)pk.dip[2] << 32) | pk.dip[3] : 0ull;
+    if (s0 != d0) return s0 > d0 ? 1u : 0u;
+    if (s1 != d1) return s1 > d1 ? 1u : 0u;
+    return pk.src_port > pk.dst_port ? 1u : 0u;
+}
+
+// The table key of a packet's flow: XXH64 of its canonical key (the forward key in canonical
+// direction 0, the inverse key in direction 1) -- one hash per packet.  The reference finds a
+// flow by either of its two hashes (cache.cpp:330-372: the forward hash, then the inverse one);
+// a canonical key names the same biflow (barring 64-bit collisions, which the reference's own
+// lookup shares).  The creator's forward hash (the record's flow_hash) is lo when the creator
+// went in canonical direction 0, so `flow_hash != slot key` still tells the creator's direction
+// (finalize_slot).  HF: also hf = XXH64(forward key) (record creation; a second hash only in
+// canonical direction 1).  split_biflow: lo = hf, direction 0.
+template <bool HF = true>
 __device__ __forceinline__ void canon(const DevPkt& pk, const Params& p, uint64_t& lo, uint32_t& cdir,
                                       uint64_t& hf) {
     FlowKey kf, ki;
     build_keys(pk, kf, ki);
-    hf = key_hash(kf);
     if (p.split_biflow) {
-        lo = hf;
+        hf = lo = key_hash(kf);
         cdir = 0;
         return;
     }
-    uint64_t hi = key_hash(ki);
-    lo = hf < hi ? hf : hi;
-    cdir = hf > hi ? 1u : 0u;
+    cdir = canon_dir(pk);
+    lo = key_hash(cdir ? ki : kf);
+    hf = lo;
+    if (HF && cdir) hf = key_hash(kf);
 }
 
 __device__ __forceinline__ uint32_t time_bucket(uint32_t sec, uint32_t base, uint32_t w) {
@@ -1215,6 +1240,26 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     tbl_store_rec(t, s, rec);
     clear_slot(&t.hot(s), h.key, SLOT_LIVE);
     return res;
+}
+
+// ---- process-plugin pre-classifier rules (ipxg_plugin: TCP/UDP ports, payload prefixes) ------
+// Does the parsed packet match rule r?  pay(k): byte k of its payload (k < 16, within payload_len).
+template <class B>
+__device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, const B& pay) {
+    const bool tcp = pk.l4 == 6, udp = pk.l4 == 17;
+    if (!((tcp && (r.proto_mask & 1)) || (udp && (r.proto_mask & 2)))) return false;
+    for (uint32_t k = 0; k < r.n_ports; ++k)
+        if (pk.src_port == r.ports[k] || pk.dst_port == r.ports[k]) return true;
+    for (uint32_t q = 0; q < r.n_prefixes; ++q) {
+        const uint32_t n = r.prefix_len[q];
+        if (n == 0 || n > pk.payload_len) continue;
+        const bool msk = (r.masked >> q) & 1u;
+        bool eq = true;
+        for (uint32_t k = 0; k < n && eq; ++k)
+            eq = ((pay(k) ^ r.prefix[q][k]) & (msk ? r.prefix_mask[q][k] : 0xFFu)) == 0;
+        if (eq) return true;
+    }
+    return false;
 }
 
 }  // namespace ipxg
