@@ -171,24 +171,60 @@ class ExportGather:
         self.side = torch.cuda.Stream(device=device)
         self.eng_stream = torch.cuda.ExternalStream(eng.stream(), device=device)
         self.events = []
+        self.fmt_stream = None
+        self.host_s = 0.0  # host time inside step() (the engine's IPFIX planning + the stream hand-off)
 
-    def step(self):
+    def produce(self):
+        """The pending exports as the engine's IPFIX message stream, formatted on the engine's
+        formatting stream (ipxg_device_ipfix_messages: beside the kernels of a batch submitted
+        since); the hand-off waits for push_pending()."""
         import torch
+        h0 = time.perf_counter()
         ptr, nb, nr, _ = self.eng.device_ipfix_messages(self.x)
+        ready = torch.cuda.Event()
+        if self.fmt_stream is None:  # (the engine's formatting stream exists from the first call)
+            self.fmt_stream = torch.cuda.ExternalStream(self.eng.ipfix_stream(), device=self.device)
+        ready.record(self.fmt_stream)
+        self.pending = (ptr, nb, nr, self.eng.device_ipfix_counts(), ready)
+        self.host_s += time.perf_counter() - h0
+
+    def push_pending(self):
+        """The produced stream to StreamGather on the side stream.  The bench calls it once the
+        next step's kernels are enqueued, so this host work runs beside them.  No copy: the engine
+        alternates two message buffers (ipxg_device_ipfix_messages), so this stream stays valid
+        while the next one is formatted; its send happens in the next push, and the engine's
+        stream waits for `copied` (recorded after that send) before it formats into this buffer
+        again."""
+        import torch
+        if getattr(self, "pending", None) is None:
+            return
+        h0 = time.perf_counter()
+        ptr, nb, nr, cptr, ready = self.pending
+        self.pending = None
         src = torch.as_tensor(_DevArray(ptr, max(nb, 1)), device=self.device)
-        counts = torch.as_tensor(_DevArray(self.eng.device_ipfix_counts(), 16), device=self.device).view(torch.int64)
+        counts = torch.as_tensor(_DevArray(cptr, 16), device=self.device).view(torch.int64)
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         copied = torch.cuda.Event()
-        self.side.wait_stream(self.eng_stream)
+        self.side.wait_event(ready)
         with torch.cuda.stream(self.side):
             t0.record()
-            self.g.push(src, nb, nr, copied=copied, counts=counts)
+            self.g.push(src, nb, nr, copied=copied, counts=counts, copy=False)
             t1.record()
         self.eng_stream.wait_event(copied)
         self.events.append((t0, t1))
+        self.host_s += time.perf_counter() - h0
+
+    def step(self):
+        self.produce()
+        self.push_pending()
 
     def flush(self):
+        """The last step's exports (their step() comes with a next step that does not follow),
+        then the last exchange."""
         import torch
+        if self.eng.pending():
+            self.produce()
+        self.push_pending()
         with torch.cuda.stream(self.side):
             self.g.flush()
 
@@ -641,20 +677,25 @@ def main():
     gather = ExportGather(eng, rank, world, device) if world > 1 or args.gather else None
 
     def step():
+        # with the gather: the previous step's exports are formatted (ipxg_device_ipfix_messages on
+        # the engine's formatting stream) and handed to the gather right after this step's first
+        # batch is submitted, beside its k_bin -- the tail of the batch joins the formatting
         if wl.finish:
             for k in range(wl.per_step):
                 fr, de = wl.batches[k]
                 # back to back; finish right behind (the batches were synchronised after generation)
                 eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+                if k == 0 and gather is not None:
+                    gather.step()
             eng.finish()
         else:
             fr, de = wl.batches[cursor[0]]
             cursor[0] += 1
             eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+            if gather is not None:
+                gather.step()
             eng.expire(wl.last_sec[cursor[0] - 1])  # the virtual clock: idle flows out (none idle here)
-        if gather is not None:
-            gather.step()  # IPFIX streams to rank 0 over RCCL, overlapped with the next step
-        else:
+        if gather is None:
             eng.clear_exports()
 
     for _ in range(args.warmup):
@@ -669,6 +710,7 @@ def main():
     if gather is not None:
         torch.cuda.synchronize()
         gather.device_ms()
+        gather.host_s = 0.0
         rx0 = (gather.g.received_bytes, gather.g.header_bytes, gather.g.sent_bytes, gather.g.k)
     if world > 1:
         torch.distributed.barrier()
@@ -683,6 +725,7 @@ def main():
     tm_in = eng.timing()
     st = eng.stats()
     gms = gather.device_ms() / args.steps if gather is not None else None
+    ghost = gather.host_s * 1e3 / args.steps if gather is not None else None
     if gather is not None:  # per-step exchange volume over the timed steps (rank 0 received / this rank sent)
         gx = gather.g
         g_rx = (gx.received_bytes - rx0[0]) / args.steps
@@ -797,6 +840,7 @@ def main():
                                "the stream bytes, sized by 16-byte headers gathered the step before; on a side "
                                "stream, overlapped with the next step",
                        "device_ms_per_step": round(gms, 4),
+                       "host_ms_per_step": round(ghost, 4),
                        "rank0_receives_bytes_per_step": round(g_rx),
                        "header_bytes_per_step": round(g_hdr),
                        "rank0_stream_bytes_per_step": round(g_tx)} if gather is not None else None,

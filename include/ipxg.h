@@ -488,16 +488,25 @@ int ipxg_ipfix_export(ipxg_engine* eng, ipxg_ipfix_exporter* x, const ipxg_flow_
 /* The pending exports (consumed, like ipxg_poll_exports) as messages into host memory. */
 int ipxg_poll_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, uint8_t* out, size_t cap, size_t* n_records,
                              size_t* bytes, size_t* msgs);
-/* The same into a device buffer owned by the engine (valid until the next engine call): for
- * gathering the per-GPU message streams with RCCL. */
+/* The same into a device buffer owned by the engine, for gathering the per-GPU message streams
+ * with RCCL.  Two buffers alternate: a stream stays valid until the second
+ * ipxg_device_ipfix_messages call after the one that produced it (a consumer may send stream k
+ * while the engine formats stream k+1).  Formatted on ipxg_ipfix_stream(eng), a side stream forked
+ * from the engine's stream (so it runs beside the next batch's first kernels); the engine's stream
+ * joins it before anything that appends exports.  A consumer waits for ipxg_ipfix_stream.  Called
+ * with an asynchronous batch in flight (ipxg_submit with IPXG_BATCH_ASYNC, nothing since), it
+ * formats the exports of the batches completed before it and leaves that batch running. */
 int ipxg_device_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, const uint8_t** dptr, size_t* n_records,
                                size_t* bytes, size_t* msgs);
 /* The {stream bytes, records} of the last ipxg_device_ipfix_messages call as two uint64 in device
- * memory, written in order on the engine's stream (ipxg_stream) with the messages: a consumer on
+ * memory, written in order on ipxg_ipfix_stream with the messages: a consumer on
  * another stream that waits for the engine's reads them without a host round trip (the header of
  * the multi-GPU stream gather).  Valid until the next IPFIX message call (ipxg_ipfix_export,
  * ipxg_poll_ipfix_messages, ipxg_device_ipfix_messages).  IPXG_ESTATE before the first. */
 int ipxg_device_ipfix_counts(ipxg_engine* eng, const uint64_t** dptr);
+/* The stream ipxg_device_ipfix_messages formats on (hipStream_t; the engine's own stream before
+ * the first call). */
+void* ipxg_ipfix_stream(ipxg_engine* eng);
 
 /* ---- stateless device entry points (parity tests, tools) ---------------------------- */
 /* Run the device parser on a batch; out receives n records (host pointer). */

@@ -20,25 +20,6 @@
 
 namespace ipxg {
 
-// Does the parsed packet match rule r?  pay(k): byte k of its payload (k < 16, within payload_len).
-template <class B>
-__device__ __forceinline__ bool rule_match(const DevRule& r, const DevPkt& pk, const B& pay) {
-    const bool tcp = pk.l4 == 6, udp = pk.l4 == 17;
-    if (!((tcp && (r.proto_mask & 1)) || (udp && (r.proto_mask & 2)))) return false;
-    for (uint32_t k = 0; k < r.n_ports; ++k)
-        if (pk.src_port == r.ports[k] || pk.dst_port == r.ports[k]) return true;
-    for (uint32_t q = 0; q < r.n_prefixes; ++q) {
-        const uint32_t n = r.prefix_len[q];
-        if (n == 0 || n > pk.payload_len) continue;
-        const bool msk = (r.masked >> q) & 1u;
-        bool eq = true;
-        for (uint32_t k = 0; k < n && eq; ++k)
-            eq = ((pay(k) ^ r.prefix[q][k]) & (msk ? r.prefix_mask[q][k] : 0xFFu)) == 0;
-        if (eq) return true;
-    }
-    return false;
-}
-
 typedef uint32_t bridge_u32x4 __attribute__((ext_vector_type(4)));
 
 // The 16 payload bytes at byte p of a frame at a 16-byte aligned offset o (two aligned 16-byte
@@ -61,70 +42,115 @@ __device__ __forceinline__ uint4 payload16(__amdgpu_buffer_rsrc_t arena, uint32_
     return r;
 }
 
-// Pre-classification of every packet against the plugins' rules.  Frames of the shapes k_bin's
-// wide walk takes are parsed from an 80-byte register window (and their payload's first 16 bytes
-// loaded for the prefix rules); the others by the general parser in LDS -- which parsed every
-// frame before: 0.9 ms per 10M-packet batch of the configs[2] mix, more than k_bin.
+// One packet against the plugins' rules, k_classify's test: frames of the shapes k_bin's wide walk
+// takes are parsed from an 80-byte register window (and their payload's first 16 bytes loaded for
+// the prefix rules); the others by the general parser in the lane's LDS column.  true: a rule
+// matched, lo its flow's key.
+__device__ __forceinline__ bool classify_packet(const BatchView& b, const Params& p, const DevRule* rules,
+                                                uint32_t nrules, __amdgpu_buffer_rsrc_t rs_arena, uint32_t* col,
+                                                uint32_t i, uint64_t& lo) {
+    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    const ipxg_pkt_desc d = b.desc[i];
+    DevPkt pk;
+    ParseCounts dummy = {};
+    bool reg = false, hit = false;
+    if (eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim) {
+        uint32_t w[WIDE_DW];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const bridge_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_arena, d.offset + 16u * k, 0, 0);
+            w[4 * k] = x.x;
+            w[4 * k + 1] = x.y;
+            w[4 * k + 2] = x.z;
+            w[4 * k + 3] = x.w;
+        }
+        bool ext = false;
+        reg = parse_medium<true>(w, d.caplen, p.frag_enable, pk, dummy, ext);
+        if (reg && (pk.l4 == 6 || pk.l4 == 17)) {
+            const uint4 pw = payload16(rs_arena, d.offset, pk.payload_off);
+            const uint32_t pd[4] = {pw.x, pw.y, pw.z, pw.w};
+            auto pay = [&](uint32_t k) {  // (bytes at or past caplen read as 0, as in the LDS walk)
+                const uint32_t dw = k >> 2;
+                const uint32_t v = dw == 0 ? pd[0] : dw == 1 ? pd[1] : dw == 2 ? pd[2] : pd[3];
+                return (uint32_t)pk.payload_off + k < d.caplen ? (v >> (8 * (k & 3))) & 0xFFu : 0u;
+            };
+            for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, pay);
+        }
+    }
+    if (!reg) {
+        stage_frame(col, b.arena, d.offset, d.caplen);
+        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        if (!parse_frame<true>(S, d.caplen, p.dlt, pk, dummy)) return false;
+        if (pk.ip_version != 4 && pk.ip_version != 6) return false;
+        if (pk.frag_off) return false;  // no L4 header (its ports come from the fragmentation cache)
+        auto pay = [&](uint32_t k) { return S.b(pk.payload_off + k); };
+        for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, pay);
+    }
+    if (!hit) return false;
+    uint64_t hf;
+    uint32_t cdir;
+    canon<false>(pk, p, lo, cdir, hf);
+    return true;
+}
+
+// A plugin flow's slot claimed (if new) and marked SLOT_PLUGIN before k_reduce folds the batch
+__device__ __forceinline__ void mark_plugin_flow(const TableView& t, BatchCtl* ctl, uint64_t lo, uint32_t& claimed_n) {
+    uint4 head;
+    bool claimed;
+    HotSlot* h = probe_insert(t, lo, head, claimed);
+    if (!h) {
+        atomicOr(&ctl->plugin_fail, 1u);  // table too full to mark the flow (host: error)
+        return;
+    }
+    if (claimed) claimed_n++;
+    atomicOr(&h->state, SLOT_PLUGIN);
+}
+
+// Pre-classification of every packet against the plugins' rules (when k_bin does not check them
+// itself: Params::plug off) -- which parsed every frame before: 0.9 ms per 10M-packet batch of the
+// configs[2] mix, more than k_bin.
 __global__ __launch_bounds__(IPXG_BLOCK) void k_classify(BatchView b, Params p, TableView t, const DevRule* rules,
                                                          uint32_t nrules, BatchCtl* ctl) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     uint32_t* col = &win[threadIdx.x];
     const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
-    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
     uint32_t claimed_n = 0;
     for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
-        const ipxg_pkt_desc d = b.desc[i];
-        DevPkt pk;
-        ParseCounts dummy = {};
-        bool reg = false, hit = false;
-        if (eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim) {
-            uint32_t w[WIDE_DW];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const bridge_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_arena, d.offset + 16u * k, 0, 0);
-                w[4 * k] = x.x;
-                w[4 * k + 1] = x.y;
-                w[4 * k + 2] = x.z;
-                w[4 * k + 3] = x.w;
-            }
-            bool ext = false;
-            reg = parse_medium<true>(w, d.caplen, p.frag_enable, pk, dummy, ext);
-            if (reg && (pk.l4 == 6 || pk.l4 == 17)) {
-                const uint4 pw = payload16(rs_arena, d.offset, pk.payload_off);
-                const uint32_t pd[4] = {pw.x, pw.y, pw.z, pw.w};
-                auto pay = [&](uint32_t k) {  // (bytes at or past caplen read as 0, as in the LDS walk)
-                    const uint32_t dw = k >> 2;
-                    const uint32_t v = dw == 0 ? pd[0] : dw == 1 ? pd[1] : dw == 2 ? pd[2] : pd[3];
-                    return (uint32_t)pk.payload_off + k < d.caplen ? (v >> (8 * (k & 3))) & 0xFFu : 0u;
-                };
-                for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, pay);
-            }
-        }
-        if (!reg) {
-            stage_frame(col, b.arena, d.offset, d.caplen);
-            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-            if (!parse_frame<true>(S, d.caplen, p.dlt, pk, dummy)) continue;
-            if (pk.ip_version != 4 && pk.ip_version != 6) continue;
-            if (pk.frag_off) continue;  // no L4 header (its ports come from the fragmentation cache)
-            auto pay = [&](uint32_t k) { return S.b(pk.payload_off + k); };
-            for (uint32_t r = 0; r < nrules && !hit; ++r) hit = rule_match(rules[r], pk, pay);
-        }
-        if (!hit) continue;
-        uint64_t lo, hf;
-        uint32_t cdir;
-        canon(pk, p, lo, cdir, hf);
-        uint4 head;
-        bool claimed;
-        HotSlot* h = probe_insert(t, lo, head, claimed);
-        if (!h) {
-            atomicOr(&ctl->plugin_fail, 1u);  // table too full to mark the flow (host: error)
-            continue;
-        }
-        if (claimed) claimed_n++;
-        atomicOr(&h->state, SLOT_PLUGIN);
+        uint64_t lo;
+        if (classify_packet(b, p, rules, nrules, rs_arena, col, i, lo)) mark_plugin_flow(t, ctl, lo, claimed_n);
     }
     if (claimed_n) atomicAdd(&ctl->new_keys, claimed_n);
+}
+
+// Params::plug: the marks k_bin (register walk: hits with their key, packets whose prefix test
+// lies past the window) and k_bin_slow (its TCP/UDP packets) listed, workgroup b's at
+// marks[b * slow_stride ...]: hits marked, the rest classified from their frames.
+__global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_marks(BatchView b, Params p, TableView t, const DevRule* rules,
+                                                             uint32_t nrules, BatchCtl* ctl, BinView bv) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    uint32_t* col = &win[threadIdx.x];
+    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    uint32_t claimed_n = 0;
+    for (uint32_t g = blockIdx.x; g < bv.bin_grid; g += gridDim.x) {  // (block-uniform)
+        const uint32_t n = min(bv.mark_cnt[g], bv.slow_stride);
+        const uint4* m = bv.marks + (size_t)g * bv.slow_stride;
+        for (uint32_t k = threadIdx.x; k < n; k += IPXG_BLOCK) {
+            const uint4 e = m[k];
+            const uint32_t kind = e.z >> 30, i = e.z & 0x3FFFFFFFu;
+            uint64_t lo = ((uint64_t)e.y << 32) | e.x;
+            if (kind == MARK_HIT || (i < b.n && classify_packet(b, p, rules, nrules, rs_arena, col, i, lo)))
+                mark_plugin_flow(t, ctl, lo, claimed_n);
+        }
+    }
+    if (claimed_n) atomicAdd(&ctl->new_keys, claimed_n);
+}
+
+void launch_plugin_marks(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
+                         uint32_t nrules, BatchCtl* ctl, const BinView& bv) {
+    hipLaunchKernelGGL(k_plugin_marks, dim3(bv.bin_grid ? bv.bin_grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, rules,
+                       nrules, ctl, bv);
 }
 
 void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,

@@ -226,13 +226,13 @@ __device__ __forceinline__ void tile_rank_all(uint32_t* hist, uint32_t pmask, co
 // would fit become NO_REC fillers, so k_reduce never reads half an aggregate).
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
-template <bool LISTED, bool AGG>
+template <bool LISTED, bool AGG, uint32_t PMAX = (1u << BIN_MAX_PART_BITS)>
 __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t pmask, const BinView& bv, uint32_t col,
                                           const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
                                           uint4* agg_list, const uint32_t (&r0)[BIN_K], const uint32_t (&r1)[BIN_K],
                                           const uint32_t (&r2)[BIN_K], const uint32_t (&rk)[BIN_K],
                                           const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& spilled) {
-    constexpr uint32_t PT = (1u << BIN_MAX_PART_BITS) / IPXG_BLOCK;  // partitions per thread
+    constexpr uint32_t PT = PMAX > IPXG_BLOCK ? PMAX / IPXG_BLOCK : 1;  // partitions per thread
     uint32_t* const hist = L.hist;
     uint32_t* const fill = L.fill;
     uint4* const stage = L.stage;
@@ -356,7 +356,7 @@ __device__ __forceinline__ void tile_rank(const Params& p, const BatchView& b, c
     cdir = 0;
     hf = lo;
 #else
-    canon(pk, p, lo, cdir, hf);
+    canon<false>(pk, p, lo, cdir, hf);
 #endif
     const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
     tb_or |= misc_tb(m);
@@ -482,6 +482,47 @@ __device__ __forceinline__ uint32_t slow_class(const uint4 c0, const uint4 c1, c
     return cls;
 }
 
+// The plugins' rules (Params::plug, flattened) on a packet the wide walk parsed from registers:
+// MARK_HIT when a port or payload-prefix rule matches (k_classify's rule_match), MARK_LATER when a
+// prefix rule could only be decided past the register window (k_plugin_marks tests the frame),
+// else 0.  The payload's first 4 bytes come from the window; bytes at or past caplen read as 0.
+template <int WD>
+__device__ __forceinline__ uint32_t plug_check(const Params& p, const uint32_t (&w)[WD], uint32_t caplen,
+                                               const DevPkt& pk) {
+    const uint32_t pm = pk.l4 == 6 ? 1u : 2u;  // (pk.l4 is TCP or UDP here)
+    for (uint32_t k = 0; k < p.plug_nport; ++k) {
+        const uint32_t e = p.plug_port[k];
+        if (((e >> 16) & pm) && (pk.src_port == (e & 0xFFFF) || pk.dst_port == (e & 0xFFFF))) return MARK_HIT;
+    }
+    if (!p.plug_npref) return 0;
+    const uint32_t off = pk.payload_off;
+    const bool inwin = off + PLUG_PREFIX <= 4u * WD;
+    uint32_t pay = 0;
+    if (inwin) {
+        const uint32_t q = off >> 2;
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int k = 0; k < WD; ++k) {  // (selects: no dynamic register index)
+            a = (uint32_t)k == q ? w[k] : a;
+            b = (uint32_t)k == q + 1 ? w[k] : b;
+        }
+        pay = __builtin_amdgcn_alignbyte(b, a, off & 3);
+        const int valid = (int)caplen - (int)off;
+        pay &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+    }
+    uint32_t res = 0;
+    for (uint32_t k = 0; k < p.plug_npref; ++k) {
+        const uint32_t info = p.plug_pinfo[k], n = info & 0xFF;
+        if (!((info >> 8) & pm) || n == 0 || n > pk.payload_len) continue;
+        if (!inwin) {
+            res = MARK_LATER;
+            continue;
+        }
+        if (((pay ^ p.plug_pref[k]) & p.plug_pmask[k]) == 0) return MARK_HIT;
+    }
+    return res;
+}
+
 // Every packet of the batch, in tiles of BIN_K x 256, parsed in registers by parse_fast
 // from buffer loads software-pipelined across the tiles (below).  Frames the register parser
 // does not take go to the slow list for k_bin_slow.  No LDS header staging here: LDS holds
@@ -494,15 +535,22 @@ __device__ __forceinline__ uint32_t slow_class(const uint4 c0, const uint4 c1, c
 // frames from registers as well; the remaining shapes (MPLS, PPPoE, GRE, IPv6 extension
 // headers, other TCP options, ...) still go to the slow list.
 // The host picks the variants per batch (ipxg_engine.cpp: tile_agg, wide).
+#ifndef IPXG_KBIN_PART_BITS  // timing experiment: k_bin's partition arrays smaller than BIN_MAX_PART_BITS
+#define IPXG_KBIN_PART_BITS IPXG_BIN_MAX_PART_BITS
+#endif
+constexpr uint32_t KBIN_PMAX = 1u << IPXG_KBIN_PART_BITS;
 #ifndef IPXG_BIN_NARROW_WPE
 #define IPXG_BIN_NARROW_WPE 3  // waves per SIMD of the narrow, non-aggregating k_bin (its register budget)
 #endif
-template <bool AGG, bool WIDE>
+// PLUG (with WIDE only): the process plugins' pre-classification in the same walk (Params::plug;
+// the hits' keys and the undecided packets listed for k_plugin_marks) -- no k_classify pass.
+template <bool AGG, bool WIDE, bool PLUG = false>
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : IPXG_BIN_NARROW_WPE)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
-    __shared__ uint32_t hist[1u << BIN_MAX_PART_BITS];  // 8 KiB: per-partition rank / run start
-    __shared__ uint32_t fill[1u << BIN_MAX_PART_BITS];  // 8 KiB: slots in the block's segments
+    static_assert(!PLUG || WIDE, "the plugin check reads the wide walk's window");
+    __shared__ uint32_t hist[KBIN_PMAX];  // 8 KiB: per-partition rank / run start
+    __shared__ uint32_t fill[KBIN_PMAX];  // 8 KiB: slots in the block's segments
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: tile hash keys, then the slots by partition
     __shared__ uint32_t tcnt[AGG ? TAGG_HASH : 1];      // 16 KiB: tile hash counts / aggregate ids
     __shared__ TileAgg tagg[AGG ? TAGG_CAP : 1];        // 8 KiB
@@ -512,12 +560,15 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     const BinLds L = {hist, fill, stage, tcnt, tagg, part_of, scan_s, &nagg};
     uint32_t folded = 0;
     __shared__ uint32_t nslow[2];  // slow packets of the tile (by tile parity)
+    __shared__ uint32_t nmark;     // PLUG: marks listed so far
     // timestamps (sec << 32 | usec) of each step's first and last packet per wave: the order
     // check across wave boundaries, done once per tile (within a wave it is a DPP shift)
     __shared__ uint64_t bnd_first[BIN_K][IPXG_BLOCK / 64], bnd_last[BIN_K][IPXG_BLOCK / 64];
     const uint32_t tid = threadIdx.x;
     for (uint32_t q = tid; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     if (tid < 2) nslow[tid] = 0;
+    if (tid == 0) nmark = 0;
+    uint4* const my_marks = PLUG ? bv.marks + (size_t)blockIdx.x * bv.slow_stride : nullptr;
     // the block's slow list: every packet of its tiles fits, so a slow packet is stored at
     // its rank without any device atomic (a returning one inside the pipelined loop made the
     // compiler drain every load in flight)
@@ -599,7 +650,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         const u32x2 tpred = __builtin_amdgcn_raw_buffer_load_b64(rs_desc, tile ? tile * 16u - 8u : BUF_OOB, 0, 0);
         PROBE_T(t0);
 #pragma unroll
-        for (uint32_t k = 0; k < (1u << BIN_MAX_PART_BITS) / IPXG_BLOCK; ++k)
+        for (uint32_t k = 0; k < (KBIN_PMAX + IPXG_BLOCK - 1) / IPXG_BLOCK; ++k)
             if (k * IPXG_BLOCK + tid < P) hist[k * IPXG_BLOCK + tid] = 0;
         __syncthreads();
         if (tid == 0) nslow[par ^ 1] = 0;  // the next tile's (last read before this barrier)
@@ -663,9 +714,21 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         w[4 * k + 3] = hc.c[k].w;
                     }
                     bool ext = false;
-                    if (fast_ok && fast_shape(dc) && parse_medium<false, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
+                    if (fast_ok && fast_shape(dc) && parse_medium<PLUG, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
                         have = true;
                         walked += ext ? 1 : 0;
+                        if constexpr (PLUG) {
+                            if (pk.l4 == 6 || pk.l4 == 17) {
+                                const uint32_t kind = plug_check<WD>(p, w, dc.caplen, pk);
+                                if (kind) {
+                                    uint64_t lo = 0, hf;
+                                    uint32_t cd;
+                                    if (kind == MARK_HIT) canon<false>(pk, p, lo, cd, hf);
+                                    my_marks[atomicAdd(&nmark, 1u)] =
+                                        make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), i | (kind << 30), 0);
+                                }
+                            }
+                        }
                     } else {
                         slow = true;
                     }
@@ -687,8 +750,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         PROBE_ADD(1, t1, t2);
         if (AGG) tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
         else tile_rank_all(hist, pmask, r1, rk);
-        tile_emit<false, AGG>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix,
-                              tile, spilled);
+        tile_emit<false, AGG, KBIN_PMAX>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2,
+                                         rk, ix, tile, spilled);
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         slow_fill += nslow[par];  // final: read after the tile's barriers
@@ -719,6 +782,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     }
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, blockIdx.x);
+    if (PLUG && tid == 0) bv.mark_cnt[blockIdx.x] = nmark;
     // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
@@ -792,7 +856,7 @@ __device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b,
                                             uint32_t* col, const uint4 e, const SlowWin& w, int j, ParseCounts& c,
                                             uint32_t& keyless, uint32_t& frags, uint32_t (&r0)[BIN_K],
                                             uint32_t (&r1)[BIN_K], uint32_t (&r2)[BIN_K], uint32_t (&rk)[BIN_K],
-                                            uint32_t (&ix)[BIN_K], uint32_t& tb_or) {
+                                            uint32_t (&ix)[BIN_K], uint32_t& tb_or, uint4* marks, uint32_t* nmark) {
     const ipxg_pkt_desc d = slow_desc(e);
     const uint32_t i = e.x & SLOW_IDX_MASK;
     put_window(col, b.arena, e, w);
@@ -803,6 +867,10 @@ __device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b,
         keyless++;
         return;
     }
+    // Params::plug: a TCP/UDP packet with its L4 header -- a first fragment too, as k_classify
+    // tests them -- is classified from its frame by k_plugin_marks
+    if (p.plug && !pk.frag_off && (pk.l4 == 6 || pk.l4 == 17))
+        marks[atomicAdd(nmark, 1u)] = make_uint4(0, 0, i | (MARK_LATER << 30), 0);
     if (p.frag_enable && (pk.frag_off || pk.more_fragments)) {
         frags++;
         divert_fragment(pk, p, f, ctl, i);
@@ -843,6 +911,10 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
     if (ns == 0) return;  // no work: k_reduce does not read the column
+    // Params::plug: the slow packets' plugin checks listed after k_bin's marks of this workgroup
+    __shared__ uint32_t nmark;
+    uint4* const my_marks = p.plug ? bv.marks + (size_t)blockIdx.x * bv.slow_stride : nullptr;
+    if (threadIdx.x == 0) nmark = p.plug ? bv.mark_cnt[blockIdx.x] : 0;
     for (uint32_t q = threadIdx.x; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
     const uint32_t tid = threadIdx.x;
     if (b.base_sec == BASE_FROM_DESC0) b.base_sec = b.n ? b.desc[0].ts_sec : 0;
@@ -914,7 +986,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             PROBE_ADD(0, s0, s1);
             probe_acc[3] += 1;
 #endif
-            slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix, tb_or);
+            slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix, tb_or, my_marks, &nmark);
 #ifdef IPXG_PROBE
             PROBE_T(s2);
             PROBE_ADD(1, s1, s2);
@@ -944,6 +1016,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
 #endif
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, bcol);
+    if (p.plug && tid == 0) bv.mark_cnt[blockIdx.x] = nmark;
     if (tid < ST_COUNT) hist[tid] = 0;
     __syncthreads();
     flush_counts(c, keyless, frags, hist);
@@ -958,14 +1031,15 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
 
 typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint4*, uint32_t*, uint4*,
                           unsigned long long*);
-static BinKernel bin_kernel(bool agg, bool wide) {
+static BinKernel bin_kernel(bool agg, bool wide, bool plug = false) {
+    if (plug) return agg ? k_bin<true, true, true> : k_bin<false, true, true>;  // (plug: the wide walk)
     return agg ? (wide ? k_bin<true, true> : k_bin<true, false>) : (wide ? k_bin<false, true> : k_bin<false, false>);
 }
 
-uint32_t bin_resident_blocks(int device, bool agg, bool wide) {
+uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide), IPXG_BLOCK, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide, plug), IPXG_BLOCK, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return (uint32_t)std::max(1, std::min(cus * per_cu, (int)BIN_MAX_GRID));
@@ -974,7 +1048,7 @@ uint32_t bin_resident_blocks(int device, bool agg, bool wide) {
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats) {
-    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
+    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0, p.plug != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
                        t, f, bv, ctl, slow_list, deferred_list, agg_list, stats);
 }
 
@@ -1575,6 +1649,51 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
 // wide walk takes go through the same register parser (80-byte head by buffer loads); the rest
 // through the general parser -- the gather used to parse every frame with the general LDS
 // parser, twice k_bin's time per batch on the configs[2] mix with its plugins registered.
+// Packet i parsed as the gather needs it (the wide register walk, else the general parser in the
+// lane's LDS column), its canonical key in lo; false: no IP flow key.
+__device__ __forceinline__ bool gather_key(const BatchView& b, const Params& p, const FragView& f,
+                                           __amdgpu_buffer_rsrc_t rs_desc, __amdgpu_buffer_rsrc_t rs_arena,
+                                           uint32_t* col, uint32_t i, uint64_t& lo) {
+    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    const ipxg_pkt_desc d = load_desc(rs_desc, i);
+    DevPkt pk;
+    ParseCounts c = {};
+    bool ok = false;
+    const bool reg = eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim;
+    if (reg) {
+        const Head<5> h = load_head<5>(rs_arena, d, true);
+        uint32_t w[WIDE_DW];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            w[4 * k] = h.c[k].x;
+            w[4 * k + 1] = h.c[k].y;
+            w[4 * k + 2] = h.c[k].z;
+            w[4 * k + 3] = h.c[k].w;
+        }
+        bool ext = false;
+        ok = parse_medium(w, d.caplen, p.frag_enable, pk, c, ext);
+    }
+    if (!ok) {
+        DevPkt q;
+        stage_frame(col, b.arena, d.offset, d.caplen);
+        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        if (!parse_frame<false>(S, d.caplen, p.dlt, q, c)) return false;
+        pk = q;
+    }
+    if (pk.ip_version != 4 && pk.ip_version != 6) return false;
+    if (p.frag_enable && (pk.frag_off || pk.more_fragments)) apply_frag_ports(p, f, i, pk);
+    uint64_t hf;
+    uint32_t cdir;
+    canon<false>(pk, p, lo, cdir, hf);
+    return true;
+}
+
+__device__ __forceinline__ void gather_append(const ComplexView& cx, BatchCtl* ctl, uint32_t r, uint32_t i) {
+    const uint32_t pos = atomicAdd(&cx.cursor[r], 1u);
+    if (pos < cx.len[r]) cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
+    else atomicOr(&ctl->guard, 2u);  // more packets than the flow's slot counted (guard)
+}
+
 __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Params p, FragView f, ComplexView cx,
                                                                BatchCtl* ctl) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
@@ -1583,46 +1702,87 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Para
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
-    const bool eth = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
     for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
-        const ipxg_pkt_desc d = load_desc(rs_desc, i);
-        DevPkt pk;
-        ParseCounts c = {};
-        bool ok = false;
-        const bool reg = eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim;
-        if (reg) {
-            const Head<5> h = load_head<5>(rs_arena, d, true);
-            uint32_t w[WIDE_DW];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                w[4 * k] = h.c[k].x;
-                w[4 * k + 1] = h.c[k].y;
-                w[4 * k + 2] = h.c[k].z;
-                w[4 * k + 3] = h.c[k].w;
-            }
-            bool ext = false;
-            ok = parse_medium(w, d.caplen, p.frag_enable, pk, c, ext);
-        }
-        if (!ok) {
-            DevPkt q;
-            stage_frame(col, b.arena, d.offset, d.caplen);
-            LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-            if (!parse_frame<false>(S, d.caplen, p.dlt, q, c)) continue;
-            pk = q;
-        }
-        if (pk.ip_version != 4 && pk.ip_version != 6) continue;
-        if (p.frag_enable && (pk.frag_off || pk.more_fragments)) apply_frag_ports(p, f, i, pk);
-        uint64_t lo, hf;
-        uint32_t cdir;
-        canon(pk, p, lo, cdir, hf);
+        uint64_t lo;
+        if (!gather_key(b, p, f, rs_desc, rs_arena, col, i, lo)) continue;
         const int64_t rr = complex_rank_of(cx, lo);
-        if (rr >= 0) {
-            const uint32_t r = (uint32_t)rr;
-            const uint32_t pos = atomicAdd(&cx.cursor[r], 1u);
-            if (pos < cx.len[r]) cx.list[cx.seg[r] + pos] = ((uint64_t)r << 24) | i;
-            else atomicOr(&ctl->guard, 2u);  // more packets than the flow's slot counted (guard)
+        if (rr >= 0) gather_append(cx, ctl, (uint32_t)rr, i);
+    }
+}
+
+// Would k_bin's walk for this batch (p.wide, p.tile_agg: the variant it ran) have taken packet d
+// in registers?  pk: the parse when it would.  (A frame it left to k_bin_slow was never in one of
+// its tile aggregates.)
+__device__ __forceinline__ bool kbin_takes(const Params& p, __amdgpu_buffer_rsrc_t rs_arena, const ipxg_pkt_desc& d,
+                                           DevPkt& pk) {
+    const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
+    if (!(fast_ok && fast_shape(d))) return false;
+    ParseCounts c = {};
+    bool ext = false;
+    if (!p.wide) {
+        const Head<3> h = load_head<3>(rs_arena, d, true);
+        return parse_fast(h.c[0], h.c[1], h.c[2], d.caplen, p.frag_enable, pk, c);
+    }
+    if (p.tile_agg) {
+        const Head<WIDE_DW / 4> h = load_head<WIDE_DW / 4>(rs_arena, d, true);
+        uint32_t w[WIDE_DW];
+#pragma unroll
+        for (int k = 0; k < WIDE_DW / 4; ++k) {
+            w[4 * k] = h.c[k].x;
+            w[4 * k + 1] = h.c[k].y;
+            w[4 * k + 2] = h.c[k].z;
+            w[4 * k + 3] = h.c[k].w;
+        }
+        return parse_medium<false, WIDE_DW>(w, d.caplen, p.frag_enable, pk, c, ext);
+    }
+    const Head<WIDE2_DW / 4> h = load_head<WIDE2_DW / 4>(rs_arena, d, true);
+    uint32_t w[WIDE2_DW];
+#pragma unroll
+    for (int k = 0; k < WIDE2_DW / 4; ++k) {
+        w[4 * k] = h.c[k].x;
+        w[4 * k + 1] = h.c[k].y;
+        w[4 * k + 2] = h.c[k].z;
+        w[4 * k + 3] = h.c[k].w;
+    }
+    return parse_medium<false, WIDE2_DW>(w, d.caplen, p.frag_enable, pk, c, ext);
+}
+
+// The packets k_bin folded into tile aggregates of complex flows (k_complex_gather_rec lists each
+// such aggregate's flow key and index range, which lies inside one k_bin tile): only those ranges
+// are parsed again, a workgroup per range, and a packet is taken when k_bin's walk took it and it
+// is the aggregate's flow's -- inside its tile a flow's register-walk packets are either all in
+// its aggregate or all plain records (and its slow-path packets are k_bin_slow's records), so none
+// is gathered twice.
+__global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather_ranges(BatchView b, Params p, FragView f,
+                                                                      ComplexView cx, BatchCtl* ctl,
+                                                                      const uint4* ranges, uint32_t nr) {
+    (void)f;
+    const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    for (uint32_t q = blockIdx.x; q < nr; q += gridDim.x) {  // (block-uniform)
+        const uint4 rg = ranges[q];
+        const uint64_t key = ((uint64_t)rg.y << 32) | rg.x;
+        const int64_t rr = complex_rank_of(cx, key);
+        if (rr < 0) continue;
+        const uint32_t last = min(rg.w, b.n - 1);
+        for (uint32_t i = rg.z + threadIdx.x; i <= last; i += IPXG_BLOCK) {
+            DevPkt pk;
+            if (!kbin_takes(p, rs_arena, load_desc(rs_desc, i), pk)) continue;
+            if (pk.ip_version != 4 && pk.ip_version != 6) continue;
+            uint64_t lo, hf;
+            uint32_t cdir;
+            canon<false>(pk, p, lo, cdir, hf);
+            if (lo == key) gather_append(cx, ctl, (uint32_t)rr, i);
         }
     }
+}
+
+void launch_complex_gather_ranges(hipStream_t st, const BatchView& b, const Params& p, FragView f, ComplexView cx,
+                                  BatchCtl* ctl, const uint4* ranges, uint32_t nr) {
+    uint32_t g = nr < 4096 ? nr : 4096;
+    hipLaunchKernelGGL(k_complex_gather_ranges, dim3(g ? g : 1), dim3(IPXG_BLOCK), 0, st, b, p, f, cx, ctl, ranges, nr);
 }
 
 void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
@@ -1638,7 +1798,8 @@ void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, 
 // per segment (a k_bin / k_bin_slow workgroup's records of one partition: a few records each on
 // the 1M-flow mixes).  A complex flow with packets folded into a tile aggregate (no per-packet
 // index left) flags the batch for the re-parse gather.
-__global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexView cx, BatchCtl* ctl, uint32_t nseg) {
+__global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexView cx, BatchCtl* ctl, uint32_t nseg,
+                                                           uint4* ranges, uint32_t range_cap) {
     for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nseg; s += gridDim.x * 256) {
         const uint32_t c = s % bv.cols;
         if (c >= bv.bin_grid && !bv.slow_cnt[c - bv.bin_grid]) continue;  // (a k_bin_slow column left unwritten)
@@ -1648,8 +1809,17 @@ __global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexV
             const uint4 r = seg[j];
             if (r.z == NO_REC) continue;
             if (rec_is_agg(r)) {
-                if (rec_agg_slot(r) == 0 && complex_rank_of(cx, ((uint64_t)r.y << 32) | r.x) >= 0)
-                    atomicOr(&ctl->cx_agg, 1u);
+                if (rec_agg_slot(r) == 0 && complex_rank_of(cx, ((uint64_t)r.y << 32) | r.x) >= 0) {
+                    // a k_bin aggregate (its packets inside one tile): its range is parsed again
+                    // (k_complex_gather_ranges); k_bin_slow's span tiles: the whole batch then
+                    uint32_t q = c < bv.bin_grid && j + 2 < n ? atomicAdd(&ctl->cx_ranges, 1u) : range_cap;
+                    if (q < range_cap) {
+                        const FlowAgg a = agg_decode(r, seg[j + 1], seg[j + 2]);
+                        ranges[q] = make_uint4(r.x, r.y, first_idx(a.first_n), a.last1 - 1);
+                    } else {
+                        atomicOr(&ctl->cx_agg, 1u);
+                    }
+                }
                 continue;
             }
             const int64_t rr = complex_rank_of(cx, ((uint64_t)r.y << 32) | r.x);
@@ -1662,11 +1832,12 @@ __global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexV
     }
 }
 
-void launch_complex_gather_rec(hipStream_t st, const BinView& bv, ComplexView cx, BatchCtl* ctl) {
+void launch_complex_gather_rec(hipStream_t st, const BinView& bv, ComplexView cx, BatchCtl* ctl, uint4* ranges,
+                               uint32_t range_cap) {
     const uint32_t nseg = (1u << bv.part_bits) * bv.cols;
     uint32_t g = (nseg + 255) / 256;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_complex_gather_rec, dim3(g ? g : 1), dim3(256), 0, st, bv, cx, ctl, nseg);
+    hipLaunchKernelGGL(k_complex_gather_rec, dim3(g ? g : 1), dim3(256), 0, st, bv, cx, ctl, nseg, ranges, range_cap);
 }
 
 }  // namespace ipxg

@@ -66,7 +66,9 @@ struct BatchCtl {
     uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
     uint32_t tb_any;         // OR of the time buckets of k_bin / k_bin_slow's records (0: all in bucket 0)
     uint32_t fin_deferred;   // finalise-list aggregates whose table probe failed (k_fin_list: table full)
-    uint32_t cx_agg;         // k_complex_gather_rec: a complex flow's packets were folded into a tile aggregate
+    uint32_t cx_agg;         // k_complex_gather_rec: a complex flow's packets were folded into a k_bin_slow
+                             // tile aggregate (or more k_bin aggregates than the range list holds)
+    uint32_t cx_ranges;      // k_complex_gather_rec: k_bin tile aggregates of complex flows listed
     uint32_t guard;          // bounds guards that fired (engine bug, reported as IPXG_EDEVICE): 1 more complex
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
                              // past the table
@@ -145,7 +147,16 @@ struct Params {
     uint32_t spin_max;       // strict replay: polling rounds without progress before giving up
     uint32_t classify;       // k_classify ran for the batch (process plugins): slots were claimed and
                              // marked before k_reduce, so every listed flow must find its slot
+    // plug: the plugins' rules checked inside k_bin (the wide walk) instead of by k_classify --
+    // flattened here so the check reads kernel arguments only: ports (port | proto_mask << 16) and
+    // payload prefixes of at most PLUG_PREFIX bytes (bytes little-endian in pref, compare mask in
+    // pmask, len | proto_mask << 8 in pinfo)
+    uint32_t plug;
+    uint32_t plug_nport, plug_npref;
+    uint32_t plug_port[16];
+    uint32_t plug_pref[16], plug_pmask[16], plug_pinfo[16];
 };
+constexpr uint32_t PLUG_PREFIX = 4;
 
 // ---- strict mode (ipxg_strict.hip): the reference's line table -------------------------------
 struct StrictView {
@@ -205,6 +216,8 @@ struct BinView {
     uint32_t part_bits;  // parts = 1 << part_bits
     uint32_t slow_stride;  // k_bin workgroup b lists its slow packets (16-B entries) at slow_list[b * slow_stride ...]
     uint32_t* slow_cnt;    // bin_grid: slow packets listed by each k_bin workgroup
+    uint4* marks;          // Params::plug: workgroup b's plugin marks at marks[b * slow_stride ...] (k_bin's,
+    uint32_t* mark_cnt;    //   then k_bin_slow's), mark_cnt[b] of them: {key lo, key hi, index | kind << 30, 0}
 };
 #ifndef IPXG_BIN_K
 #define IPXG_BIN_K 8  // packets per lane per k_bin tile
@@ -268,7 +281,7 @@ static_assert(sizeof(PluginFlow) == 160, "plugin flow image");
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
 // tile-aggregating variant (more LDS)
-uint32_t bin_resident_blocks(int device, bool agg, bool wide);
+uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug);
 // deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
 // 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
@@ -285,6 +298,12 @@ constexpr uint32_t FIN_DEFERRED = 0xFFFFFFFEu;    // ... its probe failed (table
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
                      bool finishing, bool deferred_only = false);
+// Params::plug: the marks k_bin and k_bin_slow listed -- plugin flows found in registers (slot
+// claimed and marked SLOT_PLUGIN here) and packets to classify from their frames (k_classify's
+// test) -- before k_reduce
+constexpr uint32_t MARK_HIT = 1u, MARK_LATER = 2u;
+void launch_plugin_marks(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
+                         uint32_t nrules, BatchCtl* ctl, const BinView& bv);
 void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableView t, const DevRule* rules,
                      uint32_t nrules, BatchCtl* ctl);
 // The host walk's inputs on the device, flows in order of their first packet (ipxg_bridge.hip):
@@ -341,7 +360,10 @@ void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, 
                            ComplexView cx, BatchCtl* ctl);
 // the same from the batch's partition records (k_bin / k_bin_slow), when every packet of the batch
 // left one (no spills, deferrals or fragments); ctl->cx_agg set: redo with the re-parse above
-void launch_complex_gather_rec(hipStream_t st, const BinView& bv, ComplexView cx, BatchCtl* ctl);
+void launch_complex_gather_rec(hipStream_t st, const BinView& bv, ComplexView cx, BatchCtl* ctl, uint4* ranges,
+                               uint32_t range_cap);
+void launch_complex_gather_ranges(hipStream_t st, const BatchView& b, const Params& p, FragView f, ComplexView cx,
+                                  BatchCtl* ctl, const uint4* ranges, uint32_t nr);
 void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                          ComplexView cx, uint32_t nranks, ExportView ex, BatchCtl* ctl,
                          unsigned long long* stats);

@@ -101,7 +101,7 @@ EXPORTED_SYMBOLS = [
     "ipxg_capture_load", "ipxg_capture_free", "ipxg_profile", "ipxg_get_timing",
     "ipxg_probe_counters", "ipxg_ipfix_basic", "ipxg_poll_ipfix", "ipxg_ipfix_exporter_init",
     "ipxg_ipfix_bound", "ipxg_ipfix_export", "ipxg_poll_ipfix_messages", "ipxg_device_ipfix_messages",
-    "ipxg_device_ipfix_counts",
+    "ipxg_device_ipfix_counts", "ipxg_ipfix_stream",
     "ipxg_parser_stats", "ipxg_top_ports", "ipxg_add_plugin", "ipxg_set_walk_threads",
     "ipxg_demux", "ipxg_demux_arena_bytes", "ipxg_demux_split",
 ]
@@ -207,12 +207,15 @@ def lib():
         L.ipxg_device_ipfix_messages.argtypes = [vp, px, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                  ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.ipxg_device_ipfix_counts.argtypes = [vp, ctypes.POINTER(vp)]
+        L.ipxg_ipfix_stream.argtypes = [vp]
+        L.ipxg_ipfix_stream.restype = vp
         L.ipxg_demux.argtypes = [ctypes.POINTER(Batch), u32, u32, vp, vp]
         L.ipxg_demux_arena_bytes.argtypes = [ctypes.POINTER(Batch), vp, u32]
         L.ipxg_demux_arena_bytes.restype = ctypes.c_uint64
         L.ipxg_demux_split.argtypes = [ctypes.POINTER(Batch), vp, u32, vp, vp, ctypes.POINTER(u32)]
         for name in EXPORTED_SYMBOLS:
-            if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_config_default", "ipxg_demux_arena_bytes",
+            if name not in ("ipxg_last_error", "ipxg_stream", "ipxg_ipfix_stream", "ipxg_config_default",
+                            "ipxg_demux_arena_bytes",
                             "ipxg_capture_free", "ipxg_ipfix_exporter_init", "ipxg_ipfix_bound"):
                 getattr(L, name).restype = ctypes.c_int
         _LIB = L
@@ -512,6 +515,10 @@ class Engine:
         self._check(lib().ipxg_device_ipfix_messages(self._h, ctypes.byref(x), ctypes.byref(p), ctypes.byref(nr),
                                                      ctypes.byref(nb), ctypes.byref(nm)), "ipxg_device_ipfix_messages")
         return p.value, nb.value, nr.value, nm.value
+
+    def ipfix_stream(self):
+        """The stream device_ipfix_messages formats on (hipStream_t as an int)."""
+        return lib().ipxg_ipfix_stream(self._h)
 
     def device_ipfix_counts(self):
         """Device pointer to the {bytes, records} (2 x uint64) of the last device_ipfix_messages

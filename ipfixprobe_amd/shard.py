@@ -98,26 +98,32 @@ class StreamGather:
         self.sent_bytes = self.sent_records = 0  # this rank's streams
         self.received_bytes = self.received_records = self.header_bytes = 0  # rank 0
 
-    def push(self, src, nbytes, records, copied=None, counts=None):
+    def push(self, src, nbytes, records, copied=None, counts=None, copy=True):
         """Step k's stream: `src` (uint8 tensor) holding `nbytes` bytes of `records` records.
         `counts` (optional): a 2-element int64 tensor on the device holding the same {nbytes,
         records}, written by the producer in stream order (Engine.device_ipfix_counts) -- the
-        header is then a device copy, no host value in it."""
+        header is then a device copy, no host value in it.  copy=False: `src` is sent as it is,
+        one push later -- the producer keeps it valid until then (the engine's two alternating
+        message buffers) and may overwrite it once `copied` has fired, which is recorded after
+        that send."""
         import torch
         import torch.distributed as dist
         self._move_prev()
         i = self.k % 2
-        if self.bufs[i].numel() < nbytes:
-            self.bufs[i] = torch.zeros(max(nbytes, 2 * self.bufs[i].numel()), dtype=torch.uint8, device=self.device)
-        if nbytes:
-            self.bufs[i][:nbytes].copy_(src[:nbytes])
+        if not copy:
+            self.bufs[i] = src
+        else:
+            if self.bufs[i].numel() < nbytes:
+                self.bufs[i] = torch.zeros(max(nbytes, 2 * self.bufs[i].numel()), dtype=torch.uint8, device=self.device)
+            if nbytes:
+                self.bufs[i][:nbytes].copy_(src[:nbytes])
         if counts is not None:
             self.hdr[i].copy_(counts)  # the producer's own device counts
         else:
             self.hdr[i][0].fill_(int(nbytes))
             self.hdr[i][1].fill_(int(records))
         if copied is not None:
-            copied.record()  # (the producer may overwrite its buffer and counts from here)
+            copied.record()  # (copy: the producer's buffer is free from here; else: the previous one is)
         if self.world > 1:
             dist.gather(self.hdr[i], self.hdrs[i] if self.rank == 0 else None, dst=0)
         if self.rank == 0:

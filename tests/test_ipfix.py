@@ -270,3 +270,56 @@ def test_poll_ipfix_messages_after_partial_poll():
     assert got.value == 7 and nrec == n - 7
     msgs, _, recs, _, _ = ipfixdec.decode(b)
     assert len(recs) == n - 7
+
+
+class _DevBytes:
+    """__cuda_array_interface__ over n bytes of device memory (the engine's message buffer)."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+@pytest.mark.gpu
+def test_device_messages_beside_a_batch_in_flight():
+    """ipxg_device_ipfix_messages called with an asynchronous batch in flight (its k_fin_list not
+    launched yet) formats the exports of the batches completed before it on the engine's
+    formatting stream, beside that batch's kernels, without completing it; the batch's tail
+    joins the formatting before it appends exports.  Over two steps the device streams carry the
+    host message path's records, sizes and message sequence (exporter state carried; the export
+    order within a step is not fixed -- workgroups reserve their export slots by atomics), with
+    the first stream consumed while the second step's batch runs, and the two alternating buffers
+    keep the first stream intact while the second is formatted."""
+    import torch
+    from ipfixprobe_amd import Engine
+    a1, d1 = synth.flow_stream(seed=31, n_flows=600, n_pkts=12000).batch()
+    a2, d2 = synth.flow_stream(seed=32, n_flows=700, n_pkts=12000, v6_share=0.3).batch()
+    with Engine() as e:
+        x = e.ipfix_exporter(odid=4, export_time=99)
+        e.submit(a1, d1)
+        e.finish()
+        want1, _, _ = e.poll_ipfix_messages(x)
+        e.submit(a2, d2, asynchronous=True)
+        e.finish()
+        want2, _, _ = e.poll_ipfix_messages(x)
+    with Engine() as e:
+        x = e.ipfix_exporter(odid=4, export_time=99)
+        e.submit(a1, d1)
+        e.finish()
+        e.submit(a2, d2, asynchronous=True)  # in flight: its tail is launched by the next call
+        p1, nb1, nr1, _ = e.device_ipfix_messages(x)
+        e.finish()  # the tail joins the formatting of stream 1
+        p2, nb2, nr2, _ = e.device_ipfix_messages(x)
+        assert p1 != p2  # (alternating buffers: stream 1 is still valid here)
+        torch.cuda.ExternalStream(e.ipfix_stream()).synchronize()
+        got1 = torch.as_tensor(_DevBytes(p1, nb1), device="cuda").cpu().numpy().tobytes()
+        got2 = torch.as_tensor(_DevBytes(p2, nb2), device="cuda").cpu().numpy().tobytes()
+        assert e.pending() == 0
+    assert len(got1) == len(want1) and len(got2) == len(want2)
+    gm1, t1, gr1, _, _ = ipfixdec.decode(got1)
+    wm1, _, wr1, _, _ = ipfixdec.decode(want1)
+    gm2, _, gr2, _, _ = ipfixdec.decode(got2, t1)
+    wm2, _, wr2, _, _ = ipfixdec.decode(want2, t1)
+    assert nr1 == len(gr1) == len(wr1) > 500 and nr2 == len(gr2) == len(wr2) > 600
+    assert ipfixdec.basic_view(gr1) == ipfixdec.basic_view(wr1)
+    assert ipfixdec.basic_view(gr2) == ipfixdec.basic_view(wr2)
+    assert [m["sequence"] for m in gm1 + gm2] == [m["sequence"] for m in wm1 + wm2]

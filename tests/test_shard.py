@@ -255,6 +255,8 @@ def test_bench_gather_flag_single_gpu():
     g = line["gather"]
     assert line["n_gpus"] == 1 and g is not None
     assert g["device_ms_per_step"] > 0
-    assert g["rank0_receives_bytes_per_step"] == g["rank0_stream_bytes_per_step"] > 0
+    # (receives lag the pushes by one step: equal up to one step's difference in stream size)
+    assert g["rank0_stream_bytes_per_step"] > 0
+    assert abs(g["rank0_receives_bytes_per_step"] - g["rank0_stream_bytes_per_step"]) <= 0.01 * g["rank0_stream_bytes_per_step"]
     # 100k flows exported per udp64 step, 81 bytes each (IPv4 basic record) plus message headers
     assert 81 * line["flows_exported_per_step"] < g["rank0_stream_bytes_per_step"] < 90 * line["flows_exported_per_step"]
