@@ -12,6 +12,7 @@ stop() { echo "STOP: $1 exited $2"; exit "$2"; }
 for W in ${WORKLOADS:-udp64 imix quic}; do
   case $W in
     udp64) ARGS="--steps 30 --warmup 3" ;;
+    gather) ARGS="--gather --steps 30 --warmup 3" ;;
     stream) ARGS="--mode stream --steps 20 --warmup 3" ;;
     imix) ARGS="--workload imix --steps 3 --warmup 1" ;;
     quic) ARGS="--workload quic --steps 5 --warmup 1" ;;
