@@ -535,10 +535,7 @@ __device__ __forceinline__ uint32_t plug_check(const Params& p, const uint32_t (
 // frames from registers as well; the remaining shapes (MPLS, PPPoE, GRE, IPv6 extension
 // headers, other TCP options, ...) still go to the slow list.
 // The host picks the variants per batch (ipxg_engine.cpp: tile_agg, wide).
-#ifndef IPXG_KBIN_PART_BITS  // timing experiment: k_bin's partition arrays smaller than BIN_MAX_PART_BITS
-#define IPXG_KBIN_PART_BITS IPXG_BIN_MAX_PART_BITS
-#endif
-constexpr uint32_t KBIN_PMAX = 1u << IPXG_KBIN_PART_BITS;
+constexpr uint32_t KBIN_PMAX = 1u << BIN_MAX_PART_BITS;  // (the host may pick up to BIN_MAX_PART_BITS)
 #ifndef IPXG_BIN_NARROW_WPE
 #define IPXG_BIN_NARROW_WPE 3  // waves per SIMD of the narrow, non-aggregating k_bin (its register budget)
 #endif
@@ -748,10 +745,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
+#ifndef IPXG_EXP_NOSKEL  // timing experiment (with IPXG_EXP_LOADONLY only): no rank / emit phase at all
         if (AGG) tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
         else tile_rank_all(hist, pmask, r1, rk);
         tile_emit<false, AGG, KBIN_PMAX>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2,
                                          rk, ix, tile, spilled);
+#endif
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         slow_fill += nslow[par];  // final: read after the tile's barriers

@@ -532,7 +532,7 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
 // table (every occupied slot it scans is zeroed).
 // guard != nullptr: a finish enqueued right behind a batch before the host has read the
 // batch's control block.  It must not run when the batch left work for the host (fragments,
-// deferred packets, the table scan, complex flows) or when the export buffer might not hold
+// deferred packets or finalise-list entries, the table scan, complex flows) or when the export buffer might not hold
 // every live record; every workgroup decides alike from fields k_finish does not change,
 // workgroup 0 reports it (guard->hold) and the host then completes the batch and finishes
 // again.
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     __shared__ uint32_t pb[6];  // FlowRecordStats buckets of the block's exports
     if (guard) {
         const bool hold = guard->frag_count || guard->deferred || guard->agg_deferred || guard->pending ||
-                          guard->complex_count ||
+                          guard->complex_count || guard->fin_deferred ||
                           (uint64_t)ex_before + guard->exported + live_before + guard->new_live > ex.cap;
         if (blockIdx.x == 0 && threadIdx.x == 0) guard->hold = hold ? 1u : 0u;
         if (hold) return;
