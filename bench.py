@@ -758,7 +758,9 @@ def main():
                               "packet_share": round(tm_in["plugin_packets"] / args.steps / pk_step, 5),
                               "bytes_per_step": round(tm_in["plugin_bytes"] / args.steps),
                               "ms_per_step": round(hw_ms, 3),
-                              "share_of_step_time": round(hw_ms / (dt / args.steps * 1e3), 4)},
+                              "share_of_step_time": round(hw_ms / (dt / args.steps * 1e3), 4),
+                              # batches whose k_bin / k_bin_slow ran during the previous batch's walk
+                              "overlapped_batches_per_step": round(tm_in["plugin_overlapped"] / args.steps, 2)},
                 "hook_calls": {p.name: p.calls() for p in plugins},
                 "what": "flows with a plugin's packet in a batch (device pre-classifier) are replayed on the host "
                         "through the hooks; ms_per_step = wall time of that host walk inside the step (pack, "

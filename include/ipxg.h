@@ -426,6 +426,8 @@ typedef struct ipxg_timing {
     uint64_t plugin_bytes;     /* their captured bytes (full caplen, copied to the host)        */
     uint64_t plugin_extra_bytes; /* of which past each frame's first 128 (full caplen
                                     for packets handed to process plugins)                    */
+    uint64_t plugin_overlapped;  /* IPXG_BATCH_ASYNC device batches whose k_bin / k_bin_slow ran
+                                    during the previous batch's host walk                      */
 } ipxg_timing;
 
 /* Per-phase shader-clock sums of the last batch's k_bin, k_reduce and k_bin_slow (16 values;

@@ -201,6 +201,22 @@ struct ipxg_engine {
         Params p;
         uint32_t n = 0;
     } inflight;
+    // The next batch's front (control-block clear, k_bin, k_bin_slow) launched from inside the host
+    // walk of the batch in flight, right after the walk's input copies: the device bins batch k+1
+    // while the hooks run on batch k.  ipxg_submit of a device batch sets `want` around completing
+    // the batch in flight; the walk launches it (`launched`) when the plugins' check rides in k_bin
+    // (a k_classify pass would write the table the walk still owns).  k_bin then defers what does
+    // not fit its segments (Params::defer_spill) instead of accumulating into the table.
+    struct {
+        bool want = false, launched = false;
+        BatchView bv;
+        uint32_t n = 0;
+        Params p;
+        BinView bins;
+        BatchCtl snap;  // the walked batch's control block, as the walk found it
+    } early;
+    BatchCtl* aux_ctl_d = nullptr;  // k_plugin_apply's guard word while ctl_d holds the next batch's
+    hipStream_t wst = nullptr;      // the host walk's input copies while the next batch's k_bin runs
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     // asynchronous host batches: two staging slots, filled on a copy stream while the other
     // slot's batch is in the kernels (the double-buffered ingest ring)
@@ -685,6 +701,7 @@ int ipxg_destroy(ipxg_engine* e) {
     if (!e) return IPXG_OK;
     if (e->st) hipStreamSynchronize(e->st);
     if (e->fst) hipStreamSynchronize(e->fst);
+    if (e->wst) hipStreamSynchronize(e->wst);
     delete e->pool;
     free_walk_copies(e);
     hipFree(e->line);
@@ -692,6 +709,8 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->slot_rank);
     hipFree(e->ex);
     hipFree(e->ctl_d);
+    hipFree(e->aux_ctl_d);
+    if (e->wst) (void)hipStreamDestroy(e->wst);
     if (e->ctl_h) hipHostFree(e->ctl_h);
     hipFree(e->misc_d);
     hipFree(e->stats_d);
@@ -893,6 +912,118 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     return IPXG_OK;
 }
 
+// The batch's front: per-batch scratch, the control block cleared, partitions sized, then k_bin and
+// k_bin_slow (binned) -- from ipxg_submit, or from the previous batch's host walk (early: its spills
+// deferred, Params::defer_spill; the export counters left alone -- ensure_export and ex_ev follow in
+// the rest).
+static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool binned, bool async, bool early, Params& p,
+                        BinView& bins) {
+    int rc;
+    // per-batch scratch sized for the worst case (every packet deferred / a fragment)
+    if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
+    if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
+    // deferred aggregates: each covers >= TAGG_MIN (3) packets, 48 bytes
+    if ((rc = ensure(e, e->adefer_a, ((size_t)n / 3 + 1) * 48))) return rc;
+    if ((rc = ensure(e, e->adefer_b, ((size_t)n / 3 + 1) * 48))) return rc;
+    if (e->cfg.frag_enable) {
+        if ((rc = ensure(e, e->frag_list, (size_t)n * 8))) return rc;
+        if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
+    }
+    // the control block, and the export counters when a clear is pending (they follow it)
+    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, e->ex_zero_pending ? CTL_EX_OFF + 3 * sizeof(uint32_t) : sizeof(BatchCtl),
+                             e->st));
+    e->ex_zero_pending = false;
+
+    p = params(e);
+    p.defer_spill = early ? 1u : 0u;
+    FragView fv = frag_view(e);
+    bins = {};
+    e->bins_valid = false;
+    if (binned) {
+        if ((rc = setup_bins(e, n, bins))) return rc;
+        e->bins_last = bins;
+        e->bins_valid = true;
+        if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
+    }
+    if (async && !early) {  // (the point an asynchronous batch's neighbour formatting forks from)
+        if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
+        HIPCHK(e, hipEventRecord(e->ex_ev, e->st));
+    }
+    if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
+    // the process plugins' flows: SLOT_PLUGIN in the table before k_reduce folds the batch;
+    // k_bin and k_bin_slow write partition records and, on a full segment, atomic slot updates
+    // (tile_emit's spill); k_classify's slot updates are atomic too, so it runs beside them
+    const bool classify = !e->plugins.empty() && binned;
+    p.classify = classify ? 1u : 0u;
+    if (classify && !p.plug) {
+        if (!e->cls_st) {
+            HIPCHK(e, hipStreamCreateWithFlags(&e->cls_st, hipStreamNonBlocking));
+            HIPCHK(e, hipEventCreateWithFlags(&e->cls_fork, hipEventDisableTiming));
+            HIPCHK(e, hipEventCreateWithFlags(&e->cls_join, hipEventDisableTiming));
+        }
+        HIPCHK(e, hipEventRecord(e->cls_fork, e->st));
+        HIPCHK(e, hipStreamWaitEvent(e->cls_st, e->cls_fork, 0));
+        launch_classify(e->cls_st, bv, p, table_view(e), (const DevRule*)e->rules_d.p, (uint32_t)e->plugins.size(),
+                        e->ctl_d);
+        HIPCHK(e, hipEventRecord(e->cls_join, e->cls_st));
+    }
+    ev_rec(e, 0);
+    if (binned) {
+        uint32_t* dl = (uint32_t*)e->defer_a.p;
+        uint4* sl = (uint4*)e->slow_list.p;
+        uint4* al = (uint4*)e->adefer_a.p;
+        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
+        ev_rec(e, 1);
+        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
+        ev_rec(e, 2);
+    }
+    HIPCHK(e, hipGetLastError());
+    return IPXG_OK;
+}
+
+// The rest of the batch after its front: the plugin marks, k_reduce (and k_fin_list for a
+// synchronous batch), or the atomic ingest; an asynchronous batch is left in flight.
+static int launch_rest(ipxg_engine* e, const BatchView& bv, Params p, const BinView& bins, uint32_t n, bool binned,
+                       bool async) {
+    int rc;
+    FragView fv = frag_view(e);
+    const bool classify = p.classify != 0;
+    if (binned) {
+        uint32_t* dl = (uint32_t*)e->defer_a.p;
+        HotSlot* fl = (HotSlot*)e->fin_list.p;
+        uint4* al = (uint4*)e->adefer_a.p;
+        if (classify && p.plug)  // the flows k_bin / k_bin_slow found: claimed and marked before k_reduce
+            launch_plugin_marks(e->st, bv, p, table_view(e), (const DevRule*)e->rules_d.p,
+                                (uint32_t)e->plugins.size(), e->ctl_d, bins);
+        else if (classify)
+            HIPCHK(e, hipStreamWaitEvent(e->st, e->cls_join, 0));
+        // the previous exports' IPFIX formatting ran beside k_bin; this batch's export writers
+        // (k_fin_list and the host paths after it) follow it
+        if ((rc = join_fmt(e))) return rc;
+        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
+        if (!async) {
+            ev_rec(e, 3);
+            launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
+            ev_rec(e, 4);
+        }
+    } else {
+        if ((rc = join_fmt(e))) return rc;
+        launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
+        ev_rec(e, 1);
+    }
+    HIPCHK(e, hipGetLastError());
+    if (async) {
+        e->inflight.on = true;  // the next call launches k_fin_list, publishes and reads the control block
+        e->inflight.tail = true;
+        e->inflight.bv = bv;
+        e->inflight.p = p;
+        e->inflight.n = n;
+        return IPXG_OK;
+    }
+    if ((rc = sync_ctl(e))) return rc;
+    return post_batch(e, bv, p, n, binned, false);
+}
+
 static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
     if (!e || !batch) return IPXG_EINVAL;
     const uint32_t n = batch->n;
@@ -929,7 +1060,23 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
                                  hipMemcpyHostToDevice, e->cst));
         HIPCHK(e, hipEventRecord(e->copied[slot], e->cst));
     }
-    if ((rc = complete_batch(e))) return rc;
+    // a device batch behind an asynchronous batch with plugins in flight: its front may run during
+    // that batch's host walk (early_front)
+    e->early.launched = false;
+    e->early.want = dev_batch && async && e->inflight.on && !e->plugins.empty() && !e->ex_zero_pending;
+    if (e->early.want) {
+        e->early.bv = bv;
+        e->early.bv.arena = batch->arena;
+        e->early.bv.desc = batch->desc;
+        e->early.bv.base_sec = BASE_FROM_DESC0;
+        e->early.n = n;
+    }
+    rc = complete_batch(e);
+    e->early.want = false;
+    if (rc) {
+        e->early.launched = false;
+        return rc;
+    }
     if (dev_batch) {
         bv.arena = batch->arena;
         bv.desc = batch->desc;
@@ -955,94 +1102,21 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
         if ((rc = join_fmt(e))) return rc;
         return strict_submit(e, bv, n);
     }
-    // per-batch scratch sized for the worst case (every packet deferred / a fragment)
-    if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
-    if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
-    // deferred aggregates: each covers >= TAGG_MIN (3) packets, 48 bytes
-    if ((rc = ensure(e, e->adefer_a, ((size_t)n / 3 + 1) * 48))) return rc;
-    if ((rc = ensure(e, e->adefer_b, ((size_t)n / 3 + 1) * 48))) return rc;
-    if (e->cfg.frag_enable) {
-        if ((rc = ensure(e, e->frag_list, (size_t)n * 8))) return rc;
-        if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
+    if (e->early.launched) {
+        // the front of this batch ran during the previous batch's host walk (early_front): the rest
+        e->early.launched = false;
+        Params p = e->early.p;
+        BinView bins = e->early.bins;
+        if ((rc = ensure_export(e, n))) return rc;
+        if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
+        HIPCHK(e, hipEventRecord(e->ex_ev, e->st));  // (after the previous batch's walk exports)
+        return launch_rest(e, bv, p, bins, n, true, true);
     }
     if ((rc = ensure_export(e, n))) return rc;
-    // the control block, and the export counters when a clear is pending (they follow it)
-    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, e->ex_zero_pending ? CTL_EX_OFF + 3 * sizeof(uint32_t) : sizeof(BatchCtl),
-                             e->st));
-    e->ex_zero_pending = false;
-
-    Params p = params(e);
-    FragView fv = frag_view(e);
+    Params p;
     BinView bins = {};
-    e->bins_valid = false;
-    if (binned) {
-        if ((rc = setup_bins(e, n, bins))) return rc;
-        e->bins_last = bins;
-        e->bins_valid = true;
-        if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
-    }
-    if (async) {  // (the point an asynchronous batch's neighbour formatting forks from)
-        if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
-        HIPCHK(e, hipEventRecord(e->ex_ev, e->st));
-    }
-    if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
-    // the process plugins' flows: SLOT_PLUGIN in the table before k_reduce folds the batch;
-    // k_bin and k_bin_slow write partition records and, on a full segment, atomic slot updates
-    // (tile_emit's spill); k_classify's slot updates are atomic too, so it runs beside them
-    const bool classify = !e->plugins.empty() && binned;
-    p.classify = classify ? 1u : 0u;
-    if (classify && !p.plug) {
-        if (!e->cls_st) {
-            HIPCHK(e, hipStreamCreateWithFlags(&e->cls_st, hipStreamNonBlocking));
-            HIPCHK(e, hipEventCreateWithFlags(&e->cls_fork, hipEventDisableTiming));
-            HIPCHK(e, hipEventCreateWithFlags(&e->cls_join, hipEventDisableTiming));
-        }
-        HIPCHK(e, hipEventRecord(e->cls_fork, e->st));
-        HIPCHK(e, hipStreamWaitEvent(e->cls_st, e->cls_fork, 0));
-        launch_classify(e->cls_st, bv, p, table_view(e), (const DevRule*)e->rules_d.p, (uint32_t)e->plugins.size(),
-                        e->ctl_d);
-        HIPCHK(e, hipEventRecord(e->cls_join, e->cls_st));
-    }
-    ev_rec(e, 0);
-    if (binned) {
-        uint32_t* dl = (uint32_t*)e->defer_a.p;
-        uint4* sl = (uint4*)e->slow_list.p;
-        HotSlot* fl = (HotSlot*)e->fin_list.p;
-        uint4* al = (uint4*)e->adefer_a.p;
-        launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
-        ev_rec(e, 1);
-        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
-        ev_rec(e, 2);
-        if (classify && p.plug)  // the flows k_bin / k_bin_slow found: claimed and marked before k_reduce
-            launch_plugin_marks(e->st, bv, p, table_view(e), (const DevRule*)e->rules_d.p,
-                                (uint32_t)e->plugins.size(), e->ctl_d, bins);
-        else if (classify)
-            HIPCHK(e, hipStreamWaitEvent(e->st, e->cls_join, 0));
-        // the previous exports' IPFIX formatting ran beside k_bin; this batch's export writers
-        // (k_fin_list and the host paths after it) follow it
-        if ((rc = join_fmt(e))) return rc;
-        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
-        if (!async) {
-            ev_rec(e, 3);
-            launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
-            ev_rec(e, 4);
-        }
-    } else {
-        if ((rc = join_fmt(e))) return rc;
-        launch_ingest(e->st, bv, p, table_view(e), fv, e->ctl_d, (uint32_t*)e->defer_a.p, e->stats_d);
-        ev_rec(e, 1);
-    }
-    HIPCHK(e, hipGetLastError());
-    if (async) {
-        e->inflight.on = true;  // the next call launches k_fin_list, publishes and reads the control block
-        e->inflight.tail = true;
-        e->inflight.bv = bv;
-        e->inflight.p = p;
-        e->inflight.n = n;
-        return IPXG_OK;
-    }
-    if ((rc = sync_ctl(e))) return rc;
-    return post_batch(e, bv, p, n, binned, false);
+    if ((rc = launch_front(e, bv, n, binned, async, false, p, bins))) return rc;
+    return launch_rest(e, bv, p, bins, n, binned, async);
 }
 
 // Everything after the batch's main kernels, from the control block in e->ctl_h: timing,
@@ -1315,6 +1389,8 @@ static int set_walk_threads_impl(ipxg_engine* e, uint32_t threads) {
 
 // After the batch's complex path (its packets gathered and sorted, the device walk done): walk
 // the plugin flows on the host and write them back.  *live_delta: records created - closed.
+static int early_front(ipxg_engine* e, const Params& p_walked, uint32_t n_walked);
+
 static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, const ComplexView& cx, uint32_t ncx,
                        uint32_t npk, int64_t* live_delta) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1447,6 +1523,13 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         fr[u] = u == 0 ? 0 : u == U ? nf
                        : (uint32_t)(std::lower_bound(first, first + nf, (uint32_t)((uint64_t)m * u / U)) - first);
     auto chunk_of = [&](unsigned u) { return (unsigned)((uint64_t)u * C / U); };
+    // with the next batch's front about to run on the engine's stream (early_front), the chunks
+    // cross on a stream of their own (the engine's stream is idle here: synchronised above)
+    hipStream_t cs = e->st;
+    if (e->early.want) {
+        if (!e->wst) HIPCHK(e, hipStreamCreateWithFlags(&e->wst, hipStreamNonBlocking));
+        cs = e->wst;
+    }
     for (unsigned c = 0; c < C; ++c) {
         unsigned u0 = 0;
         while (chunk_of(u0) < c) u0++;
@@ -1454,18 +1537,25 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         while (u1 < U && chunk_of(u1) == c) u1++;
         const uint32_t k0 = first[fr[u0]], k1 = first[fr[u1]];
         if (k1 > k0) {
-            HIPCHK(e, hipMemcpyAsync(e->hw_idx.data() + k0, o.idx + k0, (size_t)(k1 - k0) * 4, hipMemcpyDeviceToHost, e->st));
+            HIPCHK(e, hipMemcpyAsync(e->hw_idx.data() + k0, o.idx + k0, (size_t)(k1 - k0) * 4, hipMemcpyDeviceToHost, cs));
             HIPCHK(e, hipMemcpyAsync(pk + k0, (ipxg_parsed_pkt*)e->pf_parsed.p + k0, (size_t)(k1 - k0) * sizeof(ipxg_parsed_pkt),
-                                     hipMemcpyDeviceToHost, e->st));
+                                     hipMemcpyDeviceToHost, cs));
             HIPCHK(e, hipMemcpyAsync(e->hw_desc.data() + k0, (ipxg_pkt_desc*)e->pf_desc.p + k0,
-                                     (size_t)(k1 - k0) * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, e->st));
+                                     (size_t)(k1 - k0) * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, cs));
             if (off[k1] > off[k0])
                 HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data() + off[k0], (uint8_t*)e->pf_bytes.p + off[k0], off[k1] - off[k0],
-                                         hipMemcpyDeviceToHost, e->st));
+                                         hipMemcpyDeviceToHost, cs));
         }
         if (!e->walk_ev[c]) HIPCHK(e, hipEventCreateWithFlags(&e->walk_ev[c], hipEventDisableTiming));
-        HIPCHK(e, hipEventRecord(e->walk_ev[c], e->st));
+        HIPCHK(e, hipEventRecord(e->walk_ev[c], cs));
     }
+    // the next batch's front beside the copies and the hooks (its kernels on the engine's stream;
+    // the write-back below follows them there)
+    if ((rc = early_front(e, p, bv.n))) {
+        (void)hipStreamSynchronize(cs);
+        return rc;
+    }
+    BatchCtl* const apply_ctl = e->early.launched ? e->aux_ctl_d : e->ctl_d;
     WALK_MARK(1);
     while (e->hw_ex.size() < U) e->hw_ex.emplace_back(new ExportVec);
     const bool ports = e->pstat_d != nullptr;
@@ -1578,6 +1668,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     else walk_range(0);
     if (copy_fail.load()) {
         (void)hipStreamSynchronize(e->st);
+        (void)hipStreamSynchronize(cs);
         return set_err(e, IPXG_EDEVICE, "plugin walk: a copy of the walk's input failed");
     }
     if (T > 1 && e->pool->take_escaped()) {  // (walk_range catches everything: not expected)
@@ -1652,7 +1743,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     if ((rc = gather([&](unsigned u) -> const HostVec<ipxg_flow_record>& { return e->hw_ex[u]->orec; }, o.recs, 0,
                      nout)))
         return rc;
-    launch_plugin_apply(e->st, table_view(e), o.flows, o.hstate, nf, o.recs, nout, e->ctl_d);
+    launch_plugin_apply(e->st, table_view(e), o.flows, o.hstate, nf, o.recs, nout, apply_ctl);
     HIPCHK(e, hipGetLastError());
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;
@@ -1675,6 +1766,14 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         e->ex_count6 = c3[2];
     }
     HIPCHK(e, hipStreamSynchronize(e->st));
+    if (e->early.launched) {  // k_plugin_apply's guard word (post_batch's check on ctl_d otherwise)
+        uint32_t g = 0;
+        HIPCHK(e, hipMemcpy(&g, &e->aux_ctl_d->guard, sizeof(g), hipMemcpyDeviceToHost));
+        if (g) {
+            HIPCHK(e, hipMemset(&e->aux_ctl_d->guard, 0, sizeof(g)));
+            return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
+        }
+    }
     for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
     for (int k = 0; k < 6; ++k) e->host_pkts[k] += wo.pkts[k];
     e->host_unreasoned += wo.unreasoned;
@@ -1761,6 +1860,58 @@ static int add_plugin_impl(ipxg_engine* e, const ipxg_plugin* pl) {
     return IPXG_OK;
 }
 
+// What the next batch's launch takes from this batch's control block: the order check's
+// timestamp, the partition sizing, the tile aggregation and header walk choices (post_batch; the
+// early front, from the walked batch's block before its host walk ends).
+static void take_batch_knobs(ipxg_engine* e, const BatchCtl& c2, const Params& p, uint32_t n, bool binned) {
+    e->last_touched = c2.touched;
+    e->last_n = n;
+    if (binned && c2.total_slots) {  // the next batch's segment sizing
+        const uint32_t P = 1u << e->part_bits_last;
+        e->skew = (double)c2.max_part * P / c2.total_slots;
+    }
+    // Tile aggregation for the next batch: kept while it folds >= 2 % of the packets, switched
+    // on when the partitions' loads show skew (the most loaded > 2x the mean); the first batch
+    // aggregates.  Uniform traffic folds nothing and skips the aggregation's LDS passes.
+    if (binned) {
+        if (p.tile_agg) e->tile_agg = (uint64_t)c2.agg_packets * 50 >= n;
+        else e->tile_agg = e->skew > 2.0;
+        if (const char* a = std::getenv("IPXG_TILE_AGG")) e->tile_agg = std::atoi(a) != 0;  // experiments
+        // The wide walk for the next batch: switched on when >= 1/32 of the packets went to the
+        // slow list (a mix of variable-length header chains: VLAN, IPv6, TCP options, tunnels),
+        // kept while >= 1/32 are not the plain shape; plain traffic keeps the narrow 48-byte
+        // loads.  walk=wide|narrow pins it.
+        e->wide = (uint64_t)(c2.slow_count + (p.wide ? c2.walked : 0)) * 32 >= n;
+    }
+    e->prev_valid = true;
+    e->prev_sec = c2.last_sec;
+    e->prev_usec = c2.last_usec;
+}
+
+static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool binned, bool async, bool early, Params& p,
+                        BinView& bins);
+
+// The next batch's front from inside this batch's host walk (ipxg_engine::early), once the walk's
+// input has been copied out: the device state the walk still changes is the walked flows' slots
+// and the exports, which k_bin / k_bin_slow do not touch with their spills deferred.  The walked
+// batch's control block is kept in early.snap (ctl_d is the next batch's from here on).
+static int early_front(ipxg_engine* e, const Params& p_walked, uint32_t n_walked) {
+    if (!e->early.want || e->early.launched) return IPXG_OK;
+    std::memcpy(&e->early.snap, e->ctl_h, sizeof(BatchCtl));
+    take_batch_knobs(e, e->early.snap, p_walked, n_walked, true);
+    if (!plug_fold(e)) return IPXG_OK;  // (a k_classify pass would claim slots the walk still owns)
+    if (!e->aux_ctl_d) {
+        if (hipMalloc((void**)&e->aux_ctl_d, sizeof(BatchCtl)) != hipSuccess)
+            return set_err(e, IPXG_ENOMEM, "hipMalloc failed");
+        HIPCHK(e, hipMemsetAsync(e->aux_ctl_d, 0, sizeof(BatchCtl), e->st));
+    }
+    int rc;
+    if ((rc = launch_front(e, e->early.bv, e->early.n, true, true, true, e->early.p, e->early.bins))) return rc;
+    e->early.launched = true;
+    e->tm.plugin_overlapped++;
+    return IPXG_OK;
+}
+
 static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool binned, bool finishing) {
     int rc;
     FragView fv = frag_view(e);
@@ -1793,11 +1944,14 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ndef = e->ctl_h->deferred;
         nadef = e->ctl_h->agg_deferred;
     }
-    // table overflow: grow and re-apply the deferred packets and tile aggregates
+    // table overflow: grow and re-apply the deferred packets and tile aggregates -- first without
+    // growing when k_bin deferred its spills (Params::defer_spill: the table was not full)
+    bool grow = c1.spill_deferred == 0;
     while (ndef || nadef) {
         if (!slow) ev_rec(e, 5);
         slow = true;
-        if ((rc = rehash(e, e->cap * 2))) return rc;
+        if (grow && (rc = rehash(e, e->cap * 2))) return rc;
+        grow = true;
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->deferred, 0, sizeof(uint32_t), e->st));
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->agg_deferred, 0, sizeof(uint32_t), e->st));
         if (ndef)
@@ -1915,8 +2069,12 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
             int64_t dl = 0;
             if ((rc = plugin_walk(e, bv, p, cx, ncx, npk, &dl))) return rc;
             plugin_live += dl;
-            if ((rc = sync_ctl(e))) return rc;
-            if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
+            if (e->early.launched) {  // (ctl_d is the next batch's now: this batch's block from the walk's start)
+                std::memcpy(e->ctl_h, &e->early.snap, sizeof(BatchCtl));
+            } else {
+                if ((rc = sync_ctl(e))) return rc;
+                if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
+            }
         }
         if (e->prof && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);
@@ -1933,32 +2091,13 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     }
     e->live += c2.cx_new_live;
     e->live = (uint32_t)((int64_t)e->live + plugin_live);
-    e->last_touched = c2.touched;
-    e->last_n = n;
-    if (binned && c2.total_slots) {  // the next batch's segment sizing
-        const uint32_t P = 1u << e->part_bits_last;
-        e->skew = (double)c2.max_part * P / c2.total_slots;
-    }
-    // Tile aggregation for the next batch: kept while it folds >= 2 % of the packets, switched
-    // on when the partitions' loads show skew (the most loaded > 2x the mean); the first batch
-    // aggregates.  Uniform traffic folds nothing and skips the aggregation's LDS passes.
+    // (an early front took the knobs already, before the next batch's partitions replaced
+    // part_bits_last)
+    if (!e->early.launched) take_batch_knobs(e, c2, p, n, binned);
     e->agg_pkts += c2.agg_packets;
-    if (binned) {
-        if (p.tile_agg) e->tile_agg = (uint64_t)c2.agg_packets * 50 >= n;
-        else e->tile_agg = e->skew > 2.0;
-        if (const char* a = std::getenv("IPXG_TILE_AGG")) e->tile_agg = std::atoi(a) != 0;  // experiments
-        // The wide walk for the next batch: switched on when >= 1/32 of the packets went to the
-        // slow list (a mix of variable-length header chains: VLAN, IPv6, TCP options, tunnels),
-        // kept while >= 1/32 are not the plain shape; plain traffic keeps the narrow 48-byte
-        // loads.  walk=wide|narrow pins it.
-        e->wide = (uint64_t)(c2.slow_count + (p.wide ? c2.walked : 0)) * 32 >= n;
-    }
     e->spilled += c2.spilled;
     e->slow_pkts += c2.slow_count;
     e->walked_pkts += c2.walked;
-    e->prev_valid = true;
-    e->prev_sec = c2.last_sec;
-    e->prev_usec = c2.last_usec;
     e->batches++;
     // keep the load factor <= 1/2 for the next batch (dead slots are dropped by the rebuild)
     if (!finishing && (uint64_t)e->keys * 2 > e->cap) {

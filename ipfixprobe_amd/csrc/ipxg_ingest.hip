@@ -226,12 +226,16 @@ __device__ __forceinline__ void tile_rank_all(uint32_t* hist, uint32_t pmask, co
 // would fit become NO_REC fillers, so k_reduce never reads half an aggregate).
 // LISTED: packet indices come from ix[] (k_bin_slow); else record q of the lane is packet
 // tile + q * 256 + lane (k_bin).
+// defer_spill (Params::defer_spill: this batch's k_bin runs while the previous batch's host walk
+// still owns the table): what does not fit is deferred (the deferral lists, applied after k_reduce)
+// instead of accumulated into the table.
 template <bool LISTED, bool AGG, uint32_t PMAX = (1u << BIN_MAX_PART_BITS)>
 __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t pmask, const BinView& bv, uint32_t col,
                                           const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
                                           uint4* agg_list, const uint32_t (&r0)[BIN_K], const uint32_t (&r1)[BIN_K],
                                           const uint32_t (&r2)[BIN_K], const uint32_t (&rk)[BIN_K],
-                                          const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& spilled) {
+                                          const uint32_t (&ix)[BIN_K], uint32_t tile, uint32_t& spilled,
+                                          bool defer_spill) {
     constexpr uint32_t PT = PMAX > IPXG_BLOCK ? PMAX / IPXG_BLOCK : 1;  // partitions per thread
     uint32_t* const hist = L.hist;
     uint32_t* const fill = L.fill;
@@ -315,12 +319,13 @@ __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t 
 #endif
         if (valid && !fits && ai == 0) {  // segment full: accumulate straight into the table
             spilled++;
+            if (defer_spill) atomicAdd(&ctl->spill_deferred, 1u);
             if (!agg) {
-                if (!merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
+                if (defer_spill || !merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
                     defer_packet(ctl, deferred_list, r.z, true);
             } else {
                 const uint4 s0 = stage[k], s1 = stage[k + 1], s2 = stage[k + 2];
-                if (!merge_agg_probe(t, agg_decode(s0, s1, s2), &ctl->new_keys)) {
+                if (defer_spill || !merge_agg_probe(t, agg_decode(s0, s1, s2), &ctl->new_keys)) {
                     defer_agg(&ctl->agg_deferred, agg_list, s0, s1, s2);
                     atomicAdd(&ctl->a_deferred, 1u);
                 }
@@ -749,7 +754,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         if (AGG) tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
         else tile_rank_all(hist, pmask, r1, rk);
         tile_emit<false, AGG, KBIN_PMAX>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2,
-                                         rk, ix, tile, spilled);
+                                         rk, ix, tile, spilled, p.defer_spill != 0);
 #endif
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
@@ -1001,7 +1006,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         if (AGG) tile_aggregate<true>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
         else tile_rank_all(hist, pmask, r1, rk);
         tile_emit<true, AGG>(L, P, pmask, bv, bcol, t, ctl, deferred_list, agg_list, r0, r1, r2, rk, ix, tile,
-                             spilled);
+                             spilled, p.defer_spill != 0);
         PROBE_T(s4);
         PROBE_ADD(2, s3, s4);
     }

@@ -72,6 +72,7 @@ struct BatchCtl {
     uint32_t guard;          // bounds guards that fired (engine bug, reported as IPXG_EDEVICE): 1 more complex
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
                              // past the table
+    uint32_t spill_deferred; // of `deferred`: spills k_bin / k_bin_slow deferred (Params::defer_spill)
     uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -152,6 +153,8 @@ struct Params {
     // payload prefixes of at most PLUG_PREFIX bytes (bytes little-endian in pref, compare mask in
     // pmask, len | proto_mask << 8 in pinfo)
     uint32_t plug;
+    uint32_t defer_spill;    // k_bin / k_bin_slow defer what does not fit its segment (tile_emit): the
+                             // batch was launched during the previous batch's host walk
     uint32_t plug_nport, plug_npref;
     uint32_t plug_port[16];
     uint32_t plug_pref[16], plug_pmask[16], plug_pinfo[16];

@@ -77,7 +77,8 @@ class Timing(ctypes.Structure):
         [(n, ctypes.c_uint64) for n in ("ingest_launches", "reduce_launches", "finalize_launches",
                                         "slow_launches", "finish_launches", "ingest_packets")] + \
         [("plugin_ms", ctypes.c_double)] + [(n, ctypes.c_uint64) for n in ("plugin_flows", "plugin_packets",
-                                                                             "plugin_bytes", "plugin_extra_bytes")]
+                                                                             "plugin_bytes", "plugin_extra_bytes",
+                                                                             "plugin_overlapped")]
 
 
 class Capture(ctypes.Structure):

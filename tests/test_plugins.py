@@ -227,3 +227,42 @@ def test_classifier_payload_offsets_on_fuzz_corpus(batch):
     assert not d, d
     assert (want["ext"] != 0).sum() > 100
     assert eng.seen == orc.seen
+
+
+@pytest.mark.gpu
+def test_early_front_defers_spills(monkeypatch):
+    """Asynchronous device batches with a plugin registered: each batch's k_bin / k_bin_slow run
+    during the previous batch's host walk (the early front), while the walk still owns the table --
+    so what overflows a segment is deferred (Params::defer_spill) instead of accumulated into a
+    slot, and applied after k_reduce without growing the table.  An elephant flow with the segments
+    forced small (IPXG_TILE_AGG=0, IPXG_PART_BITS=8, from the second batch on) overflows them in
+    every overlapped batch; the records, the NTP plugin's flushes included, equal the oracle's."""
+    import torch
+    import test_gpu_semantics
+    from ipfixprobe_amd import Engine
+    rng = np.random.default_rng(24)
+    n, F, nb = 200_000, 5000, 4
+    fop = np.where(rng.random(n) < 0.5, 0, rng.integers(1, F, n))
+    arena, desc = test_gpu_semantics._udp_batch(rng, fop, F)
+    ref = plugins_py.NtpFlush()
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20, plugins=[ref.struct])
+    monkeypatch.setenv("IPXG_TILE_AGG", "0")
+    monkeypatch.setenv("IPXG_PART_BITS", "8")
+    a = torch.from_numpy(np.ascontiguousarray(arena)).cuda()
+    ds = [torch.from_numpy(np.ascontiguousarray(desc[k * n // nb:(k + 1) * n // nb]).view(np.uint8).reshape(-1)).cuda()
+          for k in range(nb)]
+    torch.cuda.synchronize()
+    pl = plugins_py.NtpFlush()
+    with Engine("s=16") as e:
+        e.add_plugin(pl.struct)
+        for d in ds:
+            e.submit(a, d, device=True, asynchronous=True)
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+        tm = e.timing()
+    assert tm["plugin_overlapped"] >= nb - 2, tm
+    assert st["spilled_packets"] > 0 and st["table_rehashes"] == 0, st
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+    assert (want["ext"] != 0).sum() > 0

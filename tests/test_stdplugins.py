@@ -88,15 +88,17 @@ _CALLS = {}  # hook calls of the single-threaded walk, per mix
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [1, 4, 16])
+@pytest.mark.parametrize("threads,asynchronous", [(1, False), (4, False), (16, False), (16, True)])
 @pytest.mark.parametrize("name", sorted(PLUGINS))
-def test_plugins_on_workload_match_oracle(name, threads):
+def test_plugins_on_workload_match_oracle(name, threads, asynchronous):
     """2M packets of the mix over 1M flows in four device batches with the configs' plugins
     registered: every record (plugin flushes, REINSERTs and the plugins' ext bits included)
     equals the oracle's, which calls the same hooks on every packet; the hooks saw only a small
     share of the packets on the engine (the bridge kept the rest on the device).  The host walk
     on 1, 4 and 16 threads (plugin copies per thread): the same records, and the hook calls of
-    all copies sum to the same counts."""
+    all copies sum to the same counts.  asynchronous: device batches submitted back to back with
+    IPXG_BATCH_ASYNC, so each batch's k_bin / k_bin_slow run during the previous batch's host walk
+    (the early front, its spills deferred): the same records and hook calls."""
     import torch
     import synthgen
     from ipfixprobe_amd import Engine
@@ -110,10 +112,12 @@ def test_plugins_on_workload_match_oracle(name, threads):
         for p in pls:
             e.add_plugin(p.struct)
         for fr, de in batches:
-            e.submit(fr, de, device=True)
+            e.submit(fr, de, device=True, asynchronous=asynchronous)
         e.finish()
         got = e.poll()
         st = e.stats()
+        overlapped = e.timing()["plugin_overlapped"]
+    assert (overlapped >= nb - 2) if asynchronous else overlapped == 0, overlapped
     calls = [p.calls() for p in pls]  # copies folded back into the originals at engine destroy
     if threads == 1:
         _CALLS[name] = calls
