@@ -10,6 +10,7 @@
 #include <pthread.h>
 
 #include <openssl/evp.h>
+#include <openssl/sha.h>
 
 enum { C_PRE_CREATE, C_POST_CREATE, C_PRE_UPDATE, C_POST_UPDATE, C_PRE_EXPORT, C_FLUSH, C_N };
 
@@ -435,34 +436,14 @@ typedef struct {
     uint64_t n;
 } sha256_t;
 
-static const uint32_t SHA_K[64] = {
-    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-
-#define ROR32(x, r) (((x) >> (r)) | ((x) << (32 - (r))))
-
+/* one 64-byte block: OpenSSL's low-level transform (its SHA-NI / AVX2 code, no provider lookup or
+ * lock: 88 ns a block on the container's Xeon against 630 ns for the portable C it replaced, which
+ * made 75 % of an Initial's detection) */
 static void sha256_block(uint32_t h[8], const uint8_t* p) {
-    uint32_t w[64];
-    for (int i = 0; i < 16; ++i)
-        w[i] = ((uint32_t)p[4 * i] << 24) | ((uint32_t)p[4 * i + 1] << 16) | ((uint32_t)p[4 * i + 2] << 8) | p[4 * i + 3];
-    for (int i = 16; i < 64; ++i) {
-        const uint32_t s0 = ROR32(w[i - 15], 7) ^ ROR32(w[i - 15], 18) ^ (w[i - 15] >> 3);
-        const uint32_t s1 = ROR32(w[i - 2], 17) ^ ROR32(w[i - 2], 19) ^ (w[i - 2] >> 10);
-        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-    }
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
-    for (int i = 0; i < 64; ++i) {
-        const uint32_t t1 = k + (ROR32(e, 6) ^ ROR32(e, 11) ^ ROR32(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[i] + w[i];
-        const uint32_t t2 = (ROR32(a, 2) ^ ROR32(a, 13) ^ ROR32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
-        k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-    }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+    SHA256_CTX c;
+    memcpy(c.h, h, 32);
+    SHA256_Transform(&c, p);
+    memcpy(h, c.h, 32);
 }
 
 static void sha256_init(sha256_t* s) {
