@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void k_plugin_idx(BatchView b, ComplexView cx,
         for (uint32_t j = lane; j < len; j += 64) {
             const uint32_t i = (uint32_t)(cx.sorted[seg + j] & 0xFFFFFFu);
             idx[at + j] = i;
-            clen[at + j] = b.desc[i].caplen;
+            clen[at + j] = ((uint32_t)b.desc[i].caplen + 15u) & ~15u;  // (16-byte aligned frame starts)
         }
     }
 }
@@ -301,20 +301,30 @@ void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, Fra
                        m, out, dout);
 }
 
-// Frame bytes of packet idx[k] to out + off[k] (one workgroup per packet, byte copies).
+// Frame bytes of packet idx[k] to out + off[k], a wave per packet: 16-byte copies when the frame
+// starts on 16 bytes (out + off[k] always does: k_plugin_idx rounds the lengths up), so the
+// rounded-up tail is read from inside the arena; byte copies otherwise.  (A workgroup per packet
+// with byte copies: the quic walk's 330 MB of frames per batch.)
 __global__ __launch_bounds__(256) void k_plugin_bytes(BatchView b, const uint32_t* idx, const uint64_t* off,
                                                       uint32_t m, uint8_t* out) {
-    for (uint32_t k = blockIdx.x; k < m; k += gridDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < m; k += gridDim.x * 4) {
         const ipxg_pkt_desc d = b.desc[idx[k]];
         const uint8_t* src = b.arena + d.offset;
         uint8_t* dst = out + off[k];
-        for (uint32_t j = threadIdx.x; j < d.caplen; j += 256) dst[j] = src[j];
+        const uint32_t n16 = ((uint32_t)d.caplen + 15u) >> 4;
+        if ((d.offset & 15u) == 0 && (uint64_t)d.offset + 16ull * n16 <= b.arena_lim) {
+            for (uint32_t j = lane; j < n16; j += 64)
+                reinterpret_cast<uint4*>(dst)[j] = reinterpret_cast<const uint4*>(src)[j];
+        } else {
+            for (uint32_t j = lane; j < d.caplen; j += 64) dst[j] = src[j];
+        }
     }
 }
 
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
                          uint8_t* out) {
-    const uint32_t g = m < 4096 ? m : 4096;
+    const uint32_t g = (m + 3) / 4 < 4096 ? (m + 3) / 4 : 4096;
     hipLaunchKernelGGL(k_plugin_bytes, dim3(g ? g : 1), dim3(256), 0, st, b, idx, off, m, out);
 }
 
