@@ -363,6 +363,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     while (bits < 8 && ((uint64_t)RED_MIN_FLOWS << bits) < est) bits++;
     if (const char* pb = std::getenv("IPXG_PART_BITS"))  // tuning knob (experiments only)
         bits = std::min<uint32_t>((uint32_t)std::atoi(pb), BIN_MAX_PART_BITS);
+    bits = std::min<uint32_t>(bits, IPXG_KBIN_PMAX_BITS);  // (k_bin's histograms)
     const uint32_t P = 1u << bits;
     const uint64_t tiles = ((uint64_t)n + BIN_TILE_PKTS - 1) / BIN_TILE_PKTS;
     const int ag = e->tile_agg ? 1 : 0, wd = wide_walk(e) ? 1 : 0, pl = plug_fold(e) ? 1 : 0;

@@ -540,7 +540,7 @@ __device__ __forceinline__ uint32_t plug_check(const Params& p, const uint32_t (
 // frames from registers as well; the remaining shapes (MPLS, PPPoE, GRE, IPv6 extension
 // headers, other TCP options, ...) still go to the slow list.
 // The host picks the variants per batch (ipxg_engine.cpp: tile_agg, wide).
-constexpr uint32_t KBIN_PMAX = 1u << BIN_MAX_PART_BITS;  // (the host may pick up to BIN_MAX_PART_BITS)
+constexpr uint32_t KBIN_PMAX = 1u << IPXG_KBIN_PMAX_BITS;  // (the host picks at most IPXG_KBIN_PMAX_BITS)
 #ifndef IPXG_BIN_NARROW_WPE
 #define IPXG_BIN_NARROW_WPE 3  // waves per SIMD of the narrow, non-aggregating k_bin (its register budget)
 #endif
@@ -1798,25 +1798,47 @@ void launch_complex_gather(hipStream_t st, const BatchView& b, const Params& p, 
 }
 
 // The complex flows' packets from the batch's partition records instead of the frames: 16 bytes
-// per packet read, no parse (the re-parse gather reads every frame head and parses it).  A thread
-// per segment (a k_bin / k_bin_slow workgroup's records of one partition: a few records each on
-// the 1M-flow mixes).  A complex flow with packets folded into a tile aggregate (no per-packet
-// index left) flags the batch for the re-parse gather.
+// per packet read, no parse (the re-parse gather reads every frame head and parses it).  A
+// workgroup per 256 segments (a k_bin / k_bin_slow workgroup's records of one partition: a few
+// records each on the 1M-flow mixes): their lengths scanned in LDS, then a thread per record,
+// found by a binary search over the prefix -- consecutive threads read consecutive records.
+// (Round 4 first ran a thread per segment: a lane walked its segment alone, every load of a wave
+// touched 64 lines -- 0.37 ms per 10M-packet configs[2] batch.)  A complex flow with packets
+// folded into a tile aggregate (no per-packet index left) lists the aggregate's range or flags
+// the batch for the re-parse gather.
 __global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexView cx, BatchCtl* ctl, uint32_t nseg,
                                                            uint4* ranges, uint32_t range_cap) {
-    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nseg; s += gridDim.x * 256) {
-        const uint32_t c = s % bv.cols;
-        if (c >= bv.bin_grid && !bv.slow_cnt[c - bv.bin_grid]) continue;  // (a k_bin_slow column left unwritten)
-        const uint32_t n = bv.count[s];
-        const uint4* seg = bv.rec + (size_t)s * bv.seg_cap;
-        for (uint32_t j = 0; j < n; ++j) {
+    __shared__ uint32_t pre[257];
+    __shared__ uint32_t scan_s[256 / 64 + 1];
+    for (uint32_t s0 = blockIdx.x * 256; s0 < nseg; s0 += gridDim.x * 256) {  // block-uniform
+        const uint32_t s = s0 + threadIdx.x;
+        uint32_t n = 0;
+        if (s < nseg) {
+            const uint32_t c = s % bv.cols;
+            if (c < bv.bin_grid || bv.slow_cnt[c - bv.bin_grid]) n = bv.count[s];  // (else a k_bin_slow column left unwritten)
+        }
+        uint32_t tot;
+        const uint32_t at = block_exclusive_scan<256>(n, scan_s, &tot);
+        pre[threadIdx.x] = at;
+        if (threadIdx.x == 0) pre[256] = tot;
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < tot; k += 256) {
+            uint32_t lo = 0, hi = 256;  // pre[lo] <= k < pre[hi]: lo = the segment holding record k
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (pre[mid] <= k) lo = mid;
+                else hi = mid;
+            }
+            const uint32_t ss = s0 + lo, j = k - pre[lo], sn = pre[lo + 1] - pre[lo];
+            const uint32_t c = ss % bv.cols;
+            const uint4* seg = bv.rec + (size_t)ss * bv.seg_cap;
             const uint4 r = seg[j];
             if (r.z == NO_REC) continue;
             if (rec_is_agg(r)) {
                 if (rec_agg_slot(r) == 0 && complex_rank_of(cx, ((uint64_t)r.y << 32) | r.x) >= 0) {
                     // a k_bin aggregate (its packets inside one tile): its range is parsed again
                     // (k_complex_gather_ranges); k_bin_slow's span tiles: the whole batch then
-                    uint32_t q = c < bv.bin_grid && j + 2 < n ? atomicAdd(&ctl->cx_ranges, 1u) : range_cap;
+                    uint32_t q = c < bv.bin_grid && j + 2 < sn ? atomicAdd(&ctl->cx_ranges, 1u) : range_cap;
                     if (q < range_cap) {
                         const FlowAgg a = agg_decode(r, seg[j + 1], seg[j + 2]);
                         ranges[q] = make_uint4(r.x, r.y, first_idx(a.first_n), a.last1 - 1);
@@ -1833,6 +1855,7 @@ __global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexV
             if (pos < cx.len[rk]) cx.list[cx.seg[rk] + pos] = ((uint64_t)rk << 24) | (r.z & 0xFFFFFFu);
             else atomicOr(&ctl->guard, 2u);
         }
+        __syncthreads();  // (pre is rewritten by the next group)
     }
 }
 

@@ -230,6 +230,10 @@ constexpr uint32_t BIN_TILE_PKTS = IPXG_BIN_K * 256u;  // packets per k_bin tile
 #define IPXG_BIN_MAX_PART_BITS 11
 #endif
 constexpr uint32_t BIN_MAX_PART_BITS = IPXG_BIN_MAX_PART_BITS;  // <= 2048 partitions (LDS histograms of k_bin)
+#ifndef IPXG_KBIN_PMAX_BITS  // tuning knob: k_bin's LDS partition histograms (the host caps the partitions to it)
+#define IPXG_KBIN_PMAX_BITS IPXG_BIN_MAX_PART_BITS
+#endif
+static_assert(IPXG_KBIN_PMAX_BITS <= IPXG_BIN_MAX_PART_BITS, "k_bin's histograms");
 constexpr uint32_t BIN_MAX_GRID = 2048;     // k_bin workgroups (persistent over the tiles)
 constexpr uint32_t RED_THREADS = 1024;      // k_reduce workgroup
 #ifndef IPXG_RED_ENTRIES
