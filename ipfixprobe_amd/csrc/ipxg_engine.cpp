@@ -2020,12 +2020,16 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ev_rec(e, 5);
         e->complex_total += ncx;
         const uint32_t kcap = pow2_at_least((uint64_t)ncx * 2 + 1);  // the complex flows' key set
-        if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 4 * 4 + (size_t)kcap * 12))) return rc;
+        // its bitmap: >= 16 bits per complex flow (<= 1/16 false hits), 8 KB .. 2 MB
+        const uint32_t bwords = std::min<uint32_t>(1u << 19, std::max<uint32_t>(2048, pow2_at_least((uint64_t)ncx) / 2));
+        if ((rc = ensure(e, e->cx_rank, (size_t)ncx * 4 * 4 + (size_t)kcap * 12 + (size_t)bwords * 4))) return rc;
         uint32_t* cr = (uint32_t*)e->cx_rank.p;
         unsigned long long* ck = reinterpret_cast<unsigned long long*>(cr + 4 * (size_t)ncx);
+        uint32_t* bloom = reinterpret_cast<uint32_t*>(ck + kcap) + kcap;
         HIPCHK(e, hipMemsetAsync(ck, 0, (size_t)kcap * 8, e->st));
+        HIPCHK(e, hipMemsetAsync(bloom, 0, (size_t)bwords * 4, e->st));
         ComplexView cx = {nullptr, nullptr, cr, cr + ncx, cr + 2 * (size_t)ncx, cr + 3 * (size_t)ncx,
-                          ck, reinterpret_cast<uint32_t*>(ck + kcap), kcap - 1};
+                          ck, reinterpret_cast<uint32_t*>(ck + kcap), kcap - 1, bloom, bwords - 1};
         launch_complex_rank(e->st, table_view(e), cx, e->ctl_d, e->cap, ncx);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;

@@ -381,6 +381,7 @@ __global__ __launch_bounds__(256) void k_complex_rank(TableView t, ComplexView c
         uint32_t e = (uint32_t)key & cx.kmask;  // >= 2 entries per complex flow: terminates
         while (atomicCAS(&cx.keys[e], 0ull, (unsigned long long)key) != 0ull) e = (e + 1) & cx.kmask;
         cx.key_rank[e] = r;
+        if (cx.bloom) atomicOr(&cx.bloom[((uint32_t)key >> 5) & cx.bmask], 1u << ((uint32_t)key & 31u));
     }
 }
 

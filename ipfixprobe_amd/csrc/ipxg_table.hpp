@@ -15,6 +15,7 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 // rank of the complex flow with canonical key lo, or -1
 __device__ __forceinline__ int64_t complex_rank_of(const ComplexView& cx, uint64_t lo) {
+    if (cx.bloom && !((cx.bloom[((uint32_t)lo >> 5) & cx.bmask] >> ((uint32_t)lo & 31u)) & 1u)) return -1;
     for (uint32_t e = (uint32_t)lo & cx.kmask;; e = (e + 1) & cx.kmask) {
         const unsigned long long k = cx.keys[e];
         if (k == lo) return cx.key_rank[e];
