@@ -28,9 +28,10 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 4 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+#define IPXG_ABI_VERSION 5 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
                               3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
-                              4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error) */
+                              4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
+                              5: ipxg_timing gained plugin_overlapped */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
