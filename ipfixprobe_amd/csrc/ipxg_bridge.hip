@@ -276,9 +276,10 @@ size_t plugin_order_temp(uint32_t ncx, uint32_t npk) {
     return std::max(a, std::max(c, d));
 }
 
-// Packet idx[k] (k < m): every field a hook reads (ipxg_parsed_pkt, FULL parse) and its descriptor.
+// Packet idx[k] (k < m): every field a hook reads (ipxg_parsed_pkt, FULL parse), its descriptor
+// and its index, as one WalkPkt.
 __global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_pkts(BatchView b, Params p, FragView f, const uint32_t* idx,
-                                                            uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout) {
+                                                            uint32_t m, WalkPkt* out) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     const uint32_t k = blockIdx.x * IPXG_BLOCK + threadIdx.x;
     if (k >= m) return;
@@ -291,14 +292,17 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_pkts(BatchView b, Params 
     ParseCounts c = {};
     const bool ok = parse_frame<true>(S, d.caplen, p.dlt, pk, c);
     if (ok) apply_frag_ports(p, f, i, pk);  // a fragment's ports from the fragmentation cache
-    out[k] = to_parsed(pk, ok);
-    dout[k] = d;
+    WalkPkt w;
+    w.pk = to_parsed(pk, ok);
+    w.d = d;
+    w.idx = i;
+    out[k] = w;
 }
 
 void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
-                        uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout) {
+                        uint32_t m, WalkPkt* out) {
     hipLaunchKernelGGL(k_plugin_pkts, dim3((m + IPXG_BLOCK - 1) / IPXG_BLOCK), dim3(IPXG_BLOCK), 0, st, b, p, f, idx,
-                       m, out, dout);
+                       m, out);
 }
 
 // Frame bytes of packet idx[k] to out + off[k], a wave per packet: 16-byte copies when the frame

@@ -151,14 +151,13 @@ struct ipxg_engine {
     bool strict_prune = true;                            // strict: idle-free sweep steps left out of the DAG
     uint32_t strict_wgs = STRICT_WGS_DEFAULT;            // strict: replay workgroups per XCD (0: one workgroup)
     uint32_t* st_sched = nullptr;                        // strict: the multi-workgroup scheduler block
-    DevBuf rules_d, pf_d, pf_idx, pf_parsed, pf_desc, pf_off, pf_bytes, pf_keys, pf_flen, pf_tmp, pf_live, pf_recs;
+    DevBuf rules_d, pf_d, pf_idx, pf_wpk, pf_off, pf_bytes, pf_keys, pf_flen, pf_tmp, pf_live, pf_recs;
     // their host copies, kept across batches (HostVec: page-locked malloc memory)
     HostVec<uint32_t> hw_state, hw_lpos;  // the flows' slot states (then their new ones); live record positions
     HostVec<ipxg_flow_record> hw_recs;    // the live flows' records
-    HostVec<uint32_t> hw_first, hw_idx;
+    HostVec<uint32_t> hw_first;
     HostVec<uint64_t> hw_off;
-    HostVec<ipxg_parsed_pkt> hw_parsed;
-    HostVec<ipxg_pkt_desc> hw_desc;
+    HostVec<WalkPkt> hw_wpk;  // the walked packets: parsed fields, descriptor, batch index
     HostVec<uint8_t> hw_bytes;
     bool walk_pin = true;  // HostVec page-locked (IPXG_WALK_PAGEABLE unset)
     uint64_t host_end[5] = {0, 0, 0, 0, 0};
@@ -741,7 +740,7 @@ int ipxg_destroy(ipxg_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (DevBuf* b : {&e->stage_arena[0], &e->stage_arena[1], &e->stage_desc[0], &e->stage_desc[1], &e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_parsed, &e->pf_desc, &e->pf_off, &e->pf_bytes,
+    for (DevBuf* b : {&e->stage_arena[0], &e->stage_arena[1], &e->stage_desc[0], &e->stage_desc[1], &e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_wpk, &e->pf_off, &e->pf_bytes,
                       &e->pf_keys, &e->pf_flen, &e->pf_tmp, &e->pf_live, &e->pf_recs,
                       &e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
                       &e->frag_sorted,
@@ -1470,30 +1469,26 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const uint64_t nbytes = tot[2];
     const uint32_t nlive = (uint32_t)tot[3];
     if (!nf) return IPXG_OK;
-    if ((rc = ensure(e, e->pf_parsed, (size_t)m * sizeof(ipxg_parsed_pkt) + 8))) return rc;
-    if ((rc = ensure(e, e->pf_desc, (size_t)m * sizeof(ipxg_pkt_desc) + 16))) return rc;
+    if ((rc = ensure(e, e->pf_wpk, (size_t)m * sizeof(WalkPkt) + 16))) return rc;
     if ((rc = ensure(e, e->pf_bytes, nbytes + 16))) return rc;
-    launch_plugin_pkts(e->st, bv, p, frag_view(e), o.idx, m, (ipxg_parsed_pkt*)e->pf_parsed.p,
-                       (ipxg_pkt_desc*)e->pf_desc.p);
+    launch_plugin_pkts(e->st, bv, p, frag_view(e), o.idx, m, (WalkPkt*)e->pf_wpk.p);
     launch_plugin_bytes(e->st, bv, o.idx, o.off, m, (uint8_t*)e->pf_bytes.p);
     HIPCHK(e, hipGetLastError());
     const bool pin = e->walk_pin;
     if (!e->hw_state.resize(nf, pin) || !e->hw_recs.resize(nlive, pin) || !e->hw_first.resize(nf + 1, pin) ||
-        !e->hw_idx.resize(m, pin) || !e->hw_parsed.resize(m, pin) || !e->hw_desc.resize(m, pin) ||
+        !e->hw_wpk.resize(m, pin) ||
         !e->hw_off.resize((size_t)m + 1, pin) || !e->hw_bytes.resize(nbytes + 16, pin) || !e->hw_lpos.resize(nf + 1, pin))
         return set_err(e, IPXG_ENOMEM, "host walk buffers");
     uint32_t* fstate = e->hw_state.data();
     const ipxg_flow_record* recs_in = e->hw_recs.data();
     uint32_t* lpos = e->hw_lpos.data();
     const uint32_t* first = e->hw_first.data();
-    const uint32_t* idx = e->hw_idx.data();
-    ipxg_parsed_pkt* pk = e->hw_parsed.data();
-    const ipxg_pkt_desc* de = e->hw_desc.data();
+    WalkPkt* wp = e->hw_wpk.data();
     const uint64_t* off = e->hw_off.data();
     const uint8_t* bytes = e->hw_bytes.data();
     // The walk's input in two steps (page-locked host buffers; the walk threads make no HIP call):
     // first the per-flow arrays and the live records, which the split into work units needs;
-    // then the packets -- indices, parsed fields, descriptors, frame bytes -- in WALK_CHUNKS chunks
+    // then the packets -- their WalkPkt records (parsed fields, descriptor, index), frame bytes -- in WALK_CHUNKS chunks
     // of whole work units, each chunk's copies behind an event.  The threads take units in walk
     // order and start a unit once its chunk has landed, so the hooks run while the later chunks
     // are still crossing PCIe (one round of copies took 18.5 of the configs[2] step's 37 ms host
@@ -1541,11 +1536,8 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             HIPCHK(e, hipMemcpyAsync(e->hw_recs.data() + l0, o.recs + l0, (size_t)(l1 - l0) * sizeof(ipxg_flow_record),
                                      hipMemcpyDeviceToHost, cs));
         if (k1 > k0) {
-            HIPCHK(e, hipMemcpyAsync(e->hw_idx.data() + k0, o.idx + k0, (size_t)(k1 - k0) * 4, hipMemcpyDeviceToHost, cs));
-            HIPCHK(e, hipMemcpyAsync(pk + k0, (ipxg_parsed_pkt*)e->pf_parsed.p + k0, (size_t)(k1 - k0) * sizeof(ipxg_parsed_pkt),
+            HIPCHK(e, hipMemcpyAsync(wp + k0, (WalkPkt*)e->pf_wpk.p + k0, (size_t)(k1 - k0) * sizeof(WalkPkt),
                                      hipMemcpyDeviceToHost, cs));
-            HIPCHK(e, hipMemcpyAsync(e->hw_desc.data() + k0, (ipxg_pkt_desc*)e->pf_desc.p + k0,
-                                     (size_t)(k1 - k0) * sizeof(ipxg_pkt_desc), hipMemcpyDeviceToHost, cs));
             if (off[k1] > off[k0])
                 HIPCHK(e, hipMemcpyAsync(e->hw_bytes.data() + off[k0], (uint8_t*)e->pf_bytes.p + off[k0], off[k1] - off[k0],
                                          hipMemcpyDeviceToHost, cs));
@@ -1605,14 +1597,14 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
             for (uint32_t k = first[f]; k < first[f + 1]; ++k) {
                 ipxg_packet_view v;
                 std::memset(&v, 0, sizeof(v));
-                v.pkt = &pk[k];
+                v.pkt = &wp[k].pk;
                 v.data = bytes + off[k];
-                v.caplen = de[k].caplen;
-                v.wirelen = de[k].wirelen;
-                v.ts_sec = de[k].ts_sec;
-                v.ts_usec = de[k].ts_usec;
-                v.index = idx[k];
-                w.put(pk[k], &v);
+                v.caplen = wp[k].d.caplen;
+                v.wirelen = wp[k].d.wirelen;
+                v.ts_sec = wp[k].d.ts_sec;
+                v.ts_usec = wp[k].d.ts_usec;
+                v.index = wp[k].idx;
+                w.put(wp[k].pk, &v);
             }
             // a plugin that follows every packet of a flow it claimed (ext set) keeps it on the
             // host walk until the flow holds follow_packets packets (ipxg_plugin.follow_packets)
@@ -1713,7 +1705,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     }
     for (unsigned u = 0; u < U; ++u) *live_delta += dlive[u];
     for (uint32_t k = 0; k < m; ++k) {  // (the frames' own lengths: off[] steps are rounded to 16 bytes)
-        const uint64_t cl = de[k].caplen;
+        const uint64_t cl = wp[k].d.caplen;
         e->tm.plugin_bytes += cl;
         e->tm.plugin_extra_bytes += cl > 128 ? cl - 128 : 0;
     }

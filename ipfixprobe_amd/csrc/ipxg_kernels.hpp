@@ -336,8 +336,15 @@ struct PluginOrder {
 void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, ComplexView cx, uint32_t ncx, uint32_t npk,
                          const PluginOrder& o);
 size_t plugin_order_temp(uint32_t ncx, uint32_t npk);
+// A walked packet as the host walk reads it: its parsed fields, descriptor and batch index in one
+// record, so a chunk of the walk's input crosses to the host in one copy (k_plugin_pkts)
+struct WalkPkt {
+    ipxg_parsed_pkt pk;
+    ipxg_pkt_desc d;
+    uint32_t idx;
+};
 void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
-                        uint32_t m, ipxg_parsed_pkt* out, ipxg_pkt_desc* dout);
+                        uint32_t m, WalkPkt* out);
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
                          uint8_t* out);
 // The host walk's results, read by one kernel straight from page-locked host memory (one launch
