@@ -266,3 +266,36 @@ def test_early_front_defers_spills(monkeypatch):
     d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
     assert not d, d
     assert (want["ext"] != 0).sum() > 0
+
+
+@pytest.mark.gpu
+def test_early_front_on_fuzz_corpus():
+    """The fuzz corpus (every register-walk shape, fragments, truncations) in 4096-packet device
+    batches submitted back to back with IPXG_BATCH_ASYNC: each batch's k_bin / k_bin_slow run during
+    the previous batch's host walk, fragments included (k_bin_slow lists them into the batch's own
+    fragment list while the walked batch's replay is done); records and ext bits equal the
+    oracle's."""
+    import torch
+    from ipfixprobe_amd import Engine
+    arena, desc = synth.to_batch(synth.fuzz_corpus(20000, seed=71))
+    orc = PrefixMarker()
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20, plugins=[orc.struct])
+    a = torch.from_numpy(np.ascontiguousarray(arena)).cuda()
+    step = 4096
+    ds = [torch.from_numpy(np.ascontiguousarray(desc[s:s + step]).view(np.uint8).reshape(-1)).cuda()
+          for s in range(0, len(desc), step)]
+    torch.cuda.synchronize()
+    eng = PrefixMarker()
+    with Engine("s=18") as e:
+        e.add_plugin(eng.struct)
+        for d in ds:
+            e.submit(a, d, device=True, asynchronous=True)
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+        tm = e.timing()
+    assert tm["plugin_overlapped"] >= 1, tm
+    assert st["fragmented_packets"] > 0, st
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+    assert eng.seen == orc.seen
