@@ -216,13 +216,6 @@ struct ipxg_engine {
     } early;
     BatchCtl* aux_ctl_d = nullptr;  // k_plugin_apply's guard word while ctl_d holds the next batch's
     hipStream_t wst = nullptr;      // the host walk's input copies (beside the next batch's front)
-    // the host walk's exports gathered onto the device on a stream of their own (xst), beside the
-    // next batch's kernels; xev marks their end.  The engine's stream joins it before the next
-    // export append or read (join_fmt); the walk's export buffers are reused only after it.
-    hipStream_t xst = nullptr;
-    hipEvent_t xfork = nullptr, xev = nullptr;
-    bool xg_pending = false;  // the engine's stream has not joined xev yet
-    bool xg_host = false;     // the host has not waited for xev since (the units' buffers are read)
     DevBuf slow_list, slow_cnt, fin_list;  // k_bin -> k_bin_slow, k_reduce -> k_fin_list
     // asynchronous host batches: two staging slots, filled on a copy stream while the other
     // slot's batch is in the kernels (the double-buffered ingest ring)
@@ -534,13 +527,7 @@ static int rehash(ipxg_engine* e, uint32_t new_cap) {
 // The engine's stream waits for the device IPFIX formatting in flight (ipxg_device_ipfix_messages
 // on fst: it reads the exports and the IPFIX scratch buffers) before anything that appends or
 // moves exports or reuses those buffers.  Stream order only: no host wait.
-// exports: also the host walk's export gather (every caller appends or reads exports, except
-// k_reduce's launch, which only joins the formatting)
-static int join_fmt(ipxg_engine* e, bool exports = true) {
-    if (exports && e->xg_pending) {
-        e->xg_pending = false;
-        HIPCHK(e, hipStreamWaitEvent(e->st, e->xev, 0));
-    }
+static int join_fmt(ipxg_engine* e) {
     if (!e->fmt_pending) return IPXG_OK;
     e->fmt_pending = false;
     HIPCHK(e, hipStreamWaitEvent(e->st, e->fmt_done, 0));
@@ -717,7 +704,6 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->st) hipStreamSynchronize(e->st);
     if (e->fst) hipStreamSynchronize(e->fst);
     if (e->wst) hipStreamSynchronize(e->wst);
-    if (e->xst) hipStreamSynchronize(e->xst);
     delete e->pool;
     free_walk_copies(e);
     hipFree(e->line);
@@ -727,9 +713,6 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->ctl_d);
     hipFree(e->aux_ctl_d);
     if (e->wst) (void)hipStreamDestroy(e->wst);
-    if (e->xst) (void)hipStreamDestroy(e->xst);
-    for (hipEvent_t ev : {e->xfork, e->xev})
-        if (ev) (void)hipEventDestroy(ev);
     if (e->ctl_h) hipHostFree(e->ctl_h);
     hipFree(e->misc_d);
     hipFree(e->stats_d);
@@ -966,7 +949,7 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
     }
     if (async && !early) {  // (the point an asynchronous batch's neighbour formatting forks from)
         if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
-        HIPCHK(e, hipEventRecord(e->ex_ev, e->xg_pending ? e->xst : e->st));
+        HIPCHK(e, hipEventRecord(e->ex_ev, e->st));
     }
     if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
     // the process plugins' flows: SLOT_PLUGIN in the table before k_reduce folds the batch;
@@ -1017,12 +1000,10 @@ static int launch_rest(ipxg_engine* e, const BatchView& bv, Params p, const BinV
         else if (classify)
             HIPCHK(e, hipStreamWaitEvent(e->st, e->cls_join, 0));
         // the previous exports' IPFIX formatting ran beside k_bin; this batch's export writers
-        // (k_fin_list and the host paths after it) follow it -- and the previous batch's walk
-        // exports (join_fmt before k_fin_list: k_reduce appends none)
-        if ((rc = join_fmt(e, false))) return rc;
+        // (k_fin_list and the host paths after it) follow it
+        if ((rc = join_fmt(e))) return rc;
         launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
         if (!async) {
-            if ((rc = join_fmt(e))) return rc;
             ev_rec(e, 3);
             launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
             ev_rec(e, 4);
@@ -1132,9 +1113,7 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
         BinView bins = e->early.bins;
         if ((rc = ensure_export(e, n))) return rc;
         if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
-        // (after the previous batch's walk exports: their gather's stream, which followed the
-        // engine's stream up to it, when it has not been joined)
-        HIPCHK(e, hipEventRecord(e->ex_ev, e->xg_pending ? e->xst : e->st));
+        HIPCHK(e, hipEventRecord(e->ex_ev, e->st));  // (after the previous batch's walk exports)
         return launch_rest(e, bv, p, bins, n, true, true);
     }
     if ((rc = ensure_export(e, n))) return rc;
@@ -1574,10 +1553,6 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     }
     BatchCtl* const apply_ctl = e->early.launched ? e->aux_ctl_d : e->ctl_d;
     WALK_MARK(1);
-    if (e->xg_host) {  // the previous walk's exports may still be crossing from the units' buffers
-        HIPCHK(e, hipEventSynchronize(e->xev));
-        e->xg_host = false;
-    }
     while (e->hw_ex.size() < U) e->hw_ex.emplace_back(new ExportVec);
     const bool ports = e->pstat_d != nullptr;
     if (ports && e->host_ports.size() < T) e->host_ports.resize(T);
@@ -1740,7 +1715,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     // (the threads' records and exports are read by one kernel straight from their page-locked
     // buffers -- one launch instead of a copy command per thread and array, ~10 us each)
     HIPCHK(e, hipMemcpyAsync(o.hstate, fstate, (size_t)nf * 4, hipMemcpyHostToDevice, e->st));
-    auto gather = [&](auto pick, ipxg_flow_record* dst, uint32_t at0, uint32_t& moved, hipStream_t gs) -> int {
+    auto gather = [&](auto pick, ipxg_flow_record* dst, uint32_t at0, uint32_t& moved) -> int {
         HostChunks c;
         c.count = c.max_n = 0;
         uint32_t at = at0;
@@ -1756,47 +1731,35 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
                 c.count++;
             } else {  // (not page-locked: a copy command)
                 HIPCHK(e, hipMemcpyAsync(dst + at, x.data(), (size_t)k * sizeof(ipxg_flow_record),
-                                         hipMemcpyHostToDevice, gs));
+                                         hipMemcpyHostToDevice, e->st));
             }
             at += k;
         }
-        launch_host_gather(gs, c, dst);
+        launch_host_gather(e->st, c, dst);
         HIPCHK(e, hipGetLastError());
         moved = at - at0;
         return IPXG_OK;
     };
     uint32_t nout = 0;
     if ((rc = gather([&](unsigned u) -> const HostVec<ipxg_flow_record>& { return e->hw_ex[u]->orec; }, o.recs, 0,
-                     nout, e->st)))
+                     nout)))
         return rc;
     launch_plugin_apply(e->st, table_view(e), o.flows, o.hstate, nf, o.recs, nout, apply_ctl);
     HIPCHK(e, hipGetLastError());
     if (nx) {
         if ((rc = ensure_export(e, nx))) return rc;
-        // the units' exports onto the device on the export stream, beside what follows on the
-        // engine's stream (the next batch's k_plugin_marks and k_reduce): joined before the next
-        // export append or read (join_fmt), the units' buffers reused after it (above)
-        if (!e->xst) {
-            HIPCHK(e, hipStreamCreateWithFlags(&e->xst, hipStreamNonBlocking));
-            HIPCHK(e, hipEventCreateWithFlags(&e->xfork, hipEventDisableTiming));
-            HIPCHK(e, hipEventCreateWithFlags(&e->xev, hipEventDisableTiming));
-        }
-        HIPCHK(e, hipEventRecord(e->xfork, e->st));
-        HIPCHK(e, hipStreamWaitEvent(e->xst, e->xfork, 0));
         uint32_t moved = 0;
         if ((rc = gather([&](unsigned u) -> const HostVec<ipxg_flow_record>& { return wos[u].ex; }, e->ex, e->ex_count,
-                         moved, e->xst)))
+                         moved)))
             return rc;
         size_t at = e->ex_count + moved;
         for (unsigned u = 0; u < U; ++u) {  // what overflowed the units' buffers (REINSERT chains)
             const std::vector<ipxg_flow_record>& y = wos[u].spill;
             if (!y.empty())
                 HIPCHK(e, hipMemcpyAsync(e->ex + at, y.data(), y.size() * sizeof(ipxg_flow_record),
-                                         hipMemcpyHostToDevice, e->xst));
+                                         hipMemcpyHostToDevice, e->st));
             at += y.size();
         }
-        HIPCHK(e, hipEventRecord(e->xev, e->xst));
-        e->xg_pending = e->xg_host = true;
         uint32_t c3[3] = {e->ex_count + (uint32_t)nx, 0, e->ex_count6 + (uint32_t)wo.v6};
         HIPCHK(e, hipMemcpyAsync(e->ex_count_d, c3, sizeof(c3), hipMemcpyHostToDevice, e->st));
         e->ex_zero_pending = false;  // all three counters written
@@ -2265,8 +2228,6 @@ static int finish_impl(ipxg_engine* e) {
 int ipxg_reset(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     if (e->fst) (void)hipStreamSynchronize(e->fst);  // (the formatting in flight reads what reset clears)
-    if (e->xst) (void)hipStreamSynchronize(e->xst);  // (and the walk's export gather writes it)
-    e->xg_pending = e->xg_host = false;
     e->fmt_pending = false;
     if (e->failed) {  // a process plugin's failure: the lost batch's host state is dropped too
         e->failed = false;
@@ -2311,8 +2272,7 @@ static int pending_exports_impl(ipxg_engine* e, size_t* n) {
 static int poll_exports_impl(ipxg_engine* e, ipxg_flow_record* out, size_t cap, size_t* n) {
     if (!e || !n || (cap && !out)) return IPXG_EINVAL;
     {
-        int rc0 = complete_batch(e);
-        if (!rc0) rc0 = join_fmt(e);  // (the host walk's export gather)
+        const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
     size_t k = std::min<size_t>(cap, e->ex_count - e->ex_head);
@@ -2710,8 +2670,7 @@ int ipxg_poll_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, uint8_t* ou
 int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n) {
     if (!e || !dptr || !n) return IPXG_EINVAL;
     {
-        int rc0 = complete_batch(e);
-        if (!rc0) rc0 = join_fmt(e);  // (the records are complete on the engine's stream)
+        const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
     *dptr = e->ex + e->ex_head;
@@ -2722,8 +2681,7 @@ int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n
 static int clear_exports_impl(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     {
-        int rc0 = complete_batch(e);
-        if (!rc0) rc0 = join_fmt(e);  // (appends restart at 0: after the walk's export gather)
+        const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
     e->ex_head = e->ex_count = 0;
