@@ -616,10 +616,15 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 #ifndef IPXG_BIN_DA
 #define IPXG_BIN_DA 4
 #endif
+// (head distance 1 without tile aggregation: udp64 step -0.9 %, quic -0.7 % against 2; the
+// aggregating walk keeps 2: imix +0.7 % at 1 -- gpurun_out/var5, var6)
 #ifndef IPXG_BIN_HA
-#define IPXG_BIN_HA 2
+#define IPXG_BIN_HA 1
 #endif
-    constexpr int DA = IPXG_BIN_DA, HA = IPXG_BIN_HA;
+#ifndef IPXG_BIN_HA_AGG
+#define IPXG_BIN_HA_AGG 2
+#endif
+    constexpr int DA = IPXG_BIN_DA, HA = AGG ? IPXG_BIN_HA_AGG : IPXG_BIN_HA;
     static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
     const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
     ipxg_pkt_desc Dr[DA];
