@@ -615,6 +615,8 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="run the N > 1 step's export exchange (IPFIX streams to rank 0, shard.StreamGather) at any "
                          "N, world size 1 included: its cost on one GPU")
+    ap.add_argument("--prof-every", type=int, default=8,
+                    help="HIP events around k_bin / k_bin_slow on one timed batch of every N (roofline.avg_launch_ms)")
     ap.add_argument("--cpu-selftest", action="store_true",
                     help="no GPU: the N-rank launcher and the export exchange over gloo with synthetic streams "
                          "(tests/test_launcher.py)")
@@ -703,10 +705,11 @@ def main():
     verify = None
     if args.verify and rank == 0 and wl.finish:
         verify = verify_step(eng, wl, args.strict)
-    # timed region: HIP events around the ingest kernels only (k_bin, k_bin_slow); the
-    # every-stage events cost ~35 us of host time per step, so the stage breakdown comes from a
-    # separate pass below
-    eng.profile(3)
+    # timed region: HIP events around the ingest kernels only (k_bin, k_bin_slow), on one batch of
+    # every PROF_EVERY: each event record is a packet of its own on the engine's stream (~4-5 us of
+    # GPU time, tools/gapbench), so events on every batch added ~13 us to every udp64 step; the
+    # every-stage events come from a separate (untimed) pass below
+    eng.profile(3, every=args.prof_every)
     if gather is not None:
         torch.cuda.synchronize()
         gather.device_ms()
@@ -827,6 +830,9 @@ def main():
                          "algorithmic_bytes_per_launch": alg_launch,
                          "algorithmic_bytes_per_packet": round(alg_step / pk_step, 2),
                          "avg_launch_ms": round(kms, 4),
+                         "timed_launches": int(launches),
+                         "events": "HIP events on the engine's stream around k_bin (and k_bin_slow) of one timed batch "
+                                   "in every %d" % args.prof_every,
                          "ingest": {"kernels": "k_bin+k_bin_slow", "avg_ms": round(bin_ms + slow_ms, 4),
                                     "achieved": round(ingest_gbs, 1), "frac": round(ingest_gbs / HBM_PEAK_GBS, 4)},
                          "step": {"what": "algorithmic bytes of the step / the whole step (every kernel, host "

@@ -28,10 +28,11 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 5 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+#define IPXG_ABI_VERSION 6 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
                               3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
                               4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
-                              5: ipxg_timing gained plugin_overlapped */
+                              5: ipxg_timing gained plugin_overlapped
+                              6: ipxg_profile takes a sampling period */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -436,7 +437,9 @@ typedef struct ipxg_timing {
 int ipxg_probe_counters(ipxg_engine* eng, uint64_t* out);
 /* Event timing: 1 = every stage, 2 = the ingest kernel only (two events per batch, the
  * least host overhead), 3 = k_bin and k_bin_slow (three events), 0 = off; enabling also
- * zeroes the accumulators. */
+ * zeroes the accumulators.  ABI 6: bits 8..23 of `enable` = a period p -- the events are
+ * recorded on one batch of every p (0 or 1: every batch; each event record is a packet of its
+ * own on the engine's stream, ~4-5 us of GPU time on MI355X), and the timing counts those. */
 int ipxg_profile(ipxg_engine* eng, int enable);
 int ipxg_get_timing(ipxg_engine* eng, ipxg_timing* out);
 

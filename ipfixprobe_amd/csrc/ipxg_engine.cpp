@@ -126,7 +126,7 @@ struct ipxg_engine {
     // export buffer: records [ex_head, ex_count) are pending
     ipxg_flow_record* ex = nullptr;
     uint32_t ex_cap = 0;
-    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag, [2] IPv6 records (ctl block)
+    uint32_t* ex_count_d = nullptr;  // [0] count, [1] overflow flag, [2] IPv6 records (after the ctl blocks)
     // ipxg_clear_exports' zeroing of ex_count_d, deferred to the next device work on exports (the
     // next submit folds it into its control-block memset: one fill command per step, not two)
     bool ex_zero_pending = false;
@@ -135,9 +135,39 @@ struct ipxg_engine {
     bool ex6_valid = false;          // [2] counts exactly the records [0, ex_count) (ex_head == 0)
     bool count6_on = false;          // kernels keep [2]: switched on by the first IPFIX message call
     // control / stats
-    BatchCtl* ctl_d = nullptr;  // device block: BatchCtl, then ex_count_d's two words
-    BatchCtl* ctl_h = nullptr;  // host-mapped mirror of the whole block
+    // Control blocks, double-buffered: consecutive batches alternate (launch_front), so a batch's
+    // block stays intact until the host has read it while the next batch's front already runs
+    // (`pend`); one allocation [block 0][block 1][export counters].  A block is zeroed for its next
+    // batch by k_reduce of the batch on the other block (launch_rest), or by a fill when not.
+    BatchCtl* ctl_blk[2] = {nullptr, nullptr};
+    int cur = 0;                         // the block (and event set) of the batch being launched
+    bool blk_zero[2] = {false, false};   // zeroed on the stream since its last use
+    BatchCtl* ctl_d = nullptr;  // = ctl_blk[cur] (swapped while a pending batch is completed)
+    BatchCtl* ctl_h = nullptr;  // host-mapped mirror: BatchCtl, export counters, publish sequence word
     uint32_t* ctl_hd = nullptr;  // its device address
+    uint32_t pub_seq = 0;        // the last sequence number published
+    bool no_grow = false;        // ensure() refuses to reallocate (a front launched ahead: IPXG_EGROW)
+    // A/B knobs (environment, read at ipxg_create): IPXG_SYNC_FINISH=1 -- ipxg_finish waits for its
+    // batch as before round 5; IPXG_NO_AHEAD=1 -- ipxg_submit launches no front ahead
+    bool sync_finish = false, no_ahead = false;
+    // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
+    // the host has not read: completed by the next entry point (consume_pend) -- ipxg_submit of a
+    // device batch first launches its own front behind it, gated on that block (Params::gate_mode),
+    // so the device does not wait for the host between batches.
+    struct {
+        bool on = false;
+        uint32_t mode = GATE_NONE;   // GATE_BATCH, GATE_FIN_FUSED, GATE_FIN_GUARDED
+        bool clear_after = false;    // ipxg_clear_exports since: the batch's exports are dropped
+        int blk = 0;
+        uint32_t seq = 0;
+        BatchView bv;
+        Params p;
+        uint32_t n = 0;
+        BinView bins;                // its partition records (k_complex_gather_rec), bins_valid, part_bits_last
+        bool bins_valid = false;
+        uint32_t part_bits = 0;
+        bool spec_closed = false;    // (consume_pend's result) the front launched ahead returned at once
+    } pend;
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
     unsigned long long* pstat_d = nullptr;  // ps=true: TopPorts + VlanStats (PSTAT_WORDS)
@@ -242,6 +272,7 @@ struct ipxg_engine {
     // recorded by ipxg_submit before its first kernel: every export of the batches completed
     // before it is in place (an asynchronous batch's formatting forks from here, beside its kernels)
     hipEvent_t ex_ev = nullptr;
+    bool ex_ev_valid = false;  // recorded for the batch in flight (only while fst exists)
     uint8_t* plan_h = nullptr;                  // pinned staging of the plan (asynchronous upload)
     const uint64_t* ipf_counts = nullptr;       // device: {bytes, records} of the last message call
     size_t plan_h_bytes = 0;
@@ -268,7 +299,13 @@ struct ipxg_engine {
     // stage timing
     bool prof = false;
     int prof_level = 0;  // 1: every stage, 2: k_bin only, 3: k_bin and k_bin_slow
-    hipEvent_t ev[12] = {};
+    // events on one batch of every prof_every (ipxg_profile's period): each event record is a
+    // packet of its own on the stream (~4-5 us of GPU time, tools/gapbench), so the bench samples
+    uint32_t prof_every = 1;
+    uint64_t prof_seq = 0;
+    bool prof_set[2] = {false, false};  // the batch of event set k (= its control block) is sampled
+    hipEvent_t evs[2][12] = {};  // one set per control block (a pending batch keeps its events)
+    hipEvent_t* ev = evs[0];
     bool early_timed = false;  // the batch in flight had an early front: its k_reduce is timed from ev[11]
     ipxg_timing tm = {};
 };
@@ -278,10 +315,15 @@ static void free_walk_copies(ipxg_engine* e);
 // events: 0 | k_bin | 1 | k_bin_slow | 2 | k_reduce | 3 | k_fin_list | 4;
 //         [5,6] slow paths, [7,8] k_finalize, [9,10] finish; 11: k_reduce's start after an early
 //         front (2 was recorded during the previous batch's host walk)
+static bool prof_on(const ipxg_engine* e) { return e->prof && e->prof_set[e->ev == e->evs[1] ? 1 : 0]; }
+// a batch starts (its front, or a strict batch): sampled or not
+static void prof_begin_batch(ipxg_engine* e) {
+    e->prof_set[e->cur] = e->prof && (e->prof_seq++ % e->prof_every) == 0;
+}
 static void ev_rec(ipxg_engine* e, int i) {
     // level 2: only the events around k_bin / k_ingest (0, 1), level 3 also k_bin_slow (2):
     // the others cost host time
-    if (e->prof && (e->prof_level == 1 || i <= 1 || (e->prof_level == 3 && i == 2)))
+    if (prof_on(e) && (e->prof_level == 1 || i <= 1 || (e->prof_level == 3 && i == 2)))
         (void)hipEventRecord(e->ev[i], e->st);
 }
 static double ev_ms(ipxg_engine* e, int a, int b = -1) {
@@ -304,8 +346,12 @@ static int set_err(ipxg_engine* e, int code, const std::string& msg) {
     return code;
 }
 
+// (internal) a buffer would have to grow while ipxg_engine::no_grow is set
+constexpr int IPXG_EGROW = 100;
+
 static int ensure(ipxg_engine* e, DevBuf& b, size_t need) {
     if (b.bytes >= need && b.p) return IPXG_OK;
+    if (e->no_grow) return IPXG_EGROW;  // (a front launched ahead: the pending batch may still read it)
     size_t nb = std::max<size_t>(need, b.bytes + b.bytes / 2);
     if (nb < 256) nb = 256;
     if (b.p) HIPCHK(e, hipFree(b.p));
@@ -459,11 +505,14 @@ static int alloc_table(ipxg_engine* e, uint32_t cap, SlotLine** line, uint32_t**
     return IPXG_OK;
 }
 
-constexpr size_t CTL_EX_OFF = (sizeof(BatchCtl) + 15) & ~(size_t)15;  // ex_count_d inside the ctl block
-constexpr size_t CTL_BYTES = CTL_EX_OFF + 16;
+constexpr size_t CTL_EX_OFF = (sizeof(BatchCtl) + 15) & ~(size_t)15;  // a block's stride; the export words in the mirror
+constexpr size_t CTL_BYTES = CTL_EX_OFF + 32;  // the host mirror: block, export words, sequence word
 
 static const uint32_t* ex_host(const ipxg_engine* e) {
     return reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(e->ctl_h) + CTL_EX_OFF);
+}
+static volatile uint32_t* seq_host(const ipxg_engine* e) {
+    return reinterpret_cast<volatile uint32_t*>(reinterpret_cast<char*>(e->ctl_h) + CTL_EX_OFF + 16);
 }
 
 // Wait for the stream by polling: the blocking wait (interrupt) added tens of microseconds of
@@ -484,10 +533,33 @@ static int check_ex(ipxg_engine* e) {
 }
 
 // the control block and the export counter into host-mapped memory (a one-block kernel on
-// the stream: cheaper than a D2H copy command), then wait
-static int publish_ctl(ipxg_engine* e) {
-    launch_publish(e->st, reinterpret_cast<const uint32_t*>(e->ctl_d), e->ctl_hd, (uint32_t)(CTL_BYTES / 4));
+// the stream: cheaper than a D2H copy command); seq: with a sequence number the host polls
+static int publish_ctl(ipxg_engine* e, bool with_seq = false) {
+    uint32_t seq = 0;
+    if (with_seq) {
+        if (++e->pub_seq == 0) e->pub_seq = 1;  // (0: no sequence word)
+        seq = e->pub_seq;
+    }
+    launch_publish(e->st, reinterpret_cast<const uint32_t*>(e->ctl_d), e->ex_count_d, e->ctl_hd,
+                   (uint32_t)(CTL_EX_OFF / 4), seq);
     HIPCHK(e, hipGetLastError());
+    return IPXG_OK;
+}
+
+// Wait for the publish with sequence number `seq` (publish_ctl(e, true)) by polling its word in
+// host memory: the stream may hold more work behind it (a front launched ahead).  A device error
+// or a stream that drained without the word is reported, never waited on forever.
+static int wait_seq(ipxg_engine* e, uint32_t seq) {
+    volatile uint32_t* w = seq_host(e);
+    for (uint64_t k = 1;; ++k) {
+        if (*w == seq) break;
+        if ((k & 1023) == 0) {
+            const hipError_t r = hipStreamQuery(e->st);
+            if (r != hipSuccess && r != hipErrorNotReady) HIPCHK(e, r);
+            if (r == hipSuccess && *w != seq) return set_err(e, IPXG_EDEVICE, "control block publish never arrived");
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
     return IPXG_OK;
 }
 
@@ -618,6 +690,8 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->cfg = *cfg;
     e->walk_trace = std::getenv("IPXG_WALK_TRACE") != nullptr;
     e->walk_pin = std::getenv("IPXG_WALK_PAGEABLE") == nullptr;
+    e->sync_finish = std::getenv("IPXG_SYNC_FINISH") != nullptr && std::atoi(std::getenv("IPXG_SYNC_FINISH")) != 0;
+    e->no_ahead = std::getenv("IPXG_NO_AHEAD") != nullptr && std::atoi(std::getenv("IPXG_NO_AHEAD")) != 0;
     if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -642,8 +716,16 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->cap = cap;
     e->ex_cap = 1u << 16;
     if (hipMalloc((void**)&e->ex, (size_t)e->ex_cap * sizeof(ipxg_flow_record)) != hipSuccess) return fail(IPXG_ENOMEM);
-    if (hipMalloc((void**)&e->ctl_d, CTL_BYTES) != hipSuccess) return fail(IPXG_ENOMEM);
-    e->ex_count_d = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(e->ctl_d) + CTL_EX_OFF);
+    {
+        char* blk;
+        if (hipMalloc((void**)&blk, 2 * CTL_EX_OFF + 16) != hipSuccess) return fail(IPXG_ENOMEM);
+        e->ctl_blk[0] = reinterpret_cast<BatchCtl*>(blk);
+        e->ctl_blk[1] = reinterpret_cast<BatchCtl*>(blk + CTL_EX_OFF);
+        e->ex_count_d = reinterpret_cast<uint32_t*>(blk + 2 * CTL_EX_OFF);
+        e->ctl_d = e->ctl_blk[0];
+        if (hipMemsetAsync(blk, 0, 2 * CTL_EX_OFF + 16, e->st) != hipSuccess) return fail(IPXG_EDEVICE);
+        e->blk_zero[1] = true;  // (block 0 is the current one: never marked zero)
+    }
     if (hipHostMalloc((void**)&e->ctl_h, CTL_BYTES, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return fail(IPXG_ENOMEM);
     std::memset(e->ctl_h, 0, CTL_BYTES);
@@ -710,7 +792,7 @@ int ipxg_destroy(ipxg_engine* e) {
     hipFree(e->tail);
     hipFree(e->slot_rank);
     hipFree(e->ex);
-    hipFree(e->ctl_d);
+    hipFree(e->ctl_blk[0]);
     hipFree(e->aux_ctl_d);
     if (e->wst) (void)hipStreamDestroy(e->wst);
     if (e->ctl_h) hipHostFree(e->ctl_h);
@@ -738,8 +820,9 @@ int ipxg_destroy(ipxg_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : e->walk_ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : e->ev)
-        if (ev) (void)hipEventDestroy(ev);
+    for (auto& set : e->evs)
+        for (hipEvent_t ev : set)
+            if (ev) (void)hipEventDestroy(ev);
     for (DevBuf* b : {&e->stage_arena[0], &e->stage_arena[1], &e->stage_desc[0], &e->stage_desc[1], &e->rules_d, &e->pf_d, &e->pf_idx, &e->pf_wpk, &e->pf_off, &e->pf_bytes,
                       &e->pf_keys, &e->pf_flen, &e->pf_tmp, &e->pf_live, &e->pf_recs,
                       &e->arena, &e->desc, &e->defer_a, &e->defer_b, &e->adefer_a, &e->adefer_b, &e->frag_list,
@@ -785,16 +868,16 @@ static int launch_tail(ipxg_engine* e, bool finishing) {
     return IPXG_OK;
 }
 
-static int complete_batch_impl(ipxg_engine* e);
-// (every entry point completes the batch in flight first: no C++ exception leaves it, and a
-// failed engine completes nothing)
-static int complete_batch(ipxg_engine* e) {
+static int complete_batch_impl(ipxg_engine* e, bool spec);
+// (every entry point completes the batch in flight and the pending batch first: no C++ exception
+// leaves it, and a failed engine completes nothing).  spec: ipxg_submit launched its front ahead.
+static int complete_batch(ipxg_engine* e, bool spec = false) {
     if (e->failed)
         return set_err(e, IPXG_ESTATE, "engine stopped by a process plugin error (ipxg_reset or ipxg_destroy): " +
                                            e->fail_msg);
-    if (!e->inflight.on) return IPXG_OK;
+    if (!e->inflight.on && !e->pend.on) return IPXG_OK;
     try {
-        return complete_batch_impl(e);
+        return complete_batch_impl(e, spec);
     } catch (const std::bad_alloc&) {
         return set_err(e, IPXG_ENOMEM, "host allocation failed");
     } catch (...) {
@@ -802,14 +885,42 @@ static int complete_batch(ipxg_engine* e) {
     }
 }
 
-static int complete_batch_impl(ipxg_engine* e) {
-    if (!e->inflight.on) return IPXG_OK;
-    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+// The pending state of a batch whose last kernels are enqueued: its control block published with
+// a sequence number, completed later by consume_pend.
+static void set_pend(ipxg_engine* e, uint32_t mode, const BatchView& bv, const Params& p, uint32_t n) {
+    auto& q = e->pend;
+    q.on = true;
+    q.mode = mode;
+    q.clear_after = false;
+    q.blk = e->cur;
+    q.seq = e->pub_seq;
+    q.bv = bv;
+    q.p = p;
+    q.n = n;
+    q.bins = e->bins_last;
+    q.bins_valid = e->bins_valid;
+    q.part_bits = e->part_bits_last;
+    q.spec_closed = false;
+}
+
+// The in-flight asynchronous batch's end: its tail (k_fin_list) and its control block's publish
+// are enqueued, the host does not wait (the batch is pending until consume_pend).
+static int enqueue_batch_end(ipxg_engine* e) {
     int rc;
     if ((rc = launch_tail(e, false))) return rc;
     e->inflight.on = false;
-    if ((rc = sync_ctl(e))) return rc;
-    return post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, false);
+    if ((rc = publish_ctl(e, true))) return rc;
+    set_pend(e, GATE_BATCH, e->inflight.bv, e->inflight.p, e->inflight.n);
+    return IPXG_OK;
+}
+
+static int consume_pend(ipxg_engine* e, bool spec);
+
+static int complete_batch_impl(ipxg_engine* e, bool spec) {
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    int rc;
+    if (e->inflight.on && (rc = enqueue_batch_end(e))) return rc;
+    return consume_pend(e, spec);
 }
 
 // The fragmentation cache over the batch's nf listed fragments (fragmentationCache.cpp):
@@ -850,6 +961,7 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     // every record alive now plus every record this batch creates may leave during it
     if ((rc = ensure_export(e, (size_t)e->sv.slot_mask + 1 + n))) return rc;
     HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+    prof_begin_batch(e);
     ev_rec(e, 0);
     launch_strict_prep1(e->st, bv, p, frag_view(e), e->ctl_d, e->stats_d);
     HIPCHK(e, hipGetLastError());
@@ -902,7 +1014,7 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     HIPCHK(e, hipMemcpyAsync(&tail[1], keyed + n - 1, 4, hipMemcpyDeviceToHost, e->st));
     if ((rc = sync_ctl(e))) return rc;
     if (e->ctl_h->strict_fail) return set_err(e, IPXG_EDEVICE, "strict replay stalled (engine bug)");
-    if (e->prof) {
+    if (prof_on(e)) {
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
@@ -914,13 +1026,22 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     return IPXG_OK;
 }
 
-// The batch's front: per-batch scratch, the control block cleared, partitions sized, then k_bin and
-// k_bin_slow (binned) -- from ipxg_submit, or from the previous batch's host walk (early: its spills
-// deferred, Params::defer_spill; the export counters left alone -- ensure_export and ex_ev follow in
-// the rest).
+// The batch's front: per-batch scratch, its control block (the other of the two, cleared),
+// partitions sized, then k_bin and k_bin_slow (binned) -- from ipxg_submit, or from the previous
+// batch's host walk (early: its spills deferred, Params::defer_spill).  The export counters are
+// left alone (a pending clear rides on k_reduce, launch_rest).
+// ahead: launched before the host has read the pending batch's control block (ipxg_engine::pend):
+// the front's kernels test that block and return at once when the host has work left for it;
+// nothing is reallocated (IPXG_EGROW before anything is enqueued).  reuse_blk: the front again,
+// on the block of a front launched ahead that returned (consume_pend's spec_closed).
+struct Ahead {
+    uint32_t mode;         // pend.mode
+    const BatchCtl* prev;  // the pending batch's control block
+};
 static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool binned, bool async, bool early, Params& p,
-                        BinView& bins) {
+                        BinView& bins, const Ahead* ahead = nullptr, bool reuse_blk = false) {
     int rc;
+    // every allocation first (a front launched ahead enqueues nothing before it knows they fit)
     // per-batch scratch sized for the worst case (every packet deferred / a fragment)
     if ((rc = ensure(e, e->defer_a, (size_t)n * 4))) return rc;
     if ((rc = ensure(e, e->defer_b, (size_t)n * 4))) return rc;
@@ -931,26 +1052,47 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
         if ((rc = ensure(e, e->frag_list, (size_t)n * 8))) return rc;
         if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
     }
-    // the control block, and the export counters when a clear is pending (they follow it)
-    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, e->ex_zero_pending ? CTL_EX_OFF + 3 * sizeof(uint32_t) : sizeof(BatchCtl),
-                             e->st));
-    e->ex_zero_pending = false;
+    BinView nb = {};
+    if (binned) {
+        const uint32_t bits_before = e->part_bits_last;
+        if ((rc = setup_bins(e, n, nb))) return rc;
+        if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) {
+            e->part_bits_last = bits_before;
+            return rc;
+        }
+    }
+    // the batch's control block (and event set): the other one, which k_reduce of the batch on this
+    // one zeroed (blk_zero), else a fill; the current block is never marked zero
+    if (!reuse_blk) {
+        e->cur ^= 1;
+        e->ctl_d = e->ctl_blk[e->cur];
+        e->ev = e->evs[e->cur];
+    }
+    if (!e->blk_zero[e->cur]) HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
+    e->blk_zero[e->cur] = false;
 
     p = params(e);
     p.defer_spill = early ? 1u : 0u;
-    FragView fv = frag_view(e);
-    bins = {};
-    e->bins_valid = false;
-    if (binned) {
-        if ((rc = setup_bins(e, n, bins))) return rc;
-        e->bins_last = bins;
-        e->bins_valid = true;
-        if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) return rc;
+    if (ahead) {
+        p.gate_mode = ahead->mode;
+        p.prev_ctl = ahead->prev;
+        // behind a batch: the order check continues from its last packet (read on the device); behind
+        // a finish: none, as after every finish
+        p.prev_valid = p.prev_dev = ahead->mode == GATE_BATCH ? 1u : 0u;
     }
-    if (async && !early) {  // (the point an asynchronous batch's neighbour formatting forks from)
+    FragView fv = frag_view(e);
+    bins = nb;
+    e->bins_last = bins;
+    e->bins_valid = binned;
+    // (the point an asynchronous batch's neighbour formatting forks from: only once the engine
+    // formats on its own stream -- an event record is a stream packet of its own, ~5 us of GPU time)
+    e->ex_ev_valid = false;
+    if (async && !early && e->fst) {
         if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
         HIPCHK(e, hipEventRecord(e->ex_ev, e->st));
+        e->ex_ev_valid = true;
     }
+    prof_begin_batch(e);
     if (e->pstat_d) launch_pstats(e->st, bv, p, e->pstat_d);  // ahead of the timed stages
     // the process plugins' flows: SLOT_PLUGIN in the table before k_reduce folds the batch;
     // k_bin and k_bin_slow write partition records and, on a full segment, atomic slot updates
@@ -1002,7 +1144,15 @@ static int launch_rest(ipxg_engine* e, const BatchView& bv, Params p, const BinV
         // the previous exports' IPFIX formatting ran beside k_bin; this batch's export writers
         // (k_fin_list and the host paths after it) follow it
         if ((rc = join_fmt(e))) return rc;
-        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al);
+        // k_reduce also zeroes the other control block (its batch is complete: the host read it
+        // before this launch) for the next front, and the export counters of a pending clear
+        uint32_t* zx = nullptr;
+        if (e->ex_zero_pending) {
+            zx = e->ex_count_d;
+            e->ex_zero_pending = false;
+        }
+        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al, e->ctl_blk[e->cur ^ 1], zx);
+        e->blk_zero[e->cur ^ 1] = true;
         if (!async) {
             ev_rec(e, 3);
             launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
@@ -1073,7 +1223,29 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
         e->early.bv.base_sec = BASE_FROM_DESC0;
         e->early.n = n;
     }
-    rc = complete_batch(e);
+    // A device batch behind a batch or finish whose control block the host has not read: its front
+    // (k_bin, k_bin_slow) is launched first, gated on that block, and the host completes the pending
+    // batch while the front runs -- unless a buffer would have to grow (the pending batch may still
+    // read it) or process plugins are registered (their walk has the early front instead).
+    bool ahead = false;
+    Params p;
+    BinView bins = {};
+    if (dev_batch && async && binned && !e->strict && e->plugins.empty() && !e->failed && !e->no_ahead &&
+        (e->inflight.on || e->pend.on)) {
+        if (e->inflight.on && (rc = enqueue_batch_end(e))) return rc;
+        BatchView abv = bv;
+        abv.arena = batch->arena;
+        abv.desc = batch->desc;
+        abv.base_sec = BASE_FROM_DESC0;
+        const Ahead ah{e->pend.mode, e->ctl_blk[e->pend.blk]};
+        e->no_grow = true;
+        rc = launch_front(e, abv, n, true, true, false, p, bins, &ah);
+        e->no_grow = false;
+        if (rc == IPXG_EGROW) rc = IPXG_OK;  // (nothing enqueued: the front follows the completion)
+        else if (rc) return rc;
+        else ahead = true;
+    }
+    rc = complete_batch(e, ahead);
     e->early.want = false;
     if (rc) {
         e->early.launched = false;
@@ -1096,6 +1268,13 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
         bv.desc = (const ipxg_pkt_desc*)e->desc.p;
     }
     bv.base_sec = BASE_FROM_DESC0;  // kernels read desc[0] themselves (no host round trip)
+    if (ahead) {
+        e->early_timed = false;
+        // the gate was closed (the pending batch needed the host): its kernels returned at once
+        if (e->pend.spec_closed && (rc = launch_front(e, bv, n, true, true, false, p, bins, nullptr, true))) return rc;
+        if ((rc = ensure_export(e, n))) return rc;
+        return launch_rest(e, bv, p, bins, n, true, true);
+    }
     if (e->strict) {
         if (e->ex_zero_pending) {
             e->ex_zero_pending = false;
@@ -1109,17 +1288,19 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
         e->early.launched = false;
         e->early_timed = true;
         ev_rec(e, 11);
-        Params p = e->early.p;
-        BinView bins = e->early.bins;
+        p = e->early.p;
+        bins = e->early.bins;
         if ((rc = ensure_export(e, n))) return rc;
-        if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
-        HIPCHK(e, hipEventRecord(e->ex_ev, e->st));  // (after the previous batch's walk exports)
+        e->ex_ev_valid = false;
+        if (e->fst) {
+            if (!e->ex_ev) HIPCHK(e, hipEventCreateWithFlags(&e->ex_ev, hipEventDisableTiming));
+            HIPCHK(e, hipEventRecord(e->ex_ev, e->st));  // (after the previous batch's walk exports)
+            e->ex_ev_valid = true;
+        }
         return launch_rest(e, bv, p, bins, n, true, true);
     }
     if ((rc = ensure_export(e, n))) return rc;
     e->early_timed = false;
-    Params p;
-    BinView bins = {};
     if ((rc = launch_front(e, bv, n, binned, async, false, p, bins))) return rc;
     return launch_rest(e, bv, p, bins, n, binned, async);
 }
@@ -1889,8 +2070,6 @@ static void take_batch_knobs(ipxg_engine* e, const BatchCtl& c2, const Params& p
     e->prev_usec = c2.last_usec;
 }
 
-static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool binned, bool async, bool early, Params& p,
-                        BinView& bins);
 
 // The next batch's front from inside this batch's host walk (ipxg_engine::early), once the walk's
 // input has been copied out: the device state the walk still changes is the walked flows' slots
@@ -1917,7 +2096,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     int rc;
     FragView fv = frag_view(e);
     const BatchCtl c1 = *e->ctl_h;
-    if (e->prof) {
+    if (prof_on(e)) {
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
@@ -1985,7 +2164,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     if (slow) {
         ev_rec(e, 6);
         HIPCHK(e, hipStreamSynchronize(e->st));
-        if (e->prof && e->prof_level == 1) {
+        if (prof_on(e) && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
         }
@@ -2000,7 +2179,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ev_rec(e, 8);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
-        if (e->prof && e->prof_level == 1) {
+        if (prof_on(e) && e->prof_level == 1) {
             e->tm.finalize_ms += ev_ms(e, 7);
             e->tm.finalize_launches++;
         }
@@ -2081,7 +2260,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
                 if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
             }
         }
-        if (e->prof && e->prof_level == 1) {
+        if (prof_on(e) && e->prof_level == 1) {
             e->tm.slow_ms += ev_ms(e, 5);
             e->tm.slow_launches++;
         }
@@ -2149,10 +2328,109 @@ static int expire_impl(ipxg_engine* e, int64_t now_sec) {
     return IPXG_OK;
 }
 
+// The finish proper: every live record exported FORCED by a table scan (k_finish), which also
+// empties the table (cache.cpp:276-288).
+static int finish_table(ipxg_engine* e) {
+    int rc;
+    if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
+    ev_rec(e, 9);
+    launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);  // also empties the table
+    HIPCHK(e, hipGetLastError());
+    ev_rec(e, 10);
+    if ((rc = sync_ctl(e))) return rc;
+    if (prof_on(e) && e->prof_level == 1) {
+        e->tm.finish_ms += ev_ms(e, 9);
+        e->tm.finish_launches++;
+    }
+    e->keys = e->live = 0;
+    e->prev_valid = false;
+    return IPXG_OK;
+}
+
+// Completes the pending batch (or finish): waits for its control block's publish (the sequence
+// word, not the stream: a front launched ahead may be queued behind it), then does what the host
+// does after the batch's kernels -- post_batch; for a finish, the flows its fused k_fin_list left or
+// its guarded k_finish held back -- on the batch's own control block and event set.  spec: ipxg_submit
+// launched the next batch's front ahead, gated on this block; pend.spec_closed then says that the
+// gate was closed (that front returned at once and must be launched again).
+static int consume_pend(ipxg_engine* e, bool spec) {
+    auto& q = e->pend;
+    if (!q.on) return IPXG_OK;
+    q.on = false;
+    int rc;
+    if ((rc = wait_seq(e, q.seq))) return rc;
+    const int now = e->cur;
+    const BinView bins_now = e->bins_last;
+    const bool valid_now = e->bins_valid;
+    const uint32_t bits_now = e->part_bits_last;
+    const bool swapped = now != q.blk;  // (a front launched ahead switched blocks)
+    if (swapped) {
+        e->cur = q.blk;
+        e->ctl_d = e->ctl_blk[q.blk];
+        e->ev = e->evs[q.blk];
+    }
+    e->bins_last = q.bins;
+    e->bins_valid = q.bins_valid;
+    e->part_bits_last = q.part_bits;
+    q.spec_closed = spec && gate_closed(*e->ctl_h, q.mode);
+    rc = check_ex(e);
+    if (!rc) {
+        if (q.mode == GATE_BATCH) {
+            rc = post_batch(e, q.bv, q.p, q.n, true, false);
+        } else if (q.mode == GATE_FIN_FUSED) {
+            // k_fin_list exported what it finalised: complete unless it could not fuse (host work)
+            // or left complex flows
+            const bool done = e->ctl_h->fused && !e->ctl_h->complex_count && !e->ctl_h->fin_deferred;
+            rc = post_batch(e, q.bv, q.p, q.n, true, true);
+            if (!rc && done) {
+                e->keys = e->live = 0;
+                e->prev_valid = false;
+            } else if (!rc) {
+                rc = finish_table(e);  // the remaining flows
+            }
+        } else {  // GATE_FIN_GUARDED: k_finish right behind the batch, unless its guard held it
+            const bool held = e->ctl_h->hold != 0;
+            rc = hipMemsetAsync(&e->ctl_d->hold, 0, sizeof(uint32_t), e->st) == hipSuccess ? IPXG_OK
+                     : set_err(e, IPXG_EDEVICE, "hipMemsetAsync failed");
+            if (!rc) rc = post_batch(e, q.bv, q.p, q.n, true, !held);
+            if (!rc && !held) {
+                if (prof_on(e) && e->prof_level == 1) {
+                    e->tm.finish_ms += ev_ms(e, 9);
+                    e->tm.finish_launches++;
+                }
+                e->keys = e->live = 0;
+                e->prev_valid = false;
+            } else if (!rc) {
+                rc = finish_table(e);  // the batch is complete now: finish normally
+            }
+        }
+    }
+    if (swapped) {
+        e->cur = now;
+        e->ctl_d = e->ctl_blk[now];
+        e->ev = e->evs[now];
+    }
+    if (spec && !q.spec_closed) {  // (closed: the front is launched again and sets them)
+        e->bins_last = bins_now;
+        e->bins_valid = valid_now;
+        e->part_bits_last = bits_now;
+    }
+    if (q.clear_after) {  // ipxg_clear_exports after this batch: its exports (and the follow-ups') dropped
+        e->ex_count = e->ex_head = 0;
+        e->ex6_valid = e->count6_on;
+        e->ex_zero_pending = true;
+    }
+    return rc;
+}
+
 static int finish_impl(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (e->pend.on) {  // a batch or finish still pending
+        if (e->failed) return complete_batch(e);  // (IPXG_ESTATE)
+        if ((rc = consume_pend(e, false))) return rc;
+    }
     if ((rc = join_fmt(e))) return rc;
     if (e->strict) {  // finish (cache.cpp:276-288): every record FORCED
         if ((rc = ensure_export(e, e->live))) return rc;
@@ -2169,8 +2447,11 @@ static int finish_impl(ipxg_engine* e) {
         // The batch's k_fin_list is still to be launched: into a table that was empty before
         // the batch, it exports what it finalises itself (fused finish, no table scan).
         // Otherwise the finish is enqueued right behind the batch, guarded on the device
-        // (k_finish's guard).  Either way one host round trip for batch + finish when the batch
-        // needs nothing from the host.
+        // (k_finish's guard).  Either way the host does not wait: the finish is pending (its
+        // control block published with a sequence number) and the next call completes it --
+        // ipxg_submit of a device batch after launching that batch's front behind it, so the
+        // device runs step after step without waiting for the host (workers.cpp:66-122: the
+        // reference's storage loop does not block between blocks either).
         const bool fuse = e->inflight.tail && e->live == 0 && e->keys == 0;
         if ((rc = launch_tail(e, fuse))) return rc;
         if (!fuse) {
@@ -2182,47 +2463,12 @@ static int finish_impl(ipxg_engine* e) {
         // the batch is consumed here whatever happens next: an error below must not make the
         // next call run post_batch again on a table k_finish may already have emptied
         e->inflight.on = false;
-        if ((rc = publish_ctl(e))) return rc;
-        HIPCHK(e, stream_wait(e->st));
-        if ((rc = check_ex(e))) return rc;
-        if (fuse) {
-            // complete unless k_fin_list could not fuse (host work) or left complex flows
-            const bool done = e->ctl_h->fused && !e->ctl_h->complex_count && !e->ctl_h->fin_deferred;
-            if ((rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, true))) return rc;
-            if (done) {
-                e->keys = e->live = 0;
-                e->prev_valid = false;
-                return IPXG_OK;
-            }
-            // the remaining flows: the finish below
-        }
-        const bool held = !fuse && e->ctl_h->hold != 0;
-        if (!fuse) HIPCHK(e, hipMemsetAsync(&e->ctl_d->hold, 0, sizeof(uint32_t), e->st));
-        if (!fuse && (rc = post_batch(e, e->inflight.bv, e->inflight.p, e->inflight.n, true, !held))) return rc;
-        if (!fuse && !held) {
-            if (e->prof && e->prof_level == 1) {
-                e->tm.finish_ms += ev_ms(e, 9);
-                e->tm.finish_launches++;
-            }
-            e->keys = e->live = 0;
-            e->prev_valid = false;
-            return IPXG_OK;
-        }
-        // the guard held k_finish back: the batch is complete now, finish normally
+        if ((rc = publish_ctl(e, true))) return rc;
+        set_pend(e, fuse ? GATE_FIN_FUSED : GATE_FIN_GUARDED, e->inflight.bv, e->inflight.p, e->inflight.n);
+        if (e->sync_finish) return consume_pend(e, false);
+        return IPXG_OK;
     }
-    if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
-    ev_rec(e, 9);
-    launch_finish(e->st, table_view(e), e->cap, export_view(e), e->stats_d);  // also empties the table
-    HIPCHK(e, hipGetLastError());
-    ev_rec(e, 10);
-    if ((rc = sync_ctl(e))) return rc;
-    if (e->prof && e->prof_level == 1) {
-        e->tm.finish_ms += ev_ms(e, 9);
-        e->tm.finish_launches++;
-    }
-    e->keys = e->live = 0;
-    e->prev_valid = false;
-    return IPXG_OK;
+    return finish_table(e);
 }
 
 int ipxg_reset(ipxg_engine* e) {
@@ -2607,9 +2853,10 @@ int ipxg_device_ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const uin
         HIPCHK(e, hipEventCreateWithFlags(&e->fmt_fork, hipEventDisableTiming));
         HIPCHK(e, hipEventCreateWithFlags(&e->fmt_done, hipEventDisableTiming));
     }
-    if (beside) {  // from the in-flight batch's start: not behind its kernels
+    if (beside && e->ex_ev_valid) {  // from the in-flight batch's start: not behind its kernels
         HIPCHK(e, hipStreamWaitEvent(e->fst, e->ex_ev, 0));
-    } else {
+    } else {  // (beside without ex_ev -- the first call, fst did not exist at the submit: behind the
+              // batch's k_bin / k_reduce, which append no export, so the same exports are formatted)
         HIPCHK(e, hipEventRecord(e->fmt_fork, e->st));
         HIPCHK(e, hipStreamWaitEvent(e->fst, e->fmt_fork, 0));
     }
@@ -2680,6 +2927,15 @@ int ipxg_device_exports(ipxg_engine* e, const ipxg_flow_record** dptr, size_t* n
 
 static int clear_exports_impl(ipxg_engine* e) {
     if (!e) return IPXG_EINVAL;
+    if (e->pend.on && !e->inflight.on && !e->failed) {
+        // a finish (or batch) still pending: its exports are dropped when it completes (and what its
+        // completion exports after it), without waiting for it here
+        e->pend.clear_after = true;
+        e->ex_head = e->ex_count = 0;
+        e->ex6_valid = e->count6_on;
+        e->ex_zero_pending = true;
+        return IPXG_OK;
+    }
     {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
@@ -2812,11 +3068,17 @@ int ipxg_profile(ipxg_engine* e, int enable) {
         if (rc0) return rc0;
     }
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
-    if (enable && !e->ev[0])
-        for (hipEvent_t& ev : e->ev) HIPCHK(e, hipEventCreate(&ev));
-    e->prof = enable != 0;
-    e->prof_level = (enable == 2 || enable == 3) ? enable : (enable ? 1 : 0);
-    if (enable) e->tm = ipxg_timing{};
+    if ((enable & 0xFF) && !e->evs[0][0])
+        for (auto& set : e->evs)
+            for (hipEvent_t& ev : set) HIPCHK(e, hipEventCreate(&ev));
+    const int level = enable & 0xFF;
+    const uint32_t every = ((uint32_t)enable >> 8) & 0xFFFFu;
+    e->prof = level != 0;
+    e->prof_level = (level == 2 || level == 3) ? level : (level ? 1 : 0);
+    e->prof_every = every ? every : 1;
+    e->prof_seq = 0;
+    e->prof_set[0] = e->prof_set[1] = false;
+    if (level) e->tm = ipxg_timing{};
     return IPXG_OK;
 }
 

@@ -551,6 +551,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG 
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     static_assert(!PLUG || WIDE, "the plugin check reads the wide walk's window");
+    if (gated(p)) return;  // launched ahead of the host's reading of the previous batch, which needs it
     __shared__ uint32_t hist[KBIN_PMAX];  // 8 KiB: per-partition rank / run start
     __shared__ uint32_t fill[KBIN_PMAX];  // 8 KiB: slots in the block's segments
     __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: tile hash keys, then the slots by partition
@@ -582,7 +583,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     b.base_sec = base_sec;
     const uint32_t P = 1u << bv.part_bits, pmask = P - 1;
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
-    const uint64_t ts_before = ((uint64_t)p.prev_sec << 32) | p.prev_usec;
+    const uint64_t ts_before = p.prev_dev ? ((uint64_t)p.prev_ctl->last_sec << 32) | p.prev_ctl->last_usec
+                                          : ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
     uint32_t spilled = 0, walked = 0, tb_or = 0;
     constexpr bool XP = IPXG_BIN_XPOSE && !WIDE;
@@ -898,6 +900,7 @@ template <bool AGG>
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
                 const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
+    if (gated(p)) return;  // (k_bin returned too)
     // the header columns (parse), the tile hash and the tile's slots (emit) are never live
     // together: one 32 KiB area; 76 KiB in all with aggregation (2 workgroups per CU), 48 KiB
     // without (3 per CU)
@@ -1200,7 +1203,8 @@ __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, Batc
 // k_bin_slow workgroup (bv.count gives their lengths); a prefix sum over the segment lengths
 // in LDS maps the partition's record k to its segment.
 __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
-                                                        uint32_t* deferred_list, uint4* agg_list) {
+                                                        uint32_t* deferred_list, uint4* agg_list, BatchCtl* zero_ctl,
+                                                        uint32_t* zero_ex) {
     __shared__ FlowAgg ht[RED_ENTRIES];  // 112 KiB
     __shared__ uint32_t pre[RED_MAX_COLS + 1];
     __shared__ uint32_t ne[RED_MAX_COLS];  // non-empty segments
@@ -1209,6 +1213,11 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __shared__ uint32_t fin_base;
     const uint32_t part = blockIdx.x;
     const uint32_t tid = threadIdx.x;
+    if (part == 0) {  // the other control block for the next batch, the cleared export counters
+        if (zero_ctl)
+            for (uint32_t w = tid; w < sizeof(BatchCtl) / 4; w += RED_THREADS) reinterpret_cast<uint32_t*>(zero_ctl)[w] = 0;
+        if (zero_ex && tid < 3) zero_ex[tid] = 0;
+    }
     // the columns written: every k_bin workgroup's, and those of the k_bin_slow workgroups
     // that had slow packets (the others return without writing theirs)
     const uint32_t cols = bv.cols;
@@ -1482,9 +1491,9 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 }
 
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
-                   uint32_t* deferred_list, uint4* agg_list) {
+                   uint32_t* deferred_list, uint4* agg_list, BatchCtl* zero_ctl, uint32_t* zero_ex) {
     hipLaunchKernelGGL(k_reduce, dim3(1u << bv.part_bits), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list,
-                       deferred_list, agg_list);
+                       deferred_list, agg_list, zero_ctl, zero_ex);
 }
 
 // ---- finalisation of the flows k_reduce completed -----------------------------------------

@@ -587,14 +587,25 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     if (threadIdx.x < 6 && pb[threadIdx.x]) atomicAdd(&sh[ST_PKTS_1 + threadIdx.x], (unsigned long long)pb[threadIdx.x]);
 }
 
-// Copy the control block (+ export counter) into host-mapped memory: the host reads it after
-// the stream has drained, without a D2H copy command of its own.
-__global__ __launch_bounds__(64) void k_publish(const uint32_t* src, uint32_t* dst, uint32_t words) {
-    for (uint32_t i = threadIdx.x; i < words; i += 64) dst[i] = src[i];
+// Copy a control block and the export counters into host-mapped memory, without a D2H copy
+// command of its own: [ctl_words of the block][4 export words][sequence word].  seq != 0: the
+// sequence word is written last, behind a system-scope fence of every lane's copies -- the host
+// polls it instead of waiting for the stream to drain (work queued behind this kernel keeps
+// running: ipxg_engine.cpp wait_seq).
+__global__ __launch_bounds__(64) void k_publish(const uint32_t* ctl, const uint32_t* ex, uint32_t* dst,
+                                                uint32_t ctl_words, uint32_t seq) {
+    for (uint32_t i = threadIdx.x; i < ctl_words; i += 64) dst[i] = ctl[i];
+    if (threadIdx.x < 4) dst[ctl_words + threadIdx.x] = ex[threadIdx.x];
+    if (seq) {
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&dst[ctl_words + 4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words) {
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, src, dst, words);
+void launch_publish(hipStream_t st, const uint32_t* ctl, const uint32_t* ex, uint32_t* dst, uint32_t ctl_words,
+                    uint32_t seq) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ctl, ex, dst, ctl_words, seq);
 }
 
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
@@ -729,6 +740,7 @@ __device__ __forceinline__ void vs_flush(uint32_t vid, const uint32_t (&acc)[VS_
 }
 
 __global__ __launch_bounds__(256) void k_pstats(BatchView b, Params p, unsigned long long* pstat) {
+    if (gated(p)) return;  // (a front launched ahead of the previous batch's completion: as k_bin)
     __shared__ uint32_t win[IPXG_WIN_DW * 256];
     __shared__ uint32_t vkey[64];
     __shared__ uint32_t vacc[64][VS_N];

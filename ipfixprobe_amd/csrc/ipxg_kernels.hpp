@@ -158,7 +158,31 @@ struct Params {
     uint32_t plug_nport, plug_npref;
     uint32_t plug_port[16];
     uint32_t plug_pref[16], plug_pmask[16], plug_pinfo[16];
+    // A front launched before the host has read the previous batch's control block (ipxg_submit
+    // right behind an asynchronous batch or ipxg_finish, ipxg_engine.cpp `pend`): k_bin, k_bin_slow
+    // and k_pstats first test that block (complete on the device: stream order) and return at once,
+    // writing nothing, when the host has work left for that batch (gate_closed); prev_dev: the order
+    // check's previous timestamp is that block's last_sec / last_usec, not prev_sec / prev_usec.
+    const BatchCtl* prev_ctl;
+    uint32_t gate_mode;  // GATE_NONE: no gate
+    uint32_t prev_dev;
 };
+
+// What the host still has to do for a batch after its last kernel, from its control block:
+// fragments, deferred packets or aggregates, the table scan, complex flows, a finalise-list
+// retry, a plugin slot failure or a fired guard -- and for a finish, the flows it left (GATE_FIN_*).
+// The host (consume_pend) and the gated kernels evaluate the same function on the same block.
+enum GateMode : uint32_t { GATE_NONE = 0, GATE_BATCH = 1, GATE_FIN_FUSED = 2, GATE_FIN_GUARDED = 3 };
+__host__ __device__ inline bool gate_closed(const BatchCtl& c, uint32_t mode) {
+    const bool work = c.frag_count || c.deferred || c.agg_deferred || c.pending || c.complex_count ||
+                      c.fin_deferred || c.plugin_fail || c.guard;
+    if (mode == GATE_FIN_FUSED) return work || !c.fused;
+    if (mode == GATE_FIN_GUARDED) return work || c.hold;
+    return work;
+}
+__device__ __forceinline__ bool gated(const Params& p) {
+    return p.gate_mode != GATE_NONE && gate_closed(*p.prev_ctl, p.gate_mode);
+}
 constexpr uint32_t PLUG_PREFIX = 4;
 
 // ---- strict mode (ipxg_strict.hip): the reference's line table -------------------------------
@@ -303,9 +327,13 @@ void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                      BatchCtl* ctl, const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                      unsigned long long* stats);
-// fin_list: the merged images of the slots k_reduce completed (HotSlot::pad = slot index)
+// fin_list: the merged images of the slots k_reduce completed (HotSlot::pad = slot index).
+// zero_ctl (or null): the other control block, zeroed by workgroup 0 for the next batch's front
+// (the host has read it); zero_ex (or null): the export counters, zeroed (ipxg_clear_exports) --
+// both ride on this kernel instead of a fill command of their own.
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
-                   uint32_t* deferred_list, uint4* agg_list);
+                   uint32_t* deferred_list, uint4* agg_list, BatchCtl* zero_ctl = nullptr,
+                   uint32_t* zero_ex = nullptr);
 constexpr uint32_t FIN_UNRESOLVED = 0xFFFFFFFFu;  // a finalise-list entry's pad: the flow's slot not probed yet
 constexpr uint32_t FIN_DEFERRED = 0xFFFFFFFEu;    // ... its probe failed (table full): again after a rehash
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
@@ -391,7 +419,8 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
                    ExportView ex, unsigned long long* stats);
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
                    BatchCtl* guard = nullptr, uint32_t ex_before = 0, uint32_t live_before = 0);
-void launch_publish(hipStream_t st, const uint32_t* src, uint32_t* dst, uint32_t words);
+void launch_publish(hipStream_t st, const uint32_t* ctl, const uint32_t* ex, uint32_t* dst, uint32_t ctl_words,
+                    uint32_t seq);
 void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,
                         uint8_t* out, uint64_t* offsets);
 // IPFIX message plan (host, ipxg_engine.cpp): data sets in rank order per class (class 0 = the

@@ -448,8 +448,10 @@ class Engine:
         self._check(lib().ipxg_top_ports(self._h, n, out.ctypes.data, ctypes.byref(got)), "ipxg_top_ports")
         return out[:got.value]
 
-    def profile(self, enable=True):
-        self._check(lib().ipxg_profile(self._h, int(enable)), "ipxg_profile")
+    def profile(self, enable=True, every=1):
+        """HIP-event stage timing (ipxg_profile): level 1/2/3 (True = 1), on one batch of every
+        `every` (each event record costs the stream a packet of its own)."""
+        self._check(lib().ipxg_profile(self._h, int(enable) | (int(every) << 8)), "ipxg_profile")
 
     def timing(self):
         t = Timing()

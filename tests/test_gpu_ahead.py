@@ -1,0 +1,133 @@
+"""Fronts launched ahead (round 5): ipxg_submit of a device batch behind a batch or ipxg_finish whose
+control block the host has not read launches its k_bin / k_bin_slow first, gated on that block
+(Params::gate_mode): when the pending batch needs the host (fragments, complex flows, deferrals)
+the gated kernels return at once and the front is launched again after the host's work.  ipxg_finish
+returns without waiting; the next call completes it, and ipxg_clear_exports behind it drops its
+exports when it completes.  Records must equal the oracle's whichever way the gate goes."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(__file__))
+
+import flowcmp  # noqa: E402
+import oracle_py  # noqa: E402
+import synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(arena, desc):
+    import torch
+    a = torch.from_numpy(np.ascontiguousarray(arena)).cuda()
+    d = torch.from_numpy(np.ascontiguousarray(desc).view(np.uint8).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    return a, d
+
+
+def _steps():
+    """Six independent steps: plain, fragments (its completion needs the host: the next step's
+    front launched ahead finds the gate closed), v6/VLAN, plain, fragments, plain."""
+    out = []
+    for k in range(6):
+        a, d = synth.flow_stream(seed=60 + k, n_flows=150 + 20 * k, n_pkts=3000 + 400 * k,
+                                 frag=k in (1, 4)).batch()
+        out.append((a, d))
+    return out
+
+
+@pytest.mark.parametrize("clear_every", [0, 2])
+def test_cold_steps_back_to_back(clear_every):
+    """The bench's cold step (submit async device batch, finish, clear / poll) repeated with
+    different batches: every polled step's records are exactly that batch's oracle records; a
+    cleared step leaves nothing behind in the next poll."""
+    from ipfixprobe_amd import Engine
+    steps = _steps()
+    dev = [_dev(a, d) for a, d in steps]
+    with Engine() as e:
+        for k, ((a, d), (da, dd)) in enumerate(zip(steps, dev)):
+            e.submit(da, dd, device=True, asynchronous=True)
+            e.finish()
+            if clear_every and k % clear_every == 0:
+                e.clear_exports()
+                continue
+            got = e.poll()
+            want, _ = oracle_py.run_capture(a, d, 1, cache_exp=20)
+            diff = flowcmp.diff(got, want)
+            assert not diff, "step %d: %s" % (k, diff)
+        st = e.stats()
+    assert st["batches"] == len(steps)
+
+
+def test_cleared_finish_that_needs_the_host():
+    """i=1: every flow is complex, so the fused finish leaves them and its completion exports
+    them through the sequential path and k_finish -- after ipxg_clear_exports was called
+    behind it; those exports are dropped too, and the next step's are intact."""
+    from ipfixprobe_amd import Engine
+    (a1, d1), (a2, d2) = [synth.flow_stream(seed=70 + k, n_flows=90, n_pkts=2500, frag=False).batch()
+                          for k in range(2)]
+    want, _ = oracle_py.run_capture(a2, d2, 1, cache_exp=20, inactive=1)
+    da1, dd1 = _dev(a1, d1)
+    da2, dd2 = _dev(a2, d2)
+    with Engine("i=1") as e:
+        e.submit(da1, dd1, device=True, asynchronous=True)
+        e.finish()
+        e.clear_exports()
+        e.submit(da2, dd2, device=True, asynchronous=True)
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert st["complex_flows"] > 0
+    diff = flowcmp.diff(got, want)
+    assert not diff, diff
+
+
+def test_order_check_across_batches_ahead():
+    """A batch whose first packet is earlier than the previous batch's last one: the order check
+    of a front launched ahead reads the previous timestamp from the pending batch's control block
+    (Params::prev_dev) -- the batch goes to the sequential path and the records are the oracle's
+    (which replays the packets in the given order)."""
+    a, d = synth.flow_stream(seed=80, n_flows=120, n_pkts=4000, frag=False).batch()
+    d = d.copy()
+    # batch 2 (packets 1000..1999) starts 5 s before batch 1 ends
+    d["ts_sec"][1000:2000] -= 5
+    want, _ = oracle_py.run_capture(a, d, 1, cache_exp=20)
+    from ipfixprobe_amd import Engine
+    da, _ = _dev(a, d)
+    keep = []
+    with Engine() as e:
+        for s in range(0, len(d), 1000):
+            _, dd = _dev(a, d[s:s + 1000])
+            keep.append(dd)
+            e.submit(da, dd, device=True, asynchronous=True)
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert st["complex_flows"] > 0
+    diff = flowcmp.diff(got, want)
+    assert not diff, diff
+
+
+def test_no_ahead_knob_gives_the_same_records(monkeypatch):
+    """IPXG_NO_AHEAD=1 / IPXG_SYNC_FINISH=1 (A/B knobs): the same records as the default path."""
+    from ipfixprobe_amd import Engine
+    steps = _steps()[:3]
+    outs = []
+    for env in ({}, {"IPXG_NO_AHEAD": "1", "IPXG_SYNC_FINISH": "1"}):
+        for k in ("IPXG_NO_AHEAD", "IPXG_SYNC_FINISH"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        got = []
+        with Engine() as e:
+            for a, d in steps:
+                da, dd = _dev(a, d)
+                e.submit(da, dd, device=True, asynchronous=True)
+                e.finish()
+                got.append(e.poll())
+        outs.append(got)
+    for x, y in zip(*outs):
+        diff = flowcmp.diff(x, y)
+        assert not diff, diff
