@@ -32,7 +32,8 @@ extern "C" {
                               3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
                               4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
                               5: ipxg_timing gained plugin_overlapped
-                              6: ipxg_profile takes a sampling period */
+                              6: ipxg_profile takes a sampling period; ipxg_timing gained
+                                 slow_redos */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -430,6 +431,9 @@ typedef struct ipxg_timing {
                                     for packets handed to process plugins)                    */
     uint64_t plugin_overlapped;  /* IPXG_BATCH_ASYNC device batches whose k_bin / k_bin_slow ran
                                     during the previous batch's host walk                      */
+    /* ABI 6 (always counted; zeroed by ipxg_profile): batches launched without k_bin_slow (the
+       previous batch had no slow-list packet) whose k_bin listed some -- run again from k_bin_slow */
+    uint64_t slow_redos;
 } ipxg_timing;
 
 /* Per-phase shader-clock sums of the last batch's k_bin, k_reduce and k_bin_slow (16 values;

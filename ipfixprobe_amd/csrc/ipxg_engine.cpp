@@ -167,6 +167,7 @@ struct ipxg_engine {
         bool bins_valid = false;
         uint32_t part_bits = 0;
         bool spec_closed = false;    // (consume_pend's result) the front launched ahead returned at once
+        int64_t now = 0;             // GATE_EXPIRE: ipxg_expire's clock
     } pend;
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
@@ -219,6 +220,7 @@ struct ipxg_engine {
     uint32_t plug_nport = 0, plug_npref = 0;
     uint32_t plug_port[16] = {}, plug_pref[16] = {}, plug_pmask[16] = {}, plug_pinfo[16] = {};
     DevBuf marks, mark_cnt;
+    DevBuf plug_d;  // the flattened rules on the device (Params::plug_tab)
     bool wide = false;                   // the next batch's k_bin walks every header chain (WIDE)
     bool tile_agg = true;                // the next batch aggregates frequent flows per tile
     // an IPXG_BATCH_ASYNC batch whose kernels are enqueued but whose control block the host
@@ -278,6 +280,8 @@ struct ipxg_engine {
     size_t plan_h_bytes = 0;
     hipEvent_t plan_ev = nullptr;               // the last plan upload
     uint32_t last_touched = 0;           // flow aggregates of the previous batch
+    uint32_t last_slow = 0xFFFFFFFFu;    // its slow-list packets (0: the next batch skips k_bin_slow; unknown at first)
+    bool no_slow_skip = false;           // A/B knob IPXG_NO_SLOW_SKIP=1: k_bin_slow always launched
     uint32_t last_n = 0;                 // its packets
     double skew = 1.0;                   // previous batch: most loaded partition / mean partition
     uint32_t part_bits_last = 0;         // partitions of the last binned batch (log2)
@@ -479,10 +483,7 @@ static Params params(ipxg_engine* e) {
     if (p.plug) {
         p.plug_nport = e->plug_nport;
         p.plug_npref = e->plug_npref;
-        std::memcpy(p.plug_port, e->plug_port, sizeof(p.plug_port));
-        std::memcpy(p.plug_pref, e->plug_pref, sizeof(p.plug_pref));
-        std::memcpy(p.plug_pmask, e->plug_pmask, sizeof(p.plug_pmask));
-        std::memcpy(p.plug_pinfo, e->plug_pinfo, sizeof(p.plug_pinfo));
+        p.plug_tab = (const uint32_t*)e->plug_d.p;
     }
     p.spin_max = STRICT_SPIN_MAX;
     if (const char* sm = std::getenv("IPXG_STRICT_SPIN_MAX"))  // test knob: a short watchdog
@@ -692,6 +693,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->walk_pin = std::getenv("IPXG_WALK_PAGEABLE") == nullptr;
     e->sync_finish = std::getenv("IPXG_SYNC_FINISH") != nullptr && std::atoi(std::getenv("IPXG_SYNC_FINISH")) != 0;
     e->no_ahead = std::getenv("IPXG_NO_AHEAD") != nullptr && std::atoi(std::getenv("IPXG_NO_AHEAD")) != 0;
+    e->no_slow_skip = std::getenv("IPXG_NO_SLOW_SKIP") != nullptr && std::atoi(std::getenv("IPXG_NO_SLOW_SKIP")) != 0;
     if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -831,7 +833,7 @@ int ipxg_destroy(ipxg_engine* e) {
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
                       &e->ipf_tot, &e->ipf_off, &e->ipf_msg, &e->ipf_dmsg[0], &e->ipf_dmsg[1], &e->ipf_plan, &e->st_pkt, &e->st_crec, &e->st_keyed,
                       &e->st_qx, &e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2, &e->st_succ, &e->st_pred, &e->st_indeg,
-                      &e->st_queue, &e->marks, &e->mark_cnt})
+                      &e->st_queue, &e->marks, &e->mark_cnt, &e->plug_d})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -915,6 +917,7 @@ static int enqueue_batch_end(ipxg_engine* e) {
 }
 
 static int consume_pend(ipxg_engine* e, bool spec);
+static int expire_table(ipxg_engine* e, int64_t now_sec);
 
 static int complete_batch_impl(ipxg_engine* e, bool spec) {
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
@@ -1080,6 +1083,11 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
         // a finish: none, as after every finish
         p.prev_valid = p.prev_dev = ahead->mode == GATE_BATCH ? 1u : 0u;
     }
+    // no k_bin_slow behind k_bin when the previous batch listed no slow packet (with process plugins
+    // it also lists their checks: always launched); a batch that does list one is run again from
+    // k_bin_slow by post_batch (BatchCtl::slow_redo)
+    p.slow_skip = binned && e->last_slow == 0 && e->plugins.empty() && !e->no_slow_skip ? 1u : 0u;
+    nb.slow_skip = p.slow_skip;
     FragView fv = frag_view(e);
     bins = nb;
     e->bins_last = bins;
@@ -1118,8 +1126,10 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
         uint4* al = (uint4*)e->adefer_a.p;
         launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 1);
-        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
-        ev_rec(e, 2);
+        if (!p.slow_skip) {
+            launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
+            ev_rec(e, 2);
+        }
     }
     HIPCHK(e, hipGetLastError());
     return IPXG_OK;
@@ -2038,6 +2048,13 @@ static int add_plugin_impl(ipxg_engine* e, const ipxg_plugin* pl) {
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if ((rc = ensure(e, e->rules_d, rules.size() * sizeof(DevRule)))) return rc;
     HIPCHK(e, hipMemcpyAsync(e->rules_d.p, rules.data(), rules.size() * sizeof(DevRule), hipMemcpyHostToDevice, e->st));
+    uint32_t tab[PLUG_TAB_WORDS];
+    std::memcpy(tab + PLUG_PORT, e->plug_port, sizeof(e->plug_port));
+    std::memcpy(tab + PLUG_PREF, e->plug_pref, sizeof(e->plug_pref));
+    std::memcpy(tab + PLUG_PMASK, e->plug_pmask, sizeof(e->plug_pmask));
+    std::memcpy(tab + PLUG_PINFO, e->plug_pinfo, sizeof(e->plug_pinfo));
+    if ((rc = ensure(e, e->plug_d, sizeof(tab)))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->plug_d.p, tab, sizeof(tab), hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     return IPXG_OK;
 }
@@ -2047,6 +2064,7 @@ static int add_plugin_impl(ipxg_engine* e, const ipxg_plugin* pl) {
 // early front, from the walked batch's block before its host walk ends).
 static void take_batch_knobs(ipxg_engine* e, const BatchCtl& c2, const Params& p, uint32_t n, bool binned) {
     e->last_touched = c2.touched;
+    e->last_slow = c2.slow_count;
     e->last_n = n;
     if (binned && c2.total_slots) {  // the next batch's segment sizing
         const uint32_t P = 1u << e->part_bits_last;
@@ -2095,20 +2113,45 @@ static int early_front(ipxg_engine* e, const Params& p_walked, uint32_t n_walked
 static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool binned, bool finishing) {
     int rc;
     FragView fv = frag_view(e);
-    const BatchCtl c1 = *e->ctl_h;
+    BatchCtl c1 = *e->ctl_h;
     if (prof_on(e)) {
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
         e->tm.ingest_packets += n;
-        if (binned && e->prof_level == 3) e->tm.ingest_slow_ms += ev_ms(e, 1);
+        if (binned && e->prof_level == 3 && !p.slow_skip) e->tm.ingest_slow_ms += ev_ms(e, 1);
         if (binned && e->prof_level == 1) {
-            e->tm.ingest_slow_ms += ev_ms(e, 1);
-            e->tm.reduce_ms += e->early_timed ? ev_ms(e, 11, 3) : ev_ms(e, 2);
+            if (!p.slow_skip) e->tm.ingest_slow_ms += ev_ms(e, 1);
+            e->tm.reduce_ms += e->early_timed ? ev_ms(e, 11, 3) : ev_ms(e, p.slow_skip ? 1 : 2, 3);
             e->tm.fin_ms += ev_ms(e, 3);
             e->tm.reduce_launches++;
         }
     }
     bool slow = false;
+    if (c1.slow_redo) {
+        // k_bin listed slow packets although the batch was launched without k_bin_slow (the previous
+        // batch had none): k_reduce and k_fin_list returned at once -- the slow pass, k_reduce and
+        // k_fin_list now, in order (not finishing: a finish's flows are then exported by k_finish)
+        ev_rec(e, 5);
+        slow = true;
+        p.slow_skip = 0;
+        BinView bins = e->bins_last;
+        bins.slow_skip = 0;
+        HIPCHK(e, hipMemsetAsync(&e->ctl_d->slow_redo, 0, sizeof(uint32_t), e->st));
+        launch_bin_slow(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, (uint4*)e->slow_list.p, (uint32_t*)e->defer_a.p,
+                        (uint4*)e->adefer_a.p, e->stats_d);
+        launch_reduce(e->st, table_view(e), bins, e->ctl_d, (HotSlot*)e->fin_list.p, (uint32_t*)e->defer_a.p,
+                      (uint4*)e->adefer_a.p);
+        {
+            const int rc0 = join_fmt(e);  // (k_fin_list appends exports)
+            if (rc0) return rc0;
+        }
+        launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, (HotSlot*)e->fin_list.p, e->stats_d,
+                        n, false);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = sync_ctl(e))) return rc;
+        c1 = *e->ctl_h;
+        e->tm.slow_redos++;
+    }
 
     // fragmentation cache: order fragments by (bucket, arrival) and replay the rings
     uint32_t ndef = c1.deferred, nadef = c1.agg_deferred;
@@ -2293,18 +2336,42 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
     return IPXG_OK;
 }
 
+// export_expired(now) (cache.cpp:508-523) over the whole table: k_expire exports every live record
+// idle for inactive_s and counts them into the control block (BatchCtl::expired), which the host's
+// live count follows -- no recount of the table (round 4 scanned it a second time with k_count and
+// waited for the stream twice per call: the stream step's 0.155 ms).  With an
+// asynchronous batch in flight the expire is enqueued right behind the batch's tail, guarded like
+// the finish (k_expire returns when the batch needs the host), and the call returns at once: the
+// next call completes both (consume_pend, GATE_EXPIRE) -- ipxg_submit after launching its front
+// ahead, so the streaming step does not wait for the host either (workers.cpp:83-94: the
+// reference's storage worker calls export_expired on the input's timeout, between blocks).
 static int expire_impl(ipxg_engine* e, int64_t now_sec) {
     if (e) {
         const int rc0 = join_fmt(e);  // (k_expire appends exports)
         if (rc0) return rc0;
     }
     if (!e) return IPXG_EINVAL;
+    int rc;
+    HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if (e->inflight.on && !e->strict && !e->failed && e->inflight.tail) {
+        if (e->pend.on && (rc = consume_pend(e, false))) return rc;  // (not expected: a batch is in flight)
+        // room for the batch's exports and for every record it may leave live (the guard holds otherwise)
+        if ((rc = ensure_export(e, (size_t)e->live + 2ull * e->inflight.n))) return rc;
+        if ((rc = launch_tail(e, false))) return rc;
+        e->inflight.on = false;
+        launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d, e->ctl_d,
+                      &e->ctl_d->expired, e->ex_count, e->live);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = publish_ctl(e, true))) return rc;
+        set_pend(e, GATE_EXPIRE, e->inflight.bv, e->inflight.p, e->inflight.n);
+        e->pend.now = now_sec;
+        if (e->sync_finish) return consume_pend(e, false);
+        return IPXG_OK;
+    }
     {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
-    int rc;
-    HIPCHK(e, hipSetDevice(e->cfg.device_id));
     if (e->strict) {  // the reference's export_expired(now): one sweep step (cache.cpp:508-523)
         if ((rc = ensure_export(e, 16))) return rc;
         HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
@@ -2317,14 +2384,21 @@ static int expire_impl(ipxg_engine* e, int64_t now_sec) {
         e->keys = e->live;
         return IPXG_OK;
     }
+    return expire_table(e, now_sec);
+}
+
+// One export_expired(now) over the table, unguarded, waited for: the live count follows the records
+// k_expire exported (BatchCtl::expired of the current block).
+static int expire_table(ipxg_engine* e, int64_t now_sec) {
+    int rc;
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
-    launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d);
+    HIPCHK(e, hipMemsetAsync(&e->ctl_d->expired, 0, sizeof(uint32_t), e->st));
+    launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d, nullptr,
+                  &e->ctl_d->expired);
     HIPCHK(e, hipGetLastError());
-    HIPCHK(e, hipMemsetAsync(e->ctl_d, 0, sizeof(BatchCtl), e->st));
-    launch_count(e->st, table_view(e), e->cap, e->ctl_d);
     if ((rc = sync_ctl(e))) return rc;
-    e->keys = e->ctl_h->keys;
-    e->live = e->ctl_h->live;
+    const uint32_t x = e->ctl_h->expired;
+    e->live = x > e->live ? 0u : e->live - x;
     return IPXG_OK;
 }
 
@@ -2377,6 +2451,12 @@ static int consume_pend(ipxg_engine* e, bool spec) {
     if (!rc) {
         if (q.mode == GATE_BATCH) {
             rc = post_batch(e, q.bv, q.p, q.n, true, false);
+        } else if (q.mode == GATE_EXPIRE) {  // k_expire right behind the batch, unless its guard held it
+            const bool held = e->ctl_h->hold != 0;
+            const uint32_t x = held ? 0u : e->ctl_h->expired;
+            rc = post_batch(e, q.bv, q.p, q.n, true, false);
+            if (!rc && !held) e->live = x > e->live ? 0u : e->live - x;
+            else if (!rc) rc = expire_table(e, q.now);  // the batch is complete now: expire normally
         } else if (q.mode == GATE_FIN_FUSED) {
             // k_fin_list exported what it finalised: complete unless it could not fuse (host work)
             // or left complex flows

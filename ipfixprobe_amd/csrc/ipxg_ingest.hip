@@ -377,6 +377,25 @@ __device__ __forceinline__ void tile_rank(const Params& p, const BatchView& b, c
     }
 }
 
+// The same record as one 16-byte word {hash lo, hash hi, 0, misc} (k_bin without tile aggregation
+// stages it in LDS during the packet loop: the tile's records then hold no registers there)
+__device__ __forceinline__ uint4 make_record(const Params& p, const BatchView& b, const DevPkt& pk,
+                                             const ipxg_pkt_desc& d, uint32_t& tb_or) {
+    uint64_t lo, hf;
+    uint32_t cdir;
+#ifdef IPXG_EXP_NOHASH  // timing experiment only: one cheap mixer instead of XXH64
+    lo = (((uint64_t)(pk.sip[0] ^ pk.dip[0]) << 32) | (uint32_t)(pk.src_port ^ pk.dst_port)) * 0x9E3779B97F4A7C15ull;
+    lo ^= lo >> 29;
+    cdir = 0;
+    hf = lo;
+#else
+    canon<false>(pk, p, lo, cdir, hf);
+#endif
+    const uint32_t m = pack_misc(pk, cdir, time_bucket(d.ts_sec, b.base_sec, p.bucket_w));
+    tb_or |= misc_tb(m);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), 0u, m);
+}
+
 // After the tile's packet loop (rk[q] != NO_REC: record q of this lane holds a packet):
 // count the packets per flow in the LDS hash, fold the flows with >= TAGG_MIN packets into
 // LDS aggregates, and rank the remaining packet records (rk[q] <- rank in its partition) and
@@ -496,7 +515,7 @@ __device__ __forceinline__ uint32_t plug_check(const Params& p, const uint32_t (
                                                const DevPkt& pk) {
     const uint32_t pm = pk.l4 == 6 ? 1u : 2u;  // (pk.l4 is TCP or UDP here)
     for (uint32_t k = 0; k < p.plug_nport; ++k) {
-        const uint32_t e = p.plug_port[k];
+        const uint32_t e = p.plug_tab[PLUG_PORT + k];
         if (((e >> 16) & pm) && (pk.src_port == (e & 0xFFFF) || pk.dst_port == (e & 0xFFFF))) return MARK_HIT;
     }
     if (!p.plug_npref) return 0;
@@ -517,13 +536,13 @@ __device__ __forceinline__ uint32_t plug_check(const Params& p, const uint32_t (
     }
     uint32_t res = 0;
     for (uint32_t k = 0; k < p.plug_npref; ++k) {
-        const uint32_t info = p.plug_pinfo[k], n = info & 0xFF;
+        const uint32_t info = p.plug_tab[PLUG_PINFO + k], n = info & 0xFF;
         if (!((info >> 8) & pm) || n == 0 || n > pk.payload_len) continue;
         if (!inwin) {
             res = MARK_LATER;
             continue;
         }
-        if (((pay ^ p.plug_pref[k]) & p.plug_pmask[k]) == 0) return MARK_HIT;
+        if (((pay ^ p.plug_tab[PLUG_PREF + k]) & p.plug_tab[PLUG_PMASK + k]) == 0) return MARK_HIT;
     }
     return res;
 }
@@ -587,7 +606,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                                           : ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
     uint32_t spilled = 0, walked = 0, tb_or = 0;
-    constexpr bool XP = IPXG_BIN_XPOSE && !WIDE;
+    constexpr bool XP = IPXG_BIN_XPOSE && !WIDE && AGG;
+    // Without tile aggregation the tile's records are staged in LDS as they are made (the stage
+    // array, free during the packet loop: the aggregation's tile hash and XP's transposes use it):
+    // the 32 record registers (8 steps x 4 words) are live only in the emit phase, not through the
+    // parse and hash of every step -- k_bin's register peak.
+    constexpr bool LR = !AGG;
     // the wide walk's window: 96 bytes (WIDE2_DW) without tile aggregation, 80 with it (its
     // registers: 245 VGPRs at 80 bytes)
     constexpr int WD = AGG ? WIDE_DW : WIDE2_DW;
@@ -609,8 +633,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 #ifdef IPXG_PROBE
     uint64_t probe_acc[4] = {0, 0, 0, 0};
 #endif
-    // The block's tiles are blockIdx.x, blockIdx.x + grid, ...; its step g is step g % BIN_K of
-    // its tile g / BIN_K (one packet per lane).  Software pipeline across the tiles: step g
+    // The block's tiles: F full rounds of interleaved tiles (tile k of block w is tile k * grid + w of
+    // BIN_K 256-packet steps, so the grid streams through one region of the batch at a time), then
+    // its even share of the remaining steps as one partial tile (round 5: the remainder went to the
+    // first blocks as whole tiles -- 4883 udp64 tiles over 768 blocks left a seventh round on 275
+    // of them; one contiguous range per block instead cost udp64 2 %, DRAM locality).  Step g of
+    // the block is step g % BIN_K of its tile g / BIN_K (one packet per lane).  Software pipeline across the tiles: step g
     // issues the descriptor of step g + DA and the head of step g + HA (whose descriptor
     // arrived during the DA - HA steps since it was issued), so the loads stay in flight
     // through the tile's emit phase and its barriers.  The tile's steps are unrolled and
@@ -628,7 +656,29 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 #endif
     constexpr int DA = IPXG_BIN_DA, HA = AGG ? IPXG_BIN_HA_AGG : IPXG_BIN_HA;
     static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
-    const uint32_t ntiles = (b.n + BIN_TILE - 1) / BIN_TILE;
+    const uint32_t nsteps = (b.n + IPXG_BLOCK - 1) / IPXG_BLOCK;
+    const uint32_t G = gridDim.x;
+#ifndef IPXG_BIN_BALANCE  // A/B knob: 0 = whole tiles only (the round-4 assignment) for every variant
+#define IPXG_BIN_BALANCE 1
+#endif
+    // The remainder spread evenly pays with the tiling aggregation (imix k_bin -5 %); the plain
+    // walk is bandwidth-bound -- a block alone on its CU in the last round runs faster -- and one
+    // more (partial) tile's emit per block cost it 1.4 % (udp64, gpurun_out/v5b): whole tiles there.
+    constexpr bool BAL = IPXG_BIN_BALANCE && AGG;
+    const uint32_t tiles = (nsteps + BIN_K - 1) / BIN_K;
+    const uint32_t F = BAL ? nsteps / (BIN_K * G) : (blockIdx.x < tiles ? (tiles - blockIdx.x + G - 1) / G : 0u);
+    const uint32_t rb = BAL ? F * BIN_K * G : 0u;  // the remainder's first step
+    const uint32_t rs = BAL ? nsteps - rb : 0u;     // ... and its steps (< BIN_K * G)
+    const uint32_t r_lo = rb + (uint32_t)((uint64_t)rs * blockIdx.x / G);
+    const uint32_t r_hi = rb + (uint32_t)((uint64_t)rs * (blockIdx.x + 1) / G);
+    const uint32_t ntile = F + (r_hi > r_lo ? 1u : 0u);
+    auto tile_lo = [&](uint32_t k) { return k < F ? (k * G + blockIdx.x) * BIN_K : r_lo; };  // first step
+    auto tile_lim = [&](uint32_t k) {  // packet limit (exclusive) of tile k; an empty range past the last
+        const uint32_t hi = k < F ? (k * G + blockIdx.x) * BIN_K + BIN_K : (k == F ? r_hi : r_lo);
+        return min(b.n, hi * IPXG_BLOCK);
+    };
+    // a prefetch past a tile's range reads nothing (an index past every descriptor)
+    auto clamp = [](uint32_t i, uint32_t lim) { return i < lim ? i : (BUF_OOB >> 4); };
     ipxg_pkt_desc Dr[DA];
     Head<NC> Hr[HA];
     bool Xr[HA];  // XP: ring slot h holds a transposed (contiguous) head load
@@ -638,7 +688,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // them for the path with the fewest memory operations after each load.
 #pragma unroll
     for (int k = 0; k < DA; ++k) {
-        const uint32_t i = blockIdx.x * BIN_TILE + k * IPXG_BLOCK + tid;
+        const uint32_t i = clamp((tile_lo(0) + k) * IPXG_BLOCK + tid, ntile ? tile_lim(0) : 0u);
         Dr[k] = load_desc(rs_desc, i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
@@ -651,9 +701,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     }
 #pragma unroll
     for (int q = 0; q < BIN_TILE / IPXG_BLOCK; ++q) g_dummy_rec[(DA * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
-    for (uint32_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
-        const uint32_t tile = tile_id * BIN_TILE;
-        const uint32_t next = (tile_id + gridDim.x) * BIN_TILE;  // past the batch: loads give zeros
+    for (uint32_t tk = 0; tk < ntile; ++tk) {
+        const uint32_t tile = tile_lo(tk) * IPXG_BLOCK;
+        const uint32_t lim = tile_lim(tk);
+        const uint32_t next = tile_lo(tk + 1) * IPXG_BLOCK;  // the block's next tile
+        const uint32_t next_lim = tk + 1 < ntile ? tile_lim(tk + 1) : 0u;  // (none: loads give zeros)
         // the timestamp of the packet before the tile (another workgroup's tile), for the
         // tile's first packet; consumed after the tile (zeros for the batch's first tile)
         const u32x2 tpred = __builtin_amdgcn_raw_buffer_load_b64(rs_desc, tile ? tile * 16u - 8u : BUF_OOB, 0, 0);
@@ -666,10 +718,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         PROBE_T(t1);
         PROBE_ADD(0, t0, t1);
         uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
+        if constexpr (!LR) {
 #pragma unroll
-        for (int q = 0; q < BIN_K; ++q) {
-            r0[q] = r1[q] = r2[q] = ix[q] = 0;
-            rk[q] = NO_REC;
+            for (int q = 0; q < BIN_K; ++q) {
+                r0[q] = r1[q] = r2[q] = ix[q] = 0;
+                rk[q] = NO_REC;
+            }
         }
         // The wide walk's steps are unrolled DA at a time (the register rings' period), not all
         // BIN_K: eight inlined copies of parse_medium made the kernel larger than the
@@ -692,11 +746,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             asm volatile("" ::"v"(hc.c[2].z));
             // issue: the descriptor DA steps ahead, the head HA steps ahead
             const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
-            Dr[jj % DA] = load_desc(rs_desc, ia);
+            Dr[jj % DA] = load_desc(rs_desc, j + DA < BIN_K ? clamp(ia, lim) : clamp(ia, next_lim));
             const ipxg_pkt_desc dh = Dr[(jj + HA) % DA];
             if constexpr (XP) Hr[jj % HA] = load_head_x(rs_arena, dh, want(dh), Xr[jj % HA]);
             else Hr[jj % HA] = load_head<NC>(rs_arena, dh, want(dh));
-            const bool act = i < b.n;
+            const bool act = i < lim;
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
             const uint32_t ps = (uint32_t)__builtin_amdgcn_update_dpp((int)dc.ts_sec, (int)dc.ts_sec, 0x138, 0xF, 0xF, false);
@@ -752,8 +806,22 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                 my_slow[slow_fill + atomicAdd(&nslow[par], 1u)] =
                     make_uint4(i | (slow_class(hc.c[0], hc.c[1], hc.c[2]) << 24), dc.offset,
                                (uint32_t)dc.caplen | ((uint32_t)dc.wirelen << 16), dc.ts_sec);
-            if (have) tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix, tb_or);
+            if constexpr (LR)
+                stage[j * IPXG_BLOCK + tid] = have ? make_record(p, b, pk, dc, tb_or) : make_uint4(0, 0, NO_REC, 0);
+            else if (have)
+                tile_rank<false>(p, b, pk, dc, i, j, r0, r1, r2, rk, ix, tb_or);
         }
+        }
+        if constexpr (LR) {  // the lane's own records back (tile_emit's first barrier precedes any other lane's writes)
+#pragma unroll
+            for (int q = 0; q < BIN_K; ++q) {
+                const uint4 r = stage[q * IPXG_BLOCK + tid];
+                r0[q] = r.x;
+                r1[q] = r.y;
+                rk[q] = r.z;
+                r2[q] = r.w;
+                ix[q] = 0;
+            }
         }
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
@@ -772,7 +840,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t i0 = tile + j * IPXG_BLOCK + w * 64;
             const uint64_t pred = w ? bnd_last[j][w - 1]
                                     : (j ? bnd_last[j - 1][IPXG_BLOCK / 64 - 1] : ((uint64_t)tpred.x << 32) | tpred.y);
-            if (i0 != 0 && i0 < b.n && bnd_first[j][w] < pred) nonmono = true;
+            if (i0 != 0 && i0 < lim && bnd_first[j][w] < pred) nonmono = true;
         }
         PROBE_T(t4);
         PROBE_ADD(3, t3, t4);
@@ -781,7 +849,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     if (lane_id() == 0)
         for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long*)&ctl->probe[k], (unsigned long long)probe_acc[k]);
 #endif
-    if (tid == 0 && blockIdx.x == (last / BIN_TILE) % gridDim.x) {
+    if (tid == 0 && blockIdx.x == gridDim.x - 1) {  // (its range ends with the batch)
         const ipxg_pkt_desc d = b.desc[last];  // the batch's last timestamp (next batch's order check)
         ctl->last_sec = d.ts_sec;
         ctl->last_usec = d.ts_usec;
@@ -790,6 +858,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     if (tid == 0) {
         bv.slow_cnt[blockIdx.x] = slow_fill;
         if (slow_fill) atomicAdd(&ctl->slow_count, slow_fill);
+        if (slow_fill && p.slow_skip) ctl->slow_redo = 1;  // (no k_bin_slow behind this launch)
     }
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, blockIdx.x);
@@ -1218,6 +1287,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
             for (uint32_t w = tid; w < sizeof(BatchCtl) / 4; w += RED_THREADS) reinterpret_cast<uint32_t*>(zero_ctl)[w] = 0;
         if (zero_ex && tid < 3) zero_ex[tid] = 0;
     }
+    if (bv.slow_skip && ctl->slow_redo) return;  // slow packets without a slow pass: the host runs both again
     // the columns written: every k_bin workgroup's, and those of the k_bin_slow workgroups
     // that had slow packets (the others return without writing theirs)
     const uint32_t cols = bv.cols;
@@ -1521,6 +1591,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
     __shared__ uint32_t cnt[6];  // new live, complex, exported, IPv6 exports, new keys, deferred
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t ex_base;
+    if (p.slow_skip && ctl->slow_redo) return;  // (k_reduce returned too; `fused` stays 0)
     const uint32_t nf = ctl->fin_count;  // final: k_reduce has completed
     const bool fused = finishing && !(ctl->frag_count || ctl->deferred || ctl->agg_deferred || ctl->pending);
     if (blockIdx.x == 0 && threadIdx.x == 0) ctl->fused = fused ? 1u : 0u;

@@ -480,11 +480,26 @@ static inline uint32_t scan_grid(uint32_t cap) {
 // cache.cpp:508-523, over the whole table).  Slots [blk*256*SCAN_PER_THREAD, ...); one
 // export-buffer reservation per block (a single counter saturates at ~88 returning
 // atomics/us: MI355X_MICROARCH.md "dequeue").
+// A finish or expire enqueued right behind a batch whose control block the host has not read
+// must not run when the batch left work for the host (fragments, deferred packets or
+// finalise-list entries, the table scan, complex flows, a slow pass to run again) or when the
+// export buffer might not hold every live record; every workgroup decides alike from fields the
+// kernel does not change, workgroup 0 reports it (guard->hold).
+__device__ __forceinline__ bool guard_holds(BatchCtl* guard, uint32_t ex_before, uint32_t live_before, uint32_t cap) {
+    const bool hold = guard->frag_count || guard->deferred || guard->agg_deferred || guard->pending ||
+                      guard->complex_count || guard->fin_deferred || guard->slow_redo ||
+                      (uint64_t)ex_before + guard->exported + live_before + guard->new_live > cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) guard->hold = hold ? 1u : 0u;
+    return hold;
+}
+
 __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t cap, int64_t now,
-                                                ExportView ex, unsigned long long* stats) {
+                                                ExportView ex, unsigned long long* stats, BatchCtl* guard,
+                                                uint32_t* expired, uint32_t ex_before, uint32_t live_before) {
     __shared__ uint32_t scratch[8];
     __shared__ uint32_t sc[ST_COUNT];
     __shared__ uint32_t bbase;
+    if (guard && guard_holds(guard, ex_before, live_before, ex.cap)) return;
     if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
     const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
     uint32_t mask = 0, c = 0;
@@ -507,6 +522,7 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
     uint32_t total;
     const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
     if (threadIdx.x == 0) bbase = total ? atomicAdd(ex.count, total) : 0;
+    if (threadIdx.x == 0 && total && expired) atomicAdd(expired, total);
     __syncthreads();
     uint32_t pos = bbase + off;
 #pragma unroll
@@ -525,17 +541,16 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
 }
 
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
-                   ExportView ex, unsigned long long* stats) {
-    hipLaunchKernelGGL(k_expire, dim3(scan_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats);
+                   ExportView ex, unsigned long long* stats, BatchCtl* guard, uint32_t* expired,
+                   uint32_t ex_before, uint32_t live_before) {
+    hipLaunchKernelGGL(k_expire, dim3(scan_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats, guard, expired,
+                       ex_before, live_before);
 }
 
 // Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288) and empty the
 // table (every occupied slot it scans is zeroed).
 // guard != nullptr: a finish enqueued right behind a batch before the host has read the
-// batch's control block.  It must not run when the batch left work for the host (fragments,
-// deferred packets or finalise-list entries, the table scan, complex flows) or when the export buffer might not hold
-// every live record; every workgroup decides alike from fields k_finish does not change,
-// workgroup 0 reports it (guard->hold) and the host then completes the batch and finishes
+// batch's control block (guard_holds); when it holds, the host completes the batch and finishes
 // again.
 __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
                                                 unsigned long long* stats, BatchCtl* guard, uint32_t ex_before,
@@ -543,13 +558,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
     __shared__ uint32_t scratch[8];
     __shared__ uint32_t bbase;
     __shared__ uint32_t pb[6];  // FlowRecordStats buckets of the block's exports
-    if (guard) {
-        const bool hold = guard->frag_count || guard->deferred || guard->agg_deferred || guard->pending ||
-                          guard->complex_count || guard->fin_deferred ||
-                          (uint64_t)ex_before + guard->exported + live_before + guard->new_live > ex.cap;
-        if (blockIdx.x == 0 && threadIdx.x == 0) guard->hold = hold ? 1u : 0u;
-        if (hold) return;
-    }
+    if (guard && guard_holds(guard, ex_before, live_before, ex.cap)) return;
     const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
     uint32_t mask = 0, c = 0;
 #pragma unroll
@@ -645,23 +654,6 @@ __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_ca
 
 void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail) {
     hipLaunchKernelGGL(k_rehash, dim3(table_grid(from_cap)), dim3(256), 0, st, from, from_cap, to, fail);
-}
-
-__global__ __launch_bounds__(256) void k_count(TableView t, uint32_t cap, BatchCtl* ctl) {
-    uint32_t keys = 0, live = 0;
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const HotSlot& h = t.hot(s);
-        if (h.key) {
-            keys++;
-            if (h.state & SLOT_LIVE) live++;
-        }
-    }
-    if (keys) atomicAdd(&ctl->keys, keys);
-    if (live) atomicAdd(&ctl->live, live);
-}
-
-void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl) {
-    hipLaunchKernelGGL(k_count, dim3(table_grid(cap)), dim3(256), 0, st, t, cap, ctl);
 }
 
 // ---- stateless entry points ------------------------------------------------------------------

@@ -73,6 +73,9 @@ struct BatchCtl {
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
                              // past the table
     uint32_t spill_deferred; // of `deferred`: spills k_bin / k_bin_slow deferred (Params::defer_spill)
+    uint32_t expired;        // records k_expire exported (the host's live count follows it, no table recount)
+    uint32_t slow_redo;      // k_bin listed slow packets in a batch launched without k_bin_slow (Params::slow_skip):
+                             // k_reduce and k_fin_list returned at once, the host runs all three again
     uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -156,8 +159,10 @@ struct Params {
     uint32_t defer_spill;    // k_bin / k_bin_slow defer what does not fit its segment (tile_emit): the
                              // batch was launched during the previous batch's host walk
     uint32_t plug_nport, plug_npref;
-    uint32_t plug_port[16];
-    uint32_t plug_pref[16], plug_pmask[16], plug_pinfo[16];
+    // 4 x 16 words on the device (ipxg_add_plugin uploads them): ports, prefixes, prefix masks,
+    // prefix infos -- a pointer, not 256 bytes of kernel arguments on every launch (a kernel's
+    // dispatch reads its arguments: +1 us per launch at 512 bytes, tools/gapbench)
+    const uint32_t* plug_tab;
     // A front launched before the host has read the previous batch's control block (ipxg_submit
     // right behind an asynchronous batch or ipxg_finish, ipxg_engine.cpp `pend`): k_bin, k_bin_slow
     // and k_pstats first test that block (complete on the device: stream order) and return at once,
@@ -166,24 +171,28 @@ struct Params {
     const BatchCtl* prev_ctl;
     uint32_t gate_mode;  // GATE_NONE: no gate
     uint32_t prev_dev;
+    // k_bin_slow not launched: the previous batch had no slow packet (the empty launch and its
+    // kernel boundary cost ~7 us per batch); k_bin flags slow packets it lists (BatchCtl::slow_redo)
+    uint32_t slow_skip;
 };
 
 // What the host still has to do for a batch after its last kernel, from its control block:
 // fragments, deferred packets or aggregates, the table scan, complex flows, a finalise-list
 // retry, a plugin slot failure or a fired guard -- and for a finish, the flows it left (GATE_FIN_*).
 // The host (consume_pend) and the gated kernels evaluate the same function on the same block.
-enum GateMode : uint32_t { GATE_NONE = 0, GATE_BATCH = 1, GATE_FIN_FUSED = 2, GATE_FIN_GUARDED = 3 };
+enum GateMode : uint32_t { GATE_NONE = 0, GATE_BATCH = 1, GATE_FIN_FUSED = 2, GATE_FIN_GUARDED = 3, GATE_EXPIRE = 4 };
 __host__ __device__ inline bool gate_closed(const BatchCtl& c, uint32_t mode) {
     const bool work = c.frag_count || c.deferred || c.agg_deferred || c.pending || c.complex_count ||
-                      c.fin_deferred || c.plugin_fail || c.guard;
+                      c.fin_deferred || c.plugin_fail || c.guard || c.slow_redo;
     if (mode == GATE_FIN_FUSED) return work || !c.fused;
-    if (mode == GATE_FIN_GUARDED) return work || c.hold;
+    if (mode == GATE_FIN_GUARDED || mode == GATE_EXPIRE) return work || c.hold;
     return work;
 }
 __device__ __forceinline__ bool gated(const Params& p) {
     return p.gate_mode != GATE_NONE && gate_closed(*p.prev_ctl, p.gate_mode);
 }
 constexpr uint32_t PLUG_PREFIX = 4;
+enum PlugTab : uint32_t { PLUG_PORT = 0, PLUG_PREF = 16, PLUG_PMASK = 32, PLUG_PINFO = 48, PLUG_TAB_WORDS = 64 };
 
 // ---- strict mode (ipxg_strict.hip): the reference's line table -------------------------------
 struct StrictView {
@@ -245,6 +254,7 @@ struct BinView {
     uint32_t* slow_cnt;    // bin_grid: slow packets listed by each k_bin workgroup
     uint4* marks;          // Params::plug: workgroup b's plugin marks at marks[b * slow_stride ...] (k_bin's,
     uint32_t* mark_cnt;    //   then k_bin_slow's), mark_cnt[b] of them: {key lo, key hi, index | kind << 30, 0}
+    uint32_t slow_skip;    // Params::slow_skip (k_reduce returns when k_bin flagged slow_redo)
 };
 #ifndef IPXG_BIN_K
 #define IPXG_BIN_K 8  // packets per lane per k_bin tile
@@ -415,8 +425,11 @@ void launch_complex_gather_ranges(hipStream_t st, const BatchView& b, const Para
 void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f,
                          ComplexView cx, uint32_t nranks, ExportView ex, BatchCtl* ctl,
                          unsigned long long* stats);
+// guard != nullptr: an expire enqueued right behind a batch (ipxg_expire with an asynchronous batch
+// in flight), held back exactly as k_finish's guard; expired: += the records it exports.
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
-                   ExportView ex, unsigned long long* stats);
+                   ExportView ex, unsigned long long* stats, BatchCtl* guard, uint32_t* expired,
+                   uint32_t ex_before = 0, uint32_t live_before = 0);
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
                    BatchCtl* guard = nullptr, uint32_t ex_before = 0, uint32_t live_before = 0);
 void launch_publish(hipStream_t st, const uint32_t* ctl, const uint32_t* ex, uint32_t* dst, uint32_t ctl_words,
@@ -440,7 +453,6 @@ void launch_ipfix_messages(hipStream_t st, const ipxg_flow_record* rec, uint32_t
                            const uint64_t* block_pre6, const IpfixSet* sets, uint32_t nsets4, uint32_t nsets6,
                            const IpfixMsg* msgs, uint32_t nmsgs, uint32_t odid, uint32_t export_time, uint8_t* out);
 void launch_rehash(hipStream_t st, TableView from, uint32_t from_cap, TableView to, uint32_t* fail);
-void launch_count(hipStream_t st, TableView t, uint32_t cap, BatchCtl* ctl);
 void launch_parse_batch(hipStream_t st, const BatchView& b, uint32_t dlt, ipxg_parsed_pkt* out);
 void launch_xxh64(hipStream_t st, const uint8_t* keys, uint32_t keylen, uint32_t n, uint64_t seed,
                   uint64_t* out);

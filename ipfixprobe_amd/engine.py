@@ -78,7 +78,7 @@ class Timing(ctypes.Structure):
                                         "slow_launches", "finish_launches", "ingest_packets")] + \
         [("plugin_ms", ctypes.c_double)] + [(n, ctypes.c_uint64) for n in ("plugin_flows", "plugin_packets",
                                                                              "plugin_bytes", "plugin_extra_bytes",
-                                                                             "plugin_overlapped")]
+                                                                             "plugin_overlapped", "slow_redos")]
 
 
 class Capture(ctypes.Structure):

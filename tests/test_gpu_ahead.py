@@ -131,3 +131,82 @@ def test_no_ahead_knob_gives_the_same_records(monkeypatch):
     for x, y in zip(*outs):
         diff = flowcmp.diff(x, y)
         assert not diff, diff
+
+
+def _plain_then_mixed(seed):
+    """Plain 64 B UDP frames (no slow-list packet: the next batch is launched without k_bin_slow),
+    then a mixed stream (VLAN, IPv6, TCP options, fragments: slow-list packets), later in time."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    sip = (10 << 24) + rng.integers(0, 150, n)
+    dip = (192 << 24) + (168 << 16) + rng.integers(0, 40, n)
+    a1, d1 = synth.udp_frames(sip, dip, rng.integers(1024, 1100, n), rng.integers(1, 30, n), t0=1_599_999_000)
+    a2, d2 = synth.flow_stream(seed=seed, n_flows=120, n_pkts=3000, frag=True).batch()
+    d2 = d2.copy()
+    d2["offset"] += len(a1)
+    return np.concatenate([a1, a2]), np.concatenate([d1, d2]), len(d1)
+
+
+@pytest.mark.parametrize("mode", ["sync", "async", "finish"])
+def test_slow_pass_skipped_then_needed(mode):
+    """A batch launched without k_bin_slow (the previous batch listed no slow packet) whose k_bin
+    does list some: k_reduce and k_fin_list return at once (BatchCtl::slow_redo) and the host runs
+    k_bin_slow, k_reduce and k_fin_list again -- synchronous, asynchronous, and folded into a
+    finish.  Records equal the oracle's; the redo is counted."""
+    from ipfixprobe_amd import Engine
+    arena, desc, k = _plain_then_mixed(91)
+    if mode == "finish":  # two independent steps
+        want = np.concatenate([oracle_py.run_capture(arena, desc[:k], 1, cache_exp=20)[0],
+                               oracle_py.run_capture(arena, desc[k:], 1, cache_exp=20)[0]])
+    else:
+        want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20)
+    with Engine() as e:
+        if mode == "sync":
+            e.submit(arena, desc[:k])
+            e.submit(arena, desc[k:])
+            e.finish()
+            got = e.poll()
+        else:
+            da, d1 = _dev(arena, desc[:k])
+            _, d2 = _dev(arena, desc[k:])
+            e.submit(da, d1, device=True, asynchronous=True)
+            if mode == "finish":
+                e.finish()
+                g1 = e.poll()
+            e.submit(da, d2, device=True, asynchronous=True)
+            e.finish()
+            got = e.poll() if mode == "async" else np.concatenate([g1, e.poll()])
+        tm = e.timing()
+    assert tm["slow_redos"] >= 1
+    diff = flowcmp.diff(got, want)
+    assert not diff, diff
+
+
+@pytest.mark.parametrize("poll_every", [0, 2])
+def test_async_expire_between_batches(poll_every):
+    """ipxg_expire(now) behind each asynchronous batch (the streaming step): enqueued right behind
+    the batch's tail, guarded, completed by the next call.  Records equal the oracle's (an expired
+    record's flow splits at its next packet there too); the live count the engine keeps from
+    k_expire's exports (no table recount) equals what the final finish exports."""
+    from ipfixprobe_amd import Engine
+    a, d = synth.flow_stream(seed=95, n_flows=200, n_pkts=6000, long_gap_share=0.02, frag=False).batch()
+    want, _ = oracle_py.run_capture(a, d, 1, cache_exp=20)
+    da, _ = _dev(a, d)
+    keep, out = [], []
+    with Engine() as e:
+        for k, s in enumerate(range(0, len(d), 1000)):
+            _, dd = _dev(a, d[s:s + 1000])
+            keep.append(dd)
+            e.submit(da, dd, device=True, asynchronous=True)
+            e.expire(int(d["ts_sec"][min(s + 999, len(d) - 1)]))
+            if poll_every and k % poll_every == 0:
+                out.append(e.poll())
+        out.append(e.poll())
+        live = e.stats()["flows_in_cache"]
+        e.finish()
+        rest = e.poll()
+        st = e.stats()
+    assert st["end_inactive"] > 0  # (the stream's idle gaps: expired mid-stream)
+    assert len(rest) == live
+    diff = flowcmp.diff(np.concatenate(out + [rest]), want)
+    assert not diff, diff
