@@ -511,8 +511,10 @@ int ipxg_device_ipfix_messages(ipxg_engine* eng, ipxg_ipfix_exporter* x, const u
 /* The {stream bytes, records} of the last ipxg_device_ipfix_messages call as two uint64 in device
  * memory, written in order on ipxg_ipfix_stream with the messages: a consumer on
  * another stream that waits for the engine's reads them without a host round trip (the header of
- * the multi-GPU stream gather).  Valid until the next IPFIX message call (ipxg_ipfix_export,
- * ipxg_poll_ipfix_messages, ipxg_device_ipfix_messages).  IPXG_ESTATE before the first. */
+ * the multi-GPU stream gather).  They sit at the tail of that call's message buffer (8-byte aligned
+ * past the stream), so they stay valid exactly as long as the messages: until the call after the
+ * next ipxg_device_ipfix_messages -- a consumer must make the engine's stream wait for its reads
+ * before that call.  IPXG_ESTATE before the first call. */
 int ipxg_device_ipfix_counts(ipxg_engine* eng, const uint64_t** dptr);
 /* The stream ipxg_device_ipfix_messages formats on (hipStream_t; the engine's own stream before
  * the first call). */

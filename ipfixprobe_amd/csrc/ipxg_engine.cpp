@@ -168,6 +168,9 @@ struct ipxg_engine {
         uint32_t part_bits = 0;
         bool spec_closed = false;    // (consume_pend's result) the front launched ahead returned at once
         int64_t now = 0;             // GATE_EXPIRE: ipxg_expire's clock
+        // its block reaches the host mirror by the next front's k_bin (Params::pub_*: no publish
+        // kernel of its own between batches), else consume_pend publishes it
+        bool published = false;
     } pend;
     uint32_t* misc_d = nullptr;  // [0] rehash failures
     unsigned long long* stats_d = nullptr;
@@ -295,8 +298,8 @@ struct ipxg_engine {
     // host-side counters
     BinView bins_last = {};   // the last binned batch's partition records (k_complex_gather_rec)
     bool bins_valid = false;
-    uint64_t gather_fallbacks = 0;
-    uint64_t gather_ranges = 0;  // tile aggregates of complex flows parsed again by range  // complex gathers redone by re-parse (a complex flow in a tile aggregate)
+    uint64_t gather_fallbacks = 0;  // complex gathers redone by re-parse (a complex flow in a tile aggregate)
+    uint64_t gather_ranges = 0;     // tile aggregates of complex flows parsed again by range
     uint64_t complex_total = 0, rehashes = 0, batches = 0, spilled = 0, slow_pkts = 0, agg_pkts = 0, walked_pkts = 0;
     bool prev_valid = false;
     uint32_t prev_sec = 0, prev_usec = 0;
@@ -895,7 +898,8 @@ static void set_pend(ipxg_engine* e, uint32_t mode, const BatchView& bv, const P
     q.mode = mode;
     q.clear_after = false;
     q.blk = e->cur;
-    q.seq = e->pub_seq;
+    q.seq = 0;
+    q.published = false;
     q.bv = bv;
     q.p = p;
     q.n = n;
@@ -911,7 +915,6 @@ static int enqueue_batch_end(ipxg_engine* e) {
     int rc;
     if ((rc = launch_tail(e, false))) return rc;
     e->inflight.on = false;
-    if ((rc = publish_ctl(e, true))) return rc;
     set_pend(e, GATE_BATCH, e->inflight.bv, e->inflight.p, e->inflight.n);
     return IPXG_OK;
 }
@@ -1040,6 +1043,7 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
 struct Ahead {
     uint32_t mode;         // pend.mode
     const BatchCtl* prev;  // the pending batch's control block
+    uint32_t seq;          // k_bin publishes it with this sequence number
 };
 static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool binned, bool async, bool early, Params& p,
                         BinView& bins, const Ahead* ahead = nullptr, bool reuse_blk = false) {
@@ -1082,6 +1086,10 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
         // behind a batch: the order check continues from its last packet (read on the device); behind
         // a finish: none, as after every finish
         p.prev_valid = p.prev_dev = ahead->mode == GATE_BATCH ? 1u : 0u;
+        p.pub_dst = e->ctl_hd;
+        p.pub_ex = e->ex_count_d;
+        p.pub_words = (uint32_t)(CTL_EX_OFF / 4);
+        p.pub_seq = ahead->seq;
     }
     // no k_bin_slow behind k_bin when the previous batch listed no slow packet (with process plugins
     // it also lists their checks: always launched); a batch that does list one is run again from
@@ -1247,17 +1255,33 @@ static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
         abv.arena = batch->arena;
         abv.desc = batch->desc;
         abv.base_sec = BASE_FROM_DESC0;
-        const Ahead ah{e->pend.mode, e->ctl_blk[e->pend.blk]};
+        uint32_t seq = e->pub_seq + 1;
+        if (seq == 0) seq = 1;
+        const Ahead ah{e->pend.mode, e->ctl_blk[e->pend.blk], seq};
         e->no_grow = true;
         rc = launch_front(e, abv, n, true, true, false, p, bins, &ah);
         e->no_grow = false;
-        if (rc == IPXG_EGROW) rc = IPXG_OK;  // (nothing enqueued: the front follows the completion)
-        else if (rc) return rc;
-        else ahead = true;
+        if (rc == IPXG_EGROW) {
+            rc = IPXG_OK;  // (nothing enqueued: the front follows the completion)
+        } else if (rc) {
+            return rc;
+        } else {
+            ahead = true;
+            e->pub_seq = seq;  // k_bin publishes the pending batch's block
+            e->pend.seq = seq;
+            e->pend.published = true;
+        }
     }
     rc = complete_batch(e, ahead);
     e->early.want = false;
     if (rc) {
+        // this batch's front already ran (launched ahead, or from the failed batch's host walk): its
+        // packets are counted in the statistics and its block holds them, so a retry of this submit
+        // would count them twice -- the engine stops until ipxg_reset
+        if ((e->early.launched || ahead) && !e->failed) {
+            e->failed = true;
+            e->fail_msg = std::string("the batch before this one failed after this batch's front ran: ") + e->err;
+        }
         e->early.launched = false;
         return rc;
     }
@@ -1767,6 +1791,9 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     for (unsigned c = 0; c < C; ++c) ready[c].store(0);
     std::atomic<uint32_t> next_unit{0};
     std::atomic<uint32_t> copy_fail{0};
+    // the first failure stops every thread from taking more units: the reference stops at the first
+    // PluginError, so no plugin instance advances past it
+    std::atomic<bool> stop{false};
     auto walk_unit = [&](unsigned t, unsigned u) {
         const uint32_t f0 = fr[u], f1 = fr[u + 1];
         WalkOut& wo = wos[u];
@@ -1828,6 +1855,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         }
         try {
             for (;;) {
+                if (stop.load(std::memory_order_acquire)) break;
                 const unsigned u = next_unit.fetch_add(1);
                 if (u >= U) break;
                 const unsigned c = chunk_of(u);
@@ -1836,17 +1864,21 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
                 walk_unit(t, u);
             }
         } catch (const HookFail& h) {
+            stop.store(true, std::memory_order_release);
             wfail[t] = 3;
             const ipxg_plugin& q = (t ? e->walk_pl[t - 1] : e->plugins)[h.plugin];
             const char* m = q.error ? q.error(q.ctx) : nullptr;
             wmsg[t] = "process plugin " + std::to_string(h.plugin) + " " + h.hook + ": " +
                       (m ? m : "returned IPXG_PLUGIN_ERROR");
         } catch (const std::bad_alloc&) {
+            stop.store(true, std::memory_order_release);
             wfail[t] = 2;
         } catch (const std::exception& x) {  // (a hook that threw past the C ABI)
+            stop.store(true, std::memory_order_release);
             wfail[t] = 3;
             wmsg[t] = std::string("process plugin walk: ") + x.what();
         } catch (...) {
+            stop.store(true, std::memory_order_release);
             wfail[t] = 3;
             wmsg[t] = "process plugin walk: a hook raised a non-standard exception";
         }
@@ -2362,7 +2394,6 @@ static int expire_impl(ipxg_engine* e, int64_t now_sec) {
         launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d, e->ctl_d,
                       &e->ctl_d->expired, e->ex_count, e->live);
         HIPCHK(e, hipGetLastError());
-        if ((rc = publish_ctl(e, true))) return rc;
         set_pend(e, GATE_EXPIRE, e->inflight.bv, e->inflight.p, e->inflight.n);
         e->pend.now = now_sec;
         if (e->sync_finish) return consume_pend(e, false);
@@ -2432,7 +2463,6 @@ static int consume_pend(ipxg_engine* e, bool spec) {
     if (!q.on) return IPXG_OK;
     q.on = false;
     int rc;
-    if ((rc = wait_seq(e, q.seq))) return rc;
     const int now = e->cur;
     const BinView bins_now = e->bins_last;
     const bool valid_now = e->bins_valid;
@@ -2446,8 +2476,14 @@ static int consume_pend(ipxg_engine* e, bool spec) {
     e->bins_last = q.bins;
     e->bins_valid = q.bins_valid;
     e->part_bits_last = q.part_bits;
-    q.spec_closed = spec && gate_closed(*e->ctl_h, q.mode);
-    rc = check_ex(e);
+    rc = IPXG_OK;
+    if (!q.published) {  // (no front ahead published it)
+        rc = publish_ctl(e, true);
+        q.seq = e->pub_seq;
+    }
+    if (!rc) rc = wait_seq(e, q.seq);
+    q.spec_closed = !rc && spec && gate_closed(*e->ctl_h, q.mode);
+    if (!rc) rc = check_ex(e);
     if (!rc) {
         if (q.mode == GATE_BATCH) {
             rc = post_batch(e, q.bv, q.p, q.n, true, false);
@@ -2543,7 +2579,6 @@ static int finish_impl(ipxg_engine* e) {
         // the batch is consumed here whatever happens next: an error below must not make the
         // next call run post_batch again on a table k_finish may already have emptied
         e->inflight.on = false;
-        if ((rc = publish_ctl(e, true))) return rc;
         set_pend(e, fuse ? GATE_FIN_FUSED : GATE_FIN_GUARDED, e->inflight.bv, e->inflight.p, e->inflight.n);
         if (e->sync_finish) return consume_pend(e, false);
         return IPXG_OK;
@@ -2559,6 +2594,7 @@ int ipxg_reset(ipxg_engine* e) {
         e->failed = false;
         e->fail_msg.clear();
         e->inflight.on = e->inflight.tail = false;
+        e->pend.on = false;
     }
     {
         const int rc0 = complete_batch(e);
@@ -2842,12 +2878,17 @@ static int ipfix_messages(ipxg_engine* e, ipxg_ipfix_exporter* x, const ipxg_flo
     ipfix_template_msg(plan + toff, *x);
     const uint64_t counts[2] = {P.bytes, n};
     std::memcpy(plan + coff, counts, sizeof(counts));
+    // the {bytes, records} pair lives at the tail of the message buffer itself (8-byte aligned past
+    // the stream), so it stays valid exactly as long as its stream -- the device message buffers
+    // alternate (ipxg_device_ipfix_messages), the plan does not
+    const size_t cnt_off = (P.bytes + 7) & ~(size_t)7;
     if ((rc = ensure(e, e->ipf_plan, pbytes))) return rc;
-    if ((rc = ensure(e, mb, P.bytes + 16))) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->ipf_plan.p, plan, pbytes, hipMemcpyHostToDevice, st));
-    HIPCHK(e, hipEventRecord(e->plan_ev, st));
-    e->ipf_counts = (const uint64_t*)((uint8_t*)e->ipf_plan.p + coff);
+    if ((rc = ensure(e, mb, cnt_off + 2 * sizeof(uint64_t)))) return rc;
     uint8_t* out = (uint8_t*)mb.p;
+    HIPCHK(e, hipMemcpyAsync(e->ipf_plan.p, plan, pbytes, hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(out + cnt_off, plan + coff, 2 * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipEventRecord(e->plan_ev, st));
+    e->ipf_counts = (const uint64_t*)(out + cnt_off);
     if (P.tmpl)
         HIPCHK(e, hipMemcpyAsync(out, (uint8_t*)e->ipf_plan.p + toff, IPFIX_TMPL_MSG, hipMemcpyDeviceToDevice, st));
     const IpfixSet* sets = (const IpfixSet*)e->ipf_plan.p;

@@ -186,8 +186,11 @@ __device__ __forceinline__ void xpose_head(uint4* xs, Head<4>& h) {
 }
 
 // descriptor i (zeros past the batch's end)
+#ifndef IPXG_DESC_AUX
+#define IPXG_DESC_AUX IPXG_LOAD_AUX
+#endif
 __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, uint32_t i) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, IPXG_LOAD_AUX);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, IPXG_DESC_AUX);
     ipxg_pkt_desc d;
     d.offset = v.x;
     d.caplen = (uint16_t)v.y;
@@ -570,6 +573,15 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG 
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     static_assert(!PLUG || WIDE, "the plugin check reads the wide walk's window");
+    if (p.pub_seq && blockIdx.x == 0) {  // the pending batch's control block to the host (k_publish's layout)
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.prev_ctl);
+        for (uint32_t w = threadIdx.x; w < p.pub_words; w += IPXG_BLOCK) p.pub_dst[w] = src[w];
+        if (threadIdx.x < 4) p.pub_dst[p.pub_words + threadIdx.x] = p.pub_ex[threadIdx.x];
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&p.pub_dst[p.pub_words + 4], p.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (gated(p)) return;  // launched ahead of the host's reading of the previous batch, which needs it
     __shared__ uint32_t hist[KBIN_PMAX];  // 8 KiB: per-partition rank / run start
     __shared__ uint32_t fill[KBIN_PMAX];  // 8 KiB: slots in the block's segments

@@ -171,6 +171,12 @@ struct Params {
     const BatchCtl* prev_ctl;
     uint32_t gate_mode;  // GATE_NONE: no gate
     uint32_t prev_dev;
+    // pub_seq != 0: k_bin's workgroup 0 first publishes prev_ctl (pub_words words) and the export
+    // counters into the host mirror with this sequence number (k_publish's layout), so the host reads
+    // the pending batch without a publish kernel (and its kernel boundary) between the batches
+    uint32_t* pub_dst;
+    const uint32_t* pub_ex;
+    uint32_t pub_words, pub_seq;
     // k_bin_slow not launched: the previous batch had no slow packet (the empty launch and its
     // kernel boundary cost ~7 us per batch); k_bin flags slow packets it lists (BatchCtl::slow_redo)
     uint32_t slow_skip;

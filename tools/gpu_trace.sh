@@ -10,8 +10,8 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for W in ${WORKLOADS:-udp64}; do
   case $W in
-    udp64) ARGS="--steps 30 --warmup 3"; FIRST=fillBuffer ;;
-    stream) ARGS="--mode stream --steps 20 --warmup 3"; FIRST=k_bin ;;
+    udp64) ARGS="--steps 30 --warmup 3"; FIRST="k_bin<" ;;
+    stream) ARGS="--mode stream --steps 20 --warmup 3"; FIRST="k_bin<" ;;
     imix) ARGS="--workload imix --steps 2 --warmup 1"; FIRST=k_finish ;;
     quic) ARGS="--workload quic --steps 3 --warmup 1"; FIRST=k_finish ;;
     *) echo "unknown workload $W"; exit 2 ;;

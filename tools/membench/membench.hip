@@ -7,7 +7,7 @@
 //            stride (a ballot over the offsets) -- the wave's 4 KB read as 4 contiguous 1 KB
 //            loads (lane = 16 bytes) and transposed through the wave's LDS (frames at an 80-byte
 //            pitch: conflict-free 16-byte reads), each lane then holding its frame's 48 bytes
-// Usage: membench <n_packets> <stride> <blocks>
+// Usage: membench <n_packets> <stride> <blocks> [<LDS KiB per block of the k_tiles runs>]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -31,28 +31,94 @@ __global__ __launch_bounds__(256) void k_contig(const uint4* __restrict__ a, siz
     if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <bool DESC>
+// U packets per lane per iteration (all U descriptors, then all 3U head loads in flight)
+template <bool DESC, int U = 4>
 __global__ __launch_bounds__(256) void k_frame(const uint8_t* __restrict__ arena, const Desc* __restrict__ desc,
                                                uint32_t n, uint32_t fstride, uint32_t* out) {
     uint32_t acc = 0;
     const uint32_t step = gridDim.x * 256;
-    for (uint32_t i0 = blockIdx.x * 256 * 4 + threadIdx.x; i0 < n; i0 += step * 4) {
-        uint32_t off[4];
+    for (uint32_t i0 = blockIdx.x * 256 * U + threadIdx.x; i0 < n; i0 += step * U) {
+        uint32_t off[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < U; ++k) {
             const uint32_t i = min(i0 + k * 256, n - 1);
             if (DESC) { const Desc d = desc[i]; off[k] = d.off; acc ^= d.len ^ d.s; }
             else off[k] = i * fstride;
         }
-        uint4 h[4][3];
+        uint4 h[U][3];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < U; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) h[k][c] = *reinterpret_cast<const uint4*>(arena + off[k] + 16 * c);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < U; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) acc ^= h[k][c].x ^ h[k][c].y ^ h[k][c].z ^ h[k][c].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// k_bin's load pattern in its persistent form: tiles of 8 steps x 256 packets, tile t on block
+// t % grid; per step the descriptor DA steps ahead and the 48-byte head HA steps ahead (rings in
+// registers, buffer loads with `aux`), consumed by an XOR.  LDS `lds_kb` KiB per block (occupancy).
+typedef uint32_t mb_u32x4 __attribute__((ext_vector_type(4)));
+// W: each tile also stores its 2048 16-byte records (k_bin's record volume): W = 1 sequentially
+// (coalesced 1 KB per wave store), W = 2 in 8-record runs spread over 256 partition columns of
+// per-block segments (k_bin's layout); store_nt: non-temporal stores
+template <int DA, int HA, int W = 0>
+__global__ __launch_bounds__(256) void k_tiles(const uint8_t* __restrict__ arena, const Desc* __restrict__ desc,
+                                               uint32_t n, uint32_t aux_nt, uint32_t* out, uint4* rec = nullptr,
+                                               uint32_t store_nt = 0, uint32_t seg_cap = 0) {
+    extern __shared__ uint32_t lds[];
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<Desc*>(desc), 0, (int)(n * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(arena), 0, (int)(n * 64u), 0x00020000);
+    const uint32_t tid = threadIdx.x, ntiles = (n + 2047) / 2048;
+    uint32_t acc = 0;
+    mb_u32x4 Dr[DA];
+    mb_u32x4 Hr[HA][3];
+    auto ld = [&](uint32_t i) { return __builtin_amdgcn_raw_buffer_load_b128(rd, i < n ? i * 16u : 0xFFFFFF00u, 0, 2); };
+    auto lh = [&](const mb_u32x4 d, int c) {
+        return aux_nt ? __builtin_amdgcn_raw_buffer_load_b128(ra, d.y ? d.x + 16u * c : 0xFFFFFF00u, 0, 2)
+                      : __builtin_amdgcn_raw_buffer_load_b128(ra, d.y ? d.x + 16u * c : 0xFFFFFF00u, 0, 0);
+    };
+#pragma unroll
+    for (int k = 0; k < DA; ++k) Dr[k] = ld(blockIdx.x * 2048 + k * 256 + tid);
+#pragma unroll
+    for (int h = 0; h < HA; ++h)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Hr[h][c] = lh(Dr[h], c);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t tile = t * 2048, next = (t + gridDim.x) * 2048;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const mb_u32x4 h0 = Hr[j % HA][0], h1 = Hr[j % HA][1], h2 = Hr[j % HA][2];
+            const uint32_t ia = j + DA < 8 ? tile + (j + DA) * 256 + tid : next + (j + DA - 8) * 256 + tid;
+            const mb_u32x4 dh = Dr[(j + HA) % DA];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Hr[j % HA][c] = lh(dh, c);
+            Dr[j % DA] = ld(ia);
+            acc ^= h0.x ^ h0.y ^ h1.z ^ h2.w;
+        }
+        if (W) {
+            const uint32_t k0 = (t - blockIdx.x) / gridDim.x;  // the block's tile number
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t r = q * 256 + tid;  // record r of the tile
+                size_t dst;
+                if (W == 1) dst = (size_t)tile + r;
+                else dst = ((size_t)(r >> 3) * gridDim.x + blockIdx.x) * seg_cap + k0 * 8 + (r & 7);  // partition r/8
+                const uint4 v = make_uint4(acc, r, t, q);
+                if (store_nt) {
+                    __builtin_nontemporal_store(v.x, &rec[dst].x);
+                    __builtin_nontemporal_store(v.y, &rec[dst].y);
+                    __builtin_nontemporal_store(v.z, &rec[dst].z);
+                    __builtin_nontemporal_store(v.w, &rec[dst].w);
+                } else {
+                    rec[dst] = v;
+                }
+            }
+        }
+        if (lds[0] == 0xDEADBEEF) __syncthreads();  // (never: keeps the LDS allocation)
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -135,5 +201,35 @@ int main(int argc, char** argv) {
     run("frame", (double)n * (48 + 16), [&] { hipLaunchKernelGGL(k_frame<true>, dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
     run("frame_nodesc", (double)n * 48, [&] { hipLaunchKernelGGL(k_frame<false>, dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
     run("frame_lds", (double)n * (64 + 16), [&] { hipLaunchKernelGGL(k_frame_lds, dim3(blocks), dim3(256), 0, 0, arena, desc, n, out); });
+    run("frame_u1", (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_frame<true, 1>), dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    run("frame_u2", (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_frame<true, 2>), dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    const uint32_t lds_kb = argc > 4 ? atoi(argv[4]) : 0;
+    if (lds_kb) CHK(hipFuncSetAttribute((const void*)k_tiles<4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
+    if (lds_kb) CHK(hipFuncSetAttribute((const void*)k_tiles<4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
+    if (lds_kb) CHK(hipFuncSetAttribute((const void*)k_tiles<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
+    const size_t lb = (size_t)(lds_kb ? lds_kb : 1) * 1024;
+    uint4* recb;
+    const uint32_t seg_cap = ((n + 2047) / 2048 + blocks - 1) / blocks * 8 + 8;
+    CHK(hipMalloc(&recb, (size_t)256 * blocks * seg_cap * 16 + (size_t)n * 16));
+    if (lds_kb)
+        for (const void* f : {(const void*)k_tiles<4, 1, 1>, (const void*)k_tiles<4, 1, 2>})
+            CHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
+    for (uint32_t nt : {1u, 0u})
+        for (uint32_t snt : {0u, 1u}) {
+            char nm[48];
+            snprintf(nm, sizeof nm, "w1_%s_st%s", nt ? "nt" : "def", snt ? "nt" : "def");
+            run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 1>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
+            snprintf(nm, sizeof nm, "w2_%s_st%s", nt ? "nt" : "def", snt ? "nt" : "def");
+            run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 2>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
+        }
+    for (uint32_t nt : {1u, 0u}) {
+        char nm[32];
+        snprintf(nm, sizeof nm, "tiles41_%s", nt ? "nt" : "def");
+        run(nm, (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out); });
+        snprintf(nm, sizeof nm, "tiles42_%s", nt ? "nt" : "def");
+        run(nm, (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 2>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out); });
+        snprintf(nm, sizeof nm, "tiles84_%s", nt ? "nt" : "def");
+        run(nm, (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_tiles<8, 4>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out); });
+    }
     return 0;
 }
