@@ -33,7 +33,7 @@ extern "C" {
                               4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
                               5: ipxg_timing gained plugin_overlapped
                               6: ipxg_profile takes a sampling period; ipxg_timing gained
-                                 slow_redos */
+                                 slow_redos; ipxg_plugin gained all_packets */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -123,7 +123,7 @@ typedef struct ipxg_flow_record {
     uint8_t dst_mac[6];
     uint16_t vlan_id;
     uint8_t end_reason;       /* IPXG_FLOW_END_*                                        */
-    uint8_t reserved0;
+    uint8_t reserved0;        /* IPXG_REC_PRE_EXPORTED, else zero                        */
     uint8_t reserved[8];      /* zero on export                                          */
     uint64_t ext;             /* the process plugins' per-flow handle (Flow::m_exts,
                                  see ipxg_plugin): zero on a record the engine creates,
@@ -362,6 +362,14 @@ typedef struct ipxg_packet_view {
  * the reference plugin throws PluginError: the walk stops and the call that ran it fails with
  * IPXG_EPLUGIN.  No C++ exception may leave a hook (the adapter of INTEGRATION.md catches them). */
 #define IPXG_PLUGIN_ERROR (-1)
+/* reserved0 of an exported record: the plugins' pre_export has been dealt with.  The reference
+ * calls plugins_pre_export on every export but a flush (cache.cpp:280,406,455,466,514; not in
+ * :290-320).  The host walk calls it at those sites for the flows it replays and marks every
+ * record it exports; a record the device exported (k_fin_list's evictions and timeouts,
+ * k_finish, k_expire) with a non-zero ext gets the registered plugins' pre_export, in
+ * registration order, on the calling thread inside ipxg_poll_exports -- then it carries the
+ * mark too.  (A device record with ext == 0 holds no plugin state: pre_export is not called.) */
+#define IPXG_REC_PRE_EXPORTED 0x01
 typedef struct ipxg_plugin {
     void* ctx;
     uint32_t proto_mask;
@@ -395,6 +403,11 @@ typedef struct ipxg_plugin {
      * after a hook returned IPXG_PLUGIN_ERROR, and after every walk of a batch -- pre_export
      * returns nothing, so a failure there is reported only here. */
     const char* (*error)(void* ctx);
+    /* ABI 6: 1 = the plugin's hooks act on every packet of every flow (pstats, phists, bstats and
+     * any plugin whose packets no port / prefix rule describes): every flow the batch touches is
+     * walked on the host -- the reference's behaviour (its hooks see every packet), at the host
+     * walk's rate.  The rule fields are then unused. */
+    uint32_t all_packets;
 } ipxg_plugin;
 
 /* Register a plugin (the order of registration is the order of the hook calls). */

@@ -179,6 +179,7 @@ struct ipxg_engine {
     // host walks add to the device-side counters (exports by reason, TopPorts)
     std::vector<ipxg_plugin> plugins;
     uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
+    bool plug_all = false;    // a registered plugin acts on every packet (ipxg_plugin.all_packets)
     double walk_phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};  // plugin_walk's phases (IPXG_WALK_TRACE)
     long walk_faults[7] = {0, 0, 0, 0, 0, 0, 0};        // ... and the minor page faults in each
     bool walk_trace = false;                             // IPXG_WALK_TRACE set at ipxg_create
@@ -488,6 +489,7 @@ static Params params(ipxg_engine* e) {
         p.plug_npref = e->plug_npref;
         p.plug_tab = (const uint32_t*)e->plug_d.p;
     }
+    p.plug_all = e->plug_all ? 1u : 0u;
     p.spin_max = STRICT_SPIN_MAX;
     if (const char* sm = std::getenv("IPXG_STRICT_SPIN_MAX"))  // test knob: a short watchdog
         p.spin_max = std::max<uint32_t>(16, (uint32_t)std::strtoul(sm, nullptr, 0));
@@ -532,7 +534,7 @@ static int check_ex(ipxg_engine* e) {
     if (e->ex_zero_pending) return IPXG_OK;  // the device counters are stale until zeroed; the host's are 0
     e->ex_count = ex_host(e)[0];
     e->ex_count6 = ex_host(e)[2];
-    if (ex_host(e)[1]) return set_err(e, IPXG_EDEVICE, "export buffer overflow (engine bug: capacity under-sized)");
+    if (ex_host(e)[1]) return set_err(e, IPXG_EDEVICE, "a kernel counted more exports than the export buffer holds (its capacity is sized before the launch from the live and batch counts)");
     return IPXG_OK;
 }
 
@@ -1019,7 +1021,7 @@ static int strict_submit(ipxg_engine* e, const BatchView& bv, uint32_t n) {
     HIPCHK(e, hipMemcpyAsync(&tail[0], qx + n - 1, 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(&tail[1], keyed + n - 1, 4, hipMemcpyDeviceToHost, e->st));
     if ((rc = sync_ctl(e))) return rc;
-    if (e->ctl_h->strict_fail) return set_err(e, IPXG_EDEVICE, "strict replay stalled (engine bug)");
+    if (e->ctl_h->strict_fail) return set_err(e, IPXG_EDEVICE, "strict replay: a lane waited STRICT_SPIN_MAX rounds without any packet of the batch finishing");
     if (prof_on(e)) {
         e->tm.ingest_ms += ev_ms(e, 0);
         e->tm.ingest_launches++;
@@ -1423,7 +1425,7 @@ struct FlowWalk {
     void export_flow(uint8_t reason, bool counted = true) {
         ipxg_flow_record o = rec;
         o.end_reason = reason;
-        o.reserved0 = 0;
+        o.reserved0 = IPXG_REC_PRE_EXPORTED;  // (a flush's too: the reference has no pre_export there)
         std::memset(o.reserved, 0, sizeof(o.reserved));
         if (out.ex.size() < out.ex.cap) out.ex.push_back(o);
         else out.spill.push_back(o);
@@ -1720,7 +1722,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     lpos[0] = 0;  // flow f's record in recs_in, when it is live
     for (uint32_t f = 0; f < nf; ++f) lpos[f + 1] = lpos[f] + ((fstate[f] & SLOT_LIVE) ? 1u : 0u);
     if (lpos[nf] != nlive)  // (the chunks' record copies below are sized by these positions)
-        return set_err(e, IPXG_EDEVICE, "plugin walk: live flows differ from the packed records (engine bug)");
+        return set_err(e, IPXG_EDEVICE, "plugin walk: the walked flows marked live differ in number from the records k_plugin_pack packed");
     // work units: contiguous flow ranges of about equal packet counts (flows in order of their
     // first packet), four per thread (at most HOST_CHUNKS), grouped into the copy chunks; each
     // unit's export buffer sized here for two exports per packet (more -- REINSERT chains -- go to
@@ -1995,7 +1997,7 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
         HIPCHK(e, hipMemcpy(&g, &e->aux_ctl_d->guard, sizeof(g), hipMemcpyDeviceToHost));
         if (g) {
             HIPCHK(e, hipMemset(&e->aux_ctl_d->guard, 0, sizeof(g)));
-            return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
+            return set_err(e, IPXG_EDEVICE, "k_plugin_apply: a walked flow's index or table slot was out of range");
         }
     }
     for (int k = 0; k < 5; ++k) e->host_end[k] += wo.end[k];
@@ -2033,6 +2035,7 @@ static int add_plugin_impl(ipxg_engine* e, const ipxg_plugin* pl) {
         return rc1;
     }
     e->follow_max = std::max<uint64_t>(e->follow_max, pl->follow_packets);
+    if (pl->all_packets) e->plug_all = true;  // (every touched flow walked: the rules do not matter)
     std::vector<DevRule> rules(e->plugins.size());
     for (size_t k = 0; k < rules.size(); ++k) {
         const ipxg_plugin& q = e->plugins[k];
@@ -2280,7 +2283,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         if ((uint32_t)(e->ctl_h->cx_alloc >> 32) != ncx || e->ctl_h->guard)
-            return set_err(e, IPXG_EDEVICE, "complex-flow count mismatch (engine bug)");
+            return set_err(e, IPXG_EDEVICE, "k_complex_rank found a different number of complex slots than the finalisers counted");
         const uint32_t npk = (uint32_t)(e->ctl_h->cx_alloc & 0xFFFFFFFFu);
         if ((rc = ensure(e, e->cx_list, (size_t)npk * 8 + 8))) return rc;
         if ((rc = ensure(e, e->cx_sorted, (size_t)npk * 8 + 8))) return rc;
@@ -2323,7 +2326,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ev_rec(e, 6);
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
-        if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "a complex flow's packets overran its segment (engine bug)");
+        if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "k_complex_gather: a complex flow had more packets in the batch than its slot counted (its segment's size)");
         if (!e->plugins.empty()) {  // the process plugins' flows: walked on the host
             int64_t dl = 0;
             if ((rc = plugin_walk(e, bv, p, cx, ncx, npk, &dl))) return rc;
@@ -2332,7 +2335,7 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
                 std::memcpy(e->ctl_h, &e->early.snap, sizeof(BatchCtl));
             } else {
                 if ((rc = sync_ctl(e))) return rc;
-                if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "plugin walk handed back a bad slot (engine bug)");
+                if (e->ctl_h->guard) return set_err(e, IPXG_EDEVICE, "k_plugin_apply: a walked flow's index or table slot was out of range");
             }
         }
         if (prof_on(e) && e->prof_level == 1) {
@@ -2555,7 +2558,7 @@ static int finish_impl(ipxg_engine* e) {
         HIPCHK(e, hipGetLastError());
         if ((rc = sync_ctl(e))) return rc;
         e->live = (uint32_t)((int64_t)e->live + e->ctl_h->strict_live);
-        if (e->live) return set_err(e, IPXG_EDEVICE, "strict finish left records (engine bug)");
+        if (e->live) return set_err(e, IPXG_EDEVICE, "strict finish: records still live after the whole table was exported");
         e->keys = 0;
         return IPXG_OK;
     }
@@ -2643,6 +2646,15 @@ static int poll_exports_impl(ipxg_engine* e, ipxg_flow_record* out, size_t cap, 
         HIPCHK(e, hipMemcpyAsync(out, e->ex + e->ex_head, k * sizeof(ipxg_flow_record), hipMemcpyDeviceToHost,
                                  e->st));
         HIPCHK(e, hipStreamSynchronize(e->st));
+        // pre_export of the device's exports that carry plugin state (IPXG_REC_PRE_EXPORTED)
+        if (!e->plugins.empty())
+            for (size_t i = 0; i < k; ++i) {
+                ipxg_flow_record& r = out[i];
+                if (!r.ext || (r.reserved0 & IPXG_REC_PRE_EXPORTED)) continue;
+                for (const ipxg_plugin& q : e->plugins)
+                    if (q.pre_export) q.pre_export(q.ctx, &r);
+                r.reserved0 |= IPXG_REC_PRE_EXPORTED;
+            }
     }
     e->ex_head += (uint32_t)k;
     if (k) e->ex6_valid = false;

@@ -63,13 +63,13 @@ struct BatchCtl {
     uint32_t fused;          // k_fin_list exported and emptied the flows it finalised (finish fused)
     uint32_t plugin_fail;    // k_classify found no slot for a plugin flow (table too full)
     int32_t strict_live;     // strict mode: records created - records exported
-    uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (engine bug)
+    uint32_t strict_fail;    // strict mode: a replay lane gave up waiting (IPXG_EDEVICE)
     uint32_t tb_any;         // OR of the time buckets of k_bin / k_bin_slow's records (0: all in bucket 0)
     uint32_t fin_deferred;   // finalise-list aggregates whose table probe failed (k_fin_list: table full)
     uint32_t cx_agg;         // k_complex_gather_rec: a complex flow's packets were folded into a k_bin_slow
                              // tile aggregate (or more k_bin aggregates than the range list holds)
     uint32_t cx_ranges;      // k_complex_gather_rec: k_bin tile aggregates of complex flows listed
-    uint32_t guard;          // bounds guards that fired (engine bug, reported as IPXG_EDEVICE): 1 more complex
+    uint32_t guard;          // bounds checks that failed (reported as IPXG_EDEVICE): 1 more complex
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
                              // past the table
     uint32_t spill_deferred; // of `deferred`: spills k_bin / k_bin_slow deferred (Params::defer_spill)
@@ -177,6 +177,9 @@ struct Params {
     uint32_t* pub_dst;
     const uint32_t* pub_ex;
     uint32_t pub_words, pub_seq;
+    // a registered process plugin acts on every packet (ipxg_plugin.all_packets): every flow the
+    // batch touches goes to the host walk (finalize_slot marks it SLOT_PLUGIN with SLOT_COMPLEX)
+    uint32_t plug_all;
     // k_bin_slow not launched: the previous batch had no slow packet (the empty launch and its
     // kernel boundary cost ~7 us per batch); k_bin flags slow packets it lists (BatchCtl::slow_redo)
     uint32_t slow_skip;

@@ -1171,7 +1171,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
         df = b.desc[first];
         have_df = true;
     }
-    bool cx = force_cx || (h.state & SLOT_HOST);  // a process plugin's flow: the host walks it
+    bool cx = force_cx || (h.state & SLOT_HOST) || p.plug_all;  // a process plugin's flow: the host walks it
     const uint32_t tb = h.tbits;
     if (tb >> 31) cx = true;
     else if (tb) {
@@ -1192,7 +1192,7 @@ __device__ __forceinline__ FinResult finalize_slot(const BatchView& b, const Par
     if (cx) {
         if (s != FIN_NO_SLOT) {
             HotSlot c = h;
-            c.state = h.state | SLOT_COMPLEX;
+            c.state = h.state | SLOT_COMPLEX | (p.plug_all ? SLOT_PLUGIN : 0u);
             c.pad = 0;
             t.hot(s) = c;
         }

@@ -135,7 +135,8 @@ class Plugin(ctypes.Structure):
                 ("masked", ctypes.c_uint32), ("follow_packets", ctypes.c_uint32),
                 ("prefix_mask", (ctypes.c_uint8 * 16) * 16),
                 ("copy_ctx", ctypes.c_void_p), ("free_ctx", ctypes.c_void_p),  # ABI 3 (C function pointers)
-                ("error", ERROR_FN)]  # ABI 4
+                ("error", ERROR_FN),  # ABI 4
+                ("all_packets", ctypes.c_uint32)]  # ABI 6
 
 # ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),

@@ -111,7 +111,15 @@ inline void fill_flow(ipxp::Flow& f, const ipxg_flow_record& r) {
 //   tls   payload 16 03 (handshake)      tls_parser.cpp:102-124 (record type 22, major 3)
 //   quic  UDP, long-header bit           quic_parser.cpp:1058-1117; follows 30 packets of a
 //                                        detected flow (QUIC_MAX_ELEMCOUNT, quic.cpp:340-346)
-// false for a kind without a rule here.
+//   ntp   port 123                       ntp.cpp:82-90 (post_create only, FLOW_FLUSH)
+//   sip   the 11 message-type prefixes   sip.cpp:105-172 (parse_msg_type: the payload's first
+//                                        4 bytes; post_create claims, pre_update flushes)
+//   wg    UDP, message types 1-4         wg.cpp:69-100, 140-147 (type byte, 3 zero bytes);
+//                                        follows every packet of a claimed flow (pre_update
+//                                        parses each: possible_wg, FLOW_FLUSH_WITH_REINSERT)
+//   any other plugin (pstats, phists, bstats, mqtt, rtsp -- 17 prefixes, more than a rule holds --,
+//   smtp, ...): every packet of every flow (ipxg_plugin.all_packets), as the reference calls
+//   every hook for every packet: correct for any plugin, at the host walk's rate.
 inline bool rule_for(const std::string& name, ipxg_plugin& q) {
     auto prefix = [&q](const char* s, uint8_t n) {
         q.prefix_len[q.n_prefixes] = n;
@@ -135,8 +143,20 @@ inline bool rule_for(const std::string& name, ipxg_plugin& q) {
         q.masked = 1;
         q.prefix_mask[0][0] = 0x80;
         q.follow_packets = 30;
+    } else if (name == "ntp") {
+        q.proto_mask = 3;
+        q.n_ports = 1;
+        q.ports[0] = 123;
+    } else if (name == "sip") {
+        q.proto_mask = 3;
+        for (const char* m : {"INVI", "REGI", "NOTI", "OPTI", "CANC", "INFO", "SIP/", "ACK ", "BYE ", "SUBS", "PUBL"})
+            prefix(m, 4);
+    } else if (name == "wg") {
+        q.proto_mask = 2;
+        for (const char* m : {"\x01\0\0\0", "\x02\0\0\0", "\x03\0\0\0", "\x04\0\0\0"}) prefix(m, 4);
+        q.follow_packets = 0xFFFFFFFFu;
     } else {
-        return false;
+        q.all_packets = 1;
     }
     return true;
 }

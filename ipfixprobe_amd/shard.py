@@ -3,9 +3,11 @@
 The reference scales by running one independent pipeline -- input thread + private
 NHTFlowCache -- per NIC queue, with symmetric RSS keeping both directions of a biflow on the
 same queue (ipfixprobe.cpp:381-464, dpdkDevice.cpp:230-262); caches never exchange state.
-Here: one process and one engine per GPU, and the canonical flow hash
-`lo = min(XXH64(key), XXH64(key_inv))` (the table key, cache.cpp:84-92 / ipxg_table.hpp)
-picks the rank, so both directions of a biflow land on the same GPU.  The only exchange is
+Here: one process and one engine per GPU, and a direction-free flow hash
+`lo = min(XXH64(key), XXH64(key_inv))` picks the rank, so both directions of a biflow land on
+the same GPU.  It stands for the NIC's symmetric RSS hash and is not the table key (that is
+XXH64 of the canonical-order key, ipxg_table.hpp; cache.cpp:84-92 keys on the forward and the
+inverse hash): ownership only needs some function both directions share.  The only exchange is
 the gather of the per-GPU export buffers to rank 0: `gather_records` (an all-gather of the
 record counts, then point-to-point transfers) or, for the IPFIX message streams formatted on
 each GPU every step, `StreamGather` (the exact stream bytes, point to point, sized by headers

@@ -1,5 +1,5 @@
-// ref_plugins.cpp -- TEST INFRASTRUCTURE.  The reference's own process plugins (dns, http, tls,
-// quic: their unmodified sources under /root/reference/src/plugins/process, built by
+// ref_plugins.cpp -- TEST INFRASTRUCTURE.  The reference's own process plugins (the 23 with a
+// functional test: their unmodified sources under /root/reference/src/plugins/process, built by
 // oracle/Makefile into oracle/_ref/libref_plugins.so together with this file) behind the
 // product's plugin adapter (ipfixprobe_amd/host/plugin_adapter.hpp), as ipxg_plugin structs the
 // engine's bridge (ipxg_add_plugin) and the oracle take alike.  Nothing in the product links
@@ -107,6 +107,16 @@ int ref_ext_text(uint64_t ext, char* out, int cap) {
         out[n] = 0;
     }
     return (int)s.size();
+}
+
+// The number of extensions an exported record carries: the reference's UniRec output sends one
+// record per extension (a second of the same type flushes the first, unirec.cpp:361-397), so a
+// flow with k extensions is k lines of a functional-test golden, and one with none is no line.
+int ref_ext_count(uint64_t ext) {
+    int n = 0;
+    if (ext)
+        for (ipxp::RecordExt* e = ipxg_ref::flow_of(ext)->m_exts; e; e = e->m_next) ++n;
+    return n;
 }
 
 // The consumer's release of an exported record's Flow (and its extension chain).
