@@ -150,6 +150,7 @@ struct ipxg_engine {
     // A/B knobs (environment, read at ipxg_create): IPXG_SYNC_FINISH=1 -- ipxg_finish waits for its
     // batch as before round 5; IPXG_NO_AHEAD=1 -- ipxg_submit launches no front ahead
     bool sync_finish = false, no_ahead = false;
+    bool no_line = false;  // IPXG_NO_LINE=1: k_bin without line mode (A/B knob)
     // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
     // the host has not read: completed by the next entry point (consume_pend) -- ipxg_submit of a
     // device batch first launches its own front behind it, gated on that block (Params::gate_mode),
@@ -218,7 +219,7 @@ struct ipxg_engine {
     DevBuf adefer_a, adefer_b;           // deferred tile aggregates (3 x 16 B each)
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 4 u32 arrays of nranks, then the key set
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
-    uint32_t bin_slots[2][2][2] = {};    // k_bin workgroups resident at once (its grid), [agg][wide][plug]
+    uint32_t bin_slots[2][2][2][2] = {};  // k_bin workgroups resident at once (its grid), [agg][wide][plug][line]
     // the plugins' rules flattened for k_bin's own check (Params::plug); plug_ok: they fit
     bool plug_ok = false;
     uint32_t plug_nport = 0, plug_npref = 0;
@@ -420,9 +421,11 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     const uint32_t P = 1u << bits;
     const uint64_t tiles = ((uint64_t)n + BIN_TILE_PKTS - 1) / BIN_TILE_PKTS;
     const int ag = e->tile_agg ? 1 : 0, wd = wide_walk(e) ? 1 : 0, pl = plug_fold(e) ? 1 : 0;
-    uint32_t& slots = e->bin_slots[ag][wd][pl];
+    // line mode (whole-line record stores) for the plain walk over at most BIN_LINE_P partitions
+    const int ln = !ag && !pl && P <= BIN_LINE_P && !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST) && !e->no_line ? 1 : 0;
+    uint32_t& slots = e->bin_slots[ag][wd][pl][ln];
     if (!slots) {
-        slots = bin_resident_blocks(e->cfg.device_id, ag != 0, wd != 0, pl != 0);
+        slots = bin_resident_blocks(e->cfg.device_id, ag != 0, wd != 0, pl != 0, ln != 0);
         if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
             slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
     }
@@ -432,7 +435,8 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     // aggregating batches follow a skewed one (the most loaded partition ~2.4x the mean with
     // the configs[2] Zipf mix); the others spill only if the skew changed since the last batch
     const double factor = std::max(e->tile_agg ? 3.0 : 1.5, 1.25 * e->skew);
-    const uint64_t seg = ((uint64_t)(mean * factor + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
+    uint64_t seg = ((uint64_t)(mean * factor + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
+    if (ln) seg = (seg + 8 + 7) & ~7ull;  // whole lines, and the carry's padded last line
     const uint32_t cols = 2 * grid;
     int rc;
     if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
@@ -455,6 +459,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     bv.rec = (uint4*)e->bin_rec.p;
     bv.count = (uint32_t*)e->bin_count.p;
     bv.seg_cap = (uint32_t)seg;
+    bv.line = (uint32_t)ln;
     bv.cols = cols;
     bv.bin_grid = grid;
     bv.part_bits = bits;
@@ -698,6 +703,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->walk_pin = std::getenv("IPXG_WALK_PAGEABLE") == nullptr;
     e->sync_finish = std::getenv("IPXG_SYNC_FINISH") != nullptr && std::atoi(std::getenv("IPXG_SYNC_FINISH")) != 0;
     e->no_ahead = std::getenv("IPXG_NO_AHEAD") != nullptr && std::atoi(std::getenv("IPXG_NO_AHEAD")) != 0;
+    e->no_line = std::getenv("IPXG_NO_LINE") != nullptr && std::atoi(std::getenv("IPXG_NO_LINE")) != 0;
     e->no_slow_skip = std::getenv("IPXG_NO_SLOW_SKIP") != nullptr && std::atoi(std::getenv("IPXG_NO_SLOW_SKIP")) != 0;
     if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
     int ndev = 0;

@@ -138,7 +138,8 @@ __device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y,
 #endif
 // ok: load the frame's chunks (caplen >= 48: the first 3 always; in the wide walk the later
 // ones only below caplen -- a chunk past it reads as zeros with no memory traffic)
-template <int NC>
+// AUX >= 0: that policy instead (line mode's k_bin)
+template <int NC, int AUX = -1>
 __device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok) {
     const uint32_t o = ok ? d.offset : BUF_OOB;
     Head<NC> h;
@@ -146,7 +147,7 @@ __device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, cons
     for (int k = 0; k < NC; ++k) {
         const uint32_t ok_k = k < 3 || (uint32_t)(16 * k) < d.caplen;
         h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, ok_k ? o + 16 * k : BUF_OOB, 0,
-                                                          NC > 3 ? IPXG_WIDE_LOAD_AUX : IPXG_LOAD_AUX));
+                                                          AUX >= 0 ? AUX : NC > 3 ? IPXG_WIDE_LOAD_AUX : IPXG_LOAD_AUX));
     }
     return h;
 }
@@ -189,8 +190,9 @@ __device__ __forceinline__ void xpose_head(uint4* xs, Head<4>& h) {
 #ifndef IPXG_DESC_AUX
 #define IPXG_DESC_AUX IPXG_LOAD_AUX
 #endif
+template <int AUX = -1>
 __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, uint32_t i) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, IPXG_DESC_AUX);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(desc, i * 16u, 0, AUX >= 0 ? AUX : IPXG_DESC_AUX);
     ipxg_pkt_desc d;
     d.offset = v.x;
     d.caplen = (uint16_t)v.y;
@@ -210,10 +212,10 @@ __device__ __forceinline__ void add_wave_sum(uint32_t* counter, uint32_t v) {
 }
 
 // Without tile aggregation: rank every packet record in its partition.
-__device__ __forceinline__ void tile_rank_all(uint32_t* hist, uint32_t pmask, const uint32_t (&r1)[BIN_K],
-                                              uint32_t (&rk)[BIN_K]) {
+template <int K>
+__device__ __forceinline__ void tile_rank_all(uint32_t* hist, uint32_t pmask, const uint32_t (&r1)[K], uint32_t (&rk)[K]) {
 #pragma unroll
-    for (int q = 0; q < BIN_K; ++q)
+    for (int q = 0; q < K; ++q)
         if (rk[q] != NO_REC) rk[q] = atomicAdd(&hist[r1[q] & pmask], 1u);
 }
 
@@ -344,10 +346,133 @@ __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t 
 // the block's record counts per partition (its column of bv.count)
 __device__ __forceinline__ void seg_counts(const uint32_t* fill, uint32_t P, const BinView& bv, uint32_t col) {
 #ifdef IPXG_EXP_NOEMIT
-    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + col] = 0;
+    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[seg_count_idx(bv, q, col)] = 0;
 #else
-    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[(size_t)q * bv.cols + col] = min(fill[q], bv.seg_cap);
+    for (uint32_t q = threadIdx.x; q < P; q += IPXG_BLOCK) bv.count[seg_count_idx(bv, q, col)] = min(fill[q], bv.seg_cap);
 #endif
+}
+
+// ---- line mode: whole-line record stores -------------------------------------------------
+// A tile's run of one partition is a few records (udp64: 2048 packets over 256 partitions, 8 on
+// average) at whatever offset the partition's segment has reached, so tile_emit writes most
+// 128-byte lines in two or three pieces, tiles apart.  With the frames streaming through L2 the
+// partial lines are written back partially, and a partial line costs the memory a
+// read-modify-write: tools/membench's k_bin load pattern plus k_bin's 160 MB of records takes
+// 195 us with whole-line stores and 264 us with the same runs shifted off the line boundaries
+// (default-policy frame loads; with `nt` loads 250 / 263 us).  Line mode (the non-aggregating
+// k_bin with at most LINE_P partitions) keeps each partition's last partial line in LDS (the
+// carry) and stores only whole lines: a tile completes the lines its records and the carry fill,
+// the rest stays for the next tile, and the last tile pads each carry to a whole line with
+// NO_REC fillers (k_reduce skips them).  The carry's 28 KiB is paid for with 1024-packet tiles
+// (LINE_K steps): the workgroup stays within the LDS of 3 per CU.
+constexpr uint32_t LINE_P = BIN_LINE_P;  // partitions (at most)
+constexpr int LINE_K = 4;             // packets per lane per tile
+constexpr uint32_t LINE_C = 7;        // carried records per partition (less than a line)
+constexpr uint32_t LINE_MAXL = (LINE_K * IPXG_BLOCK + LINE_C * LINE_P) / 8;  // lines one tile completes, at most
+constexpr uint32_t LINE_ITERS = (LINE_MAXL * 8 + IPXG_BLOCK - 1) / IPXG_BLOCK;   // store rounds per tile
+#ifndef IPXG_LINE_AUX
+#define IPXG_LINE_AUX 0  // cache policy of line mode's frame and descriptor loads (membench: default policy)
+#endif
+
+struct LineLds {
+    uint32_t* hist;   // LINE_P: the tile's records per partition (rank counters)
+    uint32_t* fill;   // LINE_P: records stored in the workgroup's segment (a multiple of 8)
+    uint32_t* pos;    // LINE_P: the partition's run in stage | its first completed line << 16
+    uint8_t* ccnt;    // LINE_P: carried records
+    uint8_t* lpart;   // LINE_MAXL: the partition of each line the tile completes
+    uint4* stage;     // LINE_K * 256: the tile's records, then grouped by partition
+    uint4* carry;     // LINE_P * LINE_C
+    uint32_t* scan_s;
+};
+
+// a record that found its segment full: accumulated into the table (or deferred), as tile_emit
+__device__ __forceinline__ void line_spill(const TableView& t, BatchCtl* ctl, uint32_t* deferred_list, const uint4& r,
+                                           uint32_t& spilled, bool defer_spill) {
+    spilled++;
+    if (defer_spill) atomicAdd(&ctl->spill_deferred, 1u);
+    if (defer_spill || !merge_packet_atomic(t, ((uint64_t)r.y << 32) | r.x, r.z, r.w, &ctl->new_keys))
+        defer_packet(ctl, deferred_list, r.z, true);
+}
+
+// After tile_rank_all (rk[q] = the record's rank in its partition, hist[] = the counts): the
+// tile's records grouped by partition in stage, then every line that the carry and the tile's run
+// complete stored whole (8 consecutive lanes per line, a wave stores 8 lines), then the rest
+// carried.  Fixed store rounds (LINE_ITERS; a round past the tile's lines stores to a dummy line)
+// for the reason tile_emit gives.
+template <int K>
+__device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, uint32_t pmask, const BinView& bv,
+                                                uint32_t col, const TableView& t, BatchCtl* ctl,
+                                                uint32_t* deferred_list, const uint32_t (&r0)[K],
+                                                const uint32_t (&r1)[K], const uint32_t (&r2)[K],
+                                                const uint32_t (&rk)[K], uint32_t tile, uint32_t& spilled,
+                                                bool defer_spill) {
+    const uint32_t tid = threadIdx.x;
+    __syncthreads();  // the counts are complete; every lane has its records back from stage
+    uint32_t n = 0, cc = 0, W = 0;
+    if (tid < P) {
+        n = L.hist[tid];
+        cc = L.ccnt[tid];
+        W = (cc + n) & ~7u;  // records of the lines this tile completes
+    }
+    uint32_t tot;  // (run starts in the high half, first lines in the low: no carry across, 1024 + 352)
+    const uint32_t sc = block_exclusive_scan<IPXG_BLOCK>((n << 16) | (W >> 3), L.scan_s, &tot);
+    const uint32_t nrec = (tot & 0xFFFFu) * 8;
+    if (tid < P) {
+        L.pos[tid] = (sc >> 16) | ((sc & 0xFFFFu) << 16);
+        for (uint32_t l = 0; l < (W >> 3); ++l) L.lpart[(sc & 0xFFFFu) + l] = (uint8_t)tid;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+        if (rk[q] != NO_REC)
+            L.stage[(L.pos[r1[q] & pmask] & 0xFFFFu) + rk[q]] =
+                make_uint4(r0[q], r1[q], tile + (uint32_t)q * IPXG_BLOCK + tid, r2[q]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t it = 0; it < LINE_ITERS; ++it) {
+        const uint32_t k = it * IPXG_BLOCK + tid;
+        const bool valid = k < nrec;
+        const uint32_t part = valid ? L.lpart[k >> 3] : 0u;
+        const uint32_t ps = L.pos[part], c = L.ccnt[part];
+        const uint32_t j = valid ? ((k >> 3) - (ps >> 16)) * 8 + (k & 7) : 0u;  // record j of the partition's lines
+        const uint4 r = j < c ? L.carry[part * LINE_C + j] : L.stage[(ps & 0xFFFFu) + j - c];
+        const uint32_t at = L.fill[part] + j;
+        const bool fits = valid && at < bv.seg_cap;  // (seg_cap and fill are multiples of 8: whole lines)
+        uint4* dst = fits ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + at] : &g_dummy_rec[tid & 63];
+        *dst = r;
+        if (valid && !fits) line_spill(t, ctl, deferred_list, r, spilled, defer_spill);
+    }
+    __syncthreads();  // the carry and the stage have been read
+    if (tid < P) {
+        const uint32_t st = L.pos[tid] & 0xFFFFu;
+        if (W == 0) {
+            for (uint32_t m = 0; m < n; ++m) L.carry[tid * LINE_C + cc + m] = L.stage[st + m];
+            L.ccnt[tid] = (uint8_t)(cc + n);
+        } else {
+            const uint32_t nc = cc + n - W;
+            for (uint32_t m = 0; m < nc; ++m) L.carry[tid * LINE_C + m] = L.stage[st + (W - cc) + m];
+            L.ccnt[tid] = (uint8_t)nc;
+            L.fill[tid] += W;
+        }
+    }
+    __syncthreads();  // (hist is reset by the next tile, whose packet loop rewrites the stage)
+}
+
+// The workgroup's carries after its last tile: one line per partition, padded with NO_REC.
+__device__ __forceinline__ void line_flush(const LineLds& L, uint32_t P, const BinView& bv, uint32_t col,
+                                           const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
+                                           uint32_t& spilled, bool defer_spill) {
+    for (uint32_t k = threadIdx.x; k < P * 8; k += IPXG_BLOCK) {
+        const uint32_t part = k >> 3, j = k & 7, c = L.ccnt[part];
+        if (c == 0) continue;
+        const uint32_t at = L.fill[part] + j;
+        const uint4 r = j < c ? L.carry[part * LINE_C + j] : make_uint4(0, 0, NO_REC, 0);
+        if (at < bv.seg_cap) bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + at] = r;
+        else if (j < c) line_spill(t, ctl, deferred_list, r, spilled, defer_spill);
+    }
+    __syncthreads();
+    if (threadIdx.x < P && L.ccnt[threadIdx.x]) L.fill[threadIdx.x] += 8;
+    __syncthreads();
 }
 
 // keep one keyed, unfragmented packet's record in slot j (ranked in tile_aggregate)
@@ -568,11 +693,17 @@ constexpr uint32_t KBIN_PMAX = 1u << IPXG_KBIN_PMAX_BITS;  // (the host picks at
 #endif
 // PLUG (with WIDE only): the process plugins' pre-classification in the same walk (Params::plug;
 // the hits' keys and the undecided packets listed for k_plugin_marks) -- no k_classify pass.
-template <bool AGG, bool WIDE, bool PLUG = false>
+// LINE (without AGG and PLUG): line mode (tile_emit_lines), 1024-packet tiles.
+template <bool AGG, bool WIDE, bool PLUG = false, bool LINE = false>
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : IPXG_BIN_NARROW_WPE)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     static_assert(!PLUG || WIDE, "the plugin check reads the wide walk's window");
+    static_assert(!LINE || (!AGG && !PLUG), "line mode: the plain record walk");
+    constexpr int K = LINE ? LINE_K : BIN_K;  // packets per lane per tile
+    constexpr uint32_t TILE = (uint32_t)K * IPXG_BLOCK;
+    constexpr uint32_t PM = LINE ? LINE_P : KBIN_PMAX;  // partitions (at most)
+    constexpr int LAUX = LINE ? IPXG_LINE_AUX : -1;     // load policy (-1: the walk's default)
     if (p.pub_seq && blockIdx.x == 0) {  // the pending batch's control block to the host (k_publish's layout)
         const uint32_t* src = reinterpret_cast<const uint32_t*>(p.prev_ctl);
         for (uint32_t w = threadIdx.x; w < p.pub_words; w += IPXG_BLOCK) p.pub_dst[w] = src[w];
@@ -583,23 +714,30 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             __hip_atomic_store(&p.pub_dst[p.pub_words + 4], p.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (gated(p)) return;  // launched ahead of the host's reading of the previous batch, which needs it
-    __shared__ uint32_t hist[KBIN_PMAX];  // 8 KiB: per-partition rank / run start
-    __shared__ uint32_t fill[KBIN_PMAX];  // 8 KiB: slots in the block's segments
-    __shared__ uint4 stage[BIN_TILE];                   // 32 KiB: tile hash keys, then the slots by partition
+    __shared__ uint32_t hist[PM];  // 8 KiB: per-partition rank / run start
+    __shared__ uint32_t fill[PM];  // 8 KiB: slots in the block's segments
+    __shared__ uint4 stage[TILE];                       // 32 KiB: tile hash keys, then the slots by partition
+    __shared__ uint32_t lpos[LINE ? LINE_P : 1];        // line mode (LineLds)
+    __shared__ uint8_t lccnt[LINE ? LINE_P : 1];
+    __shared__ uint8_t llpart[LINE ? LINE_MAXL : 1];
+    __shared__ uint4 lcarry[LINE ? LINE_P * LINE_C : 1];  // 28 KiB
     __shared__ uint32_t tcnt[AGG ? TAGG_HASH : 1];      // 16 KiB: tile hash counts / aggregate ids
     __shared__ TileAgg tagg[AGG ? TAGG_CAP : 1];        // 8 KiB
     __shared__ uint16_t part_of[AGG ? BIN_TILE : 1];    // 4 KiB
     __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
     __shared__ uint32_t nagg;
     const BinLds L = {hist, fill, stage, tcnt, tagg, part_of, scan_s, &nagg};
+    const LineLds LL = {hist, fill, lpos, lccnt, llpart, stage, lcarry, scan_s};
     uint32_t folded = 0;
     __shared__ uint32_t nslow[2];  // slow packets of the tile (by tile parity)
     __shared__ uint32_t nmark;     // PLUG: marks listed so far
     // timestamps (sec << 32 | usec) of each step's first and last packet per wave: the order
     // check across wave boundaries, done once per tile (within a wave it is a DPP shift)
-    __shared__ uint64_t bnd_first[BIN_K][IPXG_BLOCK / 64], bnd_last[BIN_K][IPXG_BLOCK / 64];
+    __shared__ uint64_t bnd_first[K][IPXG_BLOCK / 64], bnd_last[K][IPXG_BLOCK / 64];
     const uint32_t tid = threadIdx.x;
     for (uint32_t q = tid; q < (1u << bv.part_bits); q += IPXG_BLOCK) fill[q] = 0;
+    if (LINE)
+        for (uint32_t q = tid; q < LINE_P; q += IPXG_BLOCK) lccnt[q] = 0;
     if (tid < 2) nslow[tid] = 0;
     if (tid == 0) nmark = 0;
     uint4* const my_marks = PLUG ? bv.marks + (size_t)blockIdx.x * bv.slow_stride : nullptr;
@@ -630,7 +768,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     constexpr int NC = WIDE ? WD / 4 : (XP ? 4 : 3);
     // the wave's transpose area (XP): the stage array is free during the packet loop
     uint4* const xs = reinterpret_cast<uint4*>(stage) + (tid >> 6) * 320u;
-    static_assert(IPXG_BLOCK / 64 * 320 <= BIN_TILE, "transpose areas fit the stage array");
+    static_assert(!XP || IPXG_BLOCK / 64 * 320 <= TILE, "transpose areas fit the stage array");
     auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(d); };
     bool nonmono = false;
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
@@ -667,7 +805,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 #define IPXG_BIN_HA_AGG 2
 #endif
     constexpr int DA = IPXG_BIN_DA, HA = AGG ? IPXG_BIN_HA_AGG : IPXG_BIN_HA;
-    static_assert(BIN_K % DA == 0 && BIN_K % HA == 0 && HA < DA && DA <= BIN_K, "pipeline distances");
+    static_assert(K % DA == 0 && K % HA == 0 && HA < DA && DA <= K, "pipeline distances");
     const uint32_t nsteps = (b.n + IPXG_BLOCK - 1) / IPXG_BLOCK;
     const uint32_t G = gridDim.x;
 #ifndef IPXG_BIN_BALANCE  // A/B knob: 0 = whole tiles only (the round-4 assignment) for every variant
@@ -677,16 +815,16 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // walk is bandwidth-bound -- a block alone on its CU in the last round runs faster -- and one
     // more (partial) tile's emit per block cost it 1.4 % (udp64, gpurun_out/v5b): whole tiles there.
     constexpr bool BAL = IPXG_BIN_BALANCE && AGG;
-    const uint32_t tiles = (nsteps + BIN_K - 1) / BIN_K;
-    const uint32_t F = BAL ? nsteps / (BIN_K * G) : (blockIdx.x < tiles ? (tiles - blockIdx.x + G - 1) / G : 0u);
-    const uint32_t rb = BAL ? F * BIN_K * G : 0u;  // the remainder's first step
-    const uint32_t rs = BAL ? nsteps - rb : 0u;     // ... and its steps (< BIN_K * G)
+    const uint32_t tiles = (nsteps + K - 1) / K;
+    const uint32_t F = BAL ? nsteps / (K * G) : (blockIdx.x < tiles ? (tiles - blockIdx.x + G - 1) / G : 0u);
+    const uint32_t rb = BAL ? F * K * G : 0u;  // the remainder's first step
+    const uint32_t rs = BAL ? nsteps - rb : 0u;     // ... and its steps (< K * G)
     const uint32_t r_lo = rb + (uint32_t)((uint64_t)rs * blockIdx.x / G);
     const uint32_t r_hi = rb + (uint32_t)((uint64_t)rs * (blockIdx.x + 1) / G);
     const uint32_t ntile = F + (r_hi > r_lo ? 1u : 0u);
-    auto tile_lo = [&](uint32_t k) { return k < F ? (k * G + blockIdx.x) * BIN_K : r_lo; };  // first step
+    auto tile_lo = [&](uint32_t k) { return k < F ? (k * G + blockIdx.x) * K : r_lo; };  // first step
     auto tile_lim = [&](uint32_t k) {  // packet limit (exclusive) of tile k; an empty range past the last
-        const uint32_t hi = k < F ? (k * G + blockIdx.x) * BIN_K + BIN_K : (k == F ? r_hi : r_lo);
+        const uint32_t hi = k < F ? (k * G + blockIdx.x) * K + K : (k == F ? r_hi : r_lo);
         return min(b.n, hi * IPXG_BLOCK);
     };
     // a prefetch past a tile's range reads nothing (an index past every descriptor)
@@ -701,18 +839,20 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
 #pragma unroll
     for (int k = 0; k < DA; ++k) {
         const uint32_t i = clamp((tile_lo(0) + k) * IPXG_BLOCK + tid, ntile ? tile_lim(0) : 0u);
-        Dr[k] = load_desc(rs_desc, i);
+        Dr[k] = load_desc<LAUX>(rs_desc, i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
             if constexpr (XP) Hr[h] = load_head_x(rs_arena, Dr[h], want(Dr[h]), Xr[h]);
-            else Hr[h] = load_head<NC>(rs_arena, Dr[h], want(Dr[h]));
+            else Hr[h] = load_head<NC, LAUX>(rs_arena, Dr[h], want(Dr[h]));
         } else {
 #pragma unroll
             for (int q = 0; q < 3; ++q) g_dummy_rec[(k * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
         }
     }
+    constexpr uint32_t EMIT_ST = LINE ? LINE_ITERS : TILE / IPXG_BLOCK;  // a tile's record stores per lane
+    static_assert((DA * 3 + EMIT_ST) * 64 <= 32 * 64, "g_dummy_rec");
 #pragma unroll
-    for (int q = 0; q < BIN_TILE / IPXG_BLOCK; ++q) g_dummy_rec[(DA * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < (int)EMIT_ST; ++q) g_dummy_rec[(DA * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
     for (uint32_t tk = 0; tk < ntile; ++tk) {
         const uint32_t tile = tile_lo(tk) * IPXG_BLOCK;
         const uint32_t lim = tile_lim(tk);
@@ -723,16 +863,16 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         const u32x2 tpred = __builtin_amdgcn_raw_buffer_load_b64(rs_desc, tile ? tile * 16u - 8u : BUF_OOB, 0, 0);
         PROBE_T(t0);
 #pragma unroll
-        for (uint32_t k = 0; k < (KBIN_PMAX + IPXG_BLOCK - 1) / IPXG_BLOCK; ++k)
+        for (uint32_t k = 0; k < (PM + IPXG_BLOCK - 1) / IPXG_BLOCK; ++k)
             if (k * IPXG_BLOCK + tid < P) hist[k * IPXG_BLOCK + tid] = 0;
         __syncthreads();
         if (tid == 0) nslow[par ^ 1] = 0;  // the next tile's (last read before this barrier)
         PROBE_T(t1);
         PROBE_ADD(0, t0, t1);
-        uint32_t r0[BIN_K], r1[BIN_K], r2[BIN_K], rk[BIN_K], ix[BIN_K];
+        uint32_t r0[K], r1[K], r2[K], rk[K], ix[K];
         if constexpr (!LR) {
 #pragma unroll
-            for (int q = 0; q < BIN_K; ++q) {
+            for (int q = 0; q < K; ++q) {
                 r0[q] = r1[q] = r2[q] = ix[q] = 0;
                 rk[q] = NO_REC;
             }
@@ -740,9 +880,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         // The wide walk's steps are unrolled DA at a time (the register rings' period), not all
         // BIN_K: eight inlined copies of parse_medium made the kernel larger than the
         // instruction cache.  (Record slot j is then a runtime index: tile_rank selects.)
-        constexpr int SU = WIDE ? DA : BIN_K;
+        constexpr int SU = WIDE ? DA : K;
 #pragma unroll 1
-        for (int g = 0; g < BIN_K; g += SU) {
+        for (int g = 0; g < K; g += SU) {
 #pragma unroll
         for (int jj = 0; jj < SU; ++jj) {
             const int j = g + jj;
@@ -757,11 +897,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             // reuses it while the load is in flight and must drain every load to do so
             asm volatile("" ::"v"(hc.c[2].z));
             // issue: the descriptor DA steps ahead, the head HA steps ahead
-            const uint32_t ia = j + DA < BIN_K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - BIN_K) * IPXG_BLOCK + tid;
-            Dr[jj % DA] = load_desc(rs_desc, j + DA < BIN_K ? clamp(ia, lim) : clamp(ia, next_lim));
+            const uint32_t ia = j + DA < K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - K) * IPXG_BLOCK + tid;
+            Dr[jj % DA] = load_desc<LAUX>(rs_desc, j + DA < K ? clamp(ia, lim) : clamp(ia, next_lim));
             const ipxg_pkt_desc dh = Dr[(jj + HA) % DA];
             if constexpr (XP) Hr[jj % HA] = load_head_x(rs_arena, dh, want(dh), Xr[jj % HA]);
-            else Hr[jj % HA] = load_head<NC>(rs_arena, dh, want(dh));
+            else Hr[jj % HA] = load_head<NC, LAUX>(rs_arena, dh, want(dh));
             const bool act = i < lim;
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
@@ -826,7 +966,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         }
         if constexpr (LR) {  // the lane's own records back (tile_emit's first barrier precedes any other lane's writes)
 #pragma unroll
-            for (int q = 0; q < BIN_K; ++q) {
+            for (int q = 0; q < K; ++q) {
                 const uint4 r = stage[q * IPXG_BLOCK + tid];
                 r0[q] = r.x;
                 r1[q] = r.y;
@@ -838,16 +978,20 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         PROBE_T(t2);
         PROBE_ADD(1, t1, t2);
 #ifndef IPXG_EXP_NOSKEL  // timing experiment (with IPXG_EXP_LOADONLY only): no rank / emit phase at all
-        if (AGG) tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
-        else tile_rank_all(hist, pmask, r1, rk);
-        tile_emit<false, AGG, KBIN_PMAX>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2,
-                                         rk, ix, tile, spilled, p.defer_spill != 0);
+        if constexpr (AGG) tile_aggregate<false>(L, pmask, r0, r1, r2, rk, ix, tile, folded);
+        else tile_rank_all<K>(hist, pmask, r1, rk);
+        if constexpr (LINE)
+            tile_emit_lines<K>(LL, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, r0, r1, r2, rk, tile, spilled,
+                               p.defer_spill != 0);
+        else
+            tile_emit<false, AGG, KBIN_PMAX>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2,
+                                             rk, ix, tile, spilled, p.defer_spill != 0);
 #endif
         PROBE_T(t3);
         PROBE_ADD(2, t2, t3);
         slow_fill += nslow[par];  // final: read after the tile's barriers
         par ^= 1;
-        if (tid < BIN_K * (IPXG_BLOCK / 64)) {  // the wave boundaries of the tile
+        if (tid < K * (IPXG_BLOCK / 64)) {  // the wave boundaries of the tile
             const uint32_t j = tid / (IPXG_BLOCK / 64), w = tid % (IPXG_BLOCK / 64);
             const uint32_t i0 = tile + j * IPXG_BLOCK + w * 64;
             const uint64_t pred = w ? bnd_last[j][w - 1]
@@ -873,6 +1017,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         if (slow_fill && p.slow_skip) ctl->slow_redo = 1;  // (no k_bin_slow behind this launch)
     }
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
+    if constexpr (LINE) line_flush(LL, P, bv, blockIdx.x, t, ctl, deferred_list, spilled, p.defer_spill != 0);
     seg_counts(fill, P, bv, blockIdx.x);
     if (PLUG && tid == 0) bv.mark_cnt[blockIdx.x] = nmark;
     // block statistics, hist reused as the counter block
@@ -1124,15 +1269,16 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
 
 typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint4*, uint32_t*, uint4*,
                           unsigned long long*);
-static BinKernel bin_kernel(bool agg, bool wide, bool plug = false) {
+static BinKernel bin_kernel(bool agg, bool wide, bool plug = false, bool line = false) {
     if (plug) return agg ? k_bin<true, true, true> : k_bin<false, true, true>;  // (plug: the wide walk)
+    if (line && !agg) return wide ? k_bin<false, true, false, true> : k_bin<false, false, false, true>;
     return agg ? (wide ? k_bin<true, true> : k_bin<true, false>) : (wide ? k_bin<false, true> : k_bin<false, false>);
 }
 
-uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug) {
+uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool line) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide, plug), IPXG_BLOCK, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide, plug, line), IPXG_BLOCK, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return (uint32_t)std::max(1, std::min(cus * per_cu, (int)BIN_MAX_GRID));
@@ -1141,7 +1287,7 @@ uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug) {
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats) {
-    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0, p.plug != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
+    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0, p.plug != 0, bv.line != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
                        t, f, bv, ctl, slow_list, deferred_list, agg_list, stats);
 }
 
@@ -1292,9 +1438,9 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     __shared__ uint32_t cnt[C_N];
     __shared__ uint32_t scan_s[RED_THREADS / 64 + 1];
     __shared__ uint32_t fin_base;
-    const uint32_t part = blockIdx.x;
+    const uint32_t part = red_part(blockIdx.x, 1u << bv.part_bits);
     const uint32_t tid = threadIdx.x;
-    if (part == 0) {  // the other control block for the next batch, the cleared export counters
+    if (blockIdx.x == 0) {  // the other control block for the next batch, the cleared export counters
         if (zero_ctl)
             for (uint32_t w = tid; w < sizeof(BatchCtl) / 4; w += RED_THREADS) reinterpret_cast<uint32_t*>(zero_ctl)[w] = 0;
         if (zero_ex && tid < 3) zero_ex[tid] = 0;
@@ -1303,14 +1449,14 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     // the columns written: every k_bin workgroup's, and those of the k_bin_slow workgroups
     // that had slow packets (the others return without writing theirs)
     const uint32_t cols = bv.cols;
-    const uint32_t* cnts = bv.count + (size_t)part * bv.cols;
+
     PROBE_T(q0t);
     // segment lengths -> exclusive prefix (cols <= RED_MAX_COLS = 4 per thread)
     uint32_t v[RED_MAX_COLS / RED_THREADS], my = 0;
 #pragma unroll
     for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
         const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
-        v[q] = c < bv.bin_grid || (c < cols && bv.slow_cnt[c - bv.bin_grid]) ? cnts[c] : 0;
+        v[q] = c < bv.bin_grid || (c < cols && bv.slow_cnt[c - bv.bin_grid]) ? bv.count[seg_count_idx(bv, part, c)] : 0;
         my += v[q];
     }
     uint32_t total;
@@ -1422,6 +1568,12 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
                         ok[u] = j0 + u < ng && lane <= (cs[u] & 63) && r[u].z != NO_REC;
                         e[u] = r[u].x & (RED_ENTRIES - 1);
                     }
+#ifdef IPXG_EXP_RED_NOFOLD  // timing experiment: the record loads without the fold
+#pragma unroll
+                    for (uint32_t u = 0; u < RED_U; ++u)
+                        if (ok[u] && r[u].x == 0x9E3779B9u && r[u].y == 0x7F4A7C15u) atomicAdd(&cnt[C_FAIL], 1u);
+                    return;
+#endif
                     // the probes' first reads, issued together (no atomic of this group before them)
 #pragma unroll
                     for (uint32_t u = 0; u < RED_U; ++u) k[u] = ok[u] && !rec_is_agg(r[u]) ? ht[e[u]].key : 0ull;
@@ -1912,7 +2064,7 @@ __global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexV
         uint32_t n = 0;
         if (s < nseg) {
             const uint32_t c = s % bv.cols;
-            if (c < bv.bin_grid || bv.slow_cnt[c - bv.bin_grid]) n = bv.count[s];  // (else a k_bin_slow column left unwritten)
+            if (c < bv.bin_grid || bv.slow_cnt[c - bv.bin_grid]) n = bv.count[seg_count_idx(bv, s / bv.cols, c)];  // (else a k_bin_slow column left unwritten)
         }
         uint32_t tot;
         const uint32_t at = block_exclusive_scan<256>(n, scan_s, &tot);

@@ -251,10 +251,10 @@ struct FragView {
 // canonical flow hash (bits 32.. of lo), one segment per k_bin and per k_bin_slow workgroup
 // ("column"), so every workgroup appends to its own segments without device atomics.
 // Record = {lo, hi, packet index, pack_misc()}.  Segment (part, col) starts at record
-// (part * cols + col) * seg_cap; count[part * cols + col] = its length.
+// (part * cols + col) * seg_cap; count[seg_count_idx(part, col)] = its length.
 struct BinView {
     uint4* rec;          // parts * cols * seg_cap records
-    uint32_t* count;     // parts * cols segment lengths (zeroed per batch)
+    uint32_t* count;     // parts * cols segment lengths (seg_count_idx; every column written per batch)
     uint32_t seg_cap;    // records per segment (a full segment spills to device atomics)
     uint32_t cols;       // 2 * bin_grid: k_bin's columns, then k_bin_slow's
     uint32_t bin_grid;   // workgroups of k_bin (and of k_bin_slow)
@@ -264,7 +264,26 @@ struct BinView {
     uint4* marks;          // Params::plug: workgroup b's plugin marks at marks[b * slow_stride ...] (k_bin's,
     uint32_t* mark_cnt;    //   then k_bin_slow's), mark_cnt[b] of them: {key lo, key hi, index | kind << 30, 0}
     uint32_t slow_skip;    // Params::slow_skip (k_reduce returns when k_bin flagged slow_redo)
+    uint32_t line;         // k_bin's line mode (ipxg_ingest.hip: whole-line record stores; seg_cap % 8 == 0)
 };
+constexpr uint32_t BIN_LINE_P = 256;  // line mode's partitions, at most (ipxg_ingest.hip LINE_P)
+// The segment counts, column-major: workgroup col's counts of all partitions are contiguous, so
+// each k_bin / k_bin_slow workgroup writes whole lines of them (partition-major, every count was
+// a 4-byte piece of a line the other columns' workgroups, on other XCDs, wrote the rest of).
+// k_reduce's workgroup for a partition reads one count per column; its partition is chosen so
+// that the 32 partitions sharing a line of counts run on one XCD (red_part).
+#ifndef IPXG_COUNTS_T
+#define IPXG_COUNTS_T 1
+#endif
+__host__ __device__ inline size_t seg_count_idx(const BinView& bv, uint32_t part, uint32_t col) {
+    return IPXG_COUNTS_T ? ((size_t)col << bv.part_bits) | part : (size_t)part * bv.cols + col;
+}
+// k_reduce workgroup b's partition (of P): workgroups go to the 8 XCDs round-robin (b % 8)
+__host__ __device__ inline uint32_t red_part(uint32_t b, uint32_t P) {
+    if (!IPXG_COUNTS_T || P < 256) return b;
+    const uint32_t x = b & 7u, i = b >> 3;
+    return (i >> 5) * 256u + x * 32u + (i & 31u);
+}
 #ifndef IPXG_BIN_K
 #define IPXG_BIN_K 8  // packets per lane per k_bin tile
 #endif
@@ -337,7 +356,7 @@ static_assert(sizeof(PluginFlow) == 160, "plugin flow image");
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
 // tile-aggregating variant (more LDS)
-uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug);
+uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool line);
 // deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
 // 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,

@@ -12,6 +12,10 @@
 //   op 7  ops 1+2+2 together (the full udp fold: add64 + 2 x max32), random entry
 //   op 8  ds_max_u64 no-return, random entry
 //   op 9  random entry, ds_read_b64 then ds_write_b64 (non-atomic RMW, racy; cost only)
+//   op 10 ds_max_u32 no-return, lane-private consecutive words (atomic cost without conflicts)
+//   op 11 ds_max_u32 no-return, random word of a 4-byte array (struct-of-arrays field)
+//   op 12 ds_add_u64 no-return, random word of an 8-byte array (struct-of-arrays field)
+//   op 13 ds_read_b32 random word of a 4-byte array
 // Usage: ldsbench <op> <iters> <entries (<= 2048)>
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -56,6 +60,14 @@ __global__ __launch_bounds__(1024) void k_lds(uint32_t iters, uint32_t nent, uns
             atomicMax(reinterpret_cast<uint32_t*>(ent + 28), ~it);
         } else if constexpr (OP == 8) {
             atomicMax(reinterpret_cast<unsigned long long*>(ent + 8), (unsigned long long)it);
+        } else if constexpr (OP == 10) {
+            atomicMax(reinterpret_cast<uint32_t*>(tab) + threadIdx.x, it);
+        } else if constexpr (OP == 11) {
+            atomicMax(reinterpret_cast<uint32_t*>(tab) + e, it);
+        } else if constexpr (OP == 12) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(tab) + e, (1ull << 40) | 64u);
+        } else if constexpr (OP == 13) {
+            acc += reinterpret_cast<volatile uint32_t*>(tab)[e];
         } else if constexpr (OP == 9) {
             volatile unsigned long long* q = reinterpret_cast<volatile unsigned long long*>(ent + 8);
             *q = *q + 1;
@@ -113,7 +125,11 @@ int main(int argc, char** argv) {
         case 7: run<7>(iters, nent, cus); break;
         case 8: run<8>(iters, nent, cus); break;
         case 9: run<9>(iters, nent, cus); break;
-        default: printf("op 0..9\n"); return 2;
+        case 10: run<10>(iters, nent, cus); break;
+        case 11: run<11>(iters, nent, cus); break;
+        case 12: run<12>(iters, nent, cus); break;
+        case 13: run<13>(iters, nent, cus); break;
+        default: printf("op 0..13\n"); return 2;
     }
     return 0;
 }

@@ -106,7 +106,9 @@ __global__ __launch_bounds__(256) void k_tiles(const uint8_t* __restrict__ arena
                 const uint32_t r = q * 256 + tid;  // record r of the tile
                 size_t dst;
                 if (W == 1) dst = (size_t)tile + r;
-                else dst = ((size_t)(r >> 3) * gridDim.x + blockIdx.x) * seg_cap + k0 * 8 + (r & 7);  // partition r/8
+                else if (W == 2) dst = ((size_t)(r >> 3) * gridDim.x + blockIdx.x) * seg_cap + k0 * 8 + (r & 7);  // partition r/8
+                else  // W = 3/4/5: the same 8-record runs, each segment starting 5/4/2 records into a line (runs span 2 lines)
+                    dst = ((size_t)(r >> 3) * gridDim.x + blockIdx.x) * seg_cap + (W == 3 ? 5 : W == 4 ? 4 : 2) + k0 * 8 + (r & 7);
                 const uint4 v = make_uint4(acc, r, t, q);
                 if (store_nt) {
                     __builtin_nontemporal_store(v.x, &rec[dst].x);
@@ -169,6 +171,20 @@ __global__ __launch_bounds__(256) void k_frame_lds(const uint8_t* __restrict__ a
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// read back n16 16-byte words (the records a k_tiles<., ., 2> run wrote): k_reduce's input
+__global__ __launch_bounds__(256) void k_readback(const uint4* __restrict__ a, size_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256 * 4;
+    for (size_t base = (size_t)blockIdx.x * 256 * 4 + threadIdx.x; base < n16; base += stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = base + k * 256 < n16 ? a[base + k * 256] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 10000000;
     const uint32_t fs = argc > 2 ? atoi(argv[2]) : 64;
@@ -209,10 +225,10 @@ int main(int argc, char** argv) {
     if (lds_kb) CHK(hipFuncSetAttribute((const void*)k_tiles<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
     const size_t lb = (size_t)(lds_kb ? lds_kb : 1) * 1024;
     uint4* recb;
-    const uint32_t seg_cap = ((n + 2047) / 2048 + blocks - 1) / blocks * 8 + 8;
+    const uint32_t seg_cap = ((n + 2047) / 2048 + blocks - 1) / blocks * 8 + 16;
     CHK(hipMalloc(&recb, (size_t)256 * blocks * seg_cap * 16 + (size_t)n * 16));
     if (lds_kb)
-        for (const void* f : {(const void*)k_tiles<4, 1, 1>, (const void*)k_tiles<4, 1, 2>})
+        for (const void* f : {(const void*)k_tiles<4, 1, 1>, (const void*)k_tiles<4, 1, 2>, (const void*)k_tiles<4, 1, 3>, (const void*)k_tiles<4, 1, 4>, (const void*)k_tiles<4, 1, 5>})
             CHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
     for (uint32_t nt : {1u, 0u})
         for (uint32_t snt : {0u, 1u}) {
@@ -221,7 +237,41 @@ int main(int argc, char** argv) {
             run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 1>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
             snprintf(nm, sizeof nm, "w2_%s_st%s", nt ? "nt" : "def", snt ? "nt" : "def");
             run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 2>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
+            snprintf(nm, sizeof nm, "w3_%s_st%s", nt ? "nt" : "def", snt ? "nt" : "def");
+            run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 3>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
+            snprintf(nm, sizeof nm, "w4_%s_st%s", nt ? "nt" : "def", snt ? "nt" : "def");
+            run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 4>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
+            snprintf(nm, sizeof nm, "w5_%s_st%s", nt ? "nt" : "def", snt ? "nt" : "def");
+            run(nm, (double)n * (64 + 16 + 16), [&] { hipLaunchKernelGGL((k_tiles<4, 1, 5>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, snt, seg_cap); });
         }
+    // the record round trip: k_tiles<4, 1, 2> (k_bin's loads + its segment stores), then the
+    // records read back (timed alone) -- warm (right after) vs cold (after 1.6 GB of other reads)
+    {
+        const size_t rec16 = (size_t)256 * blocks * seg_cap;
+        uint8_t* big;
+        const size_t bigb = (size_t)1600 << 20;
+        CHK(hipMalloc(&big, bigb));
+        CHK(hipMemset(big, 2, bigb));
+        for (uint32_t nt : {1u, 0u})
+            for (int cold = 0; cold < 2; ++cold) {
+                float tot = 0;
+                const int reps = 10;
+                for (int r = 0; r < reps; ++r) {
+                    hipLaunchKernelGGL((k_tiles<4, 1, 2>), dim3(blocks), dim3(256), lb, 0, arena, desc, n, nt, out, recb, 0u, seg_cap);
+                    if (cold) hipLaunchKernelGGL(k_contig, dim3(blocks), dim3(256), 0, 0, (const uint4*)big, bigb / 16, out);
+                    CHK(hipEventRecord(e0));
+                    hipLaunchKernelGGL(k_readback, dim3(blocks), dim3(256), 0, 0, (const uint4*)recb, rec16, out);
+                    CHK(hipEventRecord(e1));
+                    CHK(hipEventSynchronize(e1));
+                    float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+                    if (r >= 2) tot += ms;
+                }
+                const double ms = tot / (reps - 2);
+                printf("readback_%s_%s blocks %5d  %8.1f us  %7.0f GB/s (%.0f MB)\n", nt ? "nt" : "def", cold ? "cold" : "warm",
+                       blocks, ms * 1e3, rec16 * 16 / (ms * 1e-3) / 1e9, rec16 * 16 / 1e6);
+            }
+        CHK(hipFree(big));
+    }
     for (uint32_t nt : {1u, 0u}) {
         char nm[32];
         snprintf(nm, sizeof nm, "tiles41_%s", nt ? "nt" : "def");
