@@ -15,7 +15,7 @@ def main():
     wl_name = sys.argv[1] if len(sys.argv) > 1 else "quic"
     dev = torch.device("cuda", 0)
     args = types.SimpleNamespace(workload=wl_name, flows=1_000_000, seed=1234, zipf=None, packets=5_000_000,
-                                 batches=2, mode="cold", warmup=0, steps=1)
+                                 batches=2, mode="cold", warmup=0, steps=1, shard=None)
     wl = bench.make_workload(args, 0, 1, dev, 0)
     eng = Engine("s=21")
     eng.profile(True)
