@@ -744,14 +744,14 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     std::memset(e->ctl_h, 0, CTL_BYTES);
     if (hipHostGetDevicePointer((void**)&e->ctl_hd, e->ctl_h, 0) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMalloc((void**)&e->misc_d, 16 * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
-    if (hipMalloc((void**)&e->stats_d, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc((void**)&e->stats_d, STAT_SHARDS * ST_STRIDE * sizeof(unsigned long long)) != hipSuccess)
         return fail(IPXG_ENOMEM);
     const uint32_t fs = cfg->frag_size ? cfg->frag_size : 10007;
     if (hipMalloc((void**)&e->frag_ent, (size_t)fs * 4 * sizeof(FragEntry)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMalloc((void**)&e->frag_cnt, (size_t)fs * sizeof(uint32_t)) != hipSuccess) return fail(IPXG_ENOMEM);
     if (hipMemsetAsync(e->frag_cnt, 0, (size_t)fs * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
     if (hipMemsetAsync(e->ex_count_d, 0, 3 * sizeof(uint32_t), e->st) != hipSuccess) return fail(IPXG_EDEVICE);
-    if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_COUNT * sizeof(unsigned long long), e->st) != hipSuccess)
+    if (hipMemsetAsync(e->stats_d, 0, STAT_SHARDS * ST_STRIDE * sizeof(unsigned long long), e->st) != hipSuccess)
         return fail(IPXG_EDEVICE);
     if (e->cfg.flags & IPXG_CFG_STRICT) {
         if (cfg->line_exp > 4 || cfg->line_exp > cfg->cache_exp || cfg->cache_exp - cfg->line_exp > 24 ||
@@ -3139,13 +3139,13 @@ int ipxg_get_stats(ipxg_engine* e, ipxg_stats* out) {
         const int rc0 = complete_batch(e);
         if (rc0) return rc0;
     }
-    unsigned long long h[STAT_SHARDS * ST_COUNT];
+    std::vector<unsigned long long> h((size_t)STAT_SHARDS * ST_STRIDE);
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
-    HIPCHK(e, hipMemcpyAsync(h, e->stats_d, sizeof(h), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(h.data(), e->stats_d, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     uint64_t s[ST_COUNT] = {};
     for (int sh = 0; sh < STAT_SHARDS; ++sh)
-        for (int k = 0; k < ST_COUNT; ++k) s[k] += h[sh * ST_COUNT + k];
+        for (int k = 0; k < ST_COUNT; ++k) s[k] += h[(size_t)sh * ST_STRIDE + k];
     std::memset(out, 0, sizeof(*out));
     out->seen_packets = s[ST_SEEN];
     out->parsed_packets = s[ST_PARSED];

@@ -205,6 +205,32 @@ __device__ __forceinline__ ipxg_pkt_desc load_desc(__amdgpu_buffer_rsrc_t desc, 
 // the target of stores that carry no record (tile_emit; k_bin's prologue)
 __device__ uint4 g_dummy_rec[32 * 64];
 
+// The control-block counts of k_bin / k_bin_slow, summed per workgroup in LDS (bc: BLK_N words,
+// zeroed) and added to the control block by one lane: every lane with a time bucket other than 0
+// once did its own atomicOr on ctl->tb_any -- ~200k atomics on one address per configs[4] launch,
+// half of k_bin_slow's time.
+enum BlkCount { BLK_SPILLED, BLK_FOLDED, BLK_WALKED, BLK_TB, BLK_N };
+__device__ __forceinline__ void block_ctl_counts(uint32_t* bc, uint32_t spilled, uint32_t folded, uint32_t walked,
+                                                 uint32_t tb_or) {
+    if (spilled) atomicAdd(&bc[BLK_SPILLED], spilled);
+    if (folded) atomicAdd(&bc[BLK_FOLDED], folded);
+    if (walked) atomicAdd(&bc[BLK_WALKED], walked);
+    if (tb_or) atomicOr(&bc[BLK_TB], tb_or);
+}
+// after a barrier
+__device__ __forceinline__ void flush_block_ctl(const uint32_t* bc, BatchCtl* ctl) {
+    if (threadIdx.x != 0) return;
+    if (bc[BLK_SPILLED]) {
+        atomicAdd(&ctl->spilled, bc[BLK_SPILLED]);
+        ctl->pending = 1;
+    }
+    if (bc[BLK_FOLDED]) atomicAdd(&ctl->agg_packets, bc[BLK_FOLDED]);
+    if (bc[BLK_WALKED]) atomicAdd(&ctl->walked, bc[BLK_WALKED]);
+    // no atomic while one bucket holds the batch, nor once the bits are set (a stale read: one more)
+    const uint32_t tb = bc[BLK_TB];
+    if (tb && (*(volatile uint32_t*)&ctl->tb_any & tb) != tb) atomicOr(&ctl->tb_any, tb);
+}
+
 // one device atomic per wave for a per-lane count (convergent: every lane calls it)
 __device__ __forceinline__ void add_wave_sum(uint32_t* counter, uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -366,7 +392,10 @@ __device__ __forceinline__ void seg_counts(const uint32_t* fill, uint32_t P, con
 // NO_REC fillers (k_reduce skips them).  The carry's 28 KiB is paid for with 1024-packet tiles
 // (LINE_K steps): the workgroup stays within the LDS of 3 per CU.
 constexpr uint32_t LINE_P = BIN_LINE_P;  // partitions (at most)
-constexpr int LINE_K = 4;             // packets per lane per tile
+#ifndef IPXG_LINE_K
+#define IPXG_LINE_K 4
+#endif
+constexpr int LINE_K = IPXG_LINE_K;   // packets per lane per tile
 constexpr uint32_t LINE_C = 7;        // carried records per partition (less than a line)
 constexpr uint32_t LINE_MAXL = (LINE_K * IPXG_BLOCK + LINE_C * LINE_P) / 8;  // lines one tile completes, at most
 constexpr uint32_t LINE_ITERS = (LINE_MAXL * 8 + IPXG_BLOCK - 1) / IPXG_BLOCK;   // store rounds per tile
@@ -1022,16 +1051,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     if (PLUG && tid == 0) bv.mark_cnt[blockIdx.x] = nmark;
     // block statistics, hist reused as the counter block
     if (tid < ST_COUNT) hist[tid] = 0;
+    if (tid < BLK_N) hist[ST_STRIDE + tid] = 0;
     __syncthreads();
     flush_counts(c, 0, 0, hist);
-    flush_block_stats(hist, stats);
-    if (spilled) {
-        atomicAdd(&ctl->spilled, spilled);
-        ctl->pending = 1;
-    }
-    if (AGG) add_wave_sum(&ctl->agg_packets, folded);
-    if (WIDE) add_wave_sum(&ctl->walked, walked);
-    if (tb_or) atomicOr(&ctl->tb_any, tb_or);  // no atomic while one bucket holds the batch
+    block_ctl_counts(hist + ST_STRIDE, spilled, AGG ? folded : 0u, WIDE ? walked : 0u, tb_or);
+    flush_block_stats(hist, stats);  // (its barrier completes the block's counters)
+    flush_block_ctl(hist + ST_STRIDE, ctl);
 }
 
 // A slow-list entry (k_bin -> k_bin_slow): {packet index, offset, caplen | wirelen << 16,
@@ -1149,6 +1174,9 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
     if (ns == 0) return;  // no work: k_reduce does not read the column
+#if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 1  // timing experiment: the launch alone
+    if (ns) return;
+#endif
     // Params::plug: the slow packets' plugin checks listed after k_bin's marks of this workgroup
     __shared__ uint32_t nmark;
     uint4* const my_marks = p.plug ? bv.marks + (size_t)blockIdx.x * bv.slow_stride : nullptr;
@@ -1224,6 +1252,9 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             PROBE_ADD(0, s0, s1);
             probe_acc[3] += 1;
 #endif
+#if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 2  // timing experiment: no parse
+            if (e0.z == 0xFFFFFFFFu)
+#endif
             slow_packet<AGG>(p, b, f, ctl, col, e0, w0, j, c, keyless, frags, r0, r1, r2, rk, ix, tb_or, my_marks, &nmark);
 #ifdef IPXG_PROBE
             PROBE_T(s2);
@@ -1255,16 +1286,23 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     __syncthreads();  // the last tile's fill updates (tile_emit's tail) are other threads'
     seg_counts(fill, P, bv, bcol);
     if (p.plug && tid == 0) bv.mark_cnt[blockIdx.x] = nmark;
+#if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 3  // timing experiment: no statistics atomics
+    return;
+#endif
     if (tid < ST_COUNT) hist[tid] = 0;
+    if (tid < BLK_N) hist[ST_STRIDE + tid] = 0;
     __syncthreads();
     flush_counts(c, keyless, frags, hist);
-    flush_block_stats(hist, stats);
-    if (spilled) {
-        atomicAdd(&ctl->spilled, spilled);
-        ctl->pending = 1;
-    }
-    if (AGG) add_wave_sum(&ctl->agg_packets, folded);
-    if (tb_or) atomicOr(&ctl->tb_any, tb_or);
+    block_ctl_counts(hist + ST_STRIDE, spilled, AGG ? folded : 0u, 0u, tb_or);
+#if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 4  // timing experiment: no statistics atomics
+    __syncthreads();
+#else
+    flush_block_stats(hist, stats);  // (its barrier completes the block's counters)
+#endif
+#if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 5  // timing experiment: no control-block atomics
+    return;
+#endif
+    flush_block_ctl(hist + ST_STRIDE, ctl);
 }
 
 typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint4*, uint32_t*, uint4*,

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_frag_walk(BatchView b, Params p, FragVi
         f.ports[idx] = ports;
     }
     f.cnt[bucket] = cnt;
-    if (filled) atomicAdd(&stats[ST_FRAG_FILLED], (unsigned long long)filled);
+    if (filled) atomicAdd(&stat_row(stats)[ST_FRAG_FILLED], (unsigned long long)filled);
 }
 
 void launch_frag_walk(hipStream_t st, const BatchView& b, const Params& p, FragView f, uint32_t nfrag,
@@ -428,8 +428,8 @@ __global__ __launch_bounds__(64) void k_complex_walk(BatchView b, Params p, Tabl
                 uint32_t pos = atomicAdd(ex.count, 1u);
                 store_export(ex, pos, rec, reason);
                 if (ex.count6 && rec.ip_version == 6) atomicAdd(ex.count + 2, 1u);
-                atomicAdd(&stats[ST_END_INACTIVE + reason - 1], 1ull);
-                atomicAdd(&stats[ST_PKTS_1 + pkts_bucket((uint64_t)rec.src_packets + rec.dst_packets)], 1ull);
+                atomicAdd(&stat_row(stats)[ST_END_INACTIVE + reason - 1], 1ull);
+                atomicAdd(&stat_row(stats)[ST_PKTS_1 + pkts_bucket((uint64_t)rec.src_packets + rec.dst_packets)], 1ull);
                 n_ex++;
                 live = false;
             }
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         count_v6_exports(ex, mine && rw_ipver(rec) == 6);
     }
     __syncthreads();
-    unsigned long long* const sh = &stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT];
+    unsigned long long* const sh = stat_row(stats);
     if (threadIdx.x == 0 && total) atomicAdd(&sh[ST_END_FORCED], (unsigned long long)total);
     if (threadIdx.x < 6 && pb[threadIdx.x]) atomicAdd(&sh[ST_PKTS_1 + threadIdx.x], (unsigned long long)pb[threadIdx.x]);
 }

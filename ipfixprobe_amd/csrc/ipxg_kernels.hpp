@@ -88,14 +88,26 @@ struct FragEntry {
 };
 static_assert(sizeof(FragEntry) == 64, "");
 
-// Device statistics, sharded to spread the per-block atomics.
-constexpr int STAT_SHARDS = 16;
+// Device statistics, sharded to spread the per-block atomics: workgroup b adds to row b % STAT_SHARDS
+// (256-byte rows, two lines of their own).  A kernel's workgroups mostly end together and each
+// adds its ~15 non-zero counters: with 16 rows the atomics of k_bin_slow's 768 workgroups queued
+// on 32 lines for ~33 us per launch (configs[4]: 63 -> 30 us without them); at 1024 rows about
+// one workgroup per row.
+constexpr int STAT_SHARDS = 1024;
+constexpr int ST_STRIDE = 32;  // counters per row (>= ST_COUNT)
 enum StatIdx {
     ST_SEEN, ST_PARSED, ST_UNKNOWN, ST_IPV4, ST_IPV6, ST_TCP, ST_UDP, ST_MPLS, ST_PPPOE, ST_TRILL,
     ST_VLAN, ST_IPV4_BYTES, ST_IPV6_BYTES, ST_KEYLESS, ST_FRAGMENTED, ST_FRAG_FILLED,
     ST_END_INACTIVE, ST_END_ACTIVE, ST_END_EOF, ST_END_FORCED, ST_END_NO_RES,
     ST_PKTS_1, ST_PKTS_2_5, ST_PKTS_6_10, ST_PKTS_11_20, ST_PKTS_21_50, ST_PKTS_51, ST_COUNT
 };
+static_assert(ST_COUNT <= ST_STRIDE, "statistics row");
+#ifdef __HIPCC__
+// the calling workgroup's row of the sharded statistics
+__device__ __forceinline__ unsigned long long* stat_row(unsigned long long* stats) {
+    return stats + (size_t)(blockIdx.x % STAT_SHARDS) * ST_STRIDE;
+}
+#endif
 
 // FlowRecordStats bucket of a record of n = src_packets + dst_packets packets
 // (update_flow_record_stats, cache.cpp:601-616: 0 falls to the last bucket, as there)

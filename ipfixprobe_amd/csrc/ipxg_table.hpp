@@ -69,30 +69,28 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 }
 
 // ---- block statistics ---------------------------------------------------------------------
+// Each counter summed over the wave first, then one LDS atomic per wave and non-zero counter:
+// every lane's atomic on the same 15 LDS words serialised 64-fold per wave instruction.
 __device__ __forceinline__ void flush_counts(const ParseCounts& c, uint32_t keyless, uint32_t frags,
                                              uint32_t* sc) {
-    atomicAdd(&sc[ST_SEEN], c.seen);
-    atomicAdd(&sc[ST_PARSED], c.parsed);
-    atomicAdd(&sc[ST_UNKNOWN], c.unknown);
-    atomicAdd(&sc[ST_IPV4], c.ipv4);
-    atomicAdd(&sc[ST_IPV6], c.ipv6);
-    atomicAdd(&sc[ST_TCP], c.tcp);
-    atomicAdd(&sc[ST_UDP], c.udp);
-    atomicAdd(&sc[ST_MPLS], c.mpls);
-    atomicAdd(&sc[ST_PPPOE], c.pppoe);
-    atomicAdd(&sc[ST_TRILL], c.trill);
-    atomicAdd(&sc[ST_VLAN], c.vlan);
-    atomicAdd(&sc[ST_IPV4_BYTES], c.ipv4_bytes);
-    atomicAdd(&sc[ST_IPV6_BYTES], c.ipv6_bytes);
-    atomicAdd(&sc[ST_KEYLESS], keyless);
-    atomicAdd(&sc[ST_FRAGMENTED], frags);
+    uint32_t v[15] = {c.seen, c.parsed, c.unknown, c.ipv4, c.ipv6, c.tcp, c.udp, c.mpls, c.pppoe, c.trill, c.vlan,
+                      c.ipv4_bytes, c.ipv6_bytes, keyless, frags};
+    constexpr uint32_t idx[15] = {ST_SEEN, ST_PARSED, ST_UNKNOWN, ST_IPV4, ST_IPV6, ST_TCP, ST_UDP, ST_MPLS, ST_PPPOE,
+                                  ST_TRILL, ST_VLAN, ST_IPV4_BYTES, ST_IPV6_BYTES, ST_KEYLESS, ST_FRAGMENTED};
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+        if (!__any(v[k] != 0)) continue;  // (wave-uniform)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+        if ((threadIdx.x & 63) == 0 && v[k]) atomicAdd(&sc[idx[k]], v[k]);
+    }
 }
 
 // sc: ST_COUNT block-local counters in LDS; one device atomic per non-zero counter.
 __device__ __forceinline__ void flush_block_stats(uint32_t* sc, unsigned long long* stats) {
     __syncthreads();
     if (threadIdx.x < ST_COUNT && sc[threadIdx.x])
-        atomicAdd(&stats[(blockIdx.x % STAT_SHARDS) * ST_COUNT + threadIdx.x],
+        atomicAdd(&stat_row(stats)[threadIdx.x],
                   (unsigned long long)sc[threadIdx.x]);
 }
 
