@@ -1729,9 +1729,9 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
     for (uint32_t q = 0; q < EPT; ++q)
         if (listed[q]) fin_list[pos++] = img[q];
-    if (failed) atomicOr(&cnt[C_FAIL], 1u);
-    if (n_keys) atomicAdd(&cnt[C_KEYS], n_keys);
-    if (n_touch) atomicAdd(&cnt[C_TOUCH], n_touch);
+    if (__any(failed) && (tid & 63) == 0) atomicOr(&cnt[C_FAIL], 1u);
+    wave_add_lds(&cnt[C_KEYS], n_keys);
+    wave_add_lds(&cnt[C_TOUCH], n_touch);
     __syncthreads();
     PROBE_T(q3t);
 #ifdef IPXG_PROBE
@@ -1885,18 +1885,18 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
         __syncthreads();
         if (do_export) {
             store_export_w(ex, ex_base + pos, er, reason);
-            count_export_w(sc, er, reason);
             n_ex++;
             n_v6 += rw_ipver(er) == 6 ? 1 : 0;
         }
+        count_exports_wave(sc, do_export, er, reason);
         __syncthreads();  // ex_base is rewritten by the next pass
     }
-    if (n_live) atomicAdd(&cnt[0], n_live);
-    if (n_cx) atomicAdd(&cnt[1], n_cx);
-    if (n_ex) atomicAdd(&cnt[2], n_ex);
-    if (n_v6) atomicAdd(&cnt[3], n_v6);
-    if (n_keys) atomicAdd(&cnt[4], n_keys);
-    if (n_def) atomicAdd(&cnt[5], n_def);
+    wave_add_lds(&cnt[0], n_live);
+    wave_add_lds(&cnt[1], n_cx);
+    wave_add_lds(&cnt[2], n_ex);
+    wave_add_lds(&cnt[3], n_v6);
+    wave_add_lds(&cnt[4], n_keys);
+    wave_add_lds(&cnt[5], n_def);
     flush_block_stats(sc, stats);
     if (tid == 0) {
         if (cnt[3] && ex.count6) atomicAdd(ex.count + 2, cnt[3]);  // count_v6_exports' counter

@@ -298,15 +298,15 @@ __global__ __launch_bounds__(256) void k_finalize(BatchView b, Params p, TableVi
         uint32_t pos = wave_append(ex.count, do_export);
         if (do_export) {
             store_export_w(ex, pos, er, reason);
-            count_export_w(sc, er, reason);
             ex_n++;
         }
+        count_exports_wave(sc, do_export, er, reason);
         count_v6_exports(ex, do_export && rw_ipver(er) == 6);
     }
-    atomicAdd(&cnt[0], keys);
-    atomicAdd(&cnt[1], live_n);
-    atomicAdd(&cnt[2], cx_n);
-    atomicAdd(&cnt[3], ex_n);
+    wave_add_lds(&cnt[0], keys);
+    wave_add_lds(&cnt[1], live_n);
+    wave_add_lds(&cnt[2], cx_n);
+    wave_add_lds(&cnt[3], ex_n);
     __syncthreads();
     if (threadIdx.x == 0) {
         if (cnt[0]) atomicAdd(&ctl->keys, cnt[0]);
@@ -529,12 +529,13 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const bool mine = mask >> j & 1;
         RecW rec;
+        uint8_t reason = 0;
         if (mine) {
             rec = tbl_load_rec(t, base + j * 256 + threadIdx.x);
-            const uint8_t reason = export_reason_w(rec);
+            reason = export_reason_w(rec);
             store_export_w(ex, pos++, rec, reason);
-            count_export_w(sc, rec, reason);
         }
+        count_exports_wave(sc, mine, rec, reason);
         count_v6_exports(ex, mine && rw_ipver(rec) == 6);
     }
     flush_block_stats(sc, stats);
@@ -586,7 +587,14 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         if (mine) {
             rec = tbl_load_rec(t, base + j * 256 + threadIdx.x);
             store_export_w(ex, pos++, rec, IPXG_FLOW_END_FORCED);
-            atomicAdd(&pb[pkts_bucket((uint64_t)rec.w[RW_SPK] + rec.w[RW_DPK])], 1u);
+        }
+        {  // the FlowRecordStats buckets, one LDS atomic per wave and bucket present
+            const uint32_t bk = mine ? pkts_bucket((uint64_t)rec.w[RW_SPK] + rec.w[RW_DPK]) : 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < 6; ++q) {
+                const unsigned long long m = __ballot(mine && bk == q);
+                if ((threadIdx.x & 63) == 0 && m) atomicAdd(&pb[q], (uint32_t)__popcll(m));
+            }
         }
         count_v6_exports(ex, mine && rw_ipver(rec) == 6);
     }

@@ -567,6 +567,31 @@ __device__ __forceinline__ void count_export_w(uint32_t* sc, const RecW& r, uint
     atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
     atomicAdd(&sc[ST_PKTS_1 + pkts_bucket((uint64_t)r.w[RW_SPK] + r.w[RW_DPK])], 1u);
 }
+// The same for a wave's exports (active lanes; convergent): one LDS atomic per reason and bucket
+// present -- lanes exporting alike (a finish exports every record as FORCED) otherwise serialise
+// on one LDS word.
+__device__ __forceinline__ void count_exports_wave(uint32_t* sc, bool active, const RecW& r, uint32_t reason) {
+    if (!__any(active)) return;  // (wave-uniform)
+    const uint32_t bucket = active ? pkts_bucket((uint64_t)r.w[RW_SPK] + r.w[RW_DPK]) : 0u;
+    const bool lead = (threadIdx.x & 63) == 0;
+#pragma unroll
+    for (uint32_t q = 1; q <= 5; ++q) {
+        const unsigned long long m = __ballot(active && reason == q);
+        if (lead && m) atomicAdd(&sc[ST_END_INACTIVE + q - 1], (uint32_t)__popcll(m));
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 6; ++q) {
+        const unsigned long long m = __ballot(active && bucket == q);
+        if (lead && m) atomicAdd(&sc[ST_PKTS_1 + q], (uint32_t)__popcll(m));
+    }
+}
+// v summed over the wave into one LDS word (convergent)
+__device__ __forceinline__ void wave_add_lds(uint32_t* w, uint32_t v) {
+    if (!__any(v != 0)) return;  // (wave-uniform)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(w, v);
+}
 
 // FlowRecord::create's fields (rec_create) into the word form
 __device__ __forceinline__ void rec_create_w(RecW& r, const DevPkt& pk, const ipxg_pkt_desc& d, uint64_t hf,
