@@ -760,6 +760,9 @@ def main():
                               "packets_per_step": round(tm_in["plugin_packets"] / args.steps),
                               "packet_share": round(tm_in["plugin_packets"] / args.steps / pk_step, 5),
                               "bytes_per_step": round(tm_in["plugin_bytes"] / args.steps),
+                              # what crossed PCIe for the walk: frames (whole, or the plugins' byte
+                              # budget past the headers -- ipxg_plugin.follow_bytes), packet / flow records
+                              "d2h_bytes_per_step": round(tm_in["plugin_d2h_bytes"] / args.steps),
                               "ms_per_step": round(hw_ms, 3),
                               "share_of_step_time": round(hw_ms / (dt / args.steps * 1e3), 4),
                               # batches whose k_bin / k_bin_slow ran during the previous batch's walk

@@ -28,12 +28,14 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 6 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+#define IPXG_ABI_VERSION 7 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
                               3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
                               4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
                               5: ipxg_timing gained plugin_overlapped
                               6: ipxg_profile takes a sampling period; ipxg_timing gained
-                                 slow_redos; ipxg_plugin gained all_packets */
+                                 slow_redos; ipxg_plugin gained all_packets
+                              7: ipxg_plugin gained follow_bytes; ipxg_timing gained
+                                 plugin_d2h_bytes */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -408,6 +410,14 @@ typedef struct ipxg_plugin {
      * walked on the host -- the reference's behaviour (its hooks see every packet), at the host
      * walk's rate.  The rule fields are then unused. */
     uint32_t all_packets;
+    /* ABI 7: 0 = the hooks may read any byte of a walked packet (its whole frame crosses to the
+     * host).  N > 0 = on a packet outside this plugin's rule (a packet of a flow it follows, or of
+     * a flow another plugin walks) the hooks read at most the first N payload bytes -- QUIC reads
+     * the first byte of a short-header packet and nothing more (quic.cpp:494-498,
+     * quic_parser.cpp:1105-1117, 1160-1167).  When every registered plugin declares N > 0 and none
+     * acts on all packets, a walked packet that matches no rule crosses with its headers and the
+     * largest N payload bytes; the view's caplen and the parsed fields stay the packet's own. */
+    uint32_t follow_bytes;
 } ipxg_plugin;
 
 /* Register a plugin (the order of registration is the order of the hook calls). */
@@ -447,6 +457,9 @@ typedef struct ipxg_timing {
     /* ABI 6 (always counted; zeroed by ipxg_profile): batches launched without k_bin_slow (the
        previous batch had no slow-list packet) whose k_bin listed some -- run again from k_bin_slow */
     uint64_t slow_redos;
+    /* ABI 7: bytes the plugin walk copied to the host -- frames (whole, or their byte budget:
+       ipxg_plugin.follow_bytes), packet and flow records, per-flow arrays */
+    uint64_t plugin_d2h_bytes;
 } ipxg_timing;
 
 /* Per-phase shader-clock sums of the last batch's k_bin, k_reduce and k_bin_slow (16 values;

@@ -245,8 +245,45 @@ __global__ void k_plugin_totals(const uint32_t* count, const uint32_t* first, co
     tot[3] = lpos[nf];
 }
 
-void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, ComplexView cx, uint32_t ncx, uint32_t npk,
-                         const PluginOrder& o) {
+// Packet idx[k] (k < the walked packets): every field a hook reads (ipxg_parsed_pkt, FULL parse),
+// its descriptor and its index, as one WalkPkt; with a byte budget, also the length of it that
+// crosses to the host (clen[k], 16-byte rounded): the whole frame when a plugin's rule matches the
+// packet (k_classify's test on the parsed packet), else its headers and `budget` payload bytes.
+__global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_pkts(BatchView b, Params p, FragView f, const uint32_t* idx,
+                                                            const uint32_t* count, const uint32_t* first, WalkPkt* out,
+                                                            const DevRule* rules, uint32_t nrules, uint32_t budget,
+                                                            uint64_t* clen) {
+    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    const uint32_t k = blockIdx.x * IPXG_BLOCK + threadIdx.x;
+    if (k >= first[*count]) return;
+    const uint32_t i = idx[k];
+    const ipxg_pkt_desc d = b.desc[i];
+    uint32_t* col = &win[threadIdx.x];
+    stage_frame(col, b.arena, d.offset, d.caplen);
+    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    DevPkt pk;
+    ParseCounts c = {};
+    const bool ok = parse_frame<true>(S, d.caplen, p.dlt, pk, c);
+    if (budget) {
+        // (an unparsed frame and a fragment -- its ports come from the fragmentation cache -- cross whole)
+        bool full = !ok || pk.frag_off || pk.more_fragments;
+        if (!full && (pk.ip_version == 4 || pk.ip_version == 6) && (pk.l4 == 6 || pk.l4 == 17)) {
+            auto pay = [&](uint32_t j) { return S.b(pk.payload_off + j); };
+            for (uint32_t r = 0; r < nrules && !full; ++r) full = rule_match(rules[r], pk, pay);
+        }
+        const uint32_t n = full ? d.caplen : min((uint32_t)d.caplen, (uint32_t)pk.payload_off + budget);
+        clen[k] = (n + 15u) & ~15u;
+    }
+    if (ok) apply_frag_ports(p, f, i, pk);  // a fragment's ports from the fragmentation cache
+    WalkPkt w;
+    w.pk = to_parsed(pk, ok);
+    w.d = d;
+    w.idx = i;
+    out[k] = w;
+}
+
+void launch_plugin_order(hipStream_t st, const BatchView& b, const Params& p, FragView f, TableView t, ComplexView cx,
+                         uint32_t ncx, uint32_t npk, const PluginOrder& o) {
     hipLaunchKernelGGL(k_plugin_keys, dim3((ncx + 255) / 256), dim3(256), 0, st, t, cx, ncx, o.keys, o.count);
     size_t tb = o.temp_bytes;
     (void)sort_keys_u64(o.temp, tb, o.keys, o.skeys, ncx, 56, st);
@@ -262,6 +299,8 @@ void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, Comple
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_plugin_idx, dim3(g ? g : 1), dim3(256), 0, st, b, cx, o.flows, o.count, o.first, o.idx,
                        o.clen);
+    hipLaunchKernelGGL(k_plugin_pkts, dim3((npk + IPXG_BLOCK - 1) / IPXG_BLOCK), dim3(IPXG_BLOCK), 0, st, b, p, f,
+                       o.idx, o.count, o.first, o.wpk, o.rules, o.nrules, o.budget, o.clen);
     tb = o.temp_bytes;
     (void)exclusive_scan_u64(o.temp, tb, o.clen, o.off, npk + 1, st);
     hipLaunchKernelGGL(k_plugin_totals, dim3(1), dim3(1), 0, st, o.count, o.first, o.off, o.lpos, o.tot);
@@ -276,35 +315,6 @@ size_t plugin_order_temp(uint32_t ncx, uint32_t npk) {
     return std::max(a, std::max(c, d));
 }
 
-// Packet idx[k] (k < m): every field a hook reads (ipxg_parsed_pkt, FULL parse), its descriptor
-// and its index, as one WalkPkt.
-__global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_pkts(BatchView b, Params p, FragView f, const uint32_t* idx,
-                                                            uint32_t m, WalkPkt* out) {
-    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
-    const uint32_t k = blockIdx.x * IPXG_BLOCK + threadIdx.x;
-    if (k >= m) return;
-    const uint32_t i = idx[k];
-    const ipxg_pkt_desc d = b.desc[i];
-    uint32_t* col = &win[threadIdx.x];
-    stage_frame(col, b.arena, d.offset, d.caplen);
-    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
-    DevPkt pk;
-    ParseCounts c = {};
-    const bool ok = parse_frame<true>(S, d.caplen, p.dlt, pk, c);
-    if (ok) apply_frag_ports(p, f, i, pk);  // a fragment's ports from the fragmentation cache
-    WalkPkt w;
-    w.pk = to_parsed(pk, ok);
-    w.d = d;
-    w.idx = i;
-    out[k] = w;
-}
-
-void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
-                        uint32_t m, WalkPkt* out) {
-    hipLaunchKernelGGL(k_plugin_pkts, dim3((m + IPXG_BLOCK - 1) / IPXG_BLOCK), dim3(IPXG_BLOCK), 0, st, b, p, f, idx,
-                       m, out);
-}
-
 // Frame bytes of packet idx[k] to out + off[k], a wave per packet: 16-byte copies when the frame
 // starts on 16 bytes (out + off[k] always does: k_plugin_idx rounds the lengths up), so the
 // rounded-up tail is read from inside the arena; byte copies otherwise.  (A workgroup per packet
@@ -316,12 +326,13 @@ __global__ __launch_bounds__(256) void k_plugin_bytes(BatchView b, const uint32_
         const ipxg_pkt_desc d = b.desc[idx[k]];
         const uint8_t* src = b.arena + d.offset;
         uint8_t* dst = out + off[k];
-        const uint32_t n16 = ((uint32_t)d.caplen + 15u) >> 4;
+        const uint32_t n16 = (uint32_t)((off[k + 1] - off[k]) >> 4);  // (the frame, or its budget)
         if ((d.offset & 15u) == 0 && (uint64_t)d.offset + 16ull * n16 <= b.arena_lim) {
             for (uint32_t j = lane; j < n16; j += 64)
                 reinterpret_cast<uint4*>(dst)[j] = reinterpret_cast<const uint4*>(src)[j];
         } else {
-            for (uint32_t j = lane; j < d.caplen; j += 64) dst[j] = src[j];
+            const uint32_t n = min((uint32_t)d.caplen, 16u * n16);
+            for (uint32_t j = lane; j < n; j += 64) dst[j] = src[j];
         }
     }
 }

@@ -180,6 +180,8 @@ struct ipxg_engine {
     // host walks add to the device-side counters (exports by reason, TopPorts)
     std::vector<ipxg_plugin> plugins;
     uint64_t follow_max = 0;  // the largest follow_packets of the registered plugins
+    uint32_t walk_budget = 0;  // payload bytes of a walked packet outside every rule (0: whole frames)
+    bool walk_full = false;    // IPXG_WALK_FULL=1: whole frames always (A/B knob)
     bool plug_all = false;    // a registered plugin acts on every packet (ipxg_plugin.all_packets)
     double walk_phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};  // plugin_walk's phases (IPXG_WALK_TRACE)
     long walk_faults[7] = {0, 0, 0, 0, 0, 0, 0};        // ... and the minor page faults in each
@@ -704,6 +706,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->sync_finish = std::getenv("IPXG_SYNC_FINISH") != nullptr && std::atoi(std::getenv("IPXG_SYNC_FINISH")) != 0;
     e->no_ahead = std::getenv("IPXG_NO_AHEAD") != nullptr && std::atoi(std::getenv("IPXG_NO_AHEAD")) != 0;
     e->no_line = std::getenv("IPXG_NO_LINE") != nullptr && std::atoi(std::getenv("IPXG_NO_LINE")) != 0;
+    e->walk_full = std::getenv("IPXG_WALK_FULL") != nullptr && std::atoi(std::getenv("IPXG_WALK_FULL")) != 0;
     e->no_slow_skip = std::getenv("IPXG_NO_SLOW_SKIP") != nullptr && std::atoi(std::getenv("IPXG_NO_SLOW_SKIP")) != 0;
     if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
     int ndev = 0;
@@ -1681,9 +1684,14 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     o.recs = (ipxg_flow_record*)e->pf_recs.p;
     o.temp = (char*)e->pf_tmp.p + 64;
     o.temp_bytes = tmp_b;
+    if ((rc = ensure(e, e->pf_wpk, (size_t)npk * sizeof(WalkPkt) + 16))) return rc;
+    o.wpk = (WalkPkt*)e->pf_wpk.p;
+    o.rules = (const DevRule*)e->rules_d.p;
+    o.nrules = (uint32_t)e->plugins.size();
+    o.budget = e->walk_budget;
     HIPCHK(e, hipMemsetAsync(o.count, 0, sizeof(uint32_t), e->st));
     HIPCHK(e, hipMemsetAsync(o.clen, 0, ((size_t)npk + 1) * 8, e->st));
-    launch_plugin_order(e->st, bv, table_view(e), cx, ncx, npk, o);
+    launch_plugin_order(e->st, bv, p, frag_view(e), table_view(e), cx, ncx, npk, o);
     HIPCHK(e, hipGetLastError());
     uint64_t tot[4] = {0, 0, 0, 0};
     HIPCHK(e, hipMemcpyAsync(tot, o.tot, sizeof(tot), hipMemcpyDeviceToHost, e->st));
@@ -1692,15 +1700,13 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     const uint64_t nbytes = tot[2];
     const uint32_t nlive = (uint32_t)tot[3];
     if (!nf) return IPXG_OK;
-    if ((rc = ensure(e, e->pf_wpk, (size_t)m * sizeof(WalkPkt) + 16))) return rc;
     if ((rc = ensure(e, e->pf_bytes, nbytes + 16))) return rc;
-    launch_plugin_pkts(e->st, bv, p, frag_view(e), o.idx, m, (WalkPkt*)e->pf_wpk.p);
     launch_plugin_bytes(e->st, bv, o.idx, o.off, m, (uint8_t*)e->pf_bytes.p);
     HIPCHK(e, hipGetLastError());
     const bool pin = e->walk_pin;
     if (!e->hw_state.resize(nf, pin) || !e->hw_recs.resize(nlive, pin) || !e->hw_first.resize(nf + 1, pin) ||
         !e->hw_wpk.resize(m, pin) ||
-        !e->hw_off.resize((size_t)m + 1, pin) || !e->hw_bytes.resize(nbytes + 16, pin) || !e->hw_lpos.resize(nf + 1, pin))
+        !e->hw_off.resize((size_t)m + 1, pin) || !e->hw_bytes.resize(nbytes + 2048, pin) || !e->hw_lpos.resize(nf + 1, pin))
         return set_err(e, IPXG_ENOMEM, "host walk buffers");
     uint32_t* fstate = e->hw_state.data();
     const ipxg_flow_record* recs_in = e->hw_recs.data();
@@ -1724,6 +1730,10 @@ static int plugin_walk(ipxg_engine* e, const BatchView& bv, const Params& p, con
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->tm.plugin_flows += nf;
     e->tm.plugin_packets += m;
+    // what crosses PCIe to the host for the walk: the frames (or their budgets), the packet and
+    // flow records, the per-flow arrays
+    e->tm.plugin_d2h_bytes += nbytes + (uint64_t)m * (sizeof(WalkPkt) + 8) + (uint64_t)nlive * sizeof(ipxg_flow_record) +
+                              (uint64_t)nf * 8 + 8;
 
     lpos[0] = 0;  // flow f's record in recs_in, when it is live
     for (uint32_t f = 0; f < nf; ++f) lpos[f + 1] = lpos[f] + ((fstate[f] & SLOT_LIVE) ? 1u : 0u);
@@ -2042,6 +2052,18 @@ static int add_plugin_impl(ipxg_engine* e, const ipxg_plugin* pl) {
     }
     e->follow_max = std::max<uint64_t>(e->follow_max, pl->follow_packets);
     if (pl->all_packets) e->plug_all = true;  // (every touched flow walked: the rules do not matter)
+    // the walk's byte budget: with every registered plugin declaring one (follow_bytes), a walked
+    // packet no rule matches crosses to the host with its headers and the largest budget's payload
+    // bytes; any plugin without one (or acting on every packet) keeps whole frames
+    {
+        uint32_t b = 0;
+        bool all = !e->plug_all && !e->walk_full;
+        for (const ipxg_plugin& q : e->plugins) {
+            if (q.follow_bytes == 0) all = false;
+            b = std::max(b, q.follow_bytes);
+        }
+        e->walk_budget = all ? b : 0u;
+    }
     std::vector<DevRule> rules(e->plugins.size());
     for (size_t k = 0; k < rules.size(); ++k) {
         const ipxg_plugin& q = e->plugins[k];

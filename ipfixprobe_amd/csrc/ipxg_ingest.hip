@@ -468,7 +468,14 @@ __device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, ui
         const uint32_t at = L.fill[part] + j;
         const bool fits = valid && at < bv.seg_cap;  // (seg_cap and fill are multiples of 8: whole lines)
         uint4* dst = fits ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + at] : &g_dummy_rec[tid & 63];
+#ifdef IPXG_NT_REC_STORE  // tuning knob: streaming (non-temporal) record stores
+        __builtin_nontemporal_store(r.x, &dst->x);
+        __builtin_nontemporal_store(r.y, &dst->y);
+        __builtin_nontemporal_store(r.z, &dst->z);
+        __builtin_nontemporal_store(r.w, &dst->w);
+#else
         *dst = r;
+#endif
         if (valid && !fits) line_spill(t, ctl, deferred_list, r, spilled, defer_spill);
     }
     __syncthreads();  // the carry and the stage have been read

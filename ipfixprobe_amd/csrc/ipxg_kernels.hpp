@@ -402,6 +402,16 @@ void launch_classify(hipStream_t st, const BatchView& b, const Params& p, TableV
 // hstate [ncx] (slot states), lflag / lpos [ncx + 1] (live flags, their exclusive prefix),
 // recs [ncx] (the live flows' records, compacted), count (zeroed by the caller),
 // tot [4] = {flows, packets, bytes, live flows}
+// A walked packet as the host walk reads it: its parsed fields, descriptor and batch index in one
+// record, so a chunk of the walk's input crosses to the host in one copy (k_plugin_pkts)
+struct WalkPkt {
+    ipxg_parsed_pkt pk;
+    ipxg_pkt_desc d;
+    uint32_t idx;
+};
+// wpk [npk]: the walked packets (k_plugin_pkts, inside launch_plugin_order); budget > 0: a walked
+// packet that no plugin's rule matches crosses with its headers and `budget` payload bytes only
+// (ipxg_plugin.follow_bytes), the rest with the whole frame
 struct PluginOrder {
     uint64_t *keys, *skeys;
     PluginFlow* flows;
@@ -410,19 +420,13 @@ struct PluginOrder {
     uint64_t *clen, *off, *tot;
     void* temp;
     size_t temp_bytes;
+    WalkPkt* wpk;
+    const DevRule* rules;
+    uint32_t nrules, budget;
 };
-void launch_plugin_order(hipStream_t st, const BatchView& b, TableView t, ComplexView cx, uint32_t ncx, uint32_t npk,
-                         const PluginOrder& o);
+void launch_plugin_order(hipStream_t st, const BatchView& b, const Params& p, FragView f, TableView t, ComplexView cx,
+                         uint32_t ncx, uint32_t npk, const PluginOrder& o);
 size_t plugin_order_temp(uint32_t ncx, uint32_t npk);
-// A walked packet as the host walk reads it: its parsed fields, descriptor and batch index in one
-// record, so a chunk of the walk's input crosses to the host in one copy (k_plugin_pkts)
-struct WalkPkt {
-    ipxg_parsed_pkt pk;
-    ipxg_pkt_desc d;
-    uint32_t idx;
-};
-void launch_plugin_pkts(hipStream_t st, const BatchView& b, const Params& p, FragView f, const uint32_t* idx,
-                        uint32_t m, WalkPkt* out);
 void launch_plugin_bytes(hipStream_t st, const BatchView& b, const uint32_t* idx, const uint64_t* off, uint32_t m,
                          uint8_t* out);
 // The host walk's results, read by one kernel straight from page-locked host memory (one launch

@@ -78,7 +78,8 @@ class Timing(ctypes.Structure):
                                         "slow_launches", "finish_launches", "ingest_packets")] + \
         [("plugin_ms", ctypes.c_double)] + [(n, ctypes.c_uint64) for n in ("plugin_flows", "plugin_packets",
                                                                              "plugin_bytes", "plugin_extra_bytes",
-                                                                             "plugin_overlapped", "slow_redos")]
+                                                                             "plugin_overlapped", "slow_redos",
+                                                                             "plugin_d2h_bytes")]
 
 
 class Capture(ctypes.Structure):
@@ -136,7 +137,8 @@ class Plugin(ctypes.Structure):
                 ("prefix_mask", (ctypes.c_uint8 * 16) * 16),
                 ("copy_ctx", ctypes.c_void_p), ("free_ctx", ctypes.c_void_p),  # ABI 3 (C function pointers)
                 ("error", ERROR_FN),  # ABI 4
-                ("all_packets", ctypes.c_uint32)]  # ABI 6
+                ("all_packets", ctypes.c_uint32),  # ABI 6
+                ("follow_bytes", ctypes.c_uint32)]  # ABI 7
 
 # ipxg_vlan_stats (VlanStats, parser-stats.hpp:126-160) and ipxg_port_stat (TopPorts::PortStats)
 VLAN_STATS_DTYPE = np.dtype([("ipv4_packets", "<u8"), ("ipv6_packets", "<u8"), ("ipv4_bytes", "<u8"),

@@ -778,6 +778,7 @@ int ipxg_std_plugin(const char* name, ipxg_plugin* out) {
         out->proto_mask = 3;
         out->n_ports = 1;
         out->ports[0] = 53;
+        out->follow_bytes = 1;  /* (outside port 53 the hooks read no payload byte) */
         out->post_create = dns_post_create;
         out->post_update = dns_post_update;
     } else if (strcmp(name, "http") == 0) {
@@ -808,6 +809,9 @@ int ipxg_std_plugin(const char* name, ipxg_plugin* out) {
         out->masked = 1;
         out->prefix_mask[0][0] = 0x80;
         out->follow_packets = 30;  /* QUIC_MAX_ELEMCOUNT, quic.hpp:58 */
+        /* outside the rule (a short header, bit 7 clear) the hooks read the payload's first byte
+           only (quic_detected above; quic_long_header_packet :1105-1117) */
+        out->follow_bytes = 1;
         out->post_create = quic_post_create;
         out->post_update = quic_post_update;
     } else {

@@ -130,6 +130,7 @@ inline bool rule_for(const std::string& name, ipxg_plugin& q) {
         q.proto_mask = 3;
         q.n_ports = 1;
         q.ports[0] = 53;
+        q.follow_bytes = 1;  // (dns.cpp reads a payload only on port 53)
     } else if (name == "http") {
         q.proto_mask = 1;
         for (const char* m : {"GET ", "POST", "PUT ", "HEAD", "DELE", "TRAC", "OPTI", "CONN", "PATC", "HTTP"})
@@ -143,6 +144,10 @@ inline bool rule_for(const std::string& name, ipxg_plugin& q) {
         q.masked = 1;
         q.prefix_mask[0][0] = 0x80;
         q.follow_packets = 30;
+        // outside the rule (short header) QUICPlugin reads the payload's first byte only:
+        // quic_parse_quic_bit and quic_long_header_packet's long-header test (quic_parser.cpp
+        // :1160-1167, :1105-1117) before it gives up (quic.cpp:494-498)
+        q.follow_bytes = 1;
     } else if (name == "ntp") {
         q.proto_mask = 3;
         q.n_ports = 1;

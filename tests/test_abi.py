@@ -39,7 +39,7 @@ def test_stdplugins_library_exports_its_header():
     assert funcs == ["ipxg_std_plugin", "ipxg_std_plugin_calls", "ipxg_std_plugin_free"]
     for f in funcs:
         assert hasattr(L, f), f
-    assert ctypes.sizeof(engine.Plugin) == 664  # = sizeof(ipxg_plugin), gcc x86-64 (ABI 6)
+    assert ctypes.sizeof(engine.Plugin) == 664  # = sizeof(ipxg_plugin), gcc x86-64 (ABI 7: follow_bytes fills the padding)
     p = engine.StdPlugin("quic")
     assert p.struct.masked == 1 and p.struct.prefix_mask[0][0] == 0x80 and p.struct.follow_packets == 30
     with pytest.raises(engine.IpxgError):

@@ -197,6 +197,38 @@ def test_bridge_with_reference_plugins_on_workload(mix, names, threads):
 
 
 @pytest.mark.gpu
+def test_walk_byte_budget_with_reference_quic(monkeypatch):
+    """ipxg_plugin.follow_bytes (ABI 7): the real QUIC plugin reads one payload byte of a packet
+    outside its rule (a short header), so with the budget its walked flows' short-header packets
+    cross to the host as headers + 1 byte.  Records and extension texts equal the whole-frame
+    walk's (IPXG_WALK_FULL=1), and far fewer bytes cross."""
+    import torch
+    import synthgen
+    from ipfixprobe_amd import Engine
+    m = synthgen.Mix("quic", 200_000, seed=78)
+    gen = synthgen.Generator(m, torch.device("cuda", 0), seed=78)
+    batches = [gen.batch(k * 200_000, 200_000) for k in range(3)]
+    torch.cuda.synchronize()
+    out = {}
+    for full in ("0", "1"):
+        monkeypatch.setenv("IPXG_WALK_FULL", full)
+        ep = RefPlugin("quic")
+        with Engine("s=19") as e:
+            e.add_plugin(ep.struct)
+            for fr, de in batches:
+                e.submit(fr, de, device=True)
+            e.finish()
+            got = e.poll()
+            tm = e.timing()
+        out[full] = (got, take_texts(got), tm)
+    (g0, t0, tm0), (g1, t1, tm1) = out["0"], out["1"]
+    assert sum(1 for t in t1 if t) > 50
+    assert keyed(g0, t0) == keyed(g1, t1)
+    assert tm0["plugin_packets"] == tm1["plugin_packets"] > 0
+    assert tm0["plugin_d2h_bytes"] < 0.6 * tm1["plugin_d2h_bytes"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("threads", [1, 16])
 def test_plugin_error_fails_the_call_cleanly(threads):
     """A process plugin that throws PluginError on its 50th hook call: the
