@@ -196,36 +196,59 @@ def test_bridge_with_reference_plugins_on_workload(mix, names, threads):
     assert keyed(got, tg) == keyed(want, tw)
 
 
+def _quic_flows_with_short_headers(n_short=20):
+    """The golden QUIC capture's packets, each followed by n_short packets of its flow whose UDP
+    payload starts as a 1-RTT short header (0x43): the real plugin detects QUIC on the Initial and
+    follows the flow (follow_packets), and reads one payload byte of each short-header packet."""
+    dl, pk = pcaputil.read_capture(os.path.join(REF, "quic_initial-sample.pcap"))
+    out = []
+    for (sec, usec, cl, wl, b) in pk:
+        out.append((sec, usec, cl, wl, b))
+        et = (b[12] << 8) | b[13]
+        if et == 0x0800 and b[23] == 17:
+            po = 14 + (b[14] & 15) * 4 + 8
+        elif et == 0x86DD and b[20] == 17:
+            po = 14 + 40 + 8
+        else:
+            continue
+        for k in range(n_short):
+            t = usec + 1000 * (k + 1)
+            bb = bytearray(b)
+            bb[po] = 0x43
+            out.append((sec + t // 1_000_000, t % 1_000_000, cl, wl, bytes(bb)))
+    return dl, out
+
+
 @pytest.mark.gpu
-def test_walk_byte_budget_with_reference_quic(monkeypatch):
+@pytest.mark.parametrize("batch", [None, 7])
+def test_walk_byte_budget_with_reference_quic(monkeypatch, batch):
     """ipxg_plugin.follow_bytes (ABI 7): the real QUIC plugin reads one payload byte of a packet
-    outside its rule (a short header), so with the budget its walked flows' short-header packets
+    outside its rule (a short header), so with the budget a followed flow's short-header packets
     cross to the host as headers + 1 byte.  Records and extension texts equal the whole-frame
-    walk's (IPXG_WALK_FULL=1), and far fewer bytes cross."""
-    import torch
-    import synthgen
+    walk's (IPXG_WALK_FULL=1) and the oracle's; far fewer bytes cross."""
     from ipfixprobe_amd import Engine
-    m = synthgen.Mix("quic", 200_000, seed=78)
-    gen = synthgen.Generator(m, torch.device("cuda", 0), seed=78)
-    batches = [gen.batch(k * 200_000, 200_000) for k in range(3)]
-    torch.cuda.synchronize()
+    dl, pk = _quic_flows_with_short_headers()
+    arena, desc = pcaputil.to_batch(pk)
     out = {}
     for full in ("0", "1"):
         monkeypatch.setenv("IPXG_WALK_FULL", full)
         ep = RefPlugin("quic")
-        with Engine("s=19") as e:
+        with Engine("s=16", datalink=dl) as e:
             e.add_plugin(ep.struct)
-            for fr, de in batches:
-                e.submit(fr, de, device=True)
+            e.submit_all(arena, desc, batch)
             e.finish()
             got = e.poll()
             tm = e.timing()
         out[full] = (got, take_texts(got), tm)
+    op = RefPlugin("quic")
+    want, _ = oracle_py.run_capture(arena, desc, dl, cache_exp=16, plugins=[op.struct])
+    tw = take_texts(want)
     (g0, t0, tm0), (g1, t1, tm1) = out["0"], out["1"]
-    assert sum(1 for t in t1 if t) > 50
-    assert keyed(g0, t0) == keyed(g1, t1)
-    assert tm0["plugin_packets"] == tm1["plugin_packets"] > 0
-    assert tm0["plugin_d2h_bytes"] < 0.6 * tm1["plugin_d2h_bytes"]
+    assert any(tw)
+    assert keyed(g0, t0) == keyed(want, tw)
+    assert keyed(g1, t1) == keyed(want, tw)
+    assert tm0["plugin_packets"] == tm1["plugin_packets"] >= len(pk)
+    assert tm0["plugin_d2h_bytes"] < 0.5 * tm1["plugin_d2h_bytes"]
 
 
 @pytest.mark.gpu
