@@ -335,11 +335,17 @@ static void ev_rec(ipxg_engine* e, int i) {
     // level 2: only the events around k_bin / k_ingest (0, 1), level 3 also k_bin_slow (2):
     // the others cost host time
     if (prof_on(e) && (e->prof_level == 1 || i <= 1 || (e->prof_level == 3 && i == 2)))
-        (void)hipEventRecord(e->ev[i], e->st);
+        if (hipEventRecord(e->ev[i], e->st) != hipSuccess) (void)hipGetLastError();
 }
+// (an event this batch did not record -- a path it did not take -- gives 0; its error is taken
+// off HIP's last-error slot, which the next HIPCHK(hipGetLastError()) would otherwise report as
+// the failure of whatever launch came next: "invalid resource handle" in a plugin batch's walk)
 static double ev_ms(ipxg_engine* e, int a, int b = -1) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, e->ev[a], e->ev[b < 0 ? a + 1 : b]) != hipSuccess) return 0.0;
+    if (hipEventElapsedTime(&ms, e->ev[a], e->ev[b < 0 ? a + 1 : b]) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0.0;
+    }
     return ms;
 }
 

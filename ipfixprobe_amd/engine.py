@@ -5,8 +5,10 @@ plugin and the ipxg_probe tool).  This module is plumbing: it loads the in-tree
 libipxg.so -- and fails loudly if it is missing or no GPU is present; there is no CPU
 fallback anywhere in the product path.
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -320,6 +322,21 @@ def demux(arena, desc, n_shards, datalink=DLT_EN10MB):
     return out, shard_of
 
 
+# Engines still open at interpreter exit are destroyed before the module's objects are: an engine
+# frees its walk threads' copies of the registered plugins, which the plugins' owners (StdPlugin,
+# the adapter) must outlive -- at exit after an exception the objects would go in any order.
+_LIVE = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_engines():
+    for e in list(_LIVE):
+        try:
+            e.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """One ipxg engine (one HIP stream on one device) -- the StoragePlugin-shaped lifecycle:
     submit = put_pkt for a whole batch, expire = export_expired, finish = finish."""
@@ -331,6 +348,7 @@ class Engine:
         if rc:
             raise IpxgError("ipxg_create failed (rc %d): no usable HIP device?" % rc)
         self._h = h
+        _LIVE.add(self)
 
     def _check(self, rc, what):
         if rc:

@@ -269,12 +269,15 @@ def test_early_front_defers_spills(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_early_front_on_fuzz_corpus():
+@pytest.mark.parametrize("prof", [0, 2])
+def test_early_front_on_fuzz_corpus(prof):
     """The fuzz corpus (every register-walk shape, fragments, truncations) in 4096-packet device
     batches submitted back to back with IPXG_BATCH_ASYNC: each batch's k_bin / k_bin_slow run during
     the previous batch's host walk, fragments included (k_bin_slow lists them into the batch's own
     fragment list while the walked batch's replay is done); records and ext bits equal the
-    oracle's."""
+    oracle's.  prof: with sampled stage timing (ipxg_profile, every 2nd batch) as bench.py runs it --
+    a batch's unrecorded events once left "invalid resource handle" in HIP's last-error slot,
+    which failed the next launch check of a plugin batch."""
     import torch
     from ipfixprobe_amd import Engine
     arena, desc = synth.to_batch(synth.fuzz_corpus(20000, seed=71))
@@ -288,6 +291,8 @@ def test_early_front_on_fuzz_corpus():
     eng = PrefixMarker()
     with Engine("s=18") as e:
         e.add_plugin(eng.struct)
+        if prof:
+            e.profile(True, prof)
         for d in ds:
             e.submit(a, d, device=True, asynchronous=True)
         e.finish()
