@@ -25,11 +25,14 @@ for W in ${WORKLOADS:-udp64 imix quic}; do
       python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/kt_$W.json 2> $OUT/kt_$W.err
   rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/kt_$W.err; stop "kernel trace $W" $rc; }
   if [ "${PMC:-1}" = "1" ]; then
-    for C in FETCH_SIZE WRITE_SIZE; do
-      echo "== pmc $W $C"; date
-      timeout -k 10 -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$W/$C -o run -- \
-          python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/pmc_${W}_$C.json 2> $OUT/pmc_${W}_$C.err
-      rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_${W}_$C.err; stop "pmc $W $C" $rc; }
+    # (each pass its own run: FETCH_SIZE takes 3 of the 4 TCC slots, WRITE_SIZE 2; the fabric
+    # read requests by size settle how many bytes FETCH_SIZE's requests moved)
+    for C in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum"; do
+      N=$(echo $C | tr ' ' '_')
+      echo "== pmc $W $N"; date
+      timeout -k 10 -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$W/$N -o run -- \
+          python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/pmc_${W}_$N.json 2> $OUT/pmc_${W}_$N.err
+      rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_${W}_$N.err; stop "pmc $W $N" $rc; }
     done
   fi
 done
