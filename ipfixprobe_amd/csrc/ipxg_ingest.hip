@@ -1600,8 +1600,18 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
                     for (uint32_t u = 0; u < RED_U; ++u) {
                         const uint32_t n = (cs[u] & 63) + 1;
+#ifdef IPXG_RED_NT  // tuning knob: streaming (non-temporal) record loads
+                        {
+                            typedef uint32_t rv4 __attribute__((ext_vector_type(4)));
+                            const rv4 v = __builtin_nontemporal_load(reinterpret_cast<const rv4*>(
+                                &segs[(size_t)(cs[u] >> 20) * bv.seg_cap + ((cs[u] >> 6) & 0x3FFF) * 64 +
+                                      (lane < n ? lane : 0)]));
+                            r[u] = make_uint4(v.x, v.y, v.z, v.w);
+                        }
+#else
                         r[u] = segs[(size_t)(cs[u] >> 20) * bv.seg_cap + ((cs[u] >> 6) & 0x3FFF) * 64 +
                                     (lane < n ? lane : 0)];  // unconditional load
+#endif
                     }
                 };
                 auto fold = [&](const uint4(&r)[RED_U], const uint32_t(&cs)[RED_U], uint32_t j0) {
