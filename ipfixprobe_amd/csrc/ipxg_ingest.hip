@@ -1600,7 +1600,10 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
                     for (uint32_t u = 0; u < RED_U; ++u) {
                         const uint32_t n = (cs[u] & 63) + 1;
-#ifdef IPXG_RED_NT  // tuning knob: streaming (non-temporal) record loads
+#ifndef IPXG_RED_NT  // streaming (non-temporal) record loads: each is read once (udp64 step -0.5 %, gpurun_out/r5rnt2)
+#define IPXG_RED_NT 1
+#endif
+#if IPXG_RED_NT
                         {
                             typedef uint32_t rv4 __attribute__((ext_vector_type(4)));
                             const rv4 v = __builtin_nontemporal_load(reinterpret_cast<const rv4*>(
