@@ -28,14 +28,15 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 7 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+#define IPXG_ABI_VERSION 8 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
                               3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
                               4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
                               5: ipxg_timing gained plugin_overlapped
                               6: ipxg_profile takes a sampling period; ipxg_timing gained
                                  slow_redos; ipxg_plugin gained all_packets
                               7: ipxg_plugin gained follow_bytes; ipxg_timing gained
-                                 plugin_d2h_bytes */
+                                 plugin_d2h_bytes
+                              8: IPXG_BATCH_OFFSET16 (arenas up to 64 GiB) */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -43,7 +44,8 @@ extern "C" {
 #define IPXG_ENOMEM (-2)   /* device or host allocation failed                           */
 #define IPXG_EDEVICE (-3)  /* HIP runtime error (message in ipxg_last_error)             */
 #define IPXG_EALIGN (-4)   /* a frame offset is not 16-byte aligned                      */
-#define IPXG_ETOOBIG (-5)  /* batch larger than IPXG_MAX_BATCH or arena > 4 GiB          */
+#define IPXG_ETOOBIG (-5)  /* batch larger than IPXG_MAX_BATCH, or arena > 4 GiB (64 GiB
+                              with IPXG_BATCH_OFFSET16)                                  */
 #define IPXG_EIO (-6)      /* file could not be read / unsupported capture format        */
 #define IPXG_ESTATE (-7)   /* call not valid in the engine's current state               */
 #define IPXG_EPLUGIN (-8)  /* a process plugin's hook failed -- the reference's PluginError
@@ -73,9 +75,11 @@ extern "C" {
  * caplen/wirelen are uint16_t exactly as parse_packet's parameters (the pcap plugin passes
  * pcap_pkthdr's 32-bit lengths into them, pcap.cpp:54-70, i.e. truncated mod 2^16).
  * Timestamps are timeval split into unsigned 32-bit seconds and microseconds (the classic
- * pcap record header's own width).  offset must be a multiple of 16. */
+ * pcap record header's own width).  Frames at 16-byte aligned offsets take the register
+ * parsers; others the general one.  With IPXG_BATCH_OFFSET16 offset counts 16-byte units. */
 typedef struct ipxg_pkt_desc {
-    uint32_t offset;  /* byte offset of the frame inside the batch arena               */
+    uint32_t offset;  /* byte offset of the frame inside the batch arena (16-byte units
+                         with IPXG_BATCH_OFFSET16)                                      */
     uint16_t caplen;  /* captured bytes present in the arena                            */
     uint16_t wirelen; /* original length on the wire                                    */
     uint32_t ts_sec;
@@ -90,10 +94,15 @@ typedef struct ipxg_pkt_desc {
                                 * trip instead of two).  Host batches: copied into one of two
                                 * device staging slots on a copy stream while the previous
                                 * batch is in the kernels (pinned host memory for overlap) */
+#define IPXG_BATCH_OFFSET16 0x4u /* every descriptor's offset counts 16-byte units: frames
+                                  * start 16-byte aligned and the arena may hold up to
+                                  * 64 GiB - 4 KiB (the 32-bit byte offsets cap it at 4 GiB,
+                                  * 5M frames of the configs[4] mix) */
 
 typedef struct ipxg_batch {
     const uint8_t* arena;       /* frame bytes                                          */
-    uint64_t arena_len;         /* bytes valid in arena (<= 4 GiB)                      */
+    uint64_t arena_len;         /* bytes valid in arena (<= 4 GiB; IPXG_BATCH_OFFSET16:
+                                   <= 64 GiB - 4 KiB)                                   */
     const ipxg_pkt_desc* desc;  /* n descriptors in arrival order                       */
     uint32_t n;                 /* packets in this batch, <= IPXG_MAX_BATCH             */
     uint32_t flags;             /* IPXG_BATCH_*                                          */
@@ -578,7 +587,8 @@ void ipxg_capture_free(ipxg_capture* cap);
  * without an IP header go to shard 0.  Reads at most the first 64 header bytes per frame.
  * shard_of[i] (n entries) receives packet i's shard; counts[k] (n_shards) the shard sizes.
  * ipxg_demux_split then gathers shard k's frames into its own batch (arena at 16-byte aligned
- * offsets, descriptors in arrival order): arena_out must hold ipxg_demux_arena_bytes(...). */
+ * offsets, descriptors in arrival order; offsets counted as in's are, bytes or 16-byte units
+ * with IPXG_BATCH_OFFSET16): arena_out must hold ipxg_demux_arena_bytes(...). */
 int ipxg_demux(const ipxg_batch* in, uint32_t datalink, uint32_t n_shards, uint32_t* shard_of, uint32_t* counts);
 uint64_t ipxg_demux_arena_bytes(const ipxg_batch* in, const uint32_t* shard_of, uint32_t shard);
 int ipxg_demux_split(const ipxg_batch* in, const uint32_t* shard_of, uint32_t shard, uint8_t* arena_out,

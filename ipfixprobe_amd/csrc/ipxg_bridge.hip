@@ -54,7 +54,8 @@ __device__ __forceinline__ bool classify_packet(const BatchView& b, const Params
     DevPkt pk;
     ParseCounts dummy = {};
     bool reg = false, hit = false;
-    if (eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim) {
+    // (the register window by buffer loads with byte offsets; 16-byte units: the general parser)
+    if (eth && !b.oshift && fast_shape(b, d) && (uint64_t)d.offset + 80u <= b.arena_lim) {
         uint32_t w[WIDE_DW];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -78,8 +79,8 @@ __device__ __forceinline__ bool classify_packet(const BatchView& b, const Params
         }
     }
     if (!reg) {
-        stage_frame(col, b.arena, d.offset, d.caplen);
-        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        stage_frame(col, frame_ptr(b, d), d.caplen);
+        LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
         if (!parse_frame<true>(S, d.caplen, p.dlt, pk, dummy)) return false;
         if (pk.ip_version != 4 && pk.ip_version != 6) return false;
         if (pk.frag_off) return false;  // no L4 header (its ports come from the fragmentation cache)
@@ -113,8 +114,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_classify(BatchView b, Params p, 
                                                          uint32_t nrules, BatchCtl* ctl) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     uint32_t* col = &win[threadIdx.x];
-    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     uint32_t claimed_n = 0;
     for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
         uint64_t lo;
@@ -130,8 +130,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_marks(BatchView b, Params
                                                              uint32_t nrules, BatchCtl* ctl, BinView bv) {
     __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
     uint32_t* col = &win[threadIdx.x];
-    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     uint32_t claimed_n = 0;
     for (uint32_t g = blockIdx.x; g < bv.bin_grid; g += gridDim.x) {  // (block-uniform)
         const uint32_t n = min(bv.mark_cnt[g], bv.slow_stride);
@@ -259,8 +258,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_plugin_pkts(BatchView b, Params 
     const uint32_t i = idx[k];
     const ipxg_pkt_desc d = b.desc[i];
     uint32_t* col = &win[threadIdx.x];
-    stage_frame(col, b.arena, d.offset, d.caplen);
-    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    stage_frame(col, frame_ptr(b, d), d.caplen);
+    LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
     DevPkt pk;
     ParseCounts c = {};
     const bool ok = parse_frame<true>(S, d.caplen, p.dlt, pk, c);
@@ -324,10 +323,10 @@ __global__ __launch_bounds__(256) void k_plugin_bytes(BatchView b, const uint32_
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < m; k += gridDim.x * 4) {
         const ipxg_pkt_desc d = b.desc[idx[k]];
-        const uint8_t* src = b.arena + d.offset;
+        const uint8_t* src = frame_ptr(b, d);
         uint8_t* dst = out + off[k];
         const uint32_t n16 = (uint32_t)((off[k + 1] - off[k]) >> 4);  // (the frame, or its budget)
-        if ((d.offset & 15u) == 0 && (uint64_t)d.offset + 16ull * n16 <= b.arena_lim) {
+        if (frame_aligned(b, d) && frame_off(b, d) + 16ull * n16 <= b.arena_len) {
             for (uint32_t j = lane; j < n16; j += 64)
                 reinterpret_cast<uint4*>(dst)[j] = reinterpret_cast<const uint4*>(src)[j];
         } else {

@@ -86,10 +86,12 @@ int ipxg_demux(const ipxg_batch* in, uint32_t datalink, uint32_t n_shards, uint3
     if (!in || !shard_of || !counts || n_shards == 0 || (in->n && (!in->arena || !in->desc))) return IPXG_EINVAL;
     if (in->flags & IPXG_BATCH_DEVICE) return IPXG_EINVAL;  // a host ring's batch
     std::memset(counts, 0, n_shards * sizeof(uint32_t));
+    const uint32_t sh = (in->flags & IPXG_BATCH_OFFSET16) ? 4u : 0u;
     for (uint32_t i = 0; i < in->n; ++i) {
         const ipxg_pkt_desc& d = in->desc[i];
-        if ((uint64_t)d.offset + d.caplen > in->arena_len) return IPXG_EINVAL;
-        const uint32_t s = shard_of_frame(in->arena + d.offset, d.caplen, datalink, n_shards);
+        const uint64_t fo = (uint64_t)d.offset << sh;
+        if (fo + d.caplen > in->arena_len) return IPXG_EINVAL;
+        const uint32_t s = shard_of_frame(in->arena + fo, d.caplen, datalink, n_shards);
         shard_of[i] = s;
         counts[s]++;
     }
@@ -109,14 +111,16 @@ int ipxg_demux_split(const ipxg_batch* in, const uint32_t* shard_of, uint32_t sh
     if (!in || !shard_of || !n_out || (in->n && (!arena_out || !desc_out))) return IPXG_EINVAL;
     uint64_t off = 0;
     uint32_t k = 0;
+    // the shard's descriptors count offsets as the input's do (bytes, or 16-byte units)
+    const uint32_t sh = (in->flags & IPXG_BATCH_OFFSET16) ? 4u : 0u;
     for (uint32_t i = 0; i < in->n; ++i) {
         if (shard_of[i] != shard) continue;
         ipxg_pkt_desc d = in->desc[i];
-        if (off > 0xFFFFFFFFull) return IPXG_ETOOBIG;  // descriptor offsets are 32-bit
-        std::memcpy(arena_out + off, in->arena + d.offset, d.caplen);
+        if ((off >> sh) > 0xFFFFFFFFull) return IPXG_ETOOBIG;  // descriptor offsets are 32-bit
+        std::memcpy(arena_out + off, in->arena + ((uint64_t)d.offset << sh), d.caplen);
         const uint32_t pad = ((d.caplen + 15u) & ~15u) - d.caplen;
         if (pad) std::memset(arena_out + off + d.caplen, 0, pad);
-        d.offset = (uint32_t)off;
+        d.offset = (uint32_t)(off >> sh);
         desc_out[k++] = d;
         off += ((uint64_t)d.caplen + 15) & ~15ull;
     }

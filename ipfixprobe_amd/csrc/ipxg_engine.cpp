@@ -1211,21 +1211,38 @@ static int launch_rest(ipxg_engine* e, const BatchView& bv, Params p, const BinV
     return post_batch(e, bv, p, n, binned, false);
 }
 
+// The arena's size limit: 4 GiB with byte offsets, 2^32 16-byte units less a page with
+// IPXG_BATCH_OFFSET16 (descriptor offsets are 32-bit either way)
+static constexpr uint64_t ARENA16_MAX = (1ull << 36) - 4096;
+static int check_arena(ipxg_engine* e, const ipxg_batch* batch) {
+    if (batch->flags & IPXG_BATCH_OFFSET16) {
+        if (batch->arena_len > ARENA16_MAX) return set_err(e, IPXG_ETOOBIG, "arena larger than 64 GiB - 4 KiB");
+    } else if (batch->arena_len > (1ull << 32)) {
+        return set_err(e, IPXG_ETOOBIG, "arena larger than 4 GiB (IPXG_BATCH_OFFSET16 takes up to 64 GiB)");
+    }
+    return IPXG_OK;
+}
+static void set_arena_view(BatchView& bv, const ipxg_batch* batch) {
+    bv.arena_lim = (uint32_t)std::min<uint64_t>(batch->arena_len, 0xFFFFFF00ull);
+    bv.arena_len = batch->arena_len;
+    bv.oshift = (batch->flags & IPXG_BATCH_OFFSET16) ? 4u : 0u;
+}
+
 static int submit_impl(ipxg_engine* e, const ipxg_batch* batch) {
     if (!e || !batch) return IPXG_EINVAL;
     const uint32_t n = batch->n;
     if (n == 0) return IPXG_OK;
     if (n > IPXG_MAX_BATCH) return set_err(e, IPXG_ETOOBIG, "batch larger than IPXG_MAX_BATCH");
-    if (batch->arena_len > (1ull << 32)) return set_err(e, IPXG_ETOOBIG, "arena larger than 4 GiB");
-    if (!batch->arena || !batch->desc) return set_err(e, IPXG_EINVAL, "null arena/desc");
     int rc;
+    if ((rc = check_arena(e, batch))) return rc;
+    if (!batch->arena || !batch->desc) return set_err(e, IPXG_EINVAL, "null arena/desc");
     const bool binned = !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST);
     const bool dev_batch = (batch->flags & IPXG_BATCH_DEVICE) != 0;
     const bool async = (batch->flags & IPXG_BATCH_ASYNC) && binned && !e->strict;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
     BatchView bv;
     bv.n = n;
-    bv.arena_lim = (uint32_t)std::min<uint64_t>(batch->arena_len, 0xFFFFFF00ull);
+    set_arena_view(bv, batch);
     int slot = -1;
     if (!dev_batch && async) {
         // Host batch, asynchronous: its H2D copy goes into the staging slot the batch in
@@ -3269,9 +3286,10 @@ int ipxg_parse_batch(ipxg_engine* e, const ipxg_batch* batch, ipxg_parsed_pkt* o
     if (!n) return IPXG_OK;
     int rc;
     HIPCHK(e, hipSetDevice(e->cfg.device_id));
+    if ((rc = check_arena(e, batch))) return rc;
     BatchView bv;
     bv.n = n;
-    bv.arena_lim = (uint32_t)std::min<uint64_t>(batch->arena_len, 0xFFFFFF00ull);
+    set_arena_view(bv, batch);
     bv.base_sec = 0;
     if (batch->flags & IPXG_BATCH_DEVICE) {
         bv.arena = batch->arena;

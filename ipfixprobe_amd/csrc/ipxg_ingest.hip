@@ -103,10 +103,10 @@ struct BinLds {
 
 // ---- phase A ------------------------------------------------------------------------------
 // k_bin's loads are buffer loads through two wave-uniform resource descriptors (the
-// descriptor array and the frame arena): each is one 16-byte (or 8-byte) load instruction,
-// where a plain load was narrowed by the compiler to the bytes used (4 instructions for a
-// 48-byte head); a lane with nothing to load gives an offset past the buffer's end and gets
-// zeros, with no memory traffic.  The loads are unconditional, so the number in flight is
+// descriptor array and the frame arena, or the wave's 4 GiB window of it: arena_win): each is
+// one 16-byte (or 8-byte) load instruction, where a plain load was narrowed by the compiler
+// to the bytes used (4 instructions for a 48-byte head); a lane with nothing to load gives an
+// offset past the buffer's end and gets zeros, with no memory traffic.  The loads are unconditional, so the number in flight is
 // the same on every path and s_waitcnt waits for exactly the one it needs.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -139,16 +139,28 @@ __device__ __forceinline__ uint4 u4(const u32x4 v) { return make_uint4(v.x, v.y,
 // ok: load the frame's chunks (caplen >= 48: the first 3 always; in the wide walk the later
 // ones only below caplen -- a chunk past it reads as zeros with no memory traffic)
 // AUX >= 0: that policy instead (line mode's k_bin)
+// (rs: the arena or the wave's window of it, o: the frame's byte offset there)
 template <int NC, int AUX = -1>
-__device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok) {
-    const uint32_t o = ok ? d.offset : BUF_OOB;
+__device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t rs, uint32_t o, uint32_t caplen, bool ok) {
+    o = ok ? o : BUF_OOB;
     Head<NC> h;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-        const uint32_t ok_k = k < 3 || (uint32_t)(16 * k) < d.caplen;
-        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, ok_k ? o + 16 * k : BUF_OOB, 0,
+        const uint32_t ok_k = k < 3 || (uint32_t)(16 * k) < caplen;
+        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(rs, ok_k ? o + 16 * k : BUF_OOB, 0,
                                                           AUX >= 0 ? AUX : NC > 3 ? IPXG_WIDE_LOAD_AUX : IPXG_LOAD_AUX));
     }
+    return h;
+}
+// One aligned frame's head outside a pipelined walk: buffer loads with byte offsets; with
+// 16-byte units plain loads through the frame's address (the chunks below caplen)
+template <int NC>
+__device__ __forceinline__ Head<NC> load_head_at(const BatchView& b, __amdgpu_buffer_rsrc_t rs_all, const ipxg_pkt_desc& d) {
+    if (!b.oshift) return load_head<NC>(rs_all, d.offset, d.caplen, true);
+    const uint4* f = reinterpret_cast<const uint4*>(frame_ptr(b, d));
+    Head<NC> h;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) h.c[k] = (k < 3 || (uint32_t)(16 * k) < d.caplen) ? f[k] : make_uint4(0, 0, 0, 0);
     return h;
 }
 
@@ -162,17 +174,16 @@ __device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t arena, cons
 #ifndef IPXG_BIN_XPOSE
 #define IPXG_BIN_XPOSE 0
 #endif
-__device__ __forceinline__ Head<4> load_head_x(__amdgpu_buffer_rsrc_t arena, const ipxg_pkt_desc& d, bool ok,
-                                               bool& seq) {
+__device__ __forceinline__ Head<4> load_head_x(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool ok, bool& seq) {
     const uint32_t lane = lane_id();
-    const uint32_t o0 = __builtin_amdgcn_readfirstlane(d.offset);
-    seq = __ballot(ok && d.offset == o0 + 64u * lane) == ~0ull;  // wave-uniform
-    const uint32_t o = ok ? d.offset : BUF_OOB;
+    const uint32_t o0 = __builtin_amdgcn_readfirstlane(off);
+    seq = __ballot(ok && off == o0 + 64u * lane) == ~0ull;  // wave-uniform
+    const uint32_t o = ok ? off : BUF_OOB;
     Head<4> h;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t a = seq ? o0 + 1024u * k + 16u * lane : (k < 3 ? o + 16u * k : BUF_OOB);
-        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, a, 0, IPXG_LOAD_AUX));
+        h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, IPXG_LOAD_AUX));
     }
     return h;
 }
@@ -805,12 +816,11 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // the wave's transpose area (XP): the stage array is free during the packet loop
     uint4* const xs = reinterpret_cast<uint4*>(stage) + (tid >> 6) * 320u;
     static_assert(!XP || IPXG_BLOCK / 64 * 320 <= TILE, "transpose areas fit the stage array");
-    auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(d); };
+    auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(b, d); };
     bool nonmono = false;
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     const uint32_t lane = tid & 63, wave = tid >> 6;
     if (blockIdx.x == 0 && tid == 0 && p.prev_valid) {
         const ipxg_pkt_desc d0 = b.desc[0];
@@ -878,8 +888,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         Dr[k] = load_desc<LAUX>(rs_desc, i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
-            if constexpr (XP) Hr[h] = load_head_x(rs_arena, Dr[h], want(Dr[h]), Xr[h]);
-            else Hr[h] = load_head<NC, LAUX>(rs_arena, Dr[h], want(Dr[h]));
+            const bool wh = want(Dr[h]);
+            const ArenaWin aw = arena_win(b, rs_arena, Dr[h], wh);
+            uint32_t o;
+            const bool in = win_off(b, aw, Dr[h], o);
+            if constexpr (XP) Hr[h] = load_head_x(aw.rs, o, wh && in, Xr[h]);
+            else Hr[h] = load_head<NC, LAUX>(aw.rs, o, Dr[h].caplen, wh && in);
         } else {
 #pragma unroll
             for (int q = 0; q < 3; ++q) g_dummy_rec[(k * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
@@ -936,9 +950,22 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t ia = j + DA < K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - K) * IPXG_BLOCK + tid;
             Dr[jj % DA] = load_desc<LAUX>(rs_desc, j + DA < K ? clamp(ia, lim) : clamp(ia, next_lim));
             const ipxg_pkt_desc dh = Dr[(jj + HA) % DA];
-            if constexpr (XP) Hr[jj % HA] = load_head_x(rs_arena, dh, want(dh), Xr[jj % HA]);
-            else Hr[jj % HA] = load_head<NC, LAUX>(rs_arena, dh, want(dh));
+            {
+                const bool wh = want(dh);
+                const ArenaWin aw = arena_win(b, rs_arena, dh, wh);
+                uint32_t o;
+                const bool in = win_off(b, aw, dh, o);
+                if constexpr (XP) Hr[jj % HA] = load_head_x(aw.rs, o, wh && in, Xr[jj % HA]);
+                else Hr[jj % HA] = load_head<NC, LAUX>(aw.rs, o, dh.caplen, wh && in);
+            }
             const bool act = i < lim;
+            // 16-byte units: a frame outside the wave's window was not loaded (the slow path)
+            bool inw = true;
+            if (b.oshift) {  // (uniform; the window the head was loaded through, again)
+                const ArenaWin aw = arena_win(b, rs_arena, dc, want(dc));
+                uint32_t o;
+                inw = win_off(b, aw, dc, o);
+            }
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
             const uint32_t ps = (uint32_t)__builtin_amdgcn_update_dpp((int)dc.ts_sec, (int)dc.ts_sec, 0x138, 0xF, 0xF, false);
@@ -965,7 +992,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         w[4 * k + 3] = hc.c[k].w;
                     }
                     bool ext = false;
-                    if (fast_ok && fast_shape(dc) && parse_medium<PLUG, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
+                    if (fast_ok && fast_shape(b, dc) && inw && parse_medium<PLUG, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
                         have = true;
                         walked += ext ? 1 : 0;
                         if constexpr (PLUG) {
@@ -984,7 +1011,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         slow = true;
                     }
                 } else {
-                    if (fast_ok && fast_shape(dc) && parse_fast(hc.c[0], hc.c[1], hc.c[2], dc.caplen, p.frag_enable, pk, c))
+                    if (fast_ok && fast_shape(b, dc) && inw && parse_fast(hc.c[0], hc.c[1], hc.c[2], dc.caplen, p.frag_enable, pk, c))
                         have = true;
                     else
                         slow = true;
@@ -1081,28 +1108,40 @@ __device__ __forceinline__ ipxg_pkt_desc slow_desc(const uint4 e) {
 
 // The first IPXG_WIN bytes of an aligned frame as 16-byte buffer loads (a chunk at or past
 // caplen, and every chunk of an unaligned frame, reads as zeros with no memory traffic).
+// e.y: the descriptor's offset field (16-byte units with IPXG_BATCH_OFFSET16, whose frames are
+// all aligned).
 constexpr int SLOW_NCH = IPXG_WIN / 16;
 struct SlowWin {
     uint4 c[SLOW_NCH];
+    bool inw;  // the frame lies in the wave's window (byte offsets: always)
 };
 
-__device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t arena, const uint4 e) {
+__device__ __forceinline__ bool slow_aligned(const BatchView& b, const uint4 e) { return b.oshift || !(e.y & 15); }
+// (wave-collective: the wave's window, arena_win; a frame outside it is staged by byte loads)
+__device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t rs_all, const BatchView& b, const uint4 e) {
     const uint32_t cap = e.z & 0xFFFFu;
-    const uint32_t o = (e.y & 15) ? BUF_OOB : e.y;
+    ipxg_pkt_desc d;
+    d.offset = e.y;
+    const bool want = slow_aligned(b, e) && cap != 0;
+    const ArenaWin aw = arena_win(b, rs_all, d, want);
+    uint32_t o;
+    const bool in = win_off(b, aw, d, o);
     SlowWin w;
+    w.inw = in;
+    o = want && in ? o : BUF_OOB;
 #pragma unroll
     for (int k = 0; k < SLOW_NCH; ++k)
-        w.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(arena, (uint32_t)(16 * k) < cap ? o + 16 * k : BUF_OOB, 0,
+        w.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(aw.rs, (uint32_t)(16 * k) < cap ? o + 16 * k : BUF_OOB, 0,
                                                           IPXG_WIDE_LOAD_AUX));
     return w;
 }
 
 // The window into the lane's LDS column, zero-masked past caplen, plus one zero chunk so
 // straddling reads see zeros (stage_frame's layout); unaligned frames: stage_frame's byte loads.
-__device__ __forceinline__ void put_window(uint32_t* col, const uint8_t* arena, const uint4 e, const SlowWin& w) {
+__device__ __forceinline__ void put_window(uint32_t* col, const BatchView& b, const uint4 e, const SlowWin& w) {
     const uint32_t cap = e.z & 0xFFFFu;
-    if (e.y & 15) {
-        stage_frame(col, arena, e.y, cap);
+    if (!slow_aligned(b, e) || !w.inw) {
+        stage_frame(col, b.arena + ((uint64_t)e.y << b.oshift), cap);
         return;
     }
     const uint32_t nch = ((cap < IPXG_WIN ? cap : IPXG_WIN) + 15) >> 4;
@@ -1128,8 +1167,8 @@ __device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b,
                                             uint32_t (&ix)[BIN_K], uint32_t& tb_or, uint4* marks, uint32_t* nmark) {
     const ipxg_pkt_desc d = slow_desc(e);
     const uint32_t i = e.x & SLOW_IDX_MASK;
-    put_window(col, b.arena, e, w);
-    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    put_window(col, b, e, w);
+    LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
     DevPkt pk;
     if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) return;
     if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false
@@ -1177,8 +1216,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     // k_bin workgroup b's slow packets, into segment column bin_grid + b
     const uint32_t ns = bv.slow_cnt[blockIdx.x];  // final: k_bin has completed
     const uint4* const list = slow_list + (size_t)blockIdx.x * bv.slow_stride;
-    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
     if (ns == 0) return;  // no work: k_reduce does not read the column
 #if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 1  // timing experiment: the launch alone
@@ -1245,14 +1283,14 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             return j < BIN_K && k < ns ? list[tile + ord[k - tile]] : make_uint4(0, BUF_OOB, 0, 0);
         };
         uint4 e0 = entry(0), e1 = entry(1);
-        SlowWin w0 = load_win(rs_arena, e0);
+        SlowWin w0 = load_win(rs_arena, b, e0);
 #pragma unroll 1
         for (int j = 0; j < BIN_K; ++j) {
             const uint32_t k0 = tile + (uint32_t)j * IPXG_BLOCK + tid;
             if (k0 >= ns) break;
             PROBE_T(s0);
             const uint4 e2 = entry(j + 2);
-            const SlowWin w1 = load_win(rs_arena, e1);
+            const SlowWin w1 = load_win(rs_arena, b, e1);
 #ifdef IPXG_PROBE
             asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // w0 (the entry and window ahead stay in flight)
             const uint64_t s1 = __builtin_readcyclecounter();
@@ -1970,9 +2008,9 @@ __device__ __forceinline__ bool gather_key(const BatchView& b, const Params& p, 
     DevPkt pk;
     ParseCounts c = {};
     bool ok = false;
-    const bool reg = eth && fast_shape(d) && (uint64_t)d.offset + 80u <= b.arena_lim;
+    const bool reg = eth && fast_shape(b, d) && frame_off(b, d) + 80u <= b.arena_len;
     if (reg) {
-        const Head<5> h = load_head<5>(rs_arena, d, true);
+        const Head<5> h = load_head_at<5>(b, rs_arena, d);
         uint32_t w[WIDE_DW];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -1986,8 +2024,8 @@ __device__ __forceinline__ bool gather_key(const BatchView& b, const Params& p, 
     }
     if (!ok) {
         DevPkt q;
-        stage_frame(col, b.arena, d.offset, d.caplen);
-        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        stage_frame(col, frame_ptr(b, d), d.caplen);
+        LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
         if (!parse_frame<false>(S, d.caplen, p.dlt, q, c)) return false;
         pk = q;
     }
@@ -2011,8 +2049,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Para
     uint32_t* col = &win[threadIdx.x];
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     for (uint32_t i = blockIdx.x * IPXG_BLOCK + threadIdx.x; i < b.n; i += gridDim.x * IPXG_BLOCK) {
         uint64_t lo;
         if (!gather_key(b, p, f, rs_desc, rs_arena, col, i, lo)) continue;
@@ -2024,18 +2061,36 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Para
 // Would k_bin's walk for this batch (p.wide, p.tile_agg: the variant it ran) have taken packet d
 // in registers?  pk: the parse when it would.  (A frame it left to k_bin_slow was never in one of
 // its tile aggregates.)
-__device__ __forceinline__ bool kbin_takes(const Params& p, __amdgpu_buffer_rsrc_t rs_arena, const ipxg_pkt_desc& d,
-                                           DevPkt& pk) {
+// 16-byte units: k_bin's wave of packet i (the 64-aligned group) loaded through the window of
+// its first frame the walk wanted (arena_win); a frame outside it went to k_bin_slow.
+__device__ __forceinline__ bool kbin_window_has(const BatchView& b, bool fast_ok, uint32_t i, const ipxg_pkt_desc& d) {
+    if (!b.oshift) return true;
+    const uint32_t g0 = i & ~63u, g1 = min(b.n, g0 + 64u);
+    uint32_t u0 = d.offset;
+    for (uint32_t k = g0; k < g1; ++k) {
+        const ipxg_pkt_desc e = b.desc[k];
+        if (fast_ok && fast_shape(b, e)) {
+            u0 = e.offset;
+            break;
+        }
+    }
+    ArenaWin w;
+    w.ubase = u0 > WIN_UNITS / 2 ? u0 - WIN_UNITS / 2 : 0u;
+    uint32_t o;
+    return win_off(b, w, d, o);
+}
+__device__ __forceinline__ bool kbin_takes(const BatchView& b, const Params& p, __amdgpu_buffer_rsrc_t rs_arena,
+                                           uint32_t i, const ipxg_pkt_desc& d, DevPkt& pk) {
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
-    if (!(fast_ok && fast_shape(d))) return false;
+    if (!(fast_ok && fast_shape(b, d) && kbin_window_has(b, fast_ok, i, d))) return false;
     ParseCounts c = {};
     bool ext = false;
     if (!p.wide) {
-        const Head<3> h = load_head<3>(rs_arena, d, true);
+        const Head<3> h = load_head_at<3>(b, rs_arena, d);
         return parse_fast(h.c[0], h.c[1], h.c[2], d.caplen, p.frag_enable, pk, c);
     }
     if (p.tile_agg) {
-        const Head<WIDE_DW / 4> h = load_head<WIDE_DW / 4>(rs_arena, d, true);
+        const Head<WIDE_DW / 4> h = load_head_at<WIDE_DW / 4>(b, rs_arena, d);
         uint32_t w[WIDE_DW];
 #pragma unroll
         for (int k = 0; k < WIDE_DW / 4; ++k) {
@@ -2046,7 +2101,7 @@ __device__ __forceinline__ bool kbin_takes(const Params& p, __amdgpu_buffer_rsrc
         }
         return parse_medium<false, WIDE_DW>(w, d.caplen, p.frag_enable, pk, c, ext);
     }
-    const Head<WIDE2_DW / 4> h = load_head<WIDE2_DW / 4>(rs_arena, d, true);
+    const Head<WIDE2_DW / 4> h = load_head_at<WIDE2_DW / 4>(b, rs_arena, d);
     uint32_t w[WIDE2_DW];
 #pragma unroll
     for (int k = 0; k < WIDE2_DW / 4; ++k) {
@@ -2070,8 +2125,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather_ranges(BatchView 
     (void)f;
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_arena = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     for (uint32_t q = blockIdx.x; q < nr; q += gridDim.x) {  // (block-uniform)
         const uint4 rg = ranges[q];
         const uint64_t key = ((uint64_t)rg.y << 32) | rg.x;
@@ -2080,7 +2134,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather_ranges(BatchView 
         const uint32_t last = min(rg.w, b.n - 1);
         for (uint32_t i = rg.z + threadIdx.x; i <= last; i += IPXG_BLOCK) {
             DevPkt pk;
-            if (!kbin_takes(p, rs_arena, load_desc(rs_desc, i), pk)) continue;
+            if (!kbin_takes(b, p, rs_arena, i, load_desc(rs_desc, i), pk)) continue;
             if (pk.ip_version != 4 && pk.ip_version != 6) continue;
             uint64_t lo, hf;
             uint32_t cdir;

@@ -68,8 +68,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_ingest(BatchView b, Params p, Ta
             }
         }
         if (!act) continue;
-        stage_frame(col, b.arena, d.offset, d.caplen);
-        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        stage_frame(col, frame_ptr(b, d), d.caplen);
+        LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
         DevPkt pk;
         if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
         if (pk.ip_version != 4 && pk.ip_version != 6) {
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void k_frag_walk(BatchView b, Params p, FragVi
     for (uint32_t k = j; k < nfrag && (uint32_t)(f.sorted[k] >> 24) == bucket; ++k) {
         const uint32_t idx = (uint32_t)(f.sorted[k] & 0xFFFFFF);
         ipxg_pkt_desc d = b.desc[idx];
-        GlobalSrc g{b.arena + d.offset, d.caplen};
+        GlobalSrc g{frame_ptr(b, d), d.caplen};
         ParseCounts dummy = {};
         DevPkt pk;
         parse_frame<false>(g, d.caplen, p.dlt, pk, dummy);
@@ -671,8 +671,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_parse_batch(BatchView b, uint32_
     if (i >= b.n) return;
     const ipxg_pkt_desc d = b.desc[i];
     uint32_t* col = &win[threadIdx.x];
-    stage_frame(col, b.arena, d.offset, d.caplen);
-    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    stage_frame(col, frame_ptr(b, d), d.caplen);
+    LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
     DevPkt pk;
     ParseCounts c = {};
     const bool ok = parse_frame<true>(S, d.caplen, dlt, pk, c);
@@ -759,13 +759,13 @@ __global__ __launch_bounds__(256) void k_pstats(BatchView b, Params p, unsigned 
         DevPkt pk;
         ParseCounts dummy = {};
         bool ok = false, fast = false;
-        if (eth && fast_shape(d)) {
-            const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
+        if (eth && fast_shape(b, d)) {
+            const uint4* fr = reinterpret_cast<const uint4*>(frame_ptr(b, d));
             fast = ok = parse_fast(fr[0], fr[1], fr[2], d.caplen, false, pk, dummy);
         }
         if (!fast) {
-            stage_frame(&win[tid], b.arena, d.offset, d.caplen);
-            LdsFrame S{{&win[tid], {b.arena + d.offset, d.caplen}}};
+            stage_frame(&win[tid], frame_ptr(b, d), d.caplen);
+            LdsFrame S{{&win[tid], {frame_ptr(b, d), d.caplen}}};
             ok = parse_frame<false>(S, d.caplen, p.dlt, pk, dummy);
         }
         if (pk.l4 && (ok ? (pk.src_port == 0 && pk.dst_port == 0) : pk.l4 == 6)) {  // rare

@@ -247,9 +247,64 @@ struct BatchView {
     const ipxg_pkt_desc* desc;
     uint32_t n;
     uint32_t base_sec;   // tbits bucket origin (first packet's seconds), or BASE_FROM_DESC0
-    uint32_t arena_lim;  // min(arena bytes, 0xFFFFFF00): the range of k_bin's buffer loads
+    uint32_t arena_lim;  // min(arena bytes, 0xFFFFFF00): the range of the byte-offset buffer loads
+    uint32_t oshift;     // 4: descriptor offsets count 16-byte units (IPXG_BATCH_OFFSET16), else 0
+    uint64_t arena_len;  // bytes valid in the arena
 };
 constexpr uint32_t BASE_FROM_DESC0 = 0xFFFFFFFFu;
+#ifdef __HIPCC__
+// frame d's byte offset in the arena, and its address
+__device__ __forceinline__ uint64_t frame_off(const BatchView& b, const ipxg_pkt_desc& d) {
+    return (uint64_t)d.offset << b.oshift;
+}
+__device__ __forceinline__ const uint8_t* frame_ptr(const BatchView& b, const ipxg_pkt_desc& d) {
+    return b.arena + frame_off(b, d);
+}
+__device__ __forceinline__ bool frame_aligned(const BatchView& b, const ipxg_pkt_desc& d) {
+    return b.oshift != 0 || (d.offset & 15) == 0;
+}
+// The register parsers' buffer loads take 32-bit byte offsets.  With byte offsets they address
+// the whole arena (<= 4 GiB) through one resource; with 16-byte units (arenas up to 64 GiB) a
+// wave addresses a 4 GiB window of it, from 2 GiB below the first frame it loads (a record
+// index x 16 in a structured resource wraps at 4 GiB on gfx950 too -- tools/sbtest): a frame
+// outside its wave's window takes the general path (k_bin_slow, byte loads).
+constexpr uint32_t WIN_UNITS = 1u << 28;  // 4 GiB
+struct ArenaWin {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t ubase;  // the window's first 16-byte unit (unit mode)
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t arena_rsrc(const BatchView& b) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
+}
+// the window of a wave whose lanes load d where `want` (wave-uniform result); rs_all = arena_rsrc(b)
+__device__ __forceinline__ ArenaWin arena_win(const BatchView& b, __amdgpu_buffer_rsrc_t rs_all,
+                                              const ipxg_pkt_desc& d, bool want) {
+    ArenaWin w;
+    w.rs = rs_all;
+    w.ubase = 0;
+    if (b.oshift) {  // (uniform)
+        const uint64_t m = __ballot(want);
+        const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+        const uint32_t u0 = __builtin_amdgcn_readlane(d.offset, first);
+        w.ubase = __builtin_amdgcn_readfirstlane(u0 > WIN_UNITS / 2 ? u0 - WIN_UNITS / 2 : 0u);
+        const uint64_t lo = (uint64_t)w.ubase << 4;
+        const uint64_t left = b.arena_len > lo ? b.arena_len - lo : 0;
+        w.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(b.arena + lo), 0,
+                                                 (int)(uint32_t)(left < 0xFFFFFF00ull ? left : 0xFFFFFF00ull), 0x00020000);
+    }
+    return w;
+}
+// d's byte offset in window w, when the frame lies inside it (byte mode: always)
+__device__ __forceinline__ bool win_off(const BatchView& b, const ArenaWin& w, const ipxg_pkt_desc& d, uint32_t& o) {
+    if (!b.oshift) {
+        o = d.offset;
+        return true;
+    }
+    const uint32_t du = d.offset - w.ubase;
+    o = du << 4;
+    return d.offset >= w.ubase && du < WIN_UNITS - 16;  // (the head's chunks stay inside too)
+}
+#endif
 
 struct FragView {
     FragEntry* ent;      // frag_size * 4

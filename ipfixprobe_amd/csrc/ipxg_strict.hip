@@ -57,8 +57,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_strict_prep1(BatchView b, Params
     uint32_t* col = &win[tid];
     for (uint32_t i = blockIdx.x * IPXG_BLOCK + tid; i < b.n; i += gridDim.x * IPXG_BLOCK) {
         const ipxg_pkt_desc d = b.desc[i];
-        stage_frame(col, b.arena, d.offset, d.caplen);
-        LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+        stage_frame(col, frame_ptr(b, d), d.caplen);
+        LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
         DevPkt pk;
         if (!parse_frame<false>(S, d.caplen, p.dlt, pk, c)) continue;
         if (pk.ip_version != 4 && pk.ip_version != 6) {  // create_hash_key false

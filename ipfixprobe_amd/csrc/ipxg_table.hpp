@@ -699,7 +699,9 @@ __device__ __forceinline__ bool parse_fast(const uint4& c0, const uint4& c1, con
 }
 
 // a frame the register parser may take: 16-byte aligned in the arena, 48 bytes captured
-__device__ __forceinline__ bool fast_shape(const ipxg_pkt_desc& d) { return (d.offset & 15) == 0 && d.caplen >= 48; }
+__device__ __forceinline__ bool fast_shape(const BatchView& b, const ipxg_pkt_desc& d) {
+    return frame_aligned(b, d) && d.caplen >= 48;
+}
 
 // ---- register parser for the shapes of the variable-length mixes --------------------------
 // The wide walk (k_bin<., true>) loads a frame's first 80 bytes (WIDE_DW dwords) and parses
@@ -972,13 +974,11 @@ __device__ __forceinline__ ipxg_parsed_pkt to_parsed(const DevPkt& pk, bool ok) 
 // ---- header staging into LDS ------------------------------------------------------------
 // Stage the first min(caplen, IPXG_WIN) bytes of a frame into this lane's LDS column,
 // zero-masked past caplen, plus one zero chunk so straddling reads see zeros.
-__device__ __forceinline__ void stage_frame(uint32_t* col, const uint8_t* arena, uint32_t off,
-                                            uint32_t cap) {
+__device__ __forceinline__ void stage_frame(uint32_t* col, const uint8_t* f, uint32_t cap) {
     const uint32_t nbytes = cap < IPXG_WIN ? cap : IPXG_WIN;
     const uint32_t nch = (nbytes + 15) >> 4;
-    const uint8_t* f = arena + off;
     constexpr int NCH = IPXG_WIN / 16;
-    if ((off & 15) == 0) {
+    if (((uintptr_t)f & 15) == 0) {
         uint4 v[NCH];
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
@@ -1023,7 +1023,7 @@ template <bool FULL>
 __device__ __forceinline__ bool reparse(const BatchView& b, const Params& p, const FragView& f,
                                         uint32_t idx, DevPkt& pk, ipxg_pkt_desc& d) {
     d = b.desc[idx];
-    GlobalSrc g{b.arena + d.offset, d.caplen};
+    GlobalSrc g{frame_ptr(b, d), d.caplen};
     ParseCounts dummy = {};
     if (!parse_frame<FULL>(g, d.caplen, p.dlt, pk, dummy)) return false;
     apply_frag_ports(p, f, idx, pk);
@@ -1037,8 +1037,8 @@ __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p,
                                             uint32_t idx, uint32_t* col, DevPkt& pk, ipxg_pkt_desc& d) {
     d = b.desc[idx];
     ParseCounts dummy = {};
-    if ((p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB) && fast_shape(d)) {  // the common shape: registers only
-        const uint4* fr = reinterpret_cast<const uint4*>(b.arena + d.offset);
+    if ((p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB) && fast_shape(b, d)) {  // the common shape: registers only
+        const uint4* fr = reinterpret_cast<const uint4*>(frame_ptr(b, d));
         const uint4 c0 = fr[0], c1 = fr[1], c2 = fr[2];
         if (parse_fast(c0, c1, c2, d.caplen, p.frag_enable, pk, dummy)) {
             if (FULL) {  // parse_eth_hdr's MAC copy; the rest of the FULL-only fields stay zero
@@ -1055,7 +1055,7 @@ __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p,
         }
         // the wide register walk (k_bin's: tags, MPLS, PPPoE, IPv6, GRE, TCP timestamps) on the
         // 80-byte head -- the creators of the configs[2]/[4] mixes' flows, before the LDS walk
-        if ((uint64_t)d.offset + 16u * 5 <= b.arena_lim) {
+        if (frame_off(b, d) + 16u * 5 <= b.arena_len) {
             const uint4 z = make_uint4(0, 0, 0, 0);  // (chunks past caplen read as 0, as k_bin's loads)
             const uint4 c3 = 48u < d.caplen ? fr[3] : z, c4 = 64u < d.caplen ? fr[4] : z;
             const uint32_t w[WIDE_DW] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y,
@@ -1076,8 +1076,8 @@ __device__ __forceinline__ bool reparse_lds(const BatchView& b, const Params& p,
             }
         }
     }
-    stage_frame(col, b.arena, d.offset, d.caplen);
-    LdsFrame S{{col, {b.arena + d.offset, d.caplen}}};
+    stage_frame(col, frame_ptr(b, d), d.caplen);
+    LdsFrame S{{col, {frame_ptr(b, d), d.caplen}}};
     if (!parse_frame<FULL>(S, d.caplen, p.dlt, pk, dummy)) return false;
     apply_frag_ports(p, f, idx, pk);
     return true;

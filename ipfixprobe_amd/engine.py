@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("IPXG_LIB") or os.path.join(_HERE, "libipxg.so")
 DLT_EN10MB, DLT_RAW, DLT_LINUX_SLL, DLT_LINUX_SLL2 = 1, 12, 113, 276
 BATCH_DEVICE = 0x1
 BATCH_ASYNC = 0x2
+BATCH_OFFSET16 = 0x4  # descriptor offsets count 16-byte units (arenas up to 64 GiB)
 MAX_BATCH = 16 * 1024 * 1024 - 1
 
 DESC_DTYPE = np.dtype([("offset", "<u4"), ("caplen", "<u2"), ("wirelen", "<u2"),
@@ -297,11 +298,12 @@ def load_capture(path):
         lib().ipxg_capture_free(p)
 
 
-def demux(arena, desc, n_shards, datalink=DLT_EN10MB):
+def demux(arena, desc, n_shards, datalink=DLT_EN10MB, offset16=False):
     """Host symmetric demux (ipxg_demux / ipxg_demux_split): one (arena, desc) batch per shard,
     packets in arrival order, each shard's frames copied into its own arena -- the per-GPU rings
-    of the end-to-end multi-GPU path.  Returns (batches, shard_of)."""
-    b = Engine._batch(arena, desc)
+    of the end-to-end multi-GPU path (offsets counted as the input's: offset16, 16-byte units).
+    Returns (batches, shard_of)."""
+    b = Engine._batch(arena, desc, offset16=offset16)
     n = int(b.n)
     shard_of = np.zeros(n, dtype=np.uint32)
     counts = np.zeros(n_shards, dtype=np.uint32)
@@ -365,7 +367,7 @@ class Engine:
         return lib().ipxg_stream(self._h)
 
     @staticmethod
-    def _batch(arena, desc, device=False, asynchronous=False):
+    def _batch(arena, desc, device=False, asynchronous=False, offset16=False):
         b = Batch()
         if device or hasattr(arena, "data_ptr"):  # torch tensors: on the GPU, or (pinned) host
             b.arena = arena.data_ptr()
@@ -383,10 +385,14 @@ class Engine:
             b.n = len(desc)
             b.flags = BATCH_ASYNC if asynchronous else 0
             b._keep = (arena, desc)
+        if offset16:
+            b.flags |= BATCH_OFFSET16
         return b
 
-    def submit(self, arena, desc, device=False, asynchronous=False, wait_producer=True):
-        """asynchronous: may return before the batch is applied; keep the arrays / tensors alive
+    def submit(self, arena, desc, device=False, asynchronous=False, wait_producer=True, offset16=False):
+        """offset16: the descriptors' offsets count 16-byte units (IPXG_BATCH_OFFSET16: arenas
+        up to 64 GiB, every frame 16-byte aligned).
+        asynchronous: may return before the batch is applied; keep the arrays / tensors alive
         and unchanged until the next call on the engine (host batches: pinned memory lets the
         copy overlap the previous batch's kernels).  wait_producer (device
         torch tensors): the engine's stream first waits for the work queued so far on torch's
@@ -399,7 +405,7 @@ class Engine:
             if getattr(self, "_ext_stream", None) is None:
                 self._ext_stream = torch.cuda.ExternalStream(self.stream(), device=dev)
             self._ext_stream.wait_stream(torch.cuda.current_stream(dev))
-        b = self._batch(arena, desc, device, asynchronous)
+        b = self._batch(arena, desc, device, asynchronous, offset16)
         self._keep_async = b._keep if asynchronous else None
         self._check(lib().ipxg_submit(self._h, ctypes.byref(b)), "ipxg_submit")
 
@@ -551,8 +557,8 @@ class Engine:
         self._check(lib().ipxg_device_ipfix_counts(self._h, ctypes.byref(p)), "ipxg_device_ipfix_counts")
         return p.value
 
-    def parse(self, arena, desc):
-        b = self._batch(arena, desc)
+    def parse(self, arena, desc, offset16=False):
+        b = self._batch(arena, desc, offset16=offset16)
         out = np.zeros(b.n, dtype=PARSED_DTYPE)
         self._check(lib().ipxg_parse_batch(self._h, ctypes.byref(b), out.ctypes.data),
                     "ipxg_parse_batch")

@@ -54,6 +54,23 @@ def test_demux_split_keeps_frames_and_order():
             assert bytes(a[d["offset"][j]:d["offset"][j] + c]) == bytes(arena[o:o + c])
 
 
+def test_demux_with_16_byte_unit_offsets():
+    """IPXG_BATCH_OFFSET16 (ABI 8): the same frames at the same places, their offsets counted in
+    16-byte units -- the same shards, and each shard's batch again in units."""
+    arena, desc = synth.flow_stream(seed=45, n_flows=60, n_pkts=1200, frag=True, v6_share=0.5).batch()
+    one, _ = engine.demux(arena, desc, 1)  # (frames at 16-byte aligned offsets)
+    aligned, adesc = one[0]
+    udesc = adesc.copy()
+    udesc["offset"] //= 16
+    bb, sb = engine.demux(aligned, adesc, 4)
+    bu, su = engine.demux(aligned, udesc, 4, offset16=True)
+    assert np.array_equal(sb, su)
+    for (a1, d1), (a2, d2) in zip(bb, bu):
+        assert np.array_equal(a1, a2)
+        assert np.array_equal(d1["offset"], d2["offset"] * 16)
+        assert np.array_equal(d1["caplen"], d2["caplen"])
+
+
 def test_demux_is_symmetric_and_balanced():
     """Every packet of a biflow (both directions: one canonical hash) lands on one shard; many
     flows spread evenly over the shards."""

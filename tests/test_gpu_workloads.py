@@ -41,11 +41,11 @@ def test_generator_matches_host_restatement(name):
         assert np.array_equal(a[o:o + c], ha[o:o + c]), i
 
 
-def _run_batches(params, batches, finish=True):
+def _run_batches(params, batches, finish=True, offset16=False, asynchronous=False):
     from ipfixprobe_amd import Engine
     with Engine(params) as e:
         for fr, de in batches:
-            e.submit(fr, de, device=True)
+            e.submit(fr, de, device=True, offset16=offset16, asynchronous=asynchronous)
         if finish:
             e.finish()
         recs = e.poll()
@@ -122,3 +122,68 @@ def test_workload_full_size_conservation(name, n, nb):
     assert len(recs) == int(drawn.sum())
     assert st["end_forced"] == len(recs)
     assert len(np.unique(recs["flow_hash"])) == len(recs)
+
+
+@pytest.mark.parametrize("params", ["s=20", "s=20;walk=narrow", "strict=true;s=17"])
+@pytest.mark.parametrize("name", sorted(MIXES))
+def test_offset16_batches_match_byte_offsets(name, params):
+    """IPXG_BATCH_OFFSET16 (ABI 8): the generator's batches with their offsets in 16-byte units
+    (the same arena) -- records and counters equal the byte-offset run's (binned ingest with
+    either walk, and the reference's own table: strict), and the oracle's."""
+    import torch
+    gen = _gen(name, 200_000)
+    n, nb = 300_000, 3
+    byte = [gen.batch(k * n, n) for k in range(nb)]
+    unit = [gen.batch(k * n, n, offset16=True) for k in range(nb)]
+    torch.cuda.synchronize()
+    for (a1, d1), (a2, d2) in zip(byte, unit):
+        assert torch.equal(a1, a2)
+        o1 = d1.view(torch.int32).view(-1, 4)
+        o2 = d2.view(torch.int32).view(-1, 4)
+        assert torch.equal(o1[:, 0], o2[:, 0] * 16) and torch.equal(o1[:, 1:], o2[:, 1:])
+    got_b, st_b = _run_batches(params, byte)
+    got_u, st_u = _run_batches(params, unit, offset16=True, asynchronous=True)
+    d = flowcmp.diff(got_u, got_b)
+    assert not d, d
+    for k in ("seen_packets", "parsed_packets", "ipv4_packets", "ipv6_packets", "vlan_packets", "mpls_packets"):
+        assert st_u[k] == st_b[k], k
+    if "strict" not in params:
+        c = oracle_py.OracleCache(cache_exp=22)
+        for fr, de in byte:
+            c.run(fr.cpu().numpy(), de.cpu().numpy().view(pcaputil.DESC_DTYPE), 1)
+        c.finish()
+        want = c.take()
+        c.close()
+        d = flowcmp.diff(got_u, want)
+        assert not d, d
+
+
+@pytest.mark.parametrize("layout", ["lanes", "blocks"])
+def test_arena_past_4gib(layout):
+    """Frames past 4 GiB (IPXG_BATCH_OFFSET16): the configs[4] mix's frames copied 4.5 GiB up a
+    larger arena for every other packet ('lanes': a wave's frames lie 4.5 GiB apart, so half of
+    them fall outside the wave's 4 GiB load window and go the general path) or every other
+    4096-packet block ('blocks': whole waves load past 4 GiB through their window) -- records
+    and counters against the oracle over the same packets."""
+    import torch
+    gen = _gen("quic", 100_000)
+    n = 200_000
+    fr, de = gen.batch(0, n)
+    high = 9 << 29  # 4.5 GiB
+    big = torch.zeros(high + fr.numel(), dtype=torch.uint8, device=fr.device)
+    big[:fr.numel()] = fr
+    big[high:] = fr
+    d = de.view(torch.int32).view(n, 4).clone()
+    idx = torch.arange(n, device=fr.device)
+    up = (idx % 2 == 1) if layout == "lanes" else ((idx // 4096) % 2 == 1)
+    off = d[:, 0].to(torch.int64)
+    d[:, 0] = (torch.where(up, off + high, off) // 16).to(torch.int32)
+    desc = d.view(torch.uint8).reshape(-1)
+    torch.cuda.synchronize()
+    got, st = _run_batches("s=19", [(big, desc)], offset16=True)
+    want, wst = oracle_py.run_capture(fr.cpu().numpy(), de.cpu().numpy().view(pcaputil.DESC_DTYPE), 1, cache_exp=20)
+    del big
+    dd = flowcmp.diff(got, want)
+    assert not dd, dd
+    for k in ("seen_packets", "parsed_packets", "ipv4_packets", "ipv6_packets", "vlan_packets", "mpls_packets"):
+        assert st[k] == wst[k], k

@@ -269,6 +269,40 @@ def test_early_front_defers_spills(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("asynchronous", [False, True])
+def test_offset16_fuzz_corpus_with_plugin(asynchronous):
+    """IPXG_BATCH_OFFSET16 (ABI 8): the fuzz corpus (every register-walk shape, fragments,
+    truncations) at 16-byte aligned offsets, its descriptors counting 16-byte units, in 4096-packet
+    device batches with a prefix-rule plugin registered -- records and ext bits equal the oracle's
+    over the same packets."""
+    import torch
+    from ipfixprobe_amd import Engine
+    from ipfixprobe_amd import engine as ipe
+    arena0, desc0 = synth.to_batch(synth.fuzz_corpus(20000, seed=72))
+    one, _ = ipe.demux(arena0, desc0, 1)
+    arena, desc = one[0]
+    orc = PrefixMarker()
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20, plugins=[orc.struct])
+    udesc = desc.copy()
+    udesc["offset"] //= 16
+    a = torch.from_numpy(np.ascontiguousarray(arena)).cuda()
+    step = 4096
+    ds = [torch.from_numpy(np.ascontiguousarray(udesc[s:s + step]).view(np.uint8).reshape(-1)).cuda()
+          for s in range(0, len(udesc), step)]
+    torch.cuda.synchronize()
+    eng = PrefixMarker()
+    with Engine("s=18") as e:
+        e.add_plugin(eng.struct)
+        for d in ds:
+            e.submit(a, d, device=True, asynchronous=asynchronous, offset16=True)
+        e.finish()
+        got = e.poll()
+    d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
+    assert not d, d
+    assert (want["ext"] != 0).sum() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("prof", [0, 2])
 def test_early_front_on_fuzz_corpus(prof):
     """The fuzz corpus (every register-walk shape, fragments, truncations) in 4096-packet device

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_contig(const uint4* __restrict__ a, siz
 }
 
 // U packets per lane per iteration (all U descriptors, then all 3U head loads in flight)
-template <bool DESC, int U = 4>
+template <bool DESC, int U = 4, int C = 3>
 __global__ __launch_bounds__(256) void k_frame(const uint8_t* __restrict__ arena, const Desc* __restrict__ desc,
                                                uint32_t n, uint32_t fstride, uint32_t* out) {
     uint32_t acc = 0;
@@ -45,15 +45,15 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t* __restrict__ arena
             if (DESC) { const Desc d = desc[i]; off[k] = d.off; acc ^= d.len ^ d.s; }
             else off[k] = i * fstride;
         }
-        uint4 h[U][3];
+        uint4 h[U][C];
 #pragma unroll
         for (int k = 0; k < U; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) h[k][c] = *reinterpret_cast<const uint4*>(arena + off[k] + 16 * c);
+            for (int c = 0; c < C; ++c) h[k][c] = *reinterpret_cast<const uint4*>(arena + off[k] + 16 * c);
 #pragma unroll
         for (int k = 0; k < U; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) acc ^= h[k][c].x ^ h[k][c].y ^ h[k][c].z ^ h[k][c].w;
+            for (int c = 0; c < C; ++c) acc ^= h[k][c].x ^ h[k][c].y ^ h[k][c].z ^ h[k][c].w;
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -219,6 +219,10 @@ int main(int argc, char** argv) {
     run("frame_lds", (double)n * (64 + 16), [&] { hipLaunchKernelGGL(k_frame_lds, dim3(blocks), dim3(256), 0, 0, arena, desc, n, out); });
     run("frame_u1", (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_frame<true, 1>), dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
     run("frame_u2", (double)n * (64 + 16), [&] { hipLaunchKernelGGL((k_frame<true, 2>), dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    // the wide walk's 80-byte heads (5 x 16 B) at the frame stride, 4 / 8 packets per lane in flight
+    run("frame80_u4", (double)n * (80 + 16), [&] { hipLaunchKernelGGL((k_frame<true, 4, 5>), dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    run("frame80_u8", (double)n * (80 + 16), [&] { hipLaunchKernelGGL((k_frame<true, 8, 5>), dim3(blocks), dim3(256), 0, 0, arena, desc, n, fs, out); });
+    if (fs != 64) return 0;  // (the k_tiles runs below assume 64-byte frames)
     const uint32_t lds_kb = argc > 4 ? atoi(argv[4]) : 0;
     if (lds_kb) CHK(hipFuncSetAttribute((const void*)k_tiles<4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));
     if (lds_kb) CHK(hipFuncSetAttribute((const void*)k_tiles<4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_kb * 1024));

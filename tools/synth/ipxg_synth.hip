@@ -62,6 +62,7 @@ struct SynthParams {
     uint32_t fwd_q16;             // P(forward direction) * 65536
     uint32_t syn_q16, psh_q16;    // TCP: P(SYN), P(PSH|ACK) * 65536 (else ACK)
     const uint8_t* blob;          // the layouts' blob (blob_len bytes), or null
+    uint32_t oshift;              // 4: descriptor offsets in 16-byte units (IPXG_BATCH_OFFSET16), else 0
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
@@ -123,7 +124,7 @@ __device__ __forceinline__ void put16(uint8_t* h, uint32_t off, uint32_t v) {
 __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4* plan, const uint64_t* off,
                                                      uint8_t* arena, uint4* desc) {
     __shared__ uint4 hdr[64][SYNTH_TMPL / 16];
-    __shared__ uint32_t meta[64][5];  // offset, len, hdr_len, blob start (l7_off), blob bytes (0: none)
+    __shared__ uint32_t meta[64][5];  // offset / 16, len, hdr_len, blob start (l7_off), blob bytes (0: none)
     const uint32_t tid = threadIdx.x;
     const uint32_t base = blockIdx.x * 64u;
     if (tid < 64 && base + tid < P.n) {
@@ -161,14 +162,14 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4*
         if (L.size_mode == 1 && !lng) h[L.l7_off] = 0x43;  // QUIC short header (1-RTT)
         if (!F.opening)
             for (uint32_t k = 0; k < L.alt_len; ++k) h[L.l7_off + k] = L.alt[k];
-        meta[tid][0] = (uint32_t)off[i];
+        meta[tid][0] = (uint32_t)(off[i] >> 4);  // (frames start on 64 bytes)
         meta[tid][1] = len;
         meta[tid][2] = L.hdr_len;
         meta[tid][3] = L.l7_off;
         meta[tid][4] = lng && P.blob ? L.blob_len : 0u;  // (an opening QUIC flow's Initial)
         const uint64_t t = P.t0_ns + (P.first_idx + i) * (uint64_t)P.dt_ns;
         const uint64_t us = t / 1000u;
-        desc[i] = make_uint4((uint32_t)off[i], len | (len << 16), (uint32_t)(us / 1000000u), (uint32_t)(us % 1000000u));
+        desc[i] = make_uint4((uint32_t)(off[i] >> P.oshift), len | (len << 16), (uint32_t)(us / 1000000u), (uint32_t)(us % 1000000u));
     }
     __syncthreads();
     const uint32_t np = min(64u, P.n - base);
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams P, const uint4*
                     if (at >= b0 && at < b0 + bl) vb[k] = P.blob[at - b0];
                 }
             }
-            *reinterpret_cast<uint4*>(arena + o + c * 16u) = v;
+            *reinterpret_cast<uint4*>(arena + (uint64_t)o * 16u + c * 16u) = v;
         }
     }
 }

@@ -280,7 +280,7 @@ class _Params(ctypes.Structure):
                 ("rank_flow", ctypes.c_void_p), ("seed", ctypes.c_uint64), ("first_idx", ctypes.c_uint64),
                 ("t0_ns", ctypes.c_uint64), ("nflows", ctypes.c_uint32), ("n", ctypes.c_uint32),
                 ("dt_ns", ctypes.c_uint32), ("fwd_q16", ctypes.c_uint32), ("syn_q16", ctypes.c_uint32),
-                ("psh_q16", ctypes.c_uint32), ("blob", ctypes.c_void_p)]
+                ("psh_q16", ctypes.c_uint32), ("blob", ctypes.c_void_p), ("oshift", ctypes.c_uint32)]
 
 
 _LIB = None
@@ -328,18 +328,20 @@ class Generator:
         p.blob = self.d_blob.data_ptr() if self.d_blob is not None else None
         return p
 
-    def batch(self, first, n):
-        """(arena uint8, desc uint8 [n * 16]) device tensors of packets [first, first + n)."""
+    def batch(self, first, n, offset16=False):
+        """(arena uint8, desc uint8 [n * 16]) device tensors of packets [first, first + n).
+        offset16: descriptor offsets in 16-byte units (IPXG_BATCH_OFFSET16, arenas past 4 GiB)."""
         import torch
         stream = torch.cuda.current_stream(self.device).cuda_stream
         p = self._params(first, n)
+        p.oshift = 4 if offset16 else 0
         plan = torch.empty(n * 16, dtype=torch.uint8, device=self.device)
         alen = torch.empty(n, dtype=torch.int64, device=self.device)
         if lib().synth_plan(ctypes.byref(p), plan.data_ptr(), alen.data_ptr(), stream):
             raise RuntimeError("synth_plan failed")
         off, total = place(alen, torch)
-        if total + 64 >= 1 << 32:
-            raise ValueError("batch arena %d B exceeds the 4 GiB descriptor offset range" % total)
+        if total + 64 >= (1 << 36 if offset16 else 1 << 32):
+            raise ValueError("batch arena %d B exceeds the descriptor offset range" % total)
         arena = torch.zeros(total + 64, dtype=torch.uint8, device=self.device)
         desc = torch.empty(n * 16, dtype=torch.uint8, device=self.device)
         if lib().synth_write(ctypes.byref(p), plan.data_ptr(), off.data_ptr(), arena.data_ptr(), desc.data_ptr(),
