@@ -442,7 +442,7 @@ def make_workload(args, rank, world, device, local):
     if sworld > 1:  # this rank's flows only (flow-hash-range shards, the NIC-RSS analogue)
         mix.restrict(rank_flows(mix, srank, sworld, local))
     gen = synthgen.Generator(mix, device, seed=args.seed + 7919 * srank)
-    batches = [gen.batch(k * args.packets, args.packets) for k in range(args.batches)]
+    batches = [gen.batch(k * args.packets, args.packets, offset16=args.offset16) for k in range(args.batches)]
     torch.cuda.synchronize()
     cfg = {"imix": "configs[2]", "quic": "configs[4]", "imix10m": "configs[3]"}[args.workload]
     if args.shard:
@@ -453,7 +453,11 @@ def make_workload(args, rank, world, device, local):
             "flows%s; step = parse + XXH64 + biflow-cache update of every batch + finish"
             % (cfg, mixname, args.packets * args.batches, args.batches, args.packets, len(mix.flows),
                " (Zipf %.2f popularity)" % zipf if zipf else " (uniform popularity)"))
-    return Workload(args.workload, batches, len(mix.flows), args.batches, True, desc)
+    if args.offset16:
+        desc += "; descriptor offsets in 16-byte units (IPXG_BATCH_OFFSET16)"
+    wl = Workload(args.workload, batches, len(mix.flows), args.batches, True, desc)
+    wl.gen = gen
+    return wl
 
 
 def flow_owners(mix, world, local=0, hasher=None):
@@ -593,6 +597,9 @@ def main():
                          "per-GPU slice without the other N-1 GPUs)")
     ap.add_argument("--mode", default="cold", choices=["cold", "stream"], help="udp64 only")
     ap.add_argument("--packets", type=int, default=None, help="packets per batch")
+    ap.add_argument("--offset16", action="store_true",
+                    help="synthetic mixes: descriptor offsets in 16-byte units (IPXG_BATCH_OFFSET16: batch arenas "
+                         "past 4 GiB, e.g. configs[4] as 2 x 10M packets)")
     ap.add_argument("--batches", type=int, default=None, help="batches per step (imix / quic)")
     ap.add_argument("--flows", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None)
@@ -686,7 +693,7 @@ def main():
             for k in range(wl.per_step):
                 fr, de = wl.batches[k]
                 # back to back; finish right behind (the batches were synchronised after generation)
-                eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+                eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False, offset16=args.offset16)
                 if k == 0 and gather is not None:
                     gather.step()
             eng.finish()
@@ -704,7 +711,7 @@ def main():
         step()
     verify = None
     if args.verify and rank == 0 and wl.finish:
-        verify = verify_step(eng, wl, args.strict)
+        verify = verify_step(eng, wl, args.strict, args.offset16)
     # timed region: HIP events around the ingest kernels only (k_bin, k_bin_slow), on one batch of
     # every PROF_EVERY: each event record is a packet of its own on the engine's stream (~4-5 us of
     # GPU time, tools/gapbench), so events on every batch added ~13 us to every udp64 step; the
@@ -810,11 +817,14 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         fr, de = wl.batches[0]
+        label = "the first batch of the workload, "
+        if args.offset16:  # (the CPU port takes byte offsets: the batch's first packets regenerated so)
+            fr, de = wl.gen.batch(0, min(wl.packets[0], 4_000_000))
+            label = "the first %d packets of the workload (byte offsets), " % (de.numel() // 16)
         arena_np = fr.cpu().numpy()
         desc_np = de.cpu().numpy().view(DESC_NP)
         canon = canon_of(eng, arena_np, desc_np)
-        cpu = cpu_baseline(arena_np, desc_np, canon, wl.flows,
-                           label="the first batch of the workload, ")
+        cpu = cpu_baseline(arena_np, desc_np, canon, wl.flows, label=label)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpkts/s", "n_gpus": world,
@@ -877,17 +887,21 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def verify_step(eng, wl, strict=None):
+def verify_step(eng, wl, strict=None, offset16=False):
     """One step of the workload against the oracle (the first batch only for multi-batch steps,
     in its own engine state): bit-exact flow records or the first differences."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import flowcmp
     import oracle_py
     fr, de = wl.batches[0]
-    eng.submit(fr, de, device=True)
+    if offset16 and fr.numel() >= 1 << 32:
+        return "not run: the oracle takes byte offsets (arena of %d bytes)" % fr.numel()
+    eng.submit(fr, de, device=True, offset16=offset16)
     eng.finish()
     got = eng.poll()
-    d = de.cpu().numpy().view(DESC_NP)
+    d = de.cpu().numpy().view(DESC_NP).copy()
+    if offset16:
+        d["offset"] *= 16
     s = strict if strict is not None else min(30, int(math.ceil(math.log2(2 * wl.flows))) + 2)
     want, _ = oracle_py.run_capture(fr.cpu().numpy(), d, 1, cache_exp=s)
     diff = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + (["end_reason"] if strict is not None else []))
