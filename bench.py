@@ -597,9 +597,10 @@ def main():
                          "per-GPU slice without the other N-1 GPUs)")
     ap.add_argument("--mode", default="cold", choices=["cold", "stream"], help="udp64 only")
     ap.add_argument("--packets", type=int, default=None, help="packets per batch")
-    ap.add_argument("--offset16", action="store_true",
+    ap.add_argument("--offsets", default="auto", choices=["auto", "units", "bytes"],
                     help="synthetic mixes: descriptor offsets in 16-byte units (IPXG_BATCH_OFFSET16: batch arenas "
-                         "past 4 GiB, e.g. configs[4] as 2 x 10M packets)")
+                         "past 4 GiB, so a step's packets in fewer, larger batches) or in bytes (arenas <= 4 GiB); "
+                         "auto = units for imix / quic / imix10m")
     ap.add_argument("--batches", type=int, default=None, help="batches per step (imix / quic)")
     ap.add_argument("--flows", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None)
@@ -643,10 +644,21 @@ def main():
         if not 0 <= a < b:
             ap.error("--shard R/N needs 0 <= R < N")
         args.shard = (a, b)
-    # imix10m: configs[3] = 1G IMIX packets over 10M flows on 8 GPUs -> per GPU 125M packets (13 batches of
-    # 9,615,385: a batch's arena stays within the descriptors' 32-bit offsets) over 1.25M flows
-    dflt = {"udp64": (10_000_000, 1, 100_000, 3000), "imix": (10_000_000, 10, 1_000_000, 5),
-            "quic": (5_000_000, 4, 1_000_000, 10), "imix10m": (9_615_385, 13, 1_250_000, 3)}[args.workload]
+    # imix10m: configs[3] = 1G IMIX packets over 10M flows on 8 GPUs -> per GPU 125M packets over 1.25M flows.
+    # The mixes' steps in batches as large as the arena allows: with byte offsets a batch's arena stays within
+    # 4 GiB (quic 4 x 5M, imix 10 x 10M, imix10m 13 x 9,615,385); with 16-byte unit offsets (ABI 8) up to the
+    # engine's 16M-packet batch (quic 2 x 10M, imix 7 x 14,285,715, imix10m 9 x 13,888,889): the flow-state
+    # passes (k_reduce, k_fin_list) run once per batch over the flows it touches, so fewer batches cost less
+    # (auto with process plugins on the IMIX mixes: bytes -- ten 10M batches overlap their host walks
+    # with the device better than seven of 14.3M: 3.0 against 2.6 Gpkt/s, gpurun_out/o16b)
+    args.offset16 = args.workload != "udp64" and (args.offsets == "units" or (
+        args.offsets == "auto" and not (args.plugins and args.workload in ("imix", "imix10m"))))
+    if args.offset16:
+        dflt = {"udp64": (10_000_000, 1, 100_000, 3000), "imix": (14_285_715, 7, 1_000_000, 5),
+                "quic": (10_000_000, 2, 1_000_000, 10), "imix10m": (13_888_889, 9, 1_250_000, 3)}[args.workload]
+    else:
+        dflt = {"udp64": (10_000_000, 1, 100_000, 3000), "imix": (10_000_000, 10, 1_000_000, 5),
+                "quic": (5_000_000, 4, 1_000_000, 10), "imix10m": (9_615_385, 13, 1_250_000, 3)}[args.workload]
     args.packets = args.packets or dflt[0]
     args.batches = args.batches or dflt[1]
     args.flows = args.flows or dflt[2]

@@ -221,7 +221,7 @@ struct ipxg_engine {
     DevBuf adefer_a, adefer_b;           // deferred tile aggregates (3 x 16 B each)
     DevBuf cx_list, cx_sorted, cx_rank;  // cx_rank: 4 u32 arrays of nranks, then the key set
     DevBuf bin_rec, bin_count;           // k_bin -> k_reduce partitions
-    uint32_t bin_slots[2][2][2][2] = {};  // k_bin workgroups resident at once (its grid), [agg][wide][plug][line]
+    uint32_t bin_slots[2][2][2][2][2] = {};  // k_bin workgroups resident at once (its grid), [agg][wide][plug][line][g64]
     // the plugins' rules flattened for k_bin's own check (Params::plug); plug_ok: they fit
     bool plug_ok = false;
     uint32_t plug_nport = 0, plug_npref = 0;
@@ -413,7 +413,7 @@ static bool plug_fold(const ipxg_engine* e) {
            !std::getenv("IPXG_CLASSIFY_PASS");  // (A/B knob: the separate k_classify pass)
 }
 
-static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
+static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv) {
     // the flows this batch touches: the previous batch's (scaled up to a larger batch), else the
     // live table's, else one per packet
     uint64_t est = e->last_touched ? e->last_touched : e->live;
@@ -430,10 +430,12 @@ static int setup_bins(ipxg_engine* e, uint32_t n, BinView& bv) {
     const uint64_t tiles = ((uint64_t)n + BIN_TILE_PKTS - 1) / BIN_TILE_PKTS;
     const int ag = e->tile_agg ? 1 : 0, wd = wide_walk(e) ? 1 : 0, pl = plug_fold(e) ? 1 : 0;
     // line mode (whole-line record stores) for the plain walk over at most BIN_LINE_P partitions
-    const int ln = !ag && !pl && P <= BIN_LINE_P && !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST) && !e->no_line ? 1 : 0;
-    uint32_t& slots = e->bin_slots[ag][wd][pl][ln];
+    // (g64: 16-byte unit offsets, the heads read through 64-bit addresses -- k_bin's G64 variants;
+    // line mode has none)
+    const int ln = !ag && !pl && !g64 && P <= BIN_LINE_P && !(e->cfg.flags & IPXG_CFG_ATOMIC_INGEST) && !e->no_line ? 1 : 0;
+    uint32_t& slots = e->bin_slots[ag][wd][pl][ln][g64 ? 1 : 0];
     if (!slots) {
-        slots = bin_resident_blocks(e->cfg.device_id, ag != 0, wd != 0, pl != 0, ln != 0);
+        slots = bin_resident_blocks(e->cfg.device_id, ag != 0, wd != 0, pl != 0, ln != 0, g64);
         if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
             slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
     }
@@ -1079,7 +1081,7 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
     BinView nb = {};
     if (binned) {
         const uint32_t bits_before = e->part_bits_last;
-        if ((rc = setup_bins(e, n, nb))) return rc;
+        if ((rc = setup_bins(e, n, bv.oshift != 0, nb))) return rc;
         if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) {
             e->part_bits_last = bits_before;
             return rc;

@@ -103,7 +103,7 @@ struct BinLds {
 
 // ---- phase A ------------------------------------------------------------------------------
 // k_bin's loads are buffer loads through two wave-uniform resource descriptors (the
-// descriptor array and the frame arena, or the wave's 4 GiB window of it: arena_win): each is
+// descriptor array and the frame arena; 64-bit addresses with 16-byte unit offsets): each is
 // one 16-byte (or 8-byte) load instruction, where a plain load was narrowed by the compiler
 // to the bytes used (4 instructions for a 48-byte head); a lane with nothing to load gives an
 // offset past the buffer's end and gets zeros, with no memory traffic.  The loads are unconditional, so the number in flight is
@@ -149,6 +149,20 @@ __device__ __forceinline__ Head<NC> load_head(__amdgpu_buffer_rsrc_t rs, uint32_
         const uint32_t ok_k = k < 3 || (uint32_t)(16 * k) < caplen;
         h.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(rs, ok_k ? o + 16 * k : BUF_OOB, 0,
                                                           AUX >= 0 ? AUX : NC > 3 ? IPXG_WIDE_LOAD_AUX : IPXG_LOAD_AUX));
+    }
+    return h;
+}
+// The same through the frame's 64-bit address (16-byte unit offsets); a lane with nothing to
+// load reads zeros from g_zero_head (one line for the wave, no arena traffic)
+__device__ uint4 g_zero_head[8];
+template <int NC>
+__device__ __forceinline__ Head<NC> load_head_g(const uint8_t* frame, uint32_t caplen, bool ok) {
+    const uint4* f = reinterpret_cast<const uint4*>(frame);
+    Head<NC> h;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const bool ok_k = ok && (k < 3 || (uint32_t)(16 * k) < caplen);
+        h.c[k] = *(ok_k ? f + k : g_zero_head + k);
     }
     return h;
 }
@@ -741,12 +755,14 @@ constexpr uint32_t KBIN_PMAX = 1u << IPXG_KBIN_PMAX_BITS;  // (the host picks at
 // PLUG (with WIDE only): the process plugins' pre-classification in the same walk (Params::plug;
 // the hits' keys and the undecided packets listed for k_plugin_marks) -- no k_classify pass.
 // LINE (without AGG and PLUG): line mode (tile_emit_lines), 1024-packet tiles.
-template <bool AGG, bool WIDE, bool PLUG = false, bool LINE = false>
+// G64 (the batch's offsets count 16-byte units, BatchView::oshift): heads through 64-bit addresses.
+template <bool AGG, bool WIDE, bool PLUG = false, bool LINE = false, bool G64 = false>
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(AGG || WIDE ? 2 : IPXG_BIN_NARROW_WPE)))
 void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl, uint4* slow_list,
            uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
     static_assert(!PLUG || WIDE, "the plugin check reads the wide walk's window");
     static_assert(!LINE || (!AGG && !PLUG), "line mode: the plain record walk");
+    static_assert(!LINE || !G64, "line mode: byte offsets");
     constexpr int K = LINE ? LINE_K : BIN_K;  // packets per lane per tile
     constexpr uint32_t TILE = (uint32_t)K * IPXG_BLOCK;
     constexpr uint32_t PM = LINE ? LINE_P : KBIN_PMAX;  // partitions (at most)
@@ -803,7 +819,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                                           : ((uint64_t)p.prev_sec << 32) | p.prev_usec;
     ParseCounts c = {};
     uint32_t spilled = 0, walked = 0, tb_or = 0;
-    constexpr bool XP = IPXG_BIN_XPOSE && !WIDE && AGG;
+    constexpr bool XP = IPXG_BIN_XPOSE && !WIDE && AGG && !G64;
     // Without tile aggregation the tile's records are staged in LDS as they are made (the stage
     // array, free during the packet loop: the aggregation's tile hash and XP's transposes use it):
     // the 32 record registers (8 steps x 4 words) are live only in the emit phase, not through the
@@ -888,12 +904,9 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         Dr[k] = load_desc<LAUX>(rs_desc, i);
         if (k >= DA - HA) {
             const int h = k - (DA - HA);
-            const bool wh = want(Dr[h]);
-            const ArenaWin aw = arena_win(b, rs_arena, Dr[h], wh);
-            uint32_t o;
-            const bool in = win_off(b, aw, Dr[h], o);
-            if constexpr (XP) Hr[h] = load_head_x(aw.rs, o, wh && in, Xr[h]);
-            else Hr[h] = load_head<NC, LAUX>(aw.rs, o, Dr[h].caplen, wh && in);
+            if constexpr (XP) Hr[h] = load_head_x(rs_arena, Dr[h].offset, want(Dr[h]), Xr[h]);  // (byte offsets)
+            else if constexpr (G64) Hr[h] = load_head_g<NC>(b.arena + ((uint64_t)Dr[h].offset << 4), Dr[h].caplen, want(Dr[h]));
+            else Hr[h] = load_head<NC, LAUX>(rs_arena, Dr[h].offset, Dr[h].caplen, want(Dr[h]));
         } else {
 #pragma unroll
             for (int q = 0; q < 3; ++q) g_dummy_rec[(k * 3 + q) * 64 + (tid & 63)] = make_uint4(0, 0, 0, 0);
@@ -950,22 +963,10 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
             const uint32_t ia = j + DA < K ? tile + (j + DA) * IPXG_BLOCK + tid : next + (j + DA - K) * IPXG_BLOCK + tid;
             Dr[jj % DA] = load_desc<LAUX>(rs_desc, j + DA < K ? clamp(ia, lim) : clamp(ia, next_lim));
             const ipxg_pkt_desc dh = Dr[(jj + HA) % DA];
-            {
-                const bool wh = want(dh);
-                const ArenaWin aw = arena_win(b, rs_arena, dh, wh);
-                uint32_t o;
-                const bool in = win_off(b, aw, dh, o);
-                if constexpr (XP) Hr[jj % HA] = load_head_x(aw.rs, o, wh && in, Xr[jj % HA]);
-                else Hr[jj % HA] = load_head<NC, LAUX>(aw.rs, o, dh.caplen, wh && in);
-            }
+            if constexpr (XP) Hr[jj % HA] = load_head_x(rs_arena, dh.offset, want(dh), Xr[jj % HA]);
+            else if constexpr (G64) Hr[jj % HA] = load_head_g<NC>(b.arena + ((uint64_t)dh.offset << 4), dh.caplen, want(dh));
+            else Hr[jj % HA] = load_head<NC, LAUX>(rs_arena, dh.offset, dh.caplen, want(dh));
             const bool act = i < lim;
-            // 16-byte units: a frame outside the wave's window was not loaded (the slow path)
-            bool inw = true;
-            if (b.oshift) {  // (uniform; the window the head was loaded through, again)
-                const ArenaWin aw = arena_win(b, rs_arena, dc, want(dc));
-                uint32_t o;
-                inw = win_off(b, aw, dc, o);
-            }
             // order check: the predecessor's timestamp is the lane below's (DPP; lane 0 compares
             // with itself here and with the previous wave's last packet after the tile)
             const uint32_t ps = (uint32_t)__builtin_amdgcn_update_dpp((int)dc.ts_sec, (int)dc.ts_sec, 0x138, 0xF, 0xF, false);
@@ -992,7 +993,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         w[4 * k + 3] = hc.c[k].w;
                     }
                     bool ext = false;
-                    if (fast_ok && fast_shape(b, dc) && inw && parse_medium<PLUG, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
+                    if (fast_ok && fast_shape(b, dc) && parse_medium<PLUG, WD>(w, dc.caplen, p.frag_enable, pk, c, ext)) {
                         have = true;
                         walked += ext ? 1 : 0;
                         if constexpr (PLUG) {
@@ -1011,7 +1012,7 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
                         slow = true;
                     }
                 } else {
-                    if (fast_ok && fast_shape(b, dc) && inw && parse_fast(hc.c[0], hc.c[1], hc.c[2], dc.caplen, p.frag_enable, pk, c))
+                    if (fast_ok && fast_shape(b, dc) && parse_fast(hc.c[0], hc.c[1], hc.c[2], dc.caplen, p.frag_enable, pk, c))
                         have = true;
                     else
                         slow = true;
@@ -1113,25 +1114,24 @@ __device__ __forceinline__ ipxg_pkt_desc slow_desc(const uint4 e) {
 constexpr int SLOW_NCH = IPXG_WIN / 16;
 struct SlowWin {
     uint4 c[SLOW_NCH];
-    bool inw;  // the frame lies in the wave's window (byte offsets: always)
 };
 
 __device__ __forceinline__ bool slow_aligned(const BatchView& b, const uint4 e) { return b.oshift || !(e.y & 15); }
-// (wave-collective: the wave's window, arena_win; a frame outside it is staged by byte loads)
+// (G64, 16-byte units: through the frame's 64-bit address, a chunk past caplen from g_zero_head)
+template <bool G64>
 __device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t rs_all, const BatchView& b, const uint4 e) {
     const uint32_t cap = e.z & 0xFFFFu;
-    ipxg_pkt_desc d;
-    d.offset = e.y;
-    const bool want = slow_aligned(b, e) && cap != 0;
-    const ArenaWin aw = arena_win(b, rs_all, d, want);
-    uint32_t o;
-    const bool in = win_off(b, aw, d, o);
     SlowWin w;
-    w.inw = in;
-    o = want && in ? o : BUF_OOB;
+    if constexpr (G64) {
+        const uint4* f = reinterpret_cast<const uint4*>(b.arena + ((uint64_t)e.y << 4));
+#pragma unroll
+        for (int k = 0; k < SLOW_NCH; ++k) w.c[k] = *((uint32_t)(16 * k) < cap ? f + k : g_zero_head + (k & 7));
+        return w;
+    }
+    const uint32_t o = slow_aligned(b, e) ? e.y : BUF_OOB;
 #pragma unroll
     for (int k = 0; k < SLOW_NCH; ++k)
-        w.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(aw.rs, (uint32_t)(16 * k) < cap ? o + 16 * k : BUF_OOB, 0,
+        w.c[k] = u4(__builtin_amdgcn_raw_buffer_load_b128(rs_all, (uint32_t)(16 * k) < cap ? o + 16 * k : BUF_OOB, 0,
                                                           IPXG_WIDE_LOAD_AUX));
     return w;
 }
@@ -1140,8 +1140,8 @@ __device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t rs_all, const
 // straddling reads see zeros (stage_frame's layout); unaligned frames: stage_frame's byte loads.
 __device__ __forceinline__ void put_window(uint32_t* col, const BatchView& b, const uint4 e, const SlowWin& w) {
     const uint32_t cap = e.z & 0xFFFFu;
-    if (!slow_aligned(b, e) || !w.inw) {
-        stage_frame(col, b.arena + ((uint64_t)e.y << b.oshift), cap);
+    if (!slow_aligned(b, e)) {  // (byte offsets only)
+        stage_frame(col, b.arena + e.y, cap);
         return;
     }
     const uint32_t nch = ((cap < IPXG_WIN ? cap : IPXG_WIN) + 15) >> 4;
@@ -1193,7 +1193,7 @@ __device__ __forceinline__ void slow_packet(const Params& p, const BatchView& b,
 // emitted exactly like k_bin's records.  The list length is read on the device.
 // Up to 256 VGPRs (2 waves/SIMD): the packet pairs' windows take 64; two pairs in flight per
 // SIMD hide more latency than three single packets did.
-template <bool AGG>
+template <bool AGG, bool G64 = false>
 __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl* ctl,
                 const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list, unsigned long long* stats) {
@@ -1283,14 +1283,14 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             return j < BIN_K && k < ns ? list[tile + ord[k - tile]] : make_uint4(0, BUF_OOB, 0, 0);
         };
         uint4 e0 = entry(0), e1 = entry(1);
-        SlowWin w0 = load_win(rs_arena, b, e0);
+        SlowWin w0 = load_win<G64>(rs_arena, b, e0);
 #pragma unroll 1
         for (int j = 0; j < BIN_K; ++j) {
             const uint32_t k0 = tile + (uint32_t)j * IPXG_BLOCK + tid;
             if (k0 >= ns) break;
             PROBE_T(s0);
             const uint4 e2 = entry(j + 2);
-            const SlowWin w1 = load_win(rs_arena, b, e1);
+            const SlowWin w1 = load_win<G64>(rs_arena, b, e1);
 #ifdef IPXG_PROBE
             asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // w0 (the entry and window ahead stay in flight)
             const uint64_t s1 = __builtin_readcyclecounter();
@@ -1352,16 +1352,22 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
 
 typedef void (*BinKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, uint4*, uint32_t*, uint4*,
                           unsigned long long*);
-static BinKernel bin_kernel(bool agg, bool wide, bool plug = false, bool line = false) {
-    if (plug) return agg ? k_bin<true, true, true> : k_bin<false, true, true>;  // (plug: the wide walk)
-    if (line && !agg) return wide ? k_bin<false, true, false, true> : k_bin<false, false, false, true>;
-    return agg ? (wide ? k_bin<true, true> : k_bin<true, false>) : (wide ? k_bin<false, true> : k_bin<false, false>);
+template <bool G64>
+static BinKernel bin_kernel_g(bool agg, bool wide, bool plug) {
+    if (plug) return agg ? k_bin<true, true, true, false, G64> : k_bin<false, true, true, false, G64>;  // (plug: the wide walk)
+    return agg ? (wide ? k_bin<true, true, false, false, G64> : k_bin<true, false, false, false, G64>)
+               : (wide ? k_bin<false, true, false, false, G64> : k_bin<false, false, false, false, G64>);
+}
+static BinKernel bin_kernel(bool agg, bool wide, bool plug, bool line, bool g64) {
+    if (g64) return bin_kernel_g<true>(agg, wide, plug);  // (no line mode: setup_bins)
+    if (line && !agg && !plug) return wide ? k_bin<false, true, false, true> : k_bin<false, false, false, true>;
+    return bin_kernel_g<false>(agg, wide, plug);
 }
 
-uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool line) {
+uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool line, bool g64) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide, plug, line), IPXG_BLOCK, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bin_kernel(agg, wide, plug, line, g64), IPXG_BLOCK, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     return (uint32_t)std::max(1, std::min(cus * per_cu, (int)BIN_MAX_GRID));
@@ -1370,19 +1376,19 @@ uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool li
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                 BatchCtl* ctl, uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                 unsigned long long* stats) {
-    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0, p.plug != 0, bv.line != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
+    hipLaunchKernelGGL(bin_kernel(p.tile_agg != 0, p.wide != 0, p.plug != 0, bv.line != 0, b.oshift != 0), dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p,
                        t, f, bv, ctl, slow_list, deferred_list, agg_list, stats);
 }
 
 void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,
                      BatchCtl* ctl, const uint4* slow_list, uint32_t* deferred_list, uint4* agg_list,
                      unsigned long long* stats) {
-    if (p.tile_agg)
-        hipLaunchKernelGGL(k_bin_slow<true>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
-                           slow_list, deferred_list, agg_list, stats);
-    else
-        hipLaunchKernelGGL(k_bin_slow<false>, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl,
-                           slow_list, deferred_list, agg_list, stats);
+    typedef void (*SlowKernel)(BatchView, Params, TableView, FragView, BinView, BatchCtl*, const uint4*, uint32_t*,
+                               uint4*, unsigned long long*);
+    const SlowKernel k = b.oshift ? (p.tile_agg ? k_bin_slow<true, true> : k_bin_slow<false, true>)
+                                  : (p.tile_agg ? k_bin_slow<true> : k_bin_slow<false>);
+    hipLaunchKernelGGL(k, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list, deferred_list,
+                       agg_list, stats);
 }
 
 // ---- phase B ------------------------------------------------------------------------------
@@ -2061,28 +2067,10 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather(BatchView b, Para
 // Would k_bin's walk for this batch (p.wide, p.tile_agg: the variant it ran) have taken packet d
 // in registers?  pk: the parse when it would.  (A frame it left to k_bin_slow was never in one of
 // its tile aggregates.)
-// 16-byte units: k_bin's wave of packet i (the 64-aligned group) loaded through the window of
-// its first frame the walk wanted (arena_win); a frame outside it went to k_bin_slow.
-__device__ __forceinline__ bool kbin_window_has(const BatchView& b, bool fast_ok, uint32_t i, const ipxg_pkt_desc& d) {
-    if (!b.oshift) return true;
-    const uint32_t g0 = i & ~63u, g1 = min(b.n, g0 + 64u);
-    uint32_t u0 = d.offset;
-    for (uint32_t k = g0; k < g1; ++k) {
-        const ipxg_pkt_desc e = b.desc[k];
-        if (fast_ok && fast_shape(b, e)) {
-            u0 = e.offset;
-            break;
-        }
-    }
-    ArenaWin w;
-    w.ubase = u0 > WIN_UNITS / 2 ? u0 - WIN_UNITS / 2 : 0u;
-    uint32_t o;
-    return win_off(b, w, d, o);
-}
 __device__ __forceinline__ bool kbin_takes(const BatchView& b, const Params& p, __amdgpu_buffer_rsrc_t rs_arena,
-                                           uint32_t i, const ipxg_pkt_desc& d, DevPkt& pk) {
+                                           const ipxg_pkt_desc& d, DevPkt& pk) {
     const bool fast_ok = p.dlt == 0 || p.dlt == IPXG_DLT_EN10MB;
-    if (!(fast_ok && fast_shape(b, d) && kbin_window_has(b, fast_ok, i, d))) return false;
+    if (!(fast_ok && fast_shape(b, d))) return false;
     ParseCounts c = {};
     bool ext = false;
     if (!p.wide) {
@@ -2134,7 +2122,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) void k_complex_gather_ranges(BatchView 
         const uint32_t last = min(rg.w, b.n - 1);
         for (uint32_t i = rg.z + threadIdx.x; i <= last; i += IPXG_BLOCK) {
             DevPkt pk;
-            if (!kbin_takes(b, p, rs_arena, i, load_desc(rs_desc, i), pk)) continue;
+            if (!kbin_takes(b, p, rs_arena, load_desc(rs_desc, i), pk)) continue;
             if (pk.ip_version != 4 && pk.ip_version != 6) continue;
             uint64_t lo, hf;
             uint32_t cdir;

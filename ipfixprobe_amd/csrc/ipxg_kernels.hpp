@@ -263,46 +263,13 @@ __device__ __forceinline__ const uint8_t* frame_ptr(const BatchView& b, const ip
 __device__ __forceinline__ bool frame_aligned(const BatchView& b, const ipxg_pkt_desc& d) {
     return b.oshift != 0 || (d.offset & 15) == 0;
 }
-// The register parsers' buffer loads take 32-bit byte offsets.  With byte offsets they address
-// the whole arena (<= 4 GiB) through one resource; with 16-byte units (arenas up to 64 GiB) a
-// wave addresses a 4 GiB window of it, from 2 GiB below the first frame it loads (a record
-// index x 16 in a structured resource wraps at 4 GiB on gfx950 too -- tools/sbtest): a frame
-// outside its wave's window takes the general path (k_bin_slow, byte loads).
-constexpr uint32_t WIN_UNITS = 1u << 28;  // 4 GiB
-struct ArenaWin {
-    __amdgpu_buffer_rsrc_t rs;
-    uint32_t ubase;  // the window's first 16-byte unit (unit mode)
-};
+// The register parsers' buffer loads take 32-bit byte offsets: they address an arena of up to
+// 4 GiB through one resource.  With 16-byte units (arenas up to 64 GiB) the frames are read
+// through their 64-bit addresses instead (a structured resource, record index x 16, wraps at
+// 4 GiB on gfx950 too: tools/sbtest; a per-wave 4 GiB window of the arena sent the frames of
+// two receive pools far apart -- the configs[2] placement -- to the slow path).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t arena_rsrc(const BatchView& b) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(b.arena), 0, (int)b.arena_lim, 0x00020000);
-}
-// the window of a wave whose lanes load d where `want` (wave-uniform result); rs_all = arena_rsrc(b)
-__device__ __forceinline__ ArenaWin arena_win(const BatchView& b, __amdgpu_buffer_rsrc_t rs_all,
-                                              const ipxg_pkt_desc& d, bool want) {
-    ArenaWin w;
-    w.rs = rs_all;
-    w.ubase = 0;
-    if (b.oshift) {  // (uniform)
-        const uint64_t m = __ballot(want);
-        const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 0u;
-        const uint32_t u0 = __builtin_amdgcn_readlane(d.offset, first);
-        w.ubase = __builtin_amdgcn_readfirstlane(u0 > WIN_UNITS / 2 ? u0 - WIN_UNITS / 2 : 0u);
-        const uint64_t lo = (uint64_t)w.ubase << 4;
-        const uint64_t left = b.arena_len > lo ? b.arena_len - lo : 0;
-        w.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(b.arena + lo), 0,
-                                                 (int)(uint32_t)(left < 0xFFFFFF00ull ? left : 0xFFFFFF00ull), 0x00020000);
-    }
-    return w;
-}
-// d's byte offset in window w, when the frame lies inside it (byte mode: always)
-__device__ __forceinline__ bool win_off(const BatchView& b, const ArenaWin& w, const ipxg_pkt_desc& d, uint32_t& o) {
-    if (!b.oshift) {
-        o = d.offset;
-        return true;
-    }
-    const uint32_t du = d.offset - w.ubase;
-    o = du << 4;
-    return d.offset >= w.ubase && du < WIN_UNITS - 16;  // (the head's chunks stay inside too)
 }
 #endif
 
@@ -423,7 +390,7 @@ static_assert(sizeof(PluginFlow) == 160, "plugin flow image");
 // ---- launchers (ipxg_kernels.hip / ipxg_sort.hip) ---------------------------------------
 // k_bin workgroups resident on the whole device at once (its persistent grid); agg: the
 // tile-aggregating variant (more LDS)
-uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool line);
+uint32_t bin_resident_blocks(int device, bool agg, bool wide, bool plug, bool line, bool g64);
 // deferred_list: packet indices (counter ctl->deferred); agg_list: deferred tile aggregates,
 // 3 record slots each (counter ctl->agg_deferred)
 void launch_bin(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, BinView bv,

@@ -161,10 +161,9 @@ def test_offset16_batches_match_byte_offsets(name, params):
 @pytest.mark.parametrize("layout", ["lanes", "blocks"])
 def test_arena_past_4gib(layout):
     """Frames past 4 GiB (IPXG_BATCH_OFFSET16): the configs[4] mix's frames copied 4.5 GiB up a
-    larger arena for every other packet ('lanes': a wave's frames lie 4.5 GiB apart, so half of
-    them fall outside the wave's 4 GiB load window and go the general path) or every other
-    4096-packet block ('blocks': whole waves load past 4 GiB through their window) -- records
-    and counters against the oracle over the same packets."""
+    larger arena for every other packet ('lanes': a wave's frames lie 4.5 GiB apart) or every
+    other 4096-packet block ('blocks': whole waves read past 4 GiB) -- records and counters
+    against the oracle over the same packets."""
     import torch
     gen = _gen("quic", 100_000)
     n = 200_000
