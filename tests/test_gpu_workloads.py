@@ -97,19 +97,24 @@ def test_imix_batch_parity_against_oracle_single_batch():
     assert not d, d
 
 
-@pytest.mark.parametrize("name,n,nb", [("imix", 10_000_000, 10), ("quic", 5_000_000, 4)])
-def test_workload_full_size_conservation(name, n, nb):
-    """The bench's full step (imix: 100M packets, 1M flows; quic: 20M, 1M): every packet is
-    accounted to exactly one record, the record count equals the distinct flows the generator
-    drew (host restatement of its plan), and no record is split (no timeouts, no FIN/RST)."""
+@pytest.mark.parametrize("name,n,nb,units", [("imix", 10_000_000, 10, False), ("quic", 5_000_000, 4, False),
+                                              ("imix", 14_285_715, 7, True), ("quic", 10_000_000, 2, True)])
+def test_workload_full_size_conservation(name, n, nb, units):
+    """The bench's full step (imix: 100M packets, 1M flows; quic: 20M, 1M), in the batches byte
+    offsets allow and in the larger ones of 16-byte unit offsets (the bench's default, arenas past
+    4 GiB): every packet is accounted to exactly one record, the record count equals the distinct
+    flows the generator drew (host restatement of its plan), and no record is split (no timeouts,
+    no FIN/RST)."""
     import torch
     gen = _gen(name, 1_000_000)
     from ipfixprobe_amd import Engine
     drawn = np.zeros(1_000_000, dtype=bool)
     with Engine("s=21") as e:
         for k in range(nb):
-            fr, de = gen.batch(k * n, n)
-            e.submit(fr, de, device=True)
+            fr, de = gen.batch(k * n, n, offset16=units)
+            if units and name == "quic":
+                assert fr.numel() > 1 << 32  # (the arena of a 10M configs[4] batch: ~8 GB)
+            e.submit(fr, de, device=True, offset16=units)
             del fr, de
             f, _, _, _, _ = synthgen.host_plan(gen, k * n, n)
             drawn[f] = True
