@@ -649,10 +649,9 @@ def main():
     # 4 GiB (quic 4 x 5M, imix 10 x 10M, imix10m 13 x 9,615,385); with 16-byte unit offsets (ABI 8) up to the
     # engine's 16M-packet batch (quic 2 x 10M, imix 7 x 14,285,715, imix10m 9 x 13,888,889): the flow-state
     # passes (k_reduce, k_fin_list) run once per batch over the flows it touches, so fewer batches cost less
-    # (auto with process plugins on the IMIX mixes: bytes -- ten 10M batches overlap their host walks
-    # with the device better than seven of 14.3M: 3.0 against 2.6 Gpkt/s, gpurun_out/o16b)
-    args.offset16 = args.workload != "udp64" and (args.offsets == "units" or (
-        args.offsets == "auto" and not (args.plugins and args.workload in ("imix", "imix10m"))))
+    # (with process plugins too: imix + dns/http/tls 2.43-2.49 -> 3.01-3.12 Gpkt/s, quic + quic 0.43-0.47 ->
+    # 0.53-0.56, each pair on one box -- profiles/r05/plugin_offsets_ab.txt)
+    args.offset16 = args.workload != "udp64" and args.offsets != "bytes"
     if args.offset16:
         dflt = {"udp64": (10_000_000, 1, 100_000, 3000), "imix": (14_285_715, 7, 1_000_000, 5),
                 "quic": (10_000_000, 2, 1_000_000, 10), "imix10m": (13_888_889, 9, 1_250_000, 3)}[args.workload]
