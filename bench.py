@@ -299,12 +299,15 @@ def canon_of(eng, arena_np, desc_np):
     return out
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the newest profiles/*/pmc_summary[_<workload>].json:
-    the L2's fabric read requests by size (TCC_EA0_RDREQ_32B/64B/128B: 32, 64, 128 bytes each --
-    round 3 measured FETCH_SIZE = all requests x 64 B while ~99.9 % of k_bin's are 128 B, i.e.
-    FETCH_SIZE reads half, as MI355X_MICROARCH.md 'HBM' says) + WRITE_SIZE (KiB); summaries
-    without the request sizes: FETCH_SIZE x 2 + WRITE_SIZE."""
+def pmc_traffic(kernel, workload, packets_per_launch, offsets):
+    """HBM bytes per launch of `kernel` from the newest profiles/*/pmc_summary[_<workload>].json taken
+    on a run of this shape: its "_meta" (tools/pmc_summary.py) names the same workload, packets per
+    launch and descriptor offsets; of the kernel's template variants the one dispatched most often
+    (the steady state of that run).  Bytes: the L2's fabric read requests by size
+    (TCC_EA0_RDREQ_32B/64B/128B: 32, 64, 128 bytes each -- round 3 measured FETCH_SIZE = all requests x
+    64 B while ~99.9 % of k_bin's are 128 B, i.e. FETCH_SIZE reads half, as MI355X_MICROARCH.md 'HBM'
+    says) + WRITE_SIZE (KiB); summaries without the request sizes: FETCH_SIZE x 2 + WRITE_SIZE.
+    Returns (path, bytes, variant, its dispatches) or None."""
     best = None
     name = "pmc_summary.json" if workload == "udp64" else "pmc_summary_%s.json" % workload
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name))):
@@ -313,8 +316,15 @@ def pmc_traffic(kernel, workload):
                 js = json.load(f)
         except (OSError, ValueError):
             continue
+        meta = js.get("_meta")
+        if not meta or meta.get("workload") not in (workload, "udp64-" + workload) or \
+                meta.get("packets_per_launch") != packets_per_launch \
+                or meta.get("offsets") != offsets:
+            continue  # (a summary of another batch size or offset form: not this run's kernel)
         found = None  # the template variant dispatched most often (the steady state)
         for kn, v in js.items():
+            if kn == "_meta":
+                continue
             if kn.split("::")[-1].split("<")[0] == kernel and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
                 if found is None or v.get("calls", 0) > found[0]:
                     if "TCC_EA0_RDREQ_128B_sum" in v:
@@ -322,9 +332,9 @@ def pmc_traffic(kernel, workload):
                               32 * v.get("TCC_EA0_RDREQ_32B_sum", 0))
                     else:
                         rd = 2 * v["FETCH_SIZE"] * 1024.0
-                    found = (v.get("calls", 0), rd + v["WRITE_SIZE"] * 1024.0)
+                    found = (v.get("calls", 0), rd + v["WRITE_SIZE"] * 1024.0, kn)
         if found is not None:
-            best = (p, found[1])
+            best = (p, found[1], found[2], found[0])
     return best
 
 
@@ -807,7 +817,9 @@ def main():
     ingest_gbs = alg_launch / ((bin_ms + slow_ms) / 1e3) / 1e9 if bin_ms > 0 else 0.0
     step_ms = dt / args.steps * 1e3
     step_gbs = alg_step * world / (step_ms / 1e3) / 1e9
-    pmc = pmc_traffic(kname, wl.name if wl.name != "udp64-stream" else "stream")
+    pk_launch = pk_step // (wl.per_step if wl.finish else 1)
+    offsets = "units" if args.offset16 else "bytes"
+    pmc = pmc_traffic(kname, wl.name if wl.name != "udp64-stream" else "stream", pk_launch, offsets)
     # the slow pass (frames the register walks do not take) on its own: its packets per launch
     # from the engine's counter, their algorithmic bytes at the workload's mean per packet
     slow_share = (st["slow_path_packets"] - st0["slow_path_packets"]) / max(st["parsed_packets"] - st0["parsed_packets"], 1)
@@ -843,7 +855,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (generated on device, seed %d)" % args.seed,
             "config": {"workload": wl.description, "name": wl.name,
-                       "packets_per_gpu_per_step": pk_step, "flows_per_gpu": wl.flows,
+                       "packets_per_gpu_per_step": pk_step, "flows_per_gpu": wl.flows, "offsets": offsets,
                        "batches_per_step": wl.per_step, "ingest": args.ingest,
                        "parallelism": "flow-hash-range shards x%d, RCCL gather of export buffers"
                                       % world if world > 1 else "single GPU"},
@@ -851,6 +863,10 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": round(pmc[1]) if pmc else None,
                          "traffic_source": os.path.relpath(pmc[0], ROOT) if pmc else None,
+                         # the summary entry it came from: the kernel's template variant and its
+                         # dispatches in that run (the summary's _meta matched this run's shape)
+                         "traffic_entry": {"kernel": pmc[2], "dispatches": pmc[3], "packets_per_launch": pk_launch,
+                                           "offsets": offsets} if pmc else None,
                          "algorithmic_bytes_per_launch": alg_launch,
                          "algorithmic_bytes_per_packet": round(alg_step / pk_step, 2),
                          "avg_launch_ms": round(kms, 4),

@@ -298,6 +298,10 @@ void ipxg_config_default(ipxg_config* cfg);
 int ipxg_config_parse(const char* params, ipxg_config* cfg);
 
 int ipxg_create(const ipxg_config* cfg, ipxg_engine** out);
+/* Release the engine.  Pending exports are dropped; no hook of a registered plugin is called --
+ * only free_ctx, once for every copy the engine made (copy_ctx) -- also after IPXG_EPLUGIN /
+ * IPXG_ESTATE.  A registered ipxg_plugin (its ctx, hooks and free_ctx) must stay valid until this
+ * call returns; the caller frees its own instance after it (tests/plugin_lifetime.cpp). */
 int ipxg_destroy(ipxg_engine* eng);
 const char* ipxg_last_error(const ipxg_engine* eng);
 /* hipStream_t the engine launches on (for event timing by the caller). */
@@ -429,7 +433,8 @@ typedef struct ipxg_plugin {
     uint32_t follow_bytes;
 } ipxg_plugin;
 
-/* Register a plugin (the order of registration is the order of the hook calls). */
+/* Register a plugin (the order of registration is the order of the hook calls).  The struct is
+ * copied; its ctx stays the caller's and must outlive the engine (ipxg_destroy). */
 int ipxg_add_plugin(ipxg_engine* eng, const ipxg_plugin* plugin);
 /* Threads of the plugin flows' host walk: 0 = default (the host's hardware threads, at most
  * 16), 1 = the calling thread only.  Raising it after the first plugin walk fails with

@@ -151,6 +151,19 @@ struct ipxg_engine {
     // batch as before round 5; IPXG_NO_AHEAD=1 -- ipxg_submit launches no front ahead
     bool sync_finish = false, no_ahead = false;
     bool no_line = false;  // IPXG_NO_LINE=1: k_bin without line mode (A/B knob)
+    // The streamed reduce (round 6, line mode): k_reduce_stream on a stream of its own (rst) beside
+    // k_bin, forked right before k_bin (rs_fork) and joined before k_fin_list (rs_join); k_bin's
+    // progress words in `prog`, tagged with the batch's epoch (1..1023; the words are cleared when
+    // it wraps or their layout changes).  Off by default: measured slower than k_reduce after
+    // k_bin; IPXG_STREAM=1 switches it on (A/B knob).
+    bool no_stream = true;
+    hipStream_t rst = nullptr;
+    hipEvent_t rs_fork = nullptr, rs_join = nullptr;
+    DevBuf prog;
+    uint32_t prog_epoch = 0, prog_g = 0, prog_p = 0;
+    uint32_t stream_grid = 0;  // k_bin's workgroups when streamed: two per CU (<= RS_MAX_COLS)
+    uint32_t prog_mode = PROG_SC1 | PROG_TILE;  // IPXG_PROG_MODE (timing experiments)
+    uint32_t pub_every = 4, rs_sleep = 4;       // IPXG_PUB_EVERY, IPXG_RS_SLEEP (tuning knobs)
     // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
     // the host has not read: completed by the next entry point (consume_pend) -- ipxg_submit of a
     // device batch first launches its own front behind it, gated on that block (Params::gate_mode),
@@ -413,7 +426,10 @@ static bool plug_fold(const ipxg_engine* e) {
            !std::getenv("IPXG_CLASSIFY_PASS");  // (A/B knob: the separate k_classify pass)
 }
 
-static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv) {
+// stream_ok: the batch may take the streamed reduce (line mode, no k_bin_slow launched behind k_bin,
+// no process plugins, not an early front); it does when its flows fit the streamed reducer's LDS
+// tables (RS_TARGET_FLOWS per partition) and the record area a 32-bit buffer range.
+static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv, bool stream_ok = false) {
     // the flows this batch touches: the previous batch's (scaled up to a larger batch), else the
     // live table's, else one per packet
     uint64_t est = e->last_touched ? e->last_touched : e->live;
@@ -439,14 +455,32 @@ static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv) {
         if (const char* g = std::getenv("IPXG_BIN_GRID"))  // tuning knob (experiments only)
             slots = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), BIN_MAX_GRID));
     }
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, slots);
-    const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * BIN_TILE_PKTS, n);
-    const double mean = (double)per_block / P;
-    // aggregating batches follow a skewed one (the most loaded partition ~2.4x the mean with
-    // the configs[2] Zipf mix); the others spill only if the skew changed since the last batch
-    const double factor = std::max(e->tile_agg ? 3.0 : 1.5, 1.25 * e->skew);
-    uint64_t seg = ((uint64_t)(mean * factor + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
-    if (ln) seg = (seg + 8 + 7) & ~7ull;  // whole lines, and the carry's padded last line
+    if (!e->stream_grid) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->cfg.device_id) != hipSuccess || cus < 1)
+            cus = 256;
+        e->stream_grid = std::min<uint32_t>(2u * (uint32_t)cus, RS_MAX_COLS);
+        if (const char* g = std::getenv("IPXG_STREAM_GRID"))  // tuning knob (experiments only)
+            e->stream_grid = std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(g), RS_MAX_COLS));
+    }
+    auto seg_for = [&](uint32_t grid) {
+        const uint64_t per_block = std::min<uint64_t>((tiles + grid - 1) / grid * BIN_TILE_PKTS, n);
+        const double mean = (double)per_block / P;
+        // aggregating batches follow a skewed one (the most loaded partition ~2.4x the mean with
+        // the configs[2] Zipf mix); the others spill only if the skew changed since the last batch
+        const double factor = std::max(e->tile_agg ? 3.0 : 1.5, 1.25 * e->skew);
+        uint64_t seg = ((uint64_t)(mean * factor + 4.0 * std::sqrt(mean) + 16.0) + 3) & ~3ull;
+        if (ln) seg = (seg + 8 + 7) & ~7ull;  // whole lines, and the carry's padded last line
+        return seg;
+    };
+    bool sm = ln && stream_ok && !e->no_stream && est <= (uint64_t)RS_TARGET_FLOWS << bits;
+    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, sm ? e->stream_grid : slots);
+    uint64_t seg = seg_for(grid);
+    if (sm && (uint64_t)P * 2 * grid * seg * 16 >= 0xFFFFFF00ull) {  // (the record area's buffer range)
+        sm = false;
+        grid = (uint32_t)std::min<uint64_t>(tiles, slots);
+        seg = seg_for(grid);
+    }
     const uint32_t cols = 2 * grid;
     int rc;
     if ((rc = ensure(e, e->bin_rec, (size_t)P * cols * seg * sizeof(uint4)))) return rc;
@@ -473,6 +507,22 @@ static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv) {
     bv.cols = cols;
     bv.bin_grid = grid;
     bv.part_bits = bits;
+    bv.prog = nullptr;
+    bv.prog_tag = 0;
+    if (sm) {
+        if ((rc = ensure(e, e->prog, (size_t)RS_MAX_COLS * P * sizeof(uint32_t)))) return rc;
+        if (++e->prog_epoch > (PROG_EPOCH_MASK >> PROG_EPOCH_SHIFT) || grid != e->prog_g || P != e->prog_p) {
+            HIPCHK(e, hipMemsetAsync(e->prog.p, 0, (size_t)RS_MAX_COLS * P * sizeof(uint32_t), e->st));  // (epoch 0: none)
+            e->prog_epoch = 1;
+            e->prog_g = grid;
+            e->prog_p = P;
+        }
+        bv.prog = (uint32_t*)e->prog.p;
+        bv.prog_tag = e->prog_epoch << PROG_EPOCH_SHIFT;
+        bv.prog_mode = e->prog_mode;
+        bv.pub_every = e->pub_every;
+        bv.rs_sleep = e->rs_sleep;
+    }
     e->part_bits_last = bits;
     return IPXG_OK;
 }
@@ -714,6 +764,11 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->sync_finish = std::getenv("IPXG_SYNC_FINISH") != nullptr && std::atoi(std::getenv("IPXG_SYNC_FINISH")) != 0;
     e->no_ahead = std::getenv("IPXG_NO_AHEAD") != nullptr && std::atoi(std::getenv("IPXG_NO_AHEAD")) != 0;
     e->no_line = std::getenv("IPXG_NO_LINE") != nullptr && std::atoi(std::getenv("IPXG_NO_LINE")) != 0;
+    e->no_stream = !(std::getenv("IPXG_STREAM") != nullptr && std::atoi(std::getenv("IPXG_STREAM")) != 0);
+    if (const char* pm = std::getenv("IPXG_PROG_MODE")) e->prog_mode = (uint32_t)std::atoi(pm) & 3u;
+    if (const char* pe = std::getenv("IPXG_PUB_EVERY")) e->pub_every = std::max(1, std::atoi(pe));
+    if (const char* rsl = std::getenv("IPXG_RS_SLEEP")) e->rs_sleep = (uint32_t)std::max(0, std::atoi(rsl));
+    if (const char* rx = std::getenv("IPXG_RS_EXP")) e->rs_sleep |= (uint32_t)std::atoi(rx) << 16;  // (timing only)
     e->walk_full = std::getenv("IPXG_WALK_FULL") != nullptr && std::atoi(std::getenv("IPXG_WALK_FULL")) != 0;
     e->no_slow_skip = std::getenv("IPXG_NO_SLOW_SKIP") != nullptr && std::atoi(std::getenv("IPXG_NO_SLOW_SKIP")) != 0;
     if (const char* sp_env = std::getenv("IPXG_STRICT_PRUNE")) e->strict_prune = std::atoi(sp_env) != 0;
@@ -828,6 +883,12 @@ int ipxg_destroy(ipxg_engine* e) {
     if (e->cls_st) (void)hipStreamDestroy(e->cls_st);
     for (hipEvent_t ev : {e->cls_fork, e->cls_join})
         if (ev) (void)hipEventDestroy(ev);
+    if (e->rst) {
+        (void)hipStreamSynchronize(e->rst);
+        (void)hipStreamDestroy(e->rst);
+    }
+    for (hipEvent_t ev : {e->rs_fork, e->rs_join})
+        if (ev) (void)hipEventDestroy(ev);
     if (e->pstat_d) hipFree(e->pstat_d);
     hipFree(e->sv.rec);
     hipFree(e->sv.hash);
@@ -855,7 +916,7 @@ int ipxg_destroy(ipxg_engine* e) {
                       &e->bin_count, &e->slow_list, &e->slow_cnt, &e->fin_list, &e->ipf_rec, &e->ipf_out,
                       &e->ipf_tot, &e->ipf_off, &e->ipf_msg, &e->ipf_dmsg[0], &e->ipf_dmsg[1], &e->ipf_plan, &e->st_pkt, &e->st_crec, &e->st_keyed,
                       &e->st_qx, &e->st_keys, &e->st_vals, &e->st_keys2, &e->st_vals2, &e->st_succ, &e->st_pred, &e->st_indeg,
-                      &e->st_queue, &e->marks, &e->mark_cnt, &e->plug_d})
+                      &e->st_queue, &e->marks, &e->mark_cnt, &e->plug_d, &e->prog})
         hipFree(b->p);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -1079,9 +1140,11 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
         if ((rc = ensure(e, e->frag_ports, (size_t)n * 4))) return rc;
     }
     BinView nb = {};
+    // (p.slow_skip below: the streamed reduce needs k_bin's records to be the batch's only ones)
+    const bool skip_slow = binned && e->last_slow == 0 && e->plugins.empty() && !e->no_slow_skip;
     if (binned) {
         const uint32_t bits_before = e->part_bits_last;
-        if ((rc = setup_bins(e, n, bv.oshift != 0, nb))) return rc;
+        if ((rc = setup_bins(e, n, bv.oshift != 0, nb, skip_slow && !early))) return rc;
         if ((rc = ensure(e, e->fin_list, (size_t)n * sizeof(HotSlot)))) {
             e->part_bits_last = bits_before;
             return rc;
@@ -1102,9 +1165,10 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
     if (ahead) {
         p.gate_mode = ahead->mode;
         p.prev_ctl = ahead->prev;
-        // behind a batch: the order check continues from its last packet (read on the device); behind
-        // a finish: none, as after every finish
-        p.prev_valid = p.prev_dev = ahead->mode == GATE_BATCH ? 1u : 0u;
+        // behind a batch, or an expire behind a batch (k_expire leaves the block's last_sec / last_usec
+        // alone): the order check continues from its last packet (read on the device), as without a
+        // front ahead; behind a finish: none, as after every finish
+        p.prev_valid = p.prev_dev = ahead->mode == GATE_BATCH || ahead->mode == GATE_EXPIRE ? 1u : 0u;
         p.pub_dst = e->ctl_hd;
         p.pub_ex = e->ex_count_d;
         p.pub_words = (uint32_t)(CTL_EX_OFF / 4);
@@ -1113,7 +1177,7 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
     // no k_bin_slow behind k_bin when the previous batch listed no slow packet (with process plugins
     // it also lists their checks: always launched); a batch that does list one is run again from
     // k_bin_slow by post_batch (BatchCtl::slow_redo)
-    p.slow_skip = binned && e->last_slow == 0 && e->plugins.empty() && !e->no_slow_skip ? 1u : 0u;
+    p.slow_skip = skip_slow ? 1u : 0u;
     nb.slow_skip = p.slow_skip;
     FragView fv = frag_view(e);
     bins = nb;
@@ -1151,6 +1215,22 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
         uint32_t* dl = (uint32_t*)e->defer_a.p;
         uint4* sl = (uint4*)e->slow_list.p;
         uint4* al = (uint4*)e->adefer_a.p;
+        if (bins.prog) {  // the streamed reduce, forked beside k_bin (joined in launch_rest)
+            if (!e->rst) {
+                // (the highest priority: its workgroups are dispatched before k_bin's, one per CU,
+                // and k_bin's fill the room they leave -- two per CU)
+                int lo_pri = 0, hi_pri = 0;
+                HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
+                if (std::getenv("IPXG_RS_LOWPRI")) hi_pri = lo_pri;  // (A/B knob)
+                HIPCHK(e, hipStreamCreateWithPriority(&e->rst, hipStreamNonBlocking, hi_pri));
+                HIPCHK(e, hipEventCreateWithFlags(&e->rs_fork, hipEventDisableTiming));
+                HIPCHK(e, hipEventCreateWithFlags(&e->rs_join, hipEventDisableTiming));
+            }
+            HIPCHK(e, hipEventRecord(e->rs_fork, e->st));
+            HIPCHK(e, hipStreamWaitEvent(e->rst, e->rs_fork, 0));
+            launch_reduce_stream(e->rst, p, table_view(e), bins, e->ctl_d, (HotSlot*)e->fin_list.p, dl, al);
+            HIPCHK(e, hipEventRecord(e->rs_join, e->rst));
+        }
         launch_bin(e->st, bv, p, table_view(e), fv, bins, e->ctl_d, sl, dl, al, e->stats_d);
         ev_rec(e, 1);
         if (!p.slow_skip) {
@@ -1167,6 +1247,11 @@ static int launch_front(ipxg_engine* e, const BatchView& bv, uint32_t n, bool bi
 static int launch_rest(ipxg_engine* e, const BatchView& bv, Params p, const BinView& bins, uint32_t n, bool binned,
                        bool async) {
     int rc;
+    // The front has run: nothing launched from here on tests the pending batch's block, which that
+    // batch's completion re-zeroes -- a later k_bin_slow redo (post_batch) with the gate still in p
+    // found it "closed" and returned without writing its records
+    p.gate_mode = GATE_NONE;
+    p.pub_seq = 0;
     FragView fv = frag_view(e);
     const bool classify = p.classify != 0;
     if (binned) {
@@ -1183,13 +1268,17 @@ static int launch_rest(ipxg_engine* e, const BatchView& bv, Params p, const BinV
         if ((rc = join_fmt(e))) return rc;
         // k_reduce also zeroes the other control block (its batch is complete: the host read it
         // before this launch) for the next front, and the export counters of a pending clear
-        uint32_t* zx = nullptr;
-        if (e->ex_zero_pending) {
-            zx = e->ex_count_d;
-            e->ex_zero_pending = false;
+        if (bins.prog) {  // the streamed reduce ran beside k_bin (launch_front): joined here
+            HIPCHK(e, hipStreamWaitEvent(e->st, e->rs_join, 0));
+        } else {
+            uint32_t* zx = nullptr;
+            if (e->ex_zero_pending) {
+                zx = e->ex_count_d;
+                e->ex_zero_pending = false;
+            }
+            launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al, e->ctl_blk[e->cur ^ 1], zx);
+            e->blk_zero[e->cur ^ 1] = true;
         }
-        launch_reduce(e->st, table_view(e), bins, e->ctl_d, fl, dl, al, e->ctl_blk[e->cur ^ 1], zx);
-        e->blk_zero[e->cur ^ 1] = true;
         if (!async) {
             ev_rec(e, 3);
             launch_fin_list(e->st, bv, p, table_view(e), fv, export_view(e), e->ctl_d, fl, e->stats_d, n, false);
@@ -2214,6 +2303,8 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
             e->tm.reduce_launches++;
         }
     }
+    if (c1.guard & GUARD_STREAM_STALL)
+        return set_err(e, IPXG_EDEVICE, "k_reduce_stream: no k_bin progress word changed for seconds");
     bool slow = false;
     if (c1.slow_redo) {
         // k_bin listed slow packets although the batch was launched without k_bin_slow (the previous
@@ -2222,6 +2313,8 @@ static int post_batch(ipxg_engine* e, BatchView bv, Params p, uint32_t n, bool b
         ev_rec(e, 5);
         slow = true;
         p.slow_skip = 0;
+        p.gate_mode = GATE_NONE;  // (a front launched ahead: its gate was that of the batch before)
+        p.pub_seq = 0;
         BinView bins = e->bins_last;
         bins.slow_skip = 0;
         HIPCHK(e, hipMemsetAsync(&e->ctl_d->slow_redo, 0, sizeof(uint32_t), e->st));

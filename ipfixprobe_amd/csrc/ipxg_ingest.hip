@@ -428,6 +428,28 @@ constexpr uint32_t LINE_ITERS = (LINE_MAXL * 8 + IPXG_BLOCK - 1) / IPXG_BLOCK;  
 #define IPXG_LINE_AUX 0  // cache policy of line mode's frame and descriptor loads (membench: default policy)
 #endif
 
+// ---- streamed reduce: k_bin's progress words --------------------------------------------------
+// The record area as a buffer resource (the host keeps it under 4 GiB in streamed mode): sc1 stores
+// and loads, whose lines pass the writer's L2 (not coherent across XCDs) straight to the Infinity
+// Cache, where k_reduce_stream on another XCD reads them (MI355X_MICROARCH.md, hand-off table: sc1
+// stores, the writers' vmcnt(0), then an sc1 flag; sc1 polls and sc1 loads).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const BinView& bv) {
+    const uint64_t bytes = ((uint64_t)bv.cols << bv.part_bits) * bv.seg_cap * 16u;
+    return __builtin_amdgcn_make_buffer_rsrc(bv.rec, 0, (int)(uint32_t)min<uint64_t>(bytes, BUF_OOB), 0x00020000);
+}
+constexpr int AUX_SC1 = 16;  // buffer-op cache policy: sc1
+__device__ __forceinline__ void store_rec_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint4& r) {
+    u32x4 v = {r.x, r.y, r.z, r.w};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, AUX_SC1);
+}
+// partition q's progress word of column col: the whole lines stored (records fill, at most the
+// segment's), the batch's tag, done
+__device__ __forceinline__ void publish_prog(const BinView& bv, uint32_t col, uint32_t q, uint32_t fill, uint32_t done) {
+    const uint32_t lines = min(fill, bv.seg_cap) >> 3;
+    __hip_atomic_store(&bv.prog[(size_t)q * RS_MAX_COLS + col], bv.prog_tag | done | lines, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct LineLds {
     uint32_t* hist;   // LINE_P: the tile's records per partition (rank counters)
     uint32_t* fill;   // LINE_P: records stored in the workgroup's segment (a multiple of 8)
@@ -459,8 +481,9 @@ __device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, ui
                                                 uint32_t* deferred_list, const uint32_t (&r0)[K],
                                                 const uint32_t (&r1)[K], const uint32_t (&r2)[K],
                                                 const uint32_t (&rk)[K], uint32_t tile, uint32_t& spilled,
-                                                bool defer_spill) {
+                                                bool defer_spill, bool pub) {
     const uint32_t tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs_rec = rec_rsrc(bv);  // (streamed reduce: write-through record stores)
     __syncthreads();  // the counts are complete; every lane has its records back from stage
     uint32_t n = 0, cc = 0, W = 0;
     if (tid < P) {
@@ -493,6 +516,9 @@ __device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, ui
         const uint32_t at = L.fill[part] + j;
         const bool fits = valid && at < bv.seg_cap;  // (seg_cap and fill are multiples of 8: whole lines)
         uint4* dst = fits ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + at] : &g_dummy_rec[tid & 63];
+        if (bv.prog && (bv.prog_mode & PROG_SC1)) {  // (uniform) sc1: k_reduce_stream reads the line from another CU while k_bin runs
+            store_rec_sc1(rs_rec, fits ? (uint32_t)(((size_t)part * bv.cols + col) * bv.seg_cap + at) * 16u : BUF_OOB, r);
+        } else {
 #ifdef IPXG_NT_REC_STORE  // tuning knob: streaming (non-temporal) record stores
         __builtin_nontemporal_store(r.x, &dst->x);
         __builtin_nontemporal_store(r.y, &dst->y);
@@ -501,6 +527,7 @@ __device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, ui
 #else
         *dst = r;
 #endif
+        }
         if (valid && !fits) line_spill(t, ctl, deferred_list, r, spilled, defer_spill);
     }
     __syncthreads();  // the carry and the stage have been read
@@ -516,7 +543,11 @@ __device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, ui
             L.fill[tid] += W;
         }
     }
+    // streamed reduce: every wave's record stores of the tile complete (write-through), then the
+    // whole lines of each partition's segment published (one word per partition and column)
+    if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (hist is reset by the next tile, whose packet loop rewrites the stage)
+    if (pub && tid < P) publish_prog(bv, col, tid, L.fill[tid], 0u);
 }
 
 // The workgroup's carries after its last tile: one line per partition, padded with NO_REC.
@@ -528,8 +559,13 @@ __device__ __forceinline__ void line_flush(const LineLds& L, uint32_t P, const B
         if (c == 0) continue;
         const uint32_t at = L.fill[part] + j;
         const uint4 r = j < c ? L.carry[part * LINE_C + j] : make_uint4(0, 0, NO_REC, 0);
-        if (at < bv.seg_cap) bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + at] = r;
-        else if (j < c) line_spill(t, ctl, deferred_list, r, spilled, defer_spill);
+        const size_t k_at = ((size_t)part * bv.cols + col) * bv.seg_cap + at;
+        if (at < bv.seg_cap) {
+            if (bv.prog && (bv.prog_mode & PROG_SC1)) store_rec_sc1(rec_rsrc(bv), (uint32_t)k_at * 16u, r);
+            else bv.rec[k_at] = r;
+        } else if (j < c) {
+            line_spill(t, ctl, deferred_list, r, spilled, defer_spill);
+        }
     }
     __syncthreads();
     if (threadIdx.x < P && L.ccnt[threadIdx.x]) L.fill[threadIdx.x] += 8;
@@ -809,7 +845,10 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // compiler drain every load in flight)
     uint4* const my_slow = slow_list + (size_t)blockIdx.x * bv.slow_stride;
     uint32_t slow_fill = 0, par = 0;
-    if (b.n == 0) return;
+    if (b.n == 0) {
+        if (LINE && bv.prog && tid < (1u << bv.part_bits)) publish_prog(bv, blockIdx.x, tid, 0u, PROG_DONE);
+        return;
+    }
     const uint32_t last = b.n - 1;
     const uint32_t base_sec = b.base_sec == BASE_FROM_DESC0 ? b.desc[0].ts_sec : b.base_sec;
     b.base_sec = base_sec;
@@ -1046,7 +1085,8 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
         else tile_rank_all<K>(hist, pmask, r1, rk);
         if constexpr (LINE)
             tile_emit_lines<K>(LL, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, r0, r1, r2, rk, tile, spilled,
-                               p.defer_spill != 0);
+                               p.defer_spill != 0,
+                               bv.prog && (bv.prog_mode & PROG_TILE) && (tk + 1) % bv.pub_every == 0);
         else
             tile_emit<false, AGG, KBIN_PMAX>(L, P, pmask, bv, blockIdx.x, t, ctl, deferred_list, agg_list, r0, r1, r2,
                                              rk, ix, tile, spilled, p.defer_spill != 0);
@@ -1092,6 +1132,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     block_ctl_counts(hist + ST_STRIDE, spilled, AGG ? folded : 0u, WIDE ? walked : 0u, tb_or);
     flush_block_stats(hist, stats);  // (its barrier completes the block's counters)
     flush_block_ctl(hist + ST_STRIDE, ctl);
+    if (LINE && bv.prog) {  // streamed reduce: the column is complete -- its plain stores (segment counts,
+                            // control block) released to agent scope first, then the words marked done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (tid < P) publish_prog(bv, blockIdx.x, tid, fill[tid], PROG_DONE);
+    }
 }
 
 // A slow-list entry (k_bin -> k_bin_slow): {packet index, offset, caplen | wirelen << 16,
@@ -1393,8 +1439,9 @@ void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableV
 
 // ---- phase B ------------------------------------------------------------------------------
 // LDS flow table of k_reduce: linear probing on the low bits of the canonical hash
+template <uint32_t NE = RED_ENTRIES>
 __device__ __forceinline__ int lds_slot(FlowAgg* ht, uint64_t lo, bool insert) {
-    uint32_t e = (uint32_t)lo & (RED_ENTRIES - 1);
+    uint32_t e = (uint32_t)lo & (NE - 1);
     for (uint32_t probe = 0; probe < RED_MAX_PROBE; ++probe) {
         unsigned long long k = ht[e].key;
         if (k == 0) {
@@ -1403,7 +1450,7 @@ __device__ __forceinline__ int lds_slot(FlowAgg* ht, uint64_t lo, bool insert) {
             if (k == 0) return (int)e;
         }
         if (k == lo) return (int)e;
-        e = (e + 1) & (RED_ENTRIES - 1);
+        e = (e + 1) & (NE - 1);
     }
     return -1;
 }
@@ -1489,6 +1536,7 @@ __device__ __noinline__ void red_spill(const TableView& t, BatchCtl* ctl, uint32
 // record in five finds another flow in its home entry, so nearly every wave-group has a lane
 // here, and as a call (scratch saves of the caller's registers, a full vmcnt drain) it stalled
 // the group's prefetched record loads.
+template <uint32_t NE = RED_ENTRIES>
 __device__ __forceinline__ int red_probe(FlowAgg* ht, uint64_t lo, uint32_t e, unsigned long long k) {
     for (uint32_t probe = 0; probe < RED_MAX_PROBE; ++probe) {
         if (k == 0) {
@@ -1496,7 +1544,7 @@ __device__ __forceinline__ int red_probe(FlowAgg* ht, uint64_t lo, uint32_t e, u
             if (k == 0) return (int)e;
         }
         if (k == lo) return (int)e;
-        e = (e + 1) & (RED_ENTRIES - 1);
+        e = (e + 1) & (NE - 1);
         k = ht[e].key;
     }
     return -1;
@@ -1513,6 +1561,125 @@ __device__ __forceinline__ void red_record(FlowAgg* ht, const TableView& t, Batc
     const int e = lds_slot(ht, ((uint64_t)r.y << 32) | r.x, true);
     if (e >= 0) lds_fold(ht[e], r.z, r.w, one_tb);
     else red_spill(t, ctl, deferred_list, cnt, r);
+}
+
+// The end of a partition's reduce (k_reduce, k_reduce_stream), after the fold: each LDS aggregate of
+// the NE-entry table (NT threads) merged into its table slot or listed for k_fin_list, the flows
+// whose slot probe failed deferred with their records (rec_at(k): the partition's record k of
+// total), the workgroup's counts added to the control block.
+// fuse: nothing else of this batch can touch these flows (no packet went to the fragment or
+// deferred paths; spilled packets were accumulated by k_bin, before the merge): then the merged
+// slot is complete and goes on the finalise list (k_fin_list).
+template <uint32_t NE, uint32_t NT, typename RecAt>
+__device__ __forceinline__ void red_tail(FlowAgg* ht, const TableView& t, BatchCtl* ctl, HotSlot* fin_list,
+                                         uint32_t* deferred_list, uint4* agg_list, uint32_t* cnt, uint32_t* scan_s,
+                                         uint32_t* fin_base, bool one_tb, bool fuse, uint32_t total, RecAt rec_at) {
+    const uint32_t tid = threadIdx.x;
+    // (IPXG_FIN_PROBE=0: the slots probed here as before, the resolved images listed -- A/B knob)
+    const bool unresolved = fuse && IPXG_FIN_PROBE;
+    uint32_t n_keys = 0, n_touch = 0, n_list = 0;
+    constexpr uint32_t EPT = NE / NT;  // LDS entries per thread
+    HotSlot img[EPT];
+    bool listed[EPT];
+    bool failed = false;
+    // fuse: the flows go on the finalise list as they are, unresolved -- k_fin_list probes the
+    // table for them, one lane per flow at its occupancy, so the random slot reads of a 1M-flow
+    // batch overlap there instead of stalling this LDS-bound workgroup (one per CU).  Otherwise
+    // the thread's entries' home slots are read, and the empty ones claimed, together (one
+    // memory round trip for all of them, not one chain per entry); a home slot held by another
+    // key continues with the general probe.
+    uint64_t hkey[EPT];
+    unsigned long long old[EPT];
+#pragma unroll
+    for (uint32_t q = 0; q < EPT; ++q) {
+        hkey[q] = ht[tid + q * NT].key;
+        if (hkey[q] && !unresolved) img[q] = t.hot((uint32_t)hkey[q] & t.mask);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < EPT; ++q) {
+        old[q] = ~0ull;
+        if (hkey[q] && !unresolved && img[q].key == 0)
+            old[q] = atomicCAS((unsigned long long*)&t.hot((uint32_t)hkey[q] & t.mask).key, 0ull,
+                               (unsigned long long)hkey[q]);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < EPT; ++q) {
+        const uint32_t e = tid + q * NT;
+        FlowAgg a = ht[e];
+        if (one_tb) a.tbits |= 1u;  // bucket 0 (lds_fold skipped the per-record OR)
+        listed[q] = false;
+        if (a.key && unresolved) {  // the aggregate as a slot image, its slot probed by k_fin_list
+            n_touch++;
+            HotSlot u = {};
+            u.key = a.key;
+            agg_fold(u, a);
+            u.pad = FIN_UNRESOLVED;
+            img[q] = u;
+            listed[q] = true;
+            n_list++;
+        } else if (a.key) {
+            n_touch++;
+            bool claimed = false;
+            HotSlot* hp = &t.hot((uint32_t)a.key & t.mask);  // this workgroup is the slot's only writer here
+            if (img[q].key == a.key) {
+                // found at home
+            } else if (img[q].key == 0 && old[q] == 0) {
+                img[q] = HotSlot{};
+                img[q].key = a.key;
+                claimed = true;
+            } else if (img[q].key == 0 && old[q] == a.key) {
+                img[q] = *hp;  // inserted meanwhile by another path
+            } else {
+                hp = probe_insert_full(t, a.key, img[q], claimed);
+            }
+            if (claimed) n_keys++;
+            if (!hp) {
+                ht[e].tflags = a.tflags | RED_FAILED;
+                failed = true;
+            } else {
+                agg_fold(img[q], a);
+                if (fuse) {  // the merged image goes to k_fin_list, which writes the slot back
+                    img[q].pad = t.slot_index(hp);
+                    listed[q] = true;
+                    n_list++;
+                } else {
+                    *hp = img[q];
+                }
+            }
+        }
+    }
+    // one reservation on the finalise list per workgroup (a single counter saturates at ~88
+    // returning atomics per us: MI355X_MICROARCH.md "dequeue")
+    uint32_t listed_n;
+    uint32_t pos = block_exclusive_scan<NT>(n_list, scan_s, &listed_n);
+    if (tid == 0) *fin_base = listed_n ? atomicAdd(&ctl->fin_count, listed_n) : 0;
+    __syncthreads();
+    pos += *fin_base;
+#pragma unroll
+    for (uint32_t q = 0; q < EPT; ++q)
+        if (listed[q]) fin_list[pos++] = img[q];
+    if (__any(failed) && (tid & 63) == 0) atomicOr(&cnt[C_FAIL], 1u);
+    wave_add_lds(&cnt[C_KEYS], n_keys);
+    wave_add_lds(&cnt[C_TOUCH], n_touch);
+    __syncthreads();
+    if (cnt[C_FAIL]) {  // defer the packets (and aggregates) of the flows that found no slot
+        for (uint32_t k = tid; k < total; k += NT) {
+            const uint4 r = rec_at(k);
+            if (r.z == NO_REC || (rec_is_agg(r) && rec_agg_slot(r) != 0)) continue;
+            const int e = lds_slot<NE>(ht, ((uint64_t)r.y << 32) | r.x, false);
+            if (e < 0 || !(ht[e].tflags & RED_FAILED)) continue;
+            if (rec_is_agg(r))  // its payload slots follow it in the same segment
+                defer_agg(&ctl->agg_deferred, agg_list, r, rec_at(k + 1), rec_at(k + 2));
+            else
+                defer_packet(ctl, deferred_list, r.z, false);
+        }
+    }
+    if (tid == 0) {
+        if (cnt[C_KEYS]) atomicAdd(&ctl->new_keys, cnt[C_KEYS]);
+        if (cnt[C_TOUCH]) atomicAdd(&ctl->touched, cnt[C_TOUCH]);
+        if (cnt[C_SPILL]) atomicAdd(&ctl->spilled, cnt[C_SPILL]);
+        if (!fuse || cnt[C_SPILL] || cnt[C_FAIL]) ctl->pending = 1;
+    }
 }
 
 // One workgroup per partition: the partition's records sit in one segment per k_bin /
@@ -1710,93 +1877,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
     // deferred paths (spilled packets were accumulated by k_bin, before this kernel): then the
     // merged slot is complete and goes on the finalise list (k_fin_list).
     const bool fuse = ctl->frag_count == 0 && ctl->a_deferred == 0;
-    // (IPXG_FIN_PROBE=0: the slots probed here as before, the resolved images listed -- A/B knob)
-    const bool unresolved = fuse && IPXG_FIN_PROBE;
-    uint32_t n_keys = 0, n_touch = 0, n_list = 0;
-    constexpr uint32_t EPT = RED_ENTRIES / RED_THREADS;  // LDS entries per thread
-    HotSlot img[EPT];
-    bool listed[EPT];
-    bool failed = false;
-    // fuse: the flows go on the finalise list as they are, unresolved -- k_fin_list probes the
-    // table for them, one lane per flow at its occupancy, so the random slot reads of a 1M-flow
-    // batch overlap there instead of stalling this LDS-bound workgroup (one per CU).  Otherwise
-    // the thread's entries' home slots are read, and the empty ones claimed, together (one
-    // memory round trip for all of them, not one chain per entry); a home slot held by another
-    // key continues with the general probe.
-    uint64_t hkey[EPT];
-    unsigned long long old[EPT];
-#pragma unroll
-    for (uint32_t q = 0; q < EPT; ++q) {
-        hkey[q] = ht[tid + q * RED_THREADS].key;
-        if (hkey[q] && !unresolved) img[q] = t.hot((uint32_t)hkey[q] & t.mask);
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < EPT; ++q) {
-        old[q] = ~0ull;
-        if (hkey[q] && !unresolved && img[q].key == 0)
-            old[q] = atomicCAS((unsigned long long*)&t.hot((uint32_t)hkey[q] & t.mask).key, 0ull,
-                               (unsigned long long)hkey[q]);
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < EPT; ++q) {
-        const uint32_t e = tid + q * RED_THREADS;
-        FlowAgg a = ht[e];
-        if (one_tb) a.tbits |= 1u;  // bucket 0 (lds_fold skipped the per-record OR)
-        listed[q] = false;
-        if (a.key && unresolved) {  // the aggregate as a slot image, its slot probed by k_fin_list
-            n_touch++;
-            HotSlot u = {};
-            u.key = a.key;
-            agg_fold(u, a);
-            u.pad = FIN_UNRESOLVED;
-            img[q] = u;
-            listed[q] = true;
-            n_list++;
-        } else if (a.key) {
-            n_touch++;
-            bool claimed = false;
-            HotSlot* hp = &t.hot((uint32_t)a.key & t.mask);  // this workgroup is the slot's only writer here
-            if (img[q].key == a.key) {
-                // found at home
-            } else if (img[q].key == 0 && old[q] == 0) {
-                img[q] = HotSlot{};
-                img[q].key = a.key;
-                claimed = true;
-            } else if (img[q].key == 0 && old[q] == a.key) {
-                img[q] = *hp;  // inserted meanwhile by another path
-            } else {
-                hp = probe_insert_full(t, a.key, img[q], claimed);
-            }
-            if (claimed) n_keys++;
-            if (!hp) {
-                ht[e].tflags = a.tflags | RED_FAILED;
-                failed = true;
-            } else {
-                agg_fold(img[q], a);
-                if (fuse) {  // the merged image goes to k_fin_list, which writes the slot back
-                    img[q].pad = t.slot_index(hp);
-                    listed[q] = true;
-                    n_list++;
-                } else {
-                    *hp = img[q];
-                }
-            }
-        }
-    }
-    // one reservation on the finalise list per workgroup (a single counter saturates at ~88
-    // returning atomics per us: MI355X_MICROARCH.md "dequeue")
-    uint32_t listed_n;
-    uint32_t pos = block_exclusive_scan<RED_THREADS>(n_list, scan_s, &listed_n);
-    if (tid == 0) fin_base = listed_n ? atomicAdd(&ctl->fin_count, listed_n) : 0;
-    __syncthreads();
-    pos += fin_base;
-#pragma unroll
-    for (uint32_t q = 0; q < EPT; ++q)
-        if (listed[q]) fin_list[pos++] = img[q];
-    if (__any(failed) && (tid & 63) == 0) atomicOr(&cnt[C_FAIL], 1u);
-    wave_add_lds(&cnt[C_KEYS], n_keys);
-    wave_add_lds(&cnt[C_TOUCH], n_touch);
-    __syncthreads();
+    red_tail<RED_ENTRIES, RED_THREADS>(ht, t, ctl, fin_list, deferred_list, agg_list, cnt, scan_s, &fin_base, one_tb,
+                                       fuse, total, [&](uint32_t k) { return seg_record(segs, pre, cols, bv.seg_cap, k); });
     PROBE_T(q3t);
 #ifdef IPXG_PROBE
     if (tid == 0) {
@@ -1805,31 +1887,165 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
         atomicAdd((unsigned long long*)&ctl->probe[6], (unsigned long long)(q3t - q2t));
     }
 #endif
-    if (cnt[C_FAIL]) {  // defer the packets (and aggregates) of the flows that found no slot
-        for (uint32_t k = tid; k < total; k += RED_THREADS) {
-            const uint4 r = seg_record(segs, pre, cols, bv.seg_cap, k);
-            if (r.z == NO_REC || (rec_is_agg(r) && rec_agg_slot(r) != 0)) continue;
-            const int e = lds_slot(ht, ((uint64_t)r.y << 32) | r.x, false);
-            if (e < 0 || !(ht[e].tflags & RED_FAILED)) continue;
-            if (rec_is_agg(r))  // its payload slots follow it in the same segment
-                defer_agg(&ctl->agg_deferred, agg_list, r, seg_record(segs, pre, cols, bv.seg_cap, k + 1),
-                          seg_record(segs, pre, cols, bv.seg_cap, k + 2));
-            else
-                defer_packet(ctl, deferred_list, r.z, false);
-        }
-    }
-    if (tid == 0) {
-        if (cnt[C_KEYS]) atomicAdd(&ctl->new_keys, cnt[C_KEYS]);
-        if (cnt[C_TOUCH]) atomicAdd(&ctl->touched, cnt[C_TOUCH]);
-        if (cnt[C_SPILL]) atomicAdd(&ctl->spilled, cnt[C_SPILL]);
-        if (!fuse || cnt[C_SPILL] || cnt[C_FAIL]) ctl->pending = 1;
-    }
 }
 
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                    uint32_t* deferred_list, uint4* agg_list, BatchCtl* zero_ctl, uint32_t* zero_ex) {
     hipLaunchKernelGGL(k_reduce, dim3(1u << bv.part_bits), dim3(RED_THREADS), 0, st, t, bv, ctl, fin_list,
                        deferred_list, agg_list, zero_ctl, zero_ex);
+}
+
+// ---- the streamed reduce (line mode, round 6) --------------------------------------------------
+// k_reduce's fold, run while k_bin produces the records: one workgroup per partition, launched
+// beside k_bin on a stream of its own (k_bin then runs two workgroups per CU, this one the third
+// resident workgroup of its CU).  Each round it polls the partition's progress word of every k_bin
+// column (sc1 loads), folds the lines published since the previous round (sc1 loads of lines k_bin
+// stored write-through moments before: Infinity-Cache hits, not a second HBM pass of the 160 MB of
+// udp64 records), and sleeps when nothing is new.  Once every column is marked done -- k_bin
+// released its control-block words before marking it -- the partition's flows are merged and listed
+// exactly as k_reduce does (red_tail).  A slow pass flagged by k_bin (slow_redo) leaves everything to
+// the host's rerun of k_bin_slow and k_reduce: nothing is written to the table before that check, and
+// flows that found no LDS entry are only applied after it (a second pass over their records).
+constexpr uint32_t RS_THREADS = 512;  // 2 waves per SIMD: beside two k_bin workgroups' (147 VGPRs each)
+constexpr uint32_t RS_LIST = 1024;    // lines folded per poll, at most
+constexpr uint32_t RS_U = 2;          // wave loads (8 lines each) in flight per lane
+constexpr uint64_t RS_STALL_TICKS = 300000000ull;  // 3 s of the 100 MHz real-time clock without progress
+
+__device__ __forceinline__ uint32_t rs_col(const uint32_t* pre, uint32_t G, uint32_t k) {  // the last c with pre[c] <= k
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = RS_MAX_COLS / 2; step; step >>= 1) {
+        const uint32_t m = lo + step;
+        lo = (m < G && pre[m] <= k) ? m : lo;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(RS_THREADS) void k_reduce_stream(Params p, TableView t, BinView bv, BatchCtl* ctl,
+                                                              HotSlot* fin_list, uint32_t* deferred_list,
+                                                              uint4* agg_list) {
+    if (gated(p)) return;  // (k_bin returned at once too: it publishes nothing)
+    __shared__ FlowAgg ht[RS_ENTRIES];       // 56 KiB
+    __shared__ uint32_t used[RS_MAX_COLS];   // lines of each column's segment folded
+    __shared__ uint32_t list[RS_LIST + 1];   // this poll's lines (column << 20 | line); at the end the prefix
+                                             // of the columns' records (G + 1 words)
+    __shared__ uint32_t cnt[C_N];
+    __shared__ uint32_t scan_s[RS_THREADS / 64 + 1];
+    __shared__ uint32_t fin_base;
+    __shared__ uint32_t flag[2];             // [0] the LDS table was full for some flow, [1] stalled
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t P = 1u << bv.part_bits, part = red_part(blockIdx.x, P);
+    const uint32_t G = bv.bin_grid;  // (<= RS_MAX_COLS = RS_THREADS: the host)
+    {
+        uint4* z = reinterpret_cast<uint4*>(ht);
+        for (uint32_t q = tid; q < sizeof(ht) / 16; q += RS_THREADS) z[q] = make_uint4(0, 0, 0, 0);
+    }
+    if (tid < G) used[tid] = 0;
+    if (tid < C_N) cnt[tid] = 0;
+    if (tid < 2) flag[tid] = 0;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = rec_rsrc(bv);
+    const size_t seg0 = (size_t)part * bv.cols;  // segment of column c: seg0 + c
+    const uint32_t* words = bv.prog + (size_t)part * RS_MAX_COLS;
+    uint64_t t_prog = __builtin_amdgcn_s_memrealtime();
+    constexpr uint32_t NW = RS_THREADS / 64;
+    for (;;) {
+        uint32_t avail = 0;
+        bool done = true;
+        if (tid < G) {
+            const uint32_t v = __hip_atomic_load(&words[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool cur = (v & PROG_EPOCH_MASK) == bv.prog_tag;
+            const uint32_t lines = cur ? (v & PROG_LINES) : 0u;
+            avail = lines > used[tid] ? lines - used[tid] : 0u;
+            done = cur && (v & PROG_DONE) != 0;
+        }
+        uint32_t tot;
+        const uint32_t x = block_exclusive_scan<RS_THREADS>(avail, scan_s, &tot);
+        const uint32_t take = x >= RS_LIST ? 0u : min(avail, RS_LIST - x);
+        for (uint32_t j = 0; j < take; ++j) list[x + j] = (tid << 20) | (used[tid] + j);
+        // (every column done and all of its lines listed: this poll's fold is the last)
+        const bool all_done = __syncthreads_and(done && take == avail);
+        const uint32_t nl = min(tot, RS_LIST);
+        const uint32_t rs_exp = bv.rs_sleep >> 16;  // timing experiments (IPXG_RS_EXP): 1 no fold, 2 no loads
+        for (uint32_t g0 = (tid >> 6) * 8; g0 < (rs_exp == 2 ? 0u : nl); g0 += NW * 8 * RS_U) {  // uniform over the wave
+            uint4 r[RS_U];
+#pragma unroll
+            for (uint32_t u = 0; u < RS_U; ++u) {
+                const uint32_t li = g0 + u * NW * 8 + (lane >> 3);
+                uint32_t off = BUF_OOB;
+                if (li < nl) {
+                    const uint32_t e = list[li];
+                    off = (uint32_t)(((seg0 + (e >> 20)) * bv.seg_cap + (e & 0xFFFFFu) * 8u + (lane & 7)) * 16u);
+                }
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX_SC1);
+                r[u] = make_uint4(v.x, v.y, li < nl ? v.z : NO_REC, v.w);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < RS_U; ++u) {
+                if (r[u].z == NO_REC) continue;
+                if (rs_exp == 1) {
+                    if (r[u].x == 0x12345678u) flag[0] = 1;
+                    continue;
+                }
+                const int e = lds_slot<RS_ENTRIES>(ht, ((uint64_t)r[u].y << 32) | r[u].x, true);
+                if (e >= 0) lds_fold(ht[e], r[u].z, r[u].w, false);
+                else flag[0] = 1;  // (applied after the slow_redo check, below)
+            }
+        }
+        __syncthreads();
+        if (tid < G) used[tid] += take;
+        if (all_done) break;
+        if (nl == 0) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (tid == 0 && now - t_prog > RS_STALL_TICKS) flag[1] = 1;
+            for (uint32_t k = 0; k < (bv.rs_sleep & 0xFFFFu); ++k) __builtin_amdgcn_s_sleep(64);
+        } else {
+            t_prog = __builtin_amdgcn_s_memrealtime();
+        }
+        __syncthreads();
+        if (flag[1]) {  // k_bin stopped publishing (a fault would end the kernel): reported, nothing merged
+            if (tid == 0) atomicOr(&ctl->guard, GUARD_STREAM_STALL);
+            return;
+        }
+    }
+    // every column done: k_bin's control-block words are final
+    if (bv.slow_skip && __hip_atomic_load(&ctl->slow_redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    uint32_t total;
+    {
+        const uint32_t mine = tid < G ? used[tid] * 8u : 0u;
+        const uint32_t x = block_exclusive_scan<RS_THREADS>(mine, scan_s, &total);
+        if (tid < G) list[tid] = x;
+        __syncthreads();
+    }
+    if (total == 0) return;  // (uniform)
+    if (tid == 0) {  // the partition's load (segment sizing of the next batch)
+        atomicMax(&ctl->max_part, total);
+        atomicAdd(&ctl->total_slots, total);
+    }
+    auto rec_at = [&](uint32_t k) {
+        const uint32_t c = rs_col(list, G, k);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, (uint32_t)(((seg0 + c) * bv.seg_cap + (k - list[c])) * 16u), 0, AUX_SC1);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    };
+    if (flag[0]) {  // flows that found no LDS entry: their records straight into the table
+        for (uint32_t k = tid; k < total; k += RS_THREADS) {
+            const uint4 r = rec_at(k);
+            if (r.z == NO_REC || lds_slot<RS_ENTRIES>(ht, ((uint64_t)r.y << 32) | r.x, false) >= 0) continue;
+            red_spill(t, ctl, deferred_list, cnt, r);
+        }
+        __syncthreads();
+    }
+    const bool fuse = __hip_atomic_load(&ctl->frag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                      __hip_atomic_load(&ctl->a_deferred, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    red_tail<RS_ENTRIES, RS_THREADS>(ht, t, ctl, fin_list, deferred_list, agg_list, cnt, scan_s, &fin_base, false, fuse,
+                                     total, rec_at);
+}
+
+void launch_reduce_stream(hipStream_t st, const Params& p, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
+                          uint32_t* deferred_list, uint4* agg_list) {
+    hipLaunchKernelGGL(k_reduce_stream, dim3(1u << bv.part_bits), dim3(RS_THREADS), 0, st, p, t, bv, ctl, fin_list,
+                       deferred_list, agg_list);
 }
 
 // ---- finalisation of the flows k_reduce completed -----------------------------------------

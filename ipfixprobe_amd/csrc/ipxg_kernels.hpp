@@ -71,7 +71,7 @@ struct BatchCtl {
     uint32_t cx_ranges;      // k_complex_gather_rec: k_bin tile aggregates of complex flows listed
     uint32_t guard;          // bounds checks that failed (reported as IPXG_EDEVICE): 1 more complex
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
-                             // past the table
+                             // past the table, 8 (GUARD_STREAM_STALL) k_reduce_stream waited seconds for k_bin
     uint32_t spill_deferred; // of `deferred`: spills k_bin / k_bin_slow deferred (Params::defer_spill)
     uint32_t expired;        // records k_expire exported (the host's live count follows it, no table recount)
     uint32_t slow_redo;      // k_bin listed slow packets in a batch launched without k_bin_slow (Params::slow_skip):
@@ -299,8 +299,28 @@ struct BinView {
     uint32_t* mark_cnt;    //   then k_bin_slow's), mark_cnt[b] of them: {key lo, key hi, index | kind << 30, 0}
     uint32_t slow_skip;    // Params::slow_skip (k_reduce returns when k_bin flagged slow_redo)
     uint32_t line;         // k_bin's line mode (ipxg_ingest.hip: whole-line record stores; seg_cap % 8 == 0)
+    // streamed reduce (line mode, round 6): k_bin workgroup col publishes after every tile, for each
+    // partition q, prog[col << part_bits | q] = prog_tag | the whole lines of its segment stored so far
+    // (| PROG_DONE after its last tile), and k_reduce_stream folds them while k_bin runs; null: no
+    // streaming (k_reduce after k_bin)
+    uint32_t* prog;
+    uint32_t prog_tag;     // the batch's epoch << PROG_EPOCH_SHIFT (never 0): a word of an older batch reads as 0 lines
+    uint32_t prog_mode;    // PROG_SC1: write-through record stores; PROG_TILE: a publish every pub_every tiles (else: at the end)
+    uint32_t pub_every;    // tiles between k_bin's publishes
+    uint32_t rs_sleep;     // k_reduce_stream: s_sleep(64) calls between polls that found nothing new
 };
+constexpr uint32_t PROG_SC1 = 1u, PROG_TILE = 2u;
 constexpr uint32_t BIN_LINE_P = 256;  // line mode's partitions, at most (ipxg_ingest.hip LINE_P)
+// The streamed reduce (k_reduce_stream): one 1024-thread workgroup per partition beside two k_bin
+// workgroups per CU (2 x 48 KiB of LDS + its 64 KiB), a 1024-entry LDS flow table, at most
+// RS_MAX_COLS k_bin columns.  Progress words prog[partition * RS_MAX_COLS + column] (a partition's
+// words contiguous: its reducer polls 16 lines): lines in bits 0-19, the batch's epoch in 20-29, done in 31.
+constexpr uint32_t RS_ENTRIES = 1024;
+constexpr uint32_t RS_MAX_COLS = 512;
+constexpr uint32_t RS_TARGET_FLOWS = 600;  // flows per partition the host sizes the streamed reduce for
+constexpr uint32_t PROG_LINES = 0xFFFFFu, PROG_EPOCH_SHIFT = 20, PROG_EPOCH_MASK = 0x3FFu << 20,
+                   PROG_DONE = 0x80000000u;
+constexpr uint32_t GUARD_STREAM_STALL = 8u;  // BatchCtl::guard: k_reduce_stream saw no progress for seconds
 // The segment counts, column-major: workgroup col's counts of all partitions are contiguous, so
 // each k_bin / k_bin_slow workgroup writes whole lines of them (partition-major, every count was
 // a 4-byte piece of a line the other columns' workgroups, on other XCDs, wrote the rest of).
@@ -406,6 +426,11 @@ void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableV
 void launch_reduce(hipStream_t st, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
                    uint32_t* deferred_list, uint4* agg_list, BatchCtl* zero_ctl = nullptr,
                    uint32_t* zero_ex = nullptr);
+// The streamed form (bv.prog set): launched beside k_bin on a stream of its own (gated as k_bin on
+// Params::gate_mode); it folds each partition's records as k_bin publishes them and ends with
+// k_reduce's merge and finalise list once every k_bin workgroup is done.
+void launch_reduce_stream(hipStream_t st, const Params& p, TableView t, BinView bv, BatchCtl* ctl, HotSlot* fin_list,
+                          uint32_t* deferred_list, uint4* agg_list);
 constexpr uint32_t FIN_UNRESOLVED = 0xFFFFFFFFu;  // a finalise-list entry's pad: the flow's slot not probed yet
 constexpr uint32_t FIN_DEFERRED = 0xFFFFFFFEu;    // ... its probe failed (table full): again after a rehash
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,

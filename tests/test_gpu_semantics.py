@@ -216,12 +216,14 @@ def test_nonmonotonic_conserves_packets():
     assert st["complex_flows"] > 0
 
 
-def test_bench_size_parity():
+def test_bench_size_parity(monkeypatch):
     """The bench workload itself (10M 64 B packets, 100k biflows) against the oracle, through
     the bench's exact engine and step: its configuration (bench.engine_params: s=18, binned
     ingest, walk=auto), the batch submitted asynchronously from the device with the finish right
     behind it (the fused finish in k_fin_list), three steps in a row on the same engine (the
-    partition sizing and the walk choice come from the previous step from the second on)."""
+    partition sizing and the walk choice come from the previous step from the second on).  Then
+    the same with the streamed reduce (IPXG_STREAM=1, round 6: k_reduce_stream folding k_bin's
+    records while k_bin runs -- an A/B knob, off by default), from its second step on."""
     import torch
 
     import bench
@@ -241,6 +243,14 @@ def test_bench_size_parity():
             d = flowcmp.diff(got, want)
             assert not d, (step, d)
         assert e.stats()["complex_flows"] == 0
+    monkeypatch.setenv("IPXG_STREAM", "1")
+    with Engine(bench.engine_params(100_000)) as e:
+        for step in range(3):
+            e.submit(frames, desc, device=True, asynchronous=True, wait_producer=False)
+            e.finish()
+            got = e.poll()
+            d = flowcmp.diff(got, want)
+            assert not d, ("streamed", step, d)
 
 
 # ---- the binned ingest's fast and fallback paths (ipxg_ingest.hip) -------------------------

@@ -291,3 +291,77 @@ def test_plugin_error_fails_the_call_cleanly(threads):
     finally:
         e.close()  # destroyable after the failure
         lib().ref_plugin_destroy(ctypes.byref(pl))
+
+
+# ---- round 6: flowhash, icmp and mpls, which have no functional test of their own ----
+# flowhash (flow_hash.cpp:54-65) exports Flow::flow_hash as FLOW_ID: through it the reference's own code
+# reads every record's flow_hash.  icmp (icmp.cpp:34-48) keeps the type/code of an
+# ICMP flow's first packet, mpls (mpls.cpp:45-55) the top MPLS label word the parser left in
+# Packet::mplsTop (parser.cpp:614).  All three act in post_create only; behind the bridge they take
+# every packet of every flow (rule_for: all_packets).
+EXTRA = ("flowhash", "icmp", "mpls")
+CAPTURES = sorted(os.path.splitext(f)[0] for f in os.listdir(REF) if f.endswith(".pcap"))
+
+
+def _flow_ids_match(recs, texts):
+    """flowhash's text (RecordExtFLOW_HASH::get_text: flow_id="<hex>") is the record's flow_hash."""
+    return all(t == 'flow_id="%x"' % int(r["flow_hash"]) for r, t in zip(recs, texts))
+
+
+def test_extra_reference_plugins_build():
+    for name in EXTRA:
+        RefPlugin(name)
+
+
+@pytest.mark.parametrize("pcap", CAPTURES)
+def test_oracle_with_flowhash_icmp_mpls(pcap):
+    """The oracle with each plugin on every reference capture: flowhash gives every record exactly one
+    extension whose FLOW_ID is the record's flow_hash; icmp's extensions sit on ICMP / ICMPv6 flows only."""
+    dl, arena, desc = _capture(pcap)
+    for name in EXTRA:
+        pl = RefPlugin(name)
+        recs, _ = oracle_py.run_capture(arena, desc, dl, plugins=[pl.struct])
+        texts, counts = take_exts(recs)
+        if name == "flowhash":
+            assert (counts == 1).all()  # (arp.pcap: no flow at all)
+            assert _flow_ids_match(recs, texts)
+        elif name == "icmp":
+            assert all(int(r["ip_proto"]) in (1, 58) for r, t in zip(recs, texts) if t)
+        else:
+            assert all(t.startswith("mpls_label_1=") for t in texts if t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pcap", CAPTURES)
+def test_bridge_with_flowhash_icmp_mpls_matches_oracle(pcap):
+    """The engine's bridge with flowhash, icmp and mpls on every reference capture, in one batch and in
+    batches of 7 packets: records and extension texts equal the oracle's, and flowhash's FLOW_ID equals
+    the engine's own record's flow_hash."""
+    from ipfixprobe_amd import run_capture
+    dl, arena, desc = _capture(pcap)
+    for name in EXTRA:
+        for batch in (None, 7):
+            ep, op = RefPlugin(name), RefPlugin(name)
+            got, _ = run_capture(arena, desc, datalink=dl, params="s=16", batch=batch, plugins=[ep.struct])
+            want, _ = oracle_py.run_capture(arena, desc, dl, cache_exp=16, plugins=[op.struct])
+            (tg, cg), (tw, cw) = take_exts(got), take_exts(want)
+            assert keyed(got, zip(tg, cg)) == keyed(want, zip(tw, cw)), (name, batch)
+            if name == "flowhash":
+                assert (cg == 1).all() and _flow_ids_match(got, tg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [None, 4096])
+def test_bridge_with_flowhash_icmp_mpls_on_fuzz_corpus(batch):
+    """The three together on the fuzz corpus (MPLS stacks, EoMPLS, ICMP / ICMPv6, every other
+    encapsulation, truncated at every length), where the mpls and icmp plugins find their shapes:
+    records and extension texts equal the oracle's."""
+    import synth
+    from ipfixprobe_amd import run_capture
+    arena, desc = synth.to_batch(synth.fuzz_corpus(20000, seed=73))
+    eps, ops = [RefPlugin(x) for x in EXTRA], [RefPlugin(x) for x in EXTRA]
+    got, _ = run_capture(arena, desc, params="s=18", batch=batch, plugins=[p.struct for p in eps])
+    want, _ = oracle_py.run_capture(arena, desc, 1, cache_exp=20, plugins=[p.struct for p in ops])
+    (tg, cg), (tw, cw) = take_exts(got), take_exts(want)
+    assert keyed(got, zip(tg, cg)) == keyed(want, zip(tw, cw))
+    assert sum("mpls_label_1=" in t for t in tw) > 20 and sum("type=" in t for t in tw) > 20

@@ -32,6 +32,6 @@ for W in ${WORKLOADS:-udp64 imix quic imix10m}; do
     rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_${W}_$N.err; stop $rc "pmc $W $N"; }
   done
   S=pmc_summary_$W.json; [ $W = udp64 ] && S=pmc_summary.json
-  python3 tools/pmc_summary.py $OUT/pmc_$W $OUT/$S || exit 1
+  python3 tools/pmc_summary.py $OUT/pmc_$W $OUT/$S $OUT/pmc_${W}_FETCH_SIZE.json || exit 1
 done
 echo "== done"; date
