@@ -97,7 +97,10 @@ typedef struct ipxg_pkt_desc {
 #define IPXG_BATCH_OFFSET16 0x4u /* every descriptor's offset counts 16-byte units: frames
                                   * start 16-byte aligned and the arena may hold up to
                                   * 64 GiB - 4 KiB (the 32-bit byte offsets cap it at 4 GiB,
-                                  * 5M frames of the configs[4] mix) */
+                                  * 5M frames of the configs[4] mix).  Every frame must lie in
+                                  * the arena (offset + caplen <= arena_len): the ingest reads
+                                  * one past it as zeros (a keyless packet), with either
+                                  * offset form, and never reads outside the arena there */
 
 typedef struct ipxg_batch {
     const uint8_t* arena;       /* frame bytes                                          */

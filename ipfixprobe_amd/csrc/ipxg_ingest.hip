@@ -871,7 +871,12 @@ void k_bin(BatchView b, Params p, TableView t, FragView f, BinView bv, BatchCtl*
     // the wave's transpose area (XP): the stage array is free during the packet loop
     uint4* const xs = reinterpret_cast<uint4*>(stage) + (tid >> 6) * 320u;
     static_assert(!XP || IPXG_BLOCK / 64 * 320 <= TILE, "transpose areas fit the stage array");
-    auto want = [&](const ipxg_pkt_desc& d) { return fast_ok && fast_shape(b, d); };
+    // (unit offsets: the heads are plain loads through 64-bit addresses, which no buffer range
+    // clamps -- a descriptor past the arena reads as zeros here, as the byte-offset buffer loads
+    // give it, instead of faulting the GPU)
+    auto want = [&](const ipxg_pkt_desc& d) {
+        return fast_ok && fast_shape(b, d) && (!G64 || ((uint64_t)d.offset << 4) + d.caplen <= b.arena_len);
+    };
     bool nonmono = false;
     const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<ipxg_pkt_desc*>(b.desc), 0, (int)(b.n * 16u), 0x00020000);
@@ -1168,10 +1173,11 @@ template <bool G64>
 __device__ __forceinline__ SlowWin load_win(__amdgpu_buffer_rsrc_t rs_all, const BatchView& b, const uint4 e) {
     const uint32_t cap = e.z & 0xFFFFu;
     SlowWin w;
-    if constexpr (G64) {
+    if constexpr (G64) {  // (a frame past the arena reads as zeros: as want() in k_bin)
         const uint4* f = reinterpret_cast<const uint4*>(b.arena + ((uint64_t)e.y << 4));
+        const bool in = ((uint64_t)e.y << 4) + cap <= b.arena_len;
 #pragma unroll
-        for (int k = 0; k < SLOW_NCH; ++k) w.c[k] = *((uint32_t)(16 * k) < cap ? f + k : g_zero_head + (k & 7));
+        for (int k = 0; k < SLOW_NCH; ++k) w.c[k] = *(in && (uint32_t)(16 * k) < cap ? f + k : g_zero_head + (k & 7));
         return w;
     }
     const uint32_t o = slow_aligned(b, e) ? e.y : BUF_OOB;

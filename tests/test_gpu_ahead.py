@@ -210,3 +210,83 @@ def test_async_expire_between_batches(poll_every):
     assert len(rest) == live
     diff = flowcmp.diff(np.concatenate(out + [rest]), want)
     assert not diff, diff
+
+
+def test_slow_pass_needed_after_cleared_finish():
+    """a plain batch's finish, ipxg_clear_exports (no poll, so the next submit
+    launches its front ahead, gated on the finish's block), then an asynchronous batch with slow-list
+    packets (its k_bin runs without k_bin_slow behind it and flags slow_redo).  The redo's k_bin_slow
+    must not inherit the front's gate: the finish's block was re-zeroed by then and read as "closed",
+    so the redo wrote nothing and k_reduce folded stale slow columns.  Records equal the oracle's for
+    the second step."""
+    from ipfixprobe_amd import Engine
+    arena, desc, k = _plain_then_mixed(93)
+    want, _ = oracle_py.run_capture(arena, desc[k:], 1, cache_exp=20)
+    da, d1 = _dev(arena, desc[:k])
+    _, d2 = _dev(arena, desc[k:])
+    with Engine() as e:
+        e.submit(da, d1, device=True, asynchronous=True)
+        e.finish()
+        e.clear_exports()
+        e.submit(da, d2, device=True, asynchronous=True)
+        e.finish()
+        got = e.poll()
+        tm = e.timing()
+    assert tm["slow_redos"] >= 1
+    diff = flowcmp.diff(got, want)
+    assert not diff, diff
+
+
+def test_order_check_behind_expire_ahead():
+    """a batch whose first packet is earlier than the previous batch's last one,
+    submitted right behind an asynchronous ipxg_expire (its front launched ahead, gated on the
+    expire): the order check continues from the previous batch's last timestamp, as without the
+    expire, so the batch goes to the sequential path (complex flows) and the records are the
+    oracle's.  (No idle flow in the stream: the expires export nothing, as the oracle's run has none.)"""
+    a, d = synth.flow_stream(seed=81, n_flows=120, n_pkts=4000, long_gap_share=0.0, frag=False).batch()
+    d = d.copy()
+    d["ts_sec"] = d["ts_sec"][0] + (d["ts_sec"] - d["ts_sec"][0]) // 25  # (564 s -> 22 s: no flow idle 30 s)
+    d["ts_sec"][2000:3000] -= 3  # batch 3 starts 3 s before batch 2 ends
+    want, _ = oracle_py.run_capture(a, d, 1, cache_exp=20)
+    from ipfixprobe_amd import Engine
+    da, _ = _dev(a, d)
+    keep = []
+    with Engine() as e:
+        for s in range(0, len(d), 1000):
+            _, dd = _dev(a, d[s:s + 1000])
+            keep.append(dd)
+            e.submit(da, dd, device=True, asynchronous=True)
+            e.expire(int(d["ts_sec"][s:s + 1000].max()))
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert st["complex_flows"] > 0
+    assert st["end_inactive"] == 0
+    diff = flowcmp.diff(got, want)
+    assert not diff, diff
+
+
+@pytest.mark.parametrize("ahead", [True, False])
+def test_rehash_behind_a_front_ahead(monkeypatch, ahead):
+    """a small table (s=10) that the pending batch's post_batch grows by the load-
+    factor rehash while the next batch's front, launched ahead, is already queued (its k_bin's spills
+    merged into the old table, its k_reduce then runs on the new one): records equal the oracle's,
+    with and without fronts ahead (IPXG_NO_AHEAD)."""
+    if not ahead:
+        monkeypatch.setenv("IPXG_NO_AHEAD", "1")
+    a, d = synth.flow_stream(seed=83, n_flows=3000, n_pkts=12000, frag=False).batch()
+    want, _ = oracle_py.run_capture(a, d, 1, cache_exp=20)
+    from ipfixprobe_amd import Engine
+    da, _ = _dev(a, d)
+    keep = []
+    with Engine("s=10") as e:
+        for s in range(0, len(d), 2000):
+            _, dd = _dev(a, d[s:s + 2000])
+            keep.append(dd)
+            e.submit(da, dd, device=True, asynchronous=True)
+        e.finish()
+        got = e.poll()
+        st = e.stats()
+    assert st["table_capacity"] > 1 << 10
+    diff = flowcmp.diff(got, want)
+    assert not diff, diff

@@ -12,6 +12,7 @@ import pytest
 import flowcmp
 import oracle_py
 import pcaputil
+import synth
 
 pytestmark = pytest.mark.gpu
 
@@ -191,3 +192,36 @@ def test_arena_past_4gib(layout):
     assert not dd, dd
     for k in ("seen_packets", "parsed_packets", "ipv4_packets", "ipv6_packets", "vlan_packets", "mpls_packets"):
         assert st[k] == wst[k], k
+
+
+@pytest.mark.parametrize("walk", [";walk=narrow", ";walk=wide"])
+def test_offset16_frames_past_the_arena_read_as_zeros(walk):
+    """with IPXG_BATCH_OFFSET16 the ingest reads heads through 64-bit addresses, which no
+    buffer range clamps.  Every other descriptor here points past arena_len (into memory the caller
+    still owns, so an unguarded read would parse those frames as flows instead of faulting): k_bin and
+    k_bin_slow must read them as zeros -- keyless packets, as the byte-offset path's buffer loads give
+    them -- and the records are the oracle's over the packets inside the arena."""
+    import torch
+    rng = np.random.default_rng(97)
+    n = 8192
+    sip = (10 << 24) + rng.integers(0, 200, n)
+    dip = (192 << 24) + (168 << 16) + rng.integers(0, 50, n)
+    arena, desc = synth.udp_frames(sip, dip, rng.integers(1024, 1200, n), rng.integers(1, 30, n))
+    inside = np.arange(n) % 2 == 0
+    # the inside packets' frames first, the outside ones after arena_len
+    order = np.concatenate([np.nonzero(inside)[0], np.nonzero(~inside)[0]])
+    frames = arena.reshape(n, 64)[order].reshape(-1)
+    pos = np.empty(n, dtype=np.int64)
+    pos[order] = np.arange(n)
+    d = desc.copy()
+    d["offset"] = (pos * 64) // 16
+    big = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
+    arena_t = big[:int(inside.sum()) * 64]  # arena_len ends before the outside frames
+    dt = torch.from_numpy(np.ascontiguousarray(d).view(np.uint8).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    got, st = _run_batches("s=18" + walk, [(arena_t, dt)], offset16=True)
+    di = desc[inside].copy()
+    want, wst = oracle_py.run_capture(arena, di, 1, cache_exp=20)
+    dd = flowcmp.diff(got, want)
+    assert not dd, dd
+    assert st["seen_packets"] == n
