@@ -327,7 +327,11 @@ int ipxg_pending_exports(ipxg_engine* eng, size_t* n);
 /* Copy up to cap exported records to host memory out and remove them from the buffer. */
 int ipxg_poll_exports(ipxg_engine* eng, ipxg_flow_record* out, size_t cap, size_t* n);
 /* Device pointer to the export buffer and its current count (no copy; valid until the next
- * engine call). */
+ * engine call).  The device-side consumers of the exports -- this call, ipxg_poll_ipfix_messages and
+ * ipxg_device_ipfix_messages -- do not call the plugins' pre_export (host code) on the records the
+ * device exported: with process plugins holding per-flow state (ext), consume the exports through
+ * ipxg_poll_exports, which does (IPXG_REC_PRE_EXPORTED).  A pre_export failure there (the instance's
+ * error()) fails that call with IPXG_EPLUGIN after handing the records over. */
 int ipxg_device_exports(ipxg_engine* eng, const ipxg_flow_record** dptr, size_t* n);
 /* Forget the pending exports without copying them (caller consumed them on device). */
 int ipxg_clear_exports(ipxg_engine* eng);

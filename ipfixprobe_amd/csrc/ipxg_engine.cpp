@@ -164,6 +164,7 @@ struct ipxg_engine {
     uint32_t stream_grid = 0;  // k_bin's workgroups when streamed: two per CU (<= RS_MAX_COLS)
     uint32_t prog_mode = PROG_SC1 | PROG_TILE;  // IPXG_PROG_MODE (timing experiments)
     uint32_t pub_every = 4, rs_sleep = 4;       // IPXG_PUB_EVERY, IPXG_RS_SLEEP (tuning knobs)
+    bool rec_sc1 = true;                        // IPXG_REC_SC1=0: k_bin's record stores not write-through
     // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
     // the host has not read: completed by the next entry point (consume_pend) -- ipxg_submit of a
     // device batch first launches its own front behind it, gated on that block (Params::gate_mode),
@@ -509,6 +510,11 @@ static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv, bool st
     bv.part_bits = bits;
     bv.prog = nullptr;
     bv.prog_tag = 0;
+    // k_bin's record stores write-through (rec_rsrc, ipxg_ingest.hip) where the record area fits the
+    // 32-bit buffer range; IPXG_REC_SC1=0: plain stores (A/B knob)
+    bv.prog_mode = e->rec_sc1 && (uint64_t)P * cols * seg * 16 < 0xFFFFFF00ull ? PROG_SC1 : 0u;
+    bv.pub_every = 1;
+    bv.rs_sleep = 0;
     if (sm) {
         if ((rc = ensure(e, e->prog, (size_t)RS_MAX_COLS * P * sizeof(uint32_t)))) return rc;
         if (++e->prog_epoch > (PROG_EPOCH_MASK >> PROG_EPOCH_SHIFT) || grid != e->prog_g || P != e->prog_p) {
@@ -519,7 +525,7 @@ static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv, bool st
         }
         bv.prog = (uint32_t*)e->prog.p;
         bv.prog_tag = e->prog_epoch << PROG_EPOCH_SHIFT;
-        bv.prog_mode = e->prog_mode;
+        bv.prog_mode = (e->prog_mode & PROG_TILE) | ((e->prog_mode & PROG_SC1) ? PROG_SC1 : 0u);
         bv.pub_every = e->pub_every;
         bv.rs_sleep = e->rs_sleep;
     }
@@ -766,6 +772,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->no_line = std::getenv("IPXG_NO_LINE") != nullptr && std::atoi(std::getenv("IPXG_NO_LINE")) != 0;
     e->no_stream = !(std::getenv("IPXG_STREAM") != nullptr && std::atoi(std::getenv("IPXG_STREAM")) != 0);
     if (const char* pm = std::getenv("IPXG_PROG_MODE")) e->prog_mode = (uint32_t)std::atoi(pm) & 3u;
+    if (const char* rs = std::getenv("IPXG_REC_SC1")) e->rec_sc1 = std::atoi(rs) != 0;
     if (const char* pe = std::getenv("IPXG_PUB_EVERY")) e->pub_every = std::max(1, std::atoi(pe));
     if (const char* rsl = std::getenv("IPXG_RS_SLEEP")) e->rs_sleep = (uint32_t)std::max(0, std::atoi(rsl));
     if (const char* rx = std::getenv("IPXG_RS_EXP")) e->rs_sleep |= (uint32_t)std::atoi(rx) << 16;  // (timing only)
@@ -2801,6 +2808,13 @@ static int poll_exports_impl(ipxg_engine* e, ipxg_flow_record* out, size_t cap, 
                     if (q.pre_export) q.pre_export(q.ctx, &r);
                 r.reserved0 |= IPXG_REC_PRE_EXPORTED;
             }
+        // pre_export returns nothing: a failure there is reported by the instance's error(), as
+        // after a walk -- the records are handed over, then the engine stops until ipxg_reset
+        for (size_t q = 0; q < e->plugins.size() && !e->failed; ++q)
+            if (const char* m = e->plugins[q].error ? e->plugins[q].error(e->plugins[q].ctx) : nullptr) {
+                e->failed = true;
+                e->fail_msg = "process plugin " + std::to_string(q) + " (pre_export): " + m;
+            }
     }
     e->ex_head += (uint32_t)k;
     if (k) e->ex6_valid = false;
@@ -2812,6 +2826,7 @@ static int poll_exports_impl(ipxg_engine* e, ipxg_flow_record* out, size_t cap, 
         HIPCHK(e, hipStreamSynchronize(e->st));
     }
     *n = k;
+    if (e->failed) return set_err(e, IPXG_EPLUGIN, e->fail_msg);
     return IPXG_OK;
 }
 

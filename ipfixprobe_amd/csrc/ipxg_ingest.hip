@@ -285,6 +285,31 @@ __device__ __forceinline__ void tile_rank_all(uint32_t* hist, uint32_t pmask, co
 // defer_spill (Params::defer_spill: this batch's k_bin runs while the previous batch's host walk
 // still owns the table): what does not fit is deferred (the deferral lists, applied after k_reduce)
 // instead of accumulated into the table.
+// ---- write-through record stores; the streamed reduce's progress words ----------------------------
+// The record area as a buffer resource (BinView::prog_mode & PROG_SC1: the host set it only for an
+// area under 4 GiB): sc1 stores, whose lines pass the writer's L2 straight on to the Infinity Cache.
+// Round 6: k_bin's records as write-through stores (the default) -- udp64 k_bin 214 -> 208 us, step
+// 0.305 -> 0.300 ms, alternating on one box (profiles/r06/sc1_ab.txt): the records leave no dirty
+// lines in L2 for the frames to evict and for the kernel's end to write back.  The streamed reduce
+// (k_reduce_stream on another XCD) reads them with sc1 loads (MI355X_MICROARCH.md, hand-off table:
+// sc1 stores, the writers' vmcnt(0), then an sc1 flag; sc1 polls and sc1 loads).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const BinView& bv) {
+    const uint64_t bytes = ((uint64_t)bv.cols << bv.part_bits) * bv.seg_cap * 16u;
+    return __builtin_amdgcn_make_buffer_rsrc(bv.rec, 0, (int)(uint32_t)min<uint64_t>(bytes, BUF_OOB), 0x00020000);
+}
+constexpr int AUX_SC1 = 16;  // buffer-op cache policy: sc1
+__device__ __forceinline__ void store_rec_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint4& r) {
+    u32x4 v = {r.x, r.y, r.z, r.w};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, AUX_SC1);
+}
+// partition q's progress word of column col: the whole lines stored (records fill, at most the
+// segment's), the batch's tag, done
+__device__ __forceinline__ void publish_prog(const BinView& bv, uint32_t col, uint32_t q, uint32_t fill, uint32_t done) {
+    const uint32_t lines = min(fill, bv.seg_cap) >> 3;
+    __hip_atomic_store(&bv.prog[(size_t)q * RS_MAX_COLS + col], bv.prog_tag | done | lines, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool LISTED, bool AGG, uint32_t PMAX = (1u << BIN_MAX_PART_BITS)>
 __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t pmask, const BinView& bv, uint32_t col,
                                           const TableView& t, BatchCtl* ctl, uint32_t* deferred_list,
@@ -365,6 +390,10 @@ __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t 
         uint4* dst = (fits || filler) ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + pos]
                                       : &g_dummy_rec[threadIdx.x & 63];
 #endif
+        if (bv.prog_mode & PROG_SC1) {  // (uniform) write-through (rec_rsrc)
+            store_rec_sc1(rec_rsrc(bv), (fits || filler) ? (uint32_t)(((size_t)part * bv.cols + col) * bv.seg_cap + pos) * 16u
+                                                         : BUF_OOB, r);
+        } else {
 #ifdef IPXG_NT_REC_STORE  // tuning knob: streaming (non-temporal) record stores
         __builtin_nontemporal_store(r.x, &dst->x);
         __builtin_nontemporal_store(r.y, &dst->y);
@@ -373,6 +402,7 @@ __device__ __forceinline__ void tile_emit(const BinLds& L, uint32_t P, uint32_t 
 #else
         *dst = r;
 #endif
+        }
         if (valid && !fits && ai == 0) {  // segment full: accumulate straight into the table
             spilled++;
             if (defer_spill) atomicAdd(&ctl->spill_deferred, 1u);
@@ -427,28 +457,6 @@ constexpr uint32_t LINE_ITERS = (LINE_MAXL * 8 + IPXG_BLOCK - 1) / IPXG_BLOCK;  
 #ifndef IPXG_LINE_AUX
 #define IPXG_LINE_AUX 0  // cache policy of line mode's frame and descriptor loads (membench: default policy)
 #endif
-
-// ---- streamed reduce: k_bin's progress words --------------------------------------------------
-// The record area as a buffer resource (the host keeps it under 4 GiB in streamed mode): sc1 stores
-// and loads, whose lines pass the writer's L2 (not coherent across XCDs) straight to the Infinity
-// Cache, where k_reduce_stream on another XCD reads them (MI355X_MICROARCH.md, hand-off table: sc1
-// stores, the writers' vmcnt(0), then an sc1 flag; sc1 polls and sc1 loads).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const BinView& bv) {
-    const uint64_t bytes = ((uint64_t)bv.cols << bv.part_bits) * bv.seg_cap * 16u;
-    return __builtin_amdgcn_make_buffer_rsrc(bv.rec, 0, (int)(uint32_t)min<uint64_t>(bytes, BUF_OOB), 0x00020000);
-}
-constexpr int AUX_SC1 = 16;  // buffer-op cache policy: sc1
-__device__ __forceinline__ void store_rec_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint4& r) {
-    u32x4 v = {r.x, r.y, r.z, r.w};
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, AUX_SC1);
-}
-// partition q's progress word of column col: the whole lines stored (records fill, at most the
-// segment's), the batch's tag, done
-__device__ __forceinline__ void publish_prog(const BinView& bv, uint32_t col, uint32_t q, uint32_t fill, uint32_t done) {
-    const uint32_t lines = min(fill, bv.seg_cap) >> 3;
-    __hip_atomic_store(&bv.prog[(size_t)q * RS_MAX_COLS + col], bv.prog_tag | done | lines, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
 
 struct LineLds {
     uint32_t* hist;   // LINE_P: the tile's records per partition (rank counters)
@@ -516,7 +524,7 @@ __device__ __forceinline__ void tile_emit_lines(const LineLds& L, uint32_t P, ui
         const uint32_t at = L.fill[part] + j;
         const bool fits = valid && at < bv.seg_cap;  // (seg_cap and fill are multiples of 8: whole lines)
         uint4* dst = fits ? &bv.rec[((size_t)part * bv.cols + col) * bv.seg_cap + at] : &g_dummy_rec[tid & 63];
-        if (bv.prog && (bv.prog_mode & PROG_SC1)) {  // (uniform) sc1: k_reduce_stream reads the line from another CU while k_bin runs
+        if (bv.prog_mode & PROG_SC1) {  // (uniform) write-through: see rec_rsrc
             store_rec_sc1(rs_rec, fits ? (uint32_t)(((size_t)part * bv.cols + col) * bv.seg_cap + at) * 16u : BUF_OOB, r);
         } else {
 #ifdef IPXG_NT_REC_STORE  // tuning knob: streaming (non-temporal) record stores
@@ -561,7 +569,7 @@ __device__ __forceinline__ void line_flush(const LineLds& L, uint32_t P, const B
         const uint4 r = j < c ? L.carry[part * LINE_C + j] : make_uint4(0, 0, NO_REC, 0);
         const size_t k_at = ((size_t)part * bv.cols + col) * bv.seg_cap + at;
         if (at < bv.seg_cap) {
-            if (bv.prog && (bv.prog_mode & PROG_SC1)) store_rec_sc1(rec_rsrc(bv), (uint32_t)k_at * 16u, r);
+            if (bv.prog_mode & PROG_SC1) store_rec_sc1(rec_rsrc(bv), (uint32_t)k_at * 16u, r);
             else bv.rec[k_at] = r;
         } else if (j < c) {
             line_spill(t, ctl, deferred_list, r, spilled, defer_spill);

@@ -9,6 +9,7 @@ sites) is checked against those goldens on the CPU; the engine's bridge (device 
 host walk of the plugin flows) against the goldens and the oracle on the GPU, including
 synthetic flows whose HTTP requests trigger FLOW_FLUSH_WITH_REINSERT and DNS flows spread over
 several batches."""
+import ctypes
 import os
 from collections import Counter
 
@@ -21,6 +22,8 @@ import pcaputil
 import plugins_py
 import synth
 from test_oracle_synth import PKT_BUCKETS
+
+FLOW_EXT_OFFSET = pcaputil.FLOW_DTYPE.fields["ext"][1]  # ipxg_flow_record.ext
 
 REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference")
 
@@ -338,3 +341,57 @@ def test_early_front_on_fuzz_corpus(prof):
     d = flowcmp.diff(got, want, fields=flowcmp.CONTRACT_FIELDS + ["ext"])
     assert not d, d
     assert eng.seen == orc.seen
+
+
+@pytest.mark.gpu
+def test_pre_export_failure_in_poll_fails_the_call():
+    """the plugins' pre_export on the records the device exported (ipxg_poll_exports) can
+    fail only through the instance's error() (pre_export returns nothing): the poll hands the records
+    over, then fails with IPXG_EPLUGIN and the plugin's message, and the engine refuses work until
+    ipxg_reset.  A port-53 plugin claims every flow in post_create (a non-zero ext); k_finish exports
+    them on the device; the first pre_export fails."""
+    from ipfixprobe_amd import Engine
+    from ipfixprobe_amd.engine import ERROR_FN, IpxgError
+
+    class FailOnExport(plugins_py.PyPlugin):
+        proto_mask = 2
+        ports = (53,)
+
+        def __init__(self):
+            super().__init__()
+            self.msg = ctypes.create_string_buffer(b"pre_export failed on purpose")
+            self.failed = False
+            self._err = ERROR_FN(self._error)
+            self.struct.error = self._err
+
+        def _post_create(self, ctx, flow, view):
+            self.calls["post_create"] += 1
+            ctypes.c_uint64.from_address(flow + FLOW_EXT_OFFSET).value = 0x5EED  # the flow's state
+            return 0
+
+        def _pre_export(self, ctx, flow):
+            self.calls["pre_export"] += 1
+            self.failed = True
+
+        def _error(self, ctx):
+            if not self.failed:
+                return None
+            self.failed = False
+            return ctypes.addressof(self.msg)
+
+    n = 2000
+    sip = (10 << 24) + np.arange(n) % 100
+    arena, desc = synth.udp_frames(sip, np.full(n, (192 << 24) + 1), np.full(n, 5000), np.full(n, 53))
+    pl = FailOnExport()
+    with Engine("s=16") as e:
+        e.add_plugin(pl.struct)
+        e.submit(arena, desc)
+        e.finish()
+        with pytest.raises(IpxgError) as ex:
+            e.poll()
+        assert ex.value.rc == -8 and "pre_export failed on purpose" in str(ex.value), str(ex.value)
+        with pytest.raises(IpxgError) as ex2:
+            e.submit(arena, desc)
+        assert ex2.value.rc == -7
+        e.reset()
+    assert pl.calls["pre_export"] >= 1

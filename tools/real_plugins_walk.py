@@ -26,11 +26,17 @@ def main(name, steps, kinds=("stand-in", "reference")):
     from ipfixprobe_amd import Engine
     from ipfixprobe_amd.engine import StdPlugin
     dev = torch.device("cuda", 0)
-    n, nb = (10_000_000, 10) if name == "imix" else (5_000_000, 4)
+    # the bench's default step shapes since ABI 8 (16-byte unit offsets: imix 7 x 14.3M, quic 2 x 10M);
+    # IPXG_RPW_BYTES=1: the byte-offset shapes of round 4 (imix 10 x 10M, quic 4 x 5M)
+    units = not os.environ.get("IPXG_RPW_BYTES")
+    if units:
+        n, nb = (14_285_715, 7) if name == "imix" else (10_000_000, 2)
+    else:
+        n, nb = (10_000_000, 10) if name == "imix" else (5_000_000, 4)
     names = ["dns", "http", "tls"] if name == "imix" else ["quic"]
     mix = synthgen.Mix(name, 1_000_000, seed=1234, zipf=1.1 if name == "imix" else None)
     gen = synthgen.Generator(mix, dev, seed=1234)
-    batches = [gen.batch(k * n, n) for k in range(nb)]
+    batches = [gen.batch(k * n, n, offset16=units) for k in range(nb)]
     torch.cuda.synchronize()
     for kind in kinds:
         pls = [StdPlugin(p) if kind == "stand-in" else test_ref_plugins.RefPlugin(p) for p in names]
@@ -40,7 +46,7 @@ def main(name, steps, kinds=("stand-in", "reference")):
 
             def step():
                 for fr, de in batches:
-                    e.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+                    e.submit(fr, de, device=True, asynchronous=True, wait_producer=False, offset16=units)
                 e.finish()
                 e.clear_exports()  # (the real plugins' exported Flow objects are left to the process)
 
@@ -54,6 +60,7 @@ def main(name, steps, kinds=("stand-in", "reference")):
             dt = (time.perf_counter() - t0) / steps
             tm = e.timing()
         print(json.dumps({"workload": name, "plugins": names, "kind": kind, "packets_per_step": n * nb,
+                          "batches_per_step": nb, "offsets": "units" if units else "bytes",
                           "ms_per_step": round(dt * 1e3, 2), "Mpkts_per_s": round(n * nb / dt / 1e6, 1),
                           "host_walk_ms_per_step": round(tm["plugin_ms"] / steps, 2),
                           "walked_flows_per_step": round(tm["plugin_flows"] / steps),
