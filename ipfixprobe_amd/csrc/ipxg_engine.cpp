@@ -164,7 +164,7 @@ struct ipxg_engine {
     uint32_t stream_grid = 0;  // k_bin's workgroups when streamed: two per CU (<= RS_MAX_COLS)
     uint32_t prog_mode = PROG_SC1 | PROG_TILE;  // IPXG_PROG_MODE (timing experiments)
     uint32_t pub_every = 4, rs_sleep = 4;       // IPXG_PUB_EVERY, IPXG_RS_SLEEP (tuning knobs)
-    bool rec_sc1 = true;                        // IPXG_REC_SC1=0: k_bin's record stores not write-through
+    uint32_t rec_sc1 = 1;                       // IPXG_REC_SC1: 0 plain record stores, 1 write-through in line mode, 2 always
     // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
     // the host has not read: completed by the next entry point (consume_pend) -- ipxg_submit of a
     // device batch first launches its own front behind it, gated on that block (Params::gate_mode),
@@ -510,9 +510,11 @@ static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv, bool st
     bv.part_bits = bits;
     bv.prog = nullptr;
     bv.prog_tag = 0;
-    // k_bin's record stores write-through (rec_rsrc, ipxg_ingest.hip) where the record area fits the
-    // 32-bit buffer range; IPXG_REC_SC1=0: plain stores (A/B knob)
-    bv.prog_mode = e->rec_sc1 && (uint64_t)P * cols * seg * 16 < 0xFFFFFF00ull ? PROG_SC1 : 0u;
+    // line mode's record stores write-through (rec_rsrc, ipxg_ingest.hip) where the record area fits
+    // the 32-bit buffer range: udp64 step -1.8 %; the partial-line stores of tile_emit (the 1M-flow
+    // mixes) lose with it (quic +1.7 %, imix +-0, profiles/r06/sc1_ab.txt).  IPXG_REC_SC1=0: plain
+    // stores (A/B knob); 2: write-through in every mode
+    bv.prog_mode = e->rec_sc1 && (ln || e->rec_sc1 == 2) && (uint64_t)P * cols * seg * 16 < 0xFFFFFF00ull ? PROG_SC1 : 0u;
     bv.pub_every = 1;
     bv.rs_sleep = 0;
     if (sm) {
@@ -772,7 +774,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->no_line = std::getenv("IPXG_NO_LINE") != nullptr && std::atoi(std::getenv("IPXG_NO_LINE")) != 0;
     e->no_stream = !(std::getenv("IPXG_STREAM") != nullptr && std::atoi(std::getenv("IPXG_STREAM")) != 0);
     if (const char* pm = std::getenv("IPXG_PROG_MODE")) e->prog_mode = (uint32_t)std::atoi(pm) & 3u;
-    if (const char* rs = std::getenv("IPXG_REC_SC1")) e->rec_sc1 = std::atoi(rs) != 0;
+    if (const char* rs = std::getenv("IPXG_REC_SC1")) e->rec_sc1 = (uint32_t)std::max(0, std::atoi(rs));
     if (const char* pe = std::getenv("IPXG_PUB_EVERY")) e->pub_every = std::max(1, std::atoi(pe));
     if (const char* rsl = std::getenv("IPXG_RS_SLEEP")) e->rs_sleep = (uint32_t)std::max(0, std::atoi(rsl));
     if (const char* rx = std::getenv("IPXG_RS_EXP")) e->rs_sleep |= (uint32_t)std::atoi(rx) << 16;  // (timing only)
