@@ -2102,7 +2102,12 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
     // flow is complex anyway, force_cx)
     const uint32_t tmax = force_cx || b.n == 0 ? TMAX_UNKNOWN : b.desc[b.n - 1].ts_sec;
     uint32_t n_live = 0, n_cx = 0, n_ex = 0, n_v6 = 0, n_keys = 0, n_def = 0;
+#ifdef IPXG_PROBE  // k_fin_list [12] list image + slot probe, [13] finalize_slot, [14] export reservation + stores,
+                   // [15] statistics and control-block counts (workgroup 0's thread 0 ... each workgroup's)
+    uint64_t probe_acc[4] = {0, 0, 0, 0};
+#endif
     for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
+        PROBE_T(f0);
         const uint32_t k = base + tid;
         bool do_export = false;  // er is exported with `reason` (a boundary split, or the fused finish)
         uint8_t reason = 0;
@@ -2147,6 +2152,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
                 if (deferred_only) fin_list[k].pad = FIN_UNRESOLVED;  // done: later re-runs skip it
             }
         }
+        PROBE_T(f1);
+        PROBE_ADD(0, f0, f1);
         if (go) {
             const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean, tmax);
             if (fr.status == FIN_COMPLEX && no_slot) {  // a complex flow: its slot now, for the sequential path
@@ -2169,6 +2176,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
             do_export = fr.do_export || fr.fin_export;
             reason = fr.fin_export ? (uint8_t)IPXG_FLOW_END_FORCED : fr.reason;
         }
+        PROBE_T(f2);
+        PROBE_ADD(1, f1, f2);
         // one reservation in the export buffer per workgroup and pass (a returning atomic per
         // wave on the one counter serialised ~1600 waves at ~12 ns each: MI355X_MICROARCH.md
         // "fanin" / "dequeue")
@@ -2184,7 +2193,10 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
         }
         count_exports_wave(sc, do_export, er, reason);
         __syncthreads();  // ex_base is rewritten by the next pass
+        PROBE_T(f3);
+        PROBE_ADD(2, f2, f3);
     }
+    PROBE_T(f4);
     wave_add_lds(&cnt[0], n_live);
     wave_add_lds(&cnt[1], n_cx);
     wave_add_lds(&cnt[2], n_ex);
@@ -2200,6 +2212,12 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
         if (cnt[4]) atomicAdd(&ctl->new_keys, cnt[4]);
         if (cnt[5]) atomicAdd(&ctl->fin_deferred, cnt[5]);
     }
+#ifdef IPXG_PROBE
+    PROBE_T(f5);
+    PROBE_ADD(3, f4, f5);
+    if (tid == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long*)&ctl->probe[12 + k], (unsigned long long)probe_acc[k]);
+#endif
 }
 
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,

@@ -36,8 +36,9 @@ def main():
         print("%-18s %12.0f cycles/workgroup-launch" % (nme, pc[k] / grid / 4))
     for k, nme in ((4, "red: prefix+zero"), (5, "red: aggregate"), (6, "red: merge+list")):
         print("%-18s %12.0f cycles/workgroup" % (nme, pc[k] / P))
-    print("red aggregate: wait for records %12.0f, fold %12.0f cycles/wave" % (pc[12] / (P * 16),
-                                                                            pc[13] / (P * 16)))
+    fin_blocks = (100_000 + 255) // 256  # (k_fin_list: one lane per listed flow)
+    for k, nme in ((12, "fin: image"), (13, "fin: finalize"), (14, "fin: export"), (15, "fin: counts")):
+        print("%-18s %12.0f cycles/workgroup (thread 0)" % (nme, pc[k] / fin_blocks))
     print("k_bin avg %.4f ms, k_reduce avg %.4f ms, k_fin_list avg %.4f ms" % (
         tm["ingest_ms"] / max(tm["ingest_launches"], 1), tm["reduce_ms"] / max(tm["reduce_launches"], 1),
         tm["fin_ms"] / max(tm["reduce_launches"], 1)))
