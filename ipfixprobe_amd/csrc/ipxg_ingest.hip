@@ -2075,23 +2075,34 @@ void launch_reduce_stream(hipStream_t st, const Params& p, TableView t, BinView 
 // full near the slot) marks the entry FIN_DEFERRED and counts it in ctl->fin_deferred -- the host
 // grows the table and runs this kernel again over those entries only (deferred_only), not
 // finishing.
-#ifndef IPXG_FIN_WAVES  // tuning knob: k_fin_list's waves per SIMD (register budget)
-#define IPXG_FIN_WAVES 3
+// Workgroups of FIN_THREADS (a multiple of 256: each lane's LDS column lies in the window of its
+// 256-lane group, stage_frame's column stride).  Round 6: a timing build without the export-slot
+// reservation (a returning atomic per workgroup and pass) and the control-block counts took udp64's
+// k_fin_list from 26 to 20.5 us; 768-thread workgroups (one per CU at 168 VGPRs), a third of the
+// reservations, moved nothing on udp64 and cost quic +9 %, imix +8 % (more passes per workgroup) --
+// the reservation's cost is its round trip in every pass, not the count (profiles/r06/fin_ab.txt).
+#ifndef IPXG_FIN_THREADS
+#define IPXG_FIN_THREADS 256
 #endif
-__global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG_FIN_WAVES))) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
+constexpr uint32_t FIN_THREADS = IPXG_FIN_THREADS;
+static_assert(FIN_THREADS % IPXG_BLOCK == 0 && FIN_THREADS <= 1024, "k_fin_list workgroup");
+#ifndef IPXG_FIN_WAVES  // tuning knob: k_fin_list's waves per SIMD (register budget)
+#define IPXG_FIN_WAVES (FIN_THREADS >= 1024 ? 4 : FIN_THREADS >= 512 ? FIN_THREADS / 256 : 3)
+#endif
+__global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPXG_FIN_WAVES))) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
                                                          ExportView ex, BatchCtl* ctl, HotSlot* fin_list,
                                                          unsigned long long* stats, uint32_t finishing,
                                                          uint32_t deferred_only) {
-    __shared__ uint32_t win[IPXG_WIN_DW * IPXG_BLOCK];
+    __shared__ uint32_t win[IPXG_WIN_DW * FIN_THREADS];
     __shared__ uint32_t sc[ST_COUNT];
     __shared__ uint32_t cnt[6];  // new live, complex, exported, IPv6 exports, new keys, deferred
-    __shared__ uint32_t scan_s[IPXG_BLOCK / 64 + 1];
+    __shared__ uint32_t scan_s[FIN_THREADS / 64 + 1];
     __shared__ uint32_t ex_base;
     if (p.slow_skip && ctl->slow_redo) return;  // (k_reduce returned too; `fused` stays 0)
     const uint32_t nf = ctl->fin_count;  // final: k_reduce has completed
     const bool fused = finishing && !(ctl->frag_count || ctl->deferred || ctl->agg_deferred || ctl->pending);
     if (blockIdx.x == 0 && threadIdx.x == 0) ctl->fused = fused ? 1u : 0u;
-    if (blockIdx.x * IPXG_BLOCK >= nf) return;
+    if (blockIdx.x * FIN_THREADS >= nf) return;
     const uint32_t tid = threadIdx.x;
     if (tid < ST_COUNT) sc[tid] = 0;
     if (tid < 6) cnt[tid] = 0;
@@ -2106,7 +2117,8 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
                    // [15] statistics and control-block counts (workgroup 0's thread 0 ... each workgroup's)
     uint64_t probe_acc[4] = {0, 0, 0, 0};
 #endif
-    for (uint32_t base = blockIdx.x * IPXG_BLOCK; base < nf; base += gridDim.x * IPXG_BLOCK) {  // block-uniform
+    uint32_t* const col = &win[(tid / IPXG_BLOCK) * (IPXG_WIN_DW * IPXG_BLOCK) + tid % IPXG_BLOCK];  // (the lane's LDS column)
+    for (uint32_t base = blockIdx.x * FIN_THREADS; base < nf; base += gridDim.x * FIN_THREADS) {  // block-uniform
         PROBE_T(f0);
         const uint32_t k = base + tid;
         bool do_export = false;  // er is exported with `reason` (a boundary split, or the fused finish)
@@ -2155,7 +2167,7 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
         PROBE_T(f1);
         PROBE_ADD(0, f0, f1);
         if (go) {
-            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, &win[tid], er, fused, slot_clean, tmax);
+            const FinResult fr = finalize_slot<true>(b, p, t, f, h.pad, h, force_cx, col, er, fused, slot_clean, tmax);
             if (fr.status == FIN_COMPLEX && no_slot) {  // a complex flow: its slot now, for the sequential path
                 HotSlot img;
                 bool claimed;
@@ -2182,9 +2194,13 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
         // wave on the one counter serialised ~1600 waves at ~12 ns each: MI355X_MICROARCH.md
         // "fanin" / "dequeue")
         uint32_t btot;
-        const uint32_t pos = block_exclusive_scan<IPXG_BLOCK>(do_export ? 1u : 0u, scan_s, &btot);
+        const uint32_t pos = block_exclusive_scan<FIN_THREADS>(do_export ? 1u : 0u, scan_s, &btot);
         if (btot == 0) continue;  // uniform
+#if defined(IPXG_EXP_FIN) && IPXG_EXP_FIN == 2  // timing experiment only: no export reservation (positions wrong)
+        if (tid == 0) ex_base = base;
+#else
         if (tid == 0) ex_base = atomicAdd(ex.count, btot);
+#endif
         __syncthreads();
         if (do_export) {
             store_export_w(ex, ex_base + pos, er, reason);
@@ -2203,6 +2219,9 @@ __global__ __launch_bounds__(IPXG_BLOCK) __attribute__((amdgpu_waves_per_eu(IPXG
     wave_add_lds(&cnt[3], n_v6);
     wave_add_lds(&cnt[4], n_keys);
     wave_add_lds(&cnt[5], n_def);
+#if defined(IPXG_EXP_FIN) && IPXG_EXP_FIN >= 1  // timing experiment only: no statistics / control-block counts
+    return;
+#endif
     flush_block_stats(sc, stats);
     if (tid == 0) {
         if (cnt[3] && ex.count6) atomicAdd(ex.count + 2, cnt[3]);  // count_v6_exports' counter
@@ -2235,14 +2254,14 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
     if (!resident) {
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fin_list, IPXG_BLOCK, 0) != hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fin_list, FIN_THREADS, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         resident = (uint32_t)std::max(1, cus * per_cu);
         slot.store(resident, std::memory_order_relaxed);
     }
-    uint32_t grid = (max_n + IPXG_BLOCK - 1) / IPXG_BLOCK;
+    uint32_t grid = (max_n + FIN_THREADS - 1) / FIN_THREADS;
     if (grid > resident) grid = resident;
-    hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(IPXG_BLOCK), 0, st, b, p, t, f, ex, ctl, fin_list,
+    hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(FIN_THREADS), 0, st, b, p, t, f, ex, ctl, fin_list,
                        stats, finishing ? 1u : 0u, deferred_only ? 1u : 0u);
 }
 
