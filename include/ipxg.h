@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IPXG_ABI_VERSION 8 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
+#define IPXG_ABI_VERSION 9 /* 2: ipxg_plugin gained masked prefixes and follow_packets;
                               3: ipxg_plugin gained copy_ctx / free_ctx (multi-threaded walk);
                               4: hooks report PluginError (IPXG_PLUGIN_ERROR, ipxg_plugin.error);
                               5: ipxg_timing gained plugin_overlapped
@@ -36,7 +36,8 @@ extern "C" {
                                  slow_redos; ipxg_plugin gained all_packets
                               7: ipxg_plugin gained follow_bytes; ipxg_timing gained
                                  plugin_d2h_bytes
-                              8: IPXG_BATCH_OFFSET16 (arenas up to 64 GiB) */
+                              8: IPXG_BATCH_OFFSET16 (arenas up to 64 GiB)
+                              9: ipxg_timing gained ex_compactions */
 
 /* ---- error codes ------------------------------------------------------------------- */
 #define IPXG_OK 0
@@ -481,6 +482,10 @@ typedef struct ipxg_timing {
     /* ABI 7: bytes the plugin walk copied to the host -- frames (whole, or their byte budget:
        ipxg_plugin.follow_bytes), packet and flow records, per-flow arrays */
     uint64_t plugin_d2h_bytes;
+    /* ABI 9 (always counted; zeroed by ipxg_profile): finishes fused into a batch's finalise pass whose
+       reserved export records had holes (flows that turned complex or found no slot), closed by a
+       compaction of the export buffer before the records were handed out */
+    uint64_t ex_compactions;
 } ipxg_timing;
 
 /* Per-phase shader-clock sums of the last batch's k_bin, k_reduce and k_bin_slow (16 values;

@@ -164,6 +164,7 @@ struct ipxg_engine {
     uint32_t stream_grid = 0;  // k_bin's workgroups when streamed: two per CU (<= RS_MAX_COLS)
     uint32_t prog_mode = PROG_SC1 | PROG_TILE;  // IPXG_PROG_MODE (timing experiments)
     uint32_t pub_every = 4, rs_sleep = 4;       // IPXG_PUB_EVERY, IPXG_RS_SLEEP (tuning knobs)
+    bool fin_lorder = true;                     // IPXG_FIN_LORDER=0: a fused finish reserves its exports per pass (A/B)
     uint32_t rec_sc1 = 1;                       // IPXG_REC_SC1: 0 plain record stores, 1 write-through in line mode, 2 always
     // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
     // the host has not read: completed by the next entry point (consume_pend) -- ipxg_submit of a
@@ -611,6 +612,24 @@ static int check_ex(ipxg_engine* e) {
     return IPXG_OK;
 }
 
+// A fused k_fin_list left holes in its export reservation (flows that turned complex or found no
+// slot; their batch goes to the sequential path anyway): closed on the device before anything reads
+// the exports, and the published count lowered to match.  The records below the host's count were
+// there before the batch; if the counters were reset meanwhile (ipxg_clear_exports), from 0.
+static int close_export_holes(ipxg_engine* e) {
+    if (e->ex_zero_pending) return IPXG_OK;  // (the exports are dropped anyway)
+    uint32_t* pub = const_cast<uint32_t*>(ex_host(e));
+    const uint32_t hi = std::min(pub[0], e->ex_cap), holes = e->ctl_h->ex_holes;
+    const uint32_t lo = e->ex_count <= hi ? e->ex_count : 0u;
+    if (holes > hi - lo) return set_err(e, IPXG_EDEVICE, "more export holes than reserved records");
+    launch_ex_compact(e->st, export_view(e), lo, hi);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    pub[0] = hi - holes;
+    e->tm.ex_compactions++;
+    return IPXG_OK;
+}
+
 // the control block and the export counter into host-mapped memory (a one-block kernel on
 // the stream: cheaper than a D2H copy command); seq: with a sequence number the host polls
 static int publish_ctl(ipxg_engine* e, bool with_seq = false) {
@@ -774,6 +793,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->no_line = std::getenv("IPXG_NO_LINE") != nullptr && std::atoi(std::getenv("IPXG_NO_LINE")) != 0;
     e->no_stream = !(std::getenv("IPXG_STREAM") != nullptr && std::atoi(std::getenv("IPXG_STREAM")) != 0);
     if (const char* pm = std::getenv("IPXG_PROG_MODE")) e->prog_mode = (uint32_t)std::atoi(pm) & 3u;
+    if (const char* fl = std::getenv("IPXG_FIN_LORDER")) e->fin_lorder = std::atoi(fl) != 0;
     if (const char* rs = std::getenv("IPXG_REC_SC1")) e->rec_sc1 = (uint32_t)std::max(0, std::atoi(rs));
     if (const char* pe = std::getenv("IPXG_PUB_EVERY")) e->pub_every = std::max(1, std::atoi(pe));
     if (const char* rsl = std::getenv("IPXG_RS_SLEEP")) e->rs_sleep = (uint32_t)std::max(0, std::atoi(rsl));
@@ -955,8 +975,11 @@ static int launch_tail(ipxg_engine* e, bool finishing) {
         if (rc0) return rc0;
     }
     ev_rec(e, 3);
+    // a finish fused into the pass writes its exports in list order from the export count, which the
+    // host knows exactly when no batch is pending (its exports counted) -- 0 after ipxg_clear_exports
+    const uint32_t ex_start = !finishing || e->pend.on || !e->fin_lorder ? EX_START_NONE : e->ex_zero_pending ? 0u : e->ex_count;
     launch_fin_list(e->st, e->inflight.bv, e->inflight.p, table_view(e), frag_view(e), export_view(e), e->ctl_d,
-                    (HotSlot*)e->fin_list.p, e->stats_d, e->inflight.n, finishing);
+                    (HotSlot*)e->fin_list.p, e->stats_d, e->inflight.n, finishing, false, ex_start);
     ev_rec(e, 4);
     HIPCHK(e, hipGetLastError());
     return IPXG_OK;
@@ -2641,6 +2664,9 @@ static int consume_pend(ipxg_engine* e, bool spec) {
     }
     if (!rc) rc = wait_seq(e, q.seq);
     q.spec_closed = !rc && spec && gate_closed(*e->ctl_h, q.mode);
+    if (!rc && (e->ctl_h->guard & GUARD_EX_START))
+        rc = set_err(e, IPXG_EDEVICE, "k_fin_list: the export counter was not at the host's count (list-order exports)");
+    if (!rc && e->ctl_h->ex_holes) rc = close_export_holes(e);
     if (!rc) rc = check_ex(e);
     if (!rc) {
         if (q.mode == GATE_BATCH) {

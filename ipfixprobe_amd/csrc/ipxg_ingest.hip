@@ -2092,10 +2092,10 @@ static_assert(FIN_THREADS % IPXG_BLOCK == 0 && FIN_THREADS <= 1024, "k_fin_list 
 __global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPXG_FIN_WAVES))) void k_fin_list(BatchView b, Params p, TableView t, FragView f,
                                                          ExportView ex, BatchCtl* ctl, HotSlot* fin_list,
                                                          unsigned long long* stats, uint32_t finishing,
-                                                         uint32_t deferred_only) {
+                                                         uint32_t deferred_only, uint32_t ex_start) {
     __shared__ uint32_t win[IPXG_WIN_DW * FIN_THREADS];
     __shared__ uint32_t sc[ST_COUNT];
-    __shared__ uint32_t cnt[6];  // new live, complex, exported, IPv6 exports, new keys, deferred
+    __shared__ uint32_t cnt[7];  // new live, complex, exported, IPv6 exports, new keys, deferred, export holes
     __shared__ uint32_t scan_s[FIN_THREADS / 64 + 1];
     __shared__ uint32_t ex_base;
     if (p.slow_skip && ctl->slow_redo) return;  // (k_reduce returned too; `fused` stays 0)
@@ -2105,10 +2105,22 @@ __global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPX
     if (blockIdx.x * FIN_THREADS >= nf) return;
     const uint32_t tid = threadIdx.x;
     if (tid < ST_COUNT) sc[tid] = 0;
-    if (tid < 6) cnt[tid] = 0;
+    if (tid < 7) cnt[tid] = 0;
     __syncthreads();
     const bool force_cx = p.force_complex || ctl->nonmono;
     const bool slot_clean = ctl->spilled == 0;  // no packet was folded into a slot directly (k_bin / k_reduce)
+    // In list order (a fused finish with ex_start != EX_START_NONE): each listed flow exports at most
+    // one record, so list entry k's export goes to record ex_start + k -- no reservation, which cost a
+    // returning atomic on the one counter per workgroup and pass, waited for before the stores (udp64
+    // k_fin_list 26 -> 20.5 us without it, profiles/r06/fin_ab.txt).  ex_start is the export count the
+    // host knows when nothing else appends before this kernel; workgroup 0 checks it against the
+    // counter (GUARD_EX_START) and sets the counter to ex_start + nf at its end (no other workgroup
+    // reads it).  Entries that do not export -- flows that turn complex or find no slot -- leave their
+    // records as holes (zeroed: end reason 0) counted in ctl->ex_holes; those flows send the batch to
+    // the host, which closes the holes (k_ex_compact) before it reads the exports.
+    const bool lorder = fused && !deferred_only && ex_start != EX_START_NONE;
+    uint32_t n_holes = 0;
+    if (lorder && blockIdx.x == 0 && tid == 0 && *ex.count != ex_start) atomicOr(&ctl->guard, GUARD_EX_START);
     // the batch's latest second: its last packet's, when no timestamp went backwards (else every
     // flow is complex anyway, force_cx)
     const uint32_t tmax = force_cx || b.n == 0 ? TMAX_UNKNOWN : b.desc[b.n - 1].ts_sec;
@@ -2193,6 +2205,22 @@ __global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPX
         // one reservation in the export buffer per workgroup and pass (a returning atomic per
         // wave on the one counter serialised ~1600 waves at ~12 ns each: MI355X_MICROARCH.md
         // "fanin" / "dequeue")
+        if (lorder) {  // uniform
+            if (k < nf) {
+                if (do_export) {
+                    store_export_w(ex, ex_start + k, er, reason);
+                    n_ex++;
+                    n_v6 += rw_ipver(er) == 6 ? 1 : 0;
+                } else {
+                    store_export_hole(ex, ex_start + k);
+                    n_holes++;
+                }
+            }
+            count_exports_wave(sc, do_export, er, reason);
+            PROBE_T(f3x);
+            PROBE_ADD(2, f2, f3x);
+            continue;
+        }
         uint32_t btot;
         const uint32_t pos = block_exclusive_scan<FIN_THREADS>(do_export ? 1u : 0u, scan_s, &btot);
         if (btot == 0) continue;  // uniform
@@ -2219,6 +2247,7 @@ __global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPX
     wave_add_lds(&cnt[3], n_v6);
     wave_add_lds(&cnt[4], n_keys);
     wave_add_lds(&cnt[5], n_def);
+    wave_add_lds(&cnt[6], n_holes);
 #if defined(IPXG_EXP_FIN) && IPXG_EXP_FIN >= 1  // timing experiment only: no statistics / control-block counts
     return;
 #endif
@@ -2227,8 +2256,12 @@ __global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPX
         if (cnt[3] && ex.count6) atomicAdd(ex.count + 2, cnt[3]);  // count_v6_exports' counter
         if (cnt[0]) atomicAdd(&ctl->new_live, cnt[0]);
         if (cnt[1]) atomicAdd(&ctl->complex_count, cnt[1]);
-        if (cnt[2]) atomicAdd(&ctl->exported, cnt[2]);
+        // (a fused finish's exports are counted by nothing but the export counter: no guarded
+        // k_finish / k_expire follows it -- the one contended control-block word per workgroup saved)
+        if (cnt[2] && !lorder) atomicAdd(&ctl->exported, cnt[2]);
         if (cnt[4]) atomicAdd(&ctl->new_keys, cnt[4]);
+        if (cnt[6]) atomicAdd(&ctl->ex_holes, cnt[6]);
+        if (lorder && blockIdx.x == 0) *ex.count = ex_start + nf;  // (workgroup 0 has list entries: nf > 0)
         if (cnt[5]) atomicAdd(&ctl->fin_deferred, cnt[5]);
     }
 #ifdef IPXG_PROBE
@@ -2241,7 +2274,7 @@ __global__ __launch_bounds__(FIN_THREADS) __attribute__((amdgpu_waves_per_eu(IPX
 
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
-                     bool finishing, bool deferred_only) {
+                     bool finishing, bool deferred_only, uint32_t ex_start) {
     // at most one wave of resident workgroups (3 per CU): a grid past it ran its last blocks'
     // several passes over the list in a second wave on a third of the chip
     // (per device, computed once; engines on several devices or threads share the cache: relaxed
@@ -2262,7 +2295,7 @@ void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableV
     uint32_t grid = (max_n + FIN_THREADS - 1) / FIN_THREADS;
     if (grid > resident) grid = resident;
     hipLaunchKernelGGL(k_fin_list, dim3(grid ? grid : 1), dim3(FIN_THREADS), 0, st, b, p, t, f, ex, ctl, fin_list,
-                       stats, finishing ? 1u : 0u, deferred_only ? 1u : 0u);
+                       stats, finishing ? 1u : 0u, deferred_only ? 1u : 0u, ex_start);
 }
 
 // ---- complex flows: their packets ----------------------------------------------------------

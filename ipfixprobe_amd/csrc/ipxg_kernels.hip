@@ -625,6 +625,35 @@ void launch_publish(hipStream_t st, const uint32_t* ctl, const uint32_t* ex, uin
     hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ctl, ex, dst, ctl_words, seq);
 }
 
+// Closes the holes a fused k_fin_list left in its export reservation (BatchCtl::ex_holes: flows that
+// turned complex or found no slot).  A rare path -- those flows send the batch to the host's sequential
+// path anyway -- so one workgroup walks [lo, hi) in 1024-record chunks: each chunk is read whole (the
+// scan's barriers) before any of it is written, and every destination lies at or below its source, so
+// the copy is in place and keeps the order.
+__global__ __launch_bounds__(1024) void k_ex_compact(ExportView ex, uint32_t lo, uint32_t hi) {
+    __shared__ uint32_t scan_s[1024 / 64 + 1];
+    uint32_t out = lo;
+    for (uint32_t base = lo; base < hi; base += 1024) {  // uniform
+        const uint32_t k = base + threadIdx.x;
+        RecW r;
+        bool keep = false;
+        if (k < hi) {
+            r = rec_load_w(&ex.buf[k]);
+            keep = ((r.w[RW_VLAN] >> 16) & 0xFF) != 0;
+        }
+        uint32_t tot;
+        const uint32_t pos = block_exclusive_scan<1024>(keep ? 1u : 0u, scan_s, &tot);
+        if (keep) rec_store_w(&ex.buf[out + pos], r);
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ex.count[0] = out;
+}
+
+void launch_ex_compact(hipStream_t st, ExportView ex, uint32_t lo, uint32_t hi) {
+    hipLaunchKernelGGL(k_ex_compact, dim3(1), dim3(1024), 0, st, ex, lo, hi);
+}
+
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
                    BatchCtl* guard, uint32_t ex_before, uint32_t live_before) {
     hipLaunchKernelGGL(k_finish, dim3(scan_grid(cap)), dim3(256), 0, st, t, cap, ex, stats, guard, ex_before,

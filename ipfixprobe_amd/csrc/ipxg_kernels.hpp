@@ -71,11 +71,14 @@ struct BatchCtl {
     uint32_t cx_ranges;      // k_complex_gather_rec: k_bin tile aggregates of complex flows listed
     uint32_t guard;          // bounds checks that failed (reported as IPXG_EDEVICE): 1 more complex
                              // slots than counted, 2 a complex flow's segment overran, 4 a plugin slot index
-                             // past the table, 8 (GUARD_STREAM_STALL) k_reduce_stream waited seconds for k_bin
+                             // past the table, 8 (GUARD_STREAM_STALL) k_reduce_stream waited seconds for k_bin,
+                             // 16 (GUARD_EX_START) k_fin_list found the export counter not at the host's count
     uint32_t spill_deferred; // of `deferred`: spills k_bin / k_bin_slow deferred (Params::defer_spill)
     uint32_t expired;        // records k_expire exported (the host's live count follows it, no table recount)
     uint32_t slow_redo;      // k_bin listed slow packets in a batch launched without k_bin_slow (Params::slow_skip):
                              // k_reduce and k_fin_list returned at once, the host runs all three again
+    uint32_t ex_holes;       // export records a fused k_fin_list reserved but did not fill (end reason 0:
+                             // flows that turned complex or found no slot); the host closes them (k_ex_compact)
     uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
 };
 
@@ -321,6 +324,7 @@ constexpr uint32_t RS_TARGET_FLOWS = 600;  // flows per partition the host sizes
 constexpr uint32_t PROG_LINES = 0xFFFFFu, PROG_EPOCH_SHIFT = 20, PROG_EPOCH_MASK = 0x3FFu << 20,
                    PROG_DONE = 0x80000000u;
 constexpr uint32_t GUARD_STREAM_STALL = 8u;  // BatchCtl::guard: k_reduce_stream saw no progress for seconds
+constexpr uint32_t GUARD_EX_START = 16u;     // ... k_fin_list's list-order exports: the export counter was not ex_start
 // The segment counts, column-major: workgroup col's counts of all partitions are contiguous, so
 // each k_bin / k_bin_slow workgroup writes whole lines of them (partition-major, every count was
 // a 4-byte piece of a line the other columns' workgroups, on other XCDs, wrote the rest of).
@@ -433,9 +437,12 @@ void launch_reduce_stream(hipStream_t st, const Params& p, TableView t, BinView 
                           uint32_t* deferred_list, uint4* agg_list);
 constexpr uint32_t FIN_UNRESOLVED = 0xFFFFFFFFu;  // a finalise-list entry's pad: the flow's slot not probed yet
 constexpr uint32_t FIN_DEFERRED = 0xFFFFFFFEu;    // ... its probe failed (table full): again after a rehash
+// ex_start: a fused finish's exports in list order from this export count (the device counter's value,
+// known to the host: nothing appends before the kernel), or EX_START_NONE (reserved per workgroup pass)
+constexpr uint32_t EX_START_NONE = 0xFFFFFFFFu;
 void launch_fin_list(hipStream_t st, const BatchView& b, const Params& p, TableView t, FragView f, ExportView ex,
                      BatchCtl* ctl, HotSlot* fin_list, unsigned long long* stats, uint32_t max_n,
-                     bool finishing, bool deferred_only = false);
+                     bool finishing, bool deferred_only = false, uint32_t ex_start = EX_START_NONE);
 // Params::plug: the marks k_bin and k_bin_slow listed -- plugin flows found in registers (slot
 // claimed and marked SLOT_PLUGIN here) and packets to classify from their frames (k_classify's
 // test) -- before k_reduce
@@ -525,6 +532,9 @@ void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, uns
                    BatchCtl* guard = nullptr, uint32_t ex_before = 0, uint32_t live_before = 0);
 void launch_publish(hipStream_t st, const uint32_t* ctl, const uint32_t* ex, uint32_t* dst, uint32_t ctl_words,
                     uint32_t seq);
+// The export records [lo, hi) with their holes (end reason 0, BatchCtl::ex_holes) dropped, in order;
+// the export count set to what remains.
+void launch_ex_compact(hipStream_t st, ExportView ex, uint32_t lo, uint32_t hi);
 void launch_ipfix_basic(hipStream_t st, const ipxg_flow_record* rec, uint32_t n, uint32_t dir, uint64_t* block_tot,
                         uint8_t* out, uint64_t* offsets);
 // IPFIX message plan (host, ipxg_engine.cpp): data sets in rank order per class (class 0 = the

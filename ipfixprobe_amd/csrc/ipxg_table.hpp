@@ -563,6 +563,17 @@ __device__ __forceinline__ void store_export_w(ExportView ex, uint32_t pos, cons
     o.w[RW_RSV] = o.w[RW_RSV + 1] = 0;                                  // reserved zero on export
     rec_store_w(&ex.buf[pos], o);
 }
+// A reserved export record left unfilled (k_fin_list's early reservation): all zero, so its end
+// reason is 0, which no export has (k_ex_compact drops it)
+__device__ __forceinline__ void store_export_hole(ExportView ex, uint32_t pos) {
+    if (pos >= ex.cap) {
+        atomicOr(ex.count + 1, 1u);
+        return;
+    }
+    uint4* q = reinterpret_cast<uint4*>(&ex.buf[pos]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = make_uint4(0, 0, 0, 0);
+}
 __device__ __forceinline__ void count_export_w(uint32_t* sc, const RecW& r, uint8_t reason) {
     atomicAdd(&sc[ST_END_INACTIVE + reason - 1], 1u);
     atomicAdd(&sc[ST_PKTS_1 + pkts_bucket((uint64_t)r.w[RW_SPK] + r.w[RW_DPK])], 1u);

@@ -82,7 +82,7 @@ class Timing(ctypes.Structure):
         [("plugin_ms", ctypes.c_double)] + [(n, ctypes.c_uint64) for n in ("plugin_flows", "plugin_packets",
                                                                              "plugin_bytes", "plugin_extra_bytes",
                                                                              "plugin_overlapped", "slow_redos",
-                                                                             "plugin_d2h_bytes")]
+                                                                             "plugin_d2h_bytes", "ex_compactions")]
 
 
 class Capture(ctypes.Structure):

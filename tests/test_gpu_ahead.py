@@ -290,3 +290,32 @@ def test_rehash_behind_a_front_ahead(monkeypatch, ahead):
     assert st["table_capacity"] > 1 << 10
     diff = flowcmp.diff(got, want)
     assert not diff, diff
+
+
+def test_fused_finish_closes_export_holes():
+    """A fused finish (an asynchronous device batch into an empty table, finished at once) writes its
+    exports in list order from the export count the host knows (no reservation per workgroup pass).
+    Flows that turn complex -- a SYN after a FIN/RST, a gap past the inactive timeout -- leave their
+    records as holes, which k_ex_compact closes before the records are handed out
+    (ipxg_timing.ex_compactions).  Every workgroup's passes mix both kinds.  Four steps on one
+    engine: the first two without a poll between them (the second starts past the first's
+    records), the third's exports cleared: the polled records are exactly the oracle's."""
+    from ipfixprobe_amd import Engine
+    steps = [synth.flow_stream(seed=95 + k, n_flows=1500, n_pkts=8000, frag=False).batch() for k in range(4)]
+    wants = [oracle_py.run_capture(a, d, 1, cache_exp=20)[0] for a, d in steps]
+    with Engine() as e:
+        for k, (a, d) in enumerate(steps):
+            da, dd = _dev(a, d)
+            e.submit(da, dd, device=True, asynchronous=True)
+            e.finish()
+            if k == 2:
+                e.clear_exports()
+            if k in (1, 3):
+                got = e.poll()
+                want = np.concatenate([wants[0], wants[1]]) if k == 1 else wants[3]
+                diff = flowcmp.diff(got, want)
+                assert not diff, "step %d: %s" % (k, diff)
+                assert len(got) == len(want)
+        st, tm = e.stats(), e.timing()
+    assert st["complex_flows"] > 0
+    assert tm["ex_compactions"] >= 3
