@@ -518,6 +518,14 @@ static int setup_bins(ipxg_engine* e, uint32_t n, bool g64, BinView& bv, bool st
     bv.prog_mode = e->rec_sc1 && (ln || e->rec_sc1 == 2) && (uint64_t)P * cols * seg * 16 < 0xFFFFFF00ull ? PROG_SC1 : 0u;
     bv.pub_every = 1;
     bv.rs_sleep = 0;
+    // IPXG_SLOW_GROUP=n (A/B knob): each k_bin_slow workgroup takes n k_bin workgroups' slow lists --
+    // denser record segments, a quarter of the count columns, but configs[4]'s slow pass went from 44
+    // to 82 us per batch at n = 4 and k_reduce from 200 to 230 (fewer, longer workgroups: the slow
+    // parser is latency-bound), so one list each.  Not with process plugins (a workgroup appends the
+    // marks of its own k_bin workgroup's list).
+    bv.slow_group = 1;
+    if (const char* sg = std::getenv("IPXG_SLOW_GROUP"))
+        bv.slow_group = e->plugins.empty() ? std::max(1u, std::min<uint32_t>((uint32_t)std::atoi(sg), SLOW_GROUP_MAX)) : 1u;
     if (sm) {
         if ((rc = ensure(e, e->prog, (size_t)RS_MAX_COLS * P * sizeof(uint32_t)))) return rc;
         if (++e->prog_epoch > (PROG_EPOCH_MASK >> PROG_EPOCH_SHIFT) || grid != e->prog_g || P != e->prog_p) {

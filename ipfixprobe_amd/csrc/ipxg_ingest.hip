@@ -1273,12 +1273,33 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
     uint32_t folded = 0;
     static_assert(sizeof(stage) >= IPXG_WIN_DW * IPXG_BLOCK * 4, "header columns exceed the stage");
     uint32_t* win = reinterpret_cast<uint32_t*>(stage);
-    // k_bin workgroup b's slow packets, into segment column bin_grid + b
-    const uint32_t ns = bv.slow_cnt[blockIdx.x];  // final: k_bin has completed
-    const uint4* const list = slow_list + (size_t)blockIdx.x * bv.slow_stride;
+    // the slow packets of k_bin workgroups blockIdx.x * G ... + G - 1 (BinView::slow_group), one list
+    // after the other, into segment column bin_grid + blockIdx.x; spre: the lists' starts
+    __shared__ uint32_t spre[SLOW_GROUP_MAX + 1];
+    const uint32_t G = bv.slow_group ? bv.slow_group : 1u;
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (uint32_t g = 0; g < G; ++g) {
+            spre[g] = s;
+            const uint32_t lb = blockIdx.x * G + g;
+            s += lb < bv.bin_grid ? bv.slow_cnt[lb] : 0u;  // final: k_bin has completed
+        }
+        spre[G] = s;
+    }
+    __syncthreads();
+    const uint32_t ns = spre[G];
+    const uint4* const list = slow_list + (size_t)blockIdx.x * G * bv.slow_stride;
+    // entry x of the merged lists (x < ns)
+    auto slow_at = [&](uint32_t x) -> uint4 {
+        if (G == 1) return list[x];
+        uint32_t g = 0;
+#pragma unroll
+        for (uint32_t q = 1; q < SLOW_GROUP_MAX; ++q) g += (q < G && spre[q] <= x) ? 1u : 0u;
+        return list[(size_t)g * bv.slow_stride + (x - spre[g])];
+    };
     const __amdgpu_buffer_rsrc_t rs_arena = arena_rsrc(b);
     const uint32_t bcol = bv.bin_grid + blockIdx.x;  // this block's segment column
-    if (ns == 0) return;  // no work: k_reduce does not read the column
+    if (ns == 0) return;  // no work: k_reduce does not read the column (uniform)
 #if defined(IPXG_EXP_SLOW) && IPXG_EXP_SLOW == 1  // timing experiment: the launch alone
     if (ns) return;
 #endif
@@ -1310,7 +1331,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
             const uint32_t k = (uint32_t)j * IPXG_BLOCK + tid;
             crk[j] = 0xFFFFFFFFu;
             if (k < nt) {
-                const uint32_t c = list[tile + k].x >> 24;
+                const uint32_t c = slow_at(tile + k).x >> 24;
                 crk[j] = (c << 16) | atomicAdd(&ccnt[c], 1u);
             }
         }
@@ -1340,7 +1361,7 @@ void k_bin_slow(BatchView b, Params p, TableView t, FragView f, BinView bv, Batc
         // larger than the instruction cache.
         auto entry = [&](int j) {
             const uint32_t k = tile + (uint32_t)j * IPXG_BLOCK + tid;
-            return j < BIN_K && k < ns ? list[tile + ord[k - tile]] : make_uint4(0, BUF_OOB, 0, 0);
+            return j < BIN_K && k < ns ? slow_at(tile + ord[k - tile]) : make_uint4(0, BUF_OOB, 0, 0);
         };
         uint4 e0 = entry(0), e1 = entry(1);
         SlowWin w0 = load_win<G64>(rs_arena, b, e0);
@@ -1447,8 +1468,10 @@ void launch_bin_slow(hipStream_t st, const BatchView& b, const Params& p, TableV
                                uint4*, unsigned long long*);
     const SlowKernel k = b.oshift ? (p.tile_agg ? k_bin_slow<true, true> : k_bin_slow<false, true>)
                                   : (p.tile_agg ? k_bin_slow<true> : k_bin_slow<false>);
-    hipLaunchKernelGGL(k, dim3(bv.bin_grid), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list, deferred_list,
-                       agg_list, stats);
+    const uint32_t g = bv.slow_group ? bv.slow_group : 1u;
+    bv.slow_group = g;
+    hipLaunchKernelGGL(k, dim3((bv.bin_grid + g - 1) / g), dim3(IPXG_BLOCK), 0, st, b, p, t, f, bv, ctl, slow_list,
+                       deferred_list, agg_list, stats);
 }
 
 // ---- phase B ------------------------------------------------------------------------------
@@ -1726,7 +1749,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce(TableView t, BinView bv,
 #pragma unroll
     for (uint32_t q = 0; q < RED_MAX_COLS / RED_THREADS; ++q) {
         const uint32_t c = tid * (RED_MAX_COLS / RED_THREADS) + q;
-        v[q] = c < bv.bin_grid || (c < cols && bv.slow_cnt[c - bv.bin_grid]) ? bv.count[seg_count_idx(bv, part, c)] : 0;
+        v[q] = c < bv.bin_grid || (c < cols && slow_col_written(bv, c - bv.bin_grid)) ? bv.count[seg_count_idx(bv, part, c)] : 0;
         my += v[q];
     }
     uint32_t total;
@@ -2464,7 +2487,7 @@ __global__ __launch_bounds__(256) void k_complex_gather_rec(BinView bv, ComplexV
         uint32_t n = 0;
         if (s < nseg) {
             const uint32_t c = s % bv.cols;
-            if (c < bv.bin_grid || bv.slow_cnt[c - bv.bin_grid]) n = bv.count[seg_count_idx(bv, s / bv.cols, c)];  // (else a k_bin_slow column left unwritten)
+            if (c < bv.bin_grid || slow_col_written(bv, c - bv.bin_grid)) n = bv.count[seg_count_idx(bv, s / bv.cols, c)];  // (else a k_bin_slow column left unwritten)
         }
         uint32_t tot;
         const uint32_t at = block_exclusive_scan<256>(n, scan_s, &tot);

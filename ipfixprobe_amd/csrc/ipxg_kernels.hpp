@@ -311,7 +311,26 @@ struct BinView {
     uint32_t prog_mode;    // PROG_SC1: write-through record stores; PROG_TILE: a publish every pub_every tiles (else: at the end)
     uint32_t pub_every;    // tiles between k_bin's publishes
     uint32_t rs_sleep;     // k_reduce_stream: s_sleep(64) calls between polls that found nothing new
+    // k_bin_slow workgroup j takes the slow lists of k_bin workgroups j * slow_group ... + slow_group - 1
+    // in turn (ceil(bin_grid / slow_group) workgroups, columns bin_grid + j): with a sparse slow path
+    // (configs[4]: ~260 packets per list) whole tiles, and record segments holding several records
+    // instead of a fraction of one -- measured slower (ipxg_engine.cpp setup_bins), so 1 by default
+    uint32_t slow_group;
 };
+constexpr uint32_t SLOW_GROUP_MAX = 8;
+#ifdef __HIPCC__
+// k_bin_slow column j (of bin_grid) holds records: one of its lists had packets (else the workgroup
+// returned without writing the column's counts)
+__device__ __forceinline__ bool slow_col_written(const BinView& bv, uint32_t j) {
+    bool w = false;
+    const uint32_t G = bv.slow_group ? bv.slow_group : 1u;  // (a view never set up: one list each)
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t b = j * G + g;
+        w = w || (b < bv.bin_grid && bv.slow_cnt[b] != 0);
+    }
+    return w;
+}
+#endif
 constexpr uint32_t PROG_SC1 = 1u, PROG_TILE = 2u;
 constexpr uint32_t BIN_LINE_P = 256;  // line mode's partitions, at most (ipxg_ingest.hip LINE_P)
 // The streamed reduce (k_reduce_stream): one 1024-thread workgroup per partition beside two k_bin

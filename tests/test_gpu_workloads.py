@@ -85,6 +85,34 @@ def test_workload_parity(name, walk):
     assert gst["parsed_packets"] == n * nb
 
 
+@pytest.mark.parametrize("group", ["1", "3", "8"])
+@pytest.mark.parametrize("name", sorted(MIXES))
+def test_slow_lists_grouped(name, group, monkeypatch):
+    """k_bin_slow workgroups taking several k_bin workgroups' slow lists (BinView::slow_group; the
+    engine picks it from the previous batch's slow count, IPXG_SLOW_GROUP pins it): 1 (one list
+    each), 3 (the last group short of lists) and 8, on three batches of each mix (every batch in
+    units as well as bytes would double the time; bytes here) against the oracle, with the
+    packet statistics."""
+    import torch
+    monkeypatch.setenv("IPXG_SLOW_GROUP", group)
+    gen = _gen(name, 200_000, seed=321)
+    n, nb = 400_000, 3
+    batches = [gen.batch(k * n, n) for k in range(nb)]
+    torch.cuda.synchronize()
+    got, gst = _run_batches("s=20", batches)
+    c = oracle_py.OracleCache(cache_exp=21)
+    for fr, de in batches:
+        c.run(fr.cpu().numpy(), de.cpu().numpy().view(pcaputil.DESC_DTYPE), 1)
+    c.finish()
+    want = c.take()
+    wst = c.stats()
+    c.close()
+    d = flowcmp.diff(got, want)
+    assert not d, d
+    for k in ("seen_packets", "parsed_packets", "ipv6_packets", "mpls_packets", "pppoe_packets"):
+        assert gst[k] == wst[k], k
+
+
 def test_imix_batch_parity_against_oracle_single_batch():
     """One 1M-packet IMIX batch (the Zipf elephant flows concentrate ~12 % of the packets on one
     flow: the binned ingest's skew handling) bit-exact against the oracle."""
