@@ -16,6 +16,7 @@ for W in ${WORKLOADS:-udp64}; do
     stream) ARGS="--mode stream --steps 300 --warmup 5" ;;
     imix) ARGS="--workload imix --steps 3 --warmup 1" ;;
     quic) ARGS="--workload quic --steps 5 --warmup 1" ;;
+    strict) ARGS="--strict 17 --steps 3 --warmup 1" ;;
   esac
   for V in ${VARS:-base}; do
     name=${V%%:*}; E=""; L=""
