@@ -399,6 +399,36 @@ def end_to_end(eng, frames, desc, packets, reps=3):
 
 
 # ---- workloads -------------------------------------------------------------------------------------
+def two_engines(eng, wl, args, local, step_on, steps, one_ms):
+    """The same cold steps on two engines in turn, each with its own stream and table (two capture
+    queues of one GPU, as the reference runs a cache per queue): step k+1's k_bin starts while step
+    k's k_reduce / k_fin_list run on the other stream.  Every step starts from an empty table and is
+    finished, so each step's records are the one-engine records (tests/test_gpu_ahead.py
+    test_two_engines_in_turn).  Reported beside the line's value, which stays the one-engine rate."""
+    import torch
+    from ipfixprobe_amd import Engine
+    eng.profile(0)
+    e2 = Engine(engine_params(wl.flows, args.ingest, args.walk), device_id=local)
+    try:
+        engs = (eng, e2)
+        for k in range(4):
+            step_on(engs[k % 2])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step_on(engs[k % 2])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        e2.close()
+    pk = sum(wl.packets[:wl.per_step])
+    ms = dt / steps * 1e3
+    return {"value": round(pk * steps / dt / 1e6, 2), "unit": "Mpkts/s", "ms_per_step": round(ms, 4),
+            "steps": steps, "vs_one_engine": round(one_ms / ms, 4),
+            "what": "the line's cold steps alternating between two engines (streams, tables): one step's "
+                    "flow-state kernels overlap the next step's k_bin; records per step unchanged"}
+
+
 def torch_int32():
     import torch
     return torch.int32
@@ -621,6 +651,8 @@ def main():
     ap.add_argument("--walk", default="auto", choices=["auto", "wide", "narrow"],
                     help="k_bin's header walk (auto: chosen per batch from the previous batch's mix)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host batch) rate")
+    ap.add_argument("--no-two-engines", action="store_true",
+                    help="skip the two-engine rate of the cold steps (two_engines in the line)")
     ap.add_argument("--strict", type=int, default=None, metavar="S",
                     help="strict mode with the reference's table of 2^S records (S=17: its default): "
                          "its evictions and sweep replayed exactly (ipxg_strict.hip)")
@@ -706,7 +738,7 @@ def main():
     cursor = [0]
     gather = ExportGather(eng, rank, world, device) if world > 1 or args.gather else None
 
-    def step():
+    def step_on(e):
         # with the gather: the previous step's exports are formatted (ipxg_device_ipfix_messages on
         # the engine's formatting stream) and handed to the gather right after this step's first
         # batch is submitted, beside its k_bin -- the tail of the batch joins the formatting
@@ -714,19 +746,22 @@ def main():
             for k in range(wl.per_step):
                 fr, de = wl.batches[k]
                 # back to back; finish right behind (the batches were synchronised after generation)
-                eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False, offset16=args.offset16)
+                e.submit(fr, de, device=True, asynchronous=True, wait_producer=False, offset16=args.offset16)
                 if k == 0 and gather is not None:
                     gather.step()
-            eng.finish()
+            e.finish()
         else:
             fr, de = wl.batches[cursor[0]]
             cursor[0] += 1
-            eng.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
+            e.submit(fr, de, device=True, asynchronous=True, wait_producer=False)
             if gather is not None:
                 gather.step()
-            eng.expire(wl.last_sec[cursor[0] - 1])  # the virtual clock: idle flows out (none idle here)
+            e.expire(wl.last_sec[cursor[0] - 1])  # the virtual clock: idle flows out (none idle here)
         if gather is None:
-            eng.clear_exports()
+            e.clear_exports()
+
+    def step():
+        step_on(eng)
 
     for _ in range(args.warmup):
         step()
@@ -837,6 +872,10 @@ def main():
             args.strict is None:
         e2e = end_to_end(eng, wl.batches[0][0], wl.batches[0][1], wl.packets[0])
         e2e["pipelined"] = end_to_end_pipelined(eng, wl.batches[0][0], wl.batches[0][1], wl.packets[0])
+    two = None
+    if rank == 0 and world == 1 and wl.finish and gather is None and not plugins and args.strict is None and \
+            not args.no_two_engines:
+        two = two_engines(eng, wl, args, local, step_on, min(args.steps, 300), step_ms)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         fr, de = wl.batches[0]
@@ -888,6 +927,7 @@ def main():
             "walked_packets_share": round((st["walked_packets"] - st0["walked_packets"]) /
                                           max(st["parsed_packets"] - st0["parsed_packets"], 1), 4),
             "e2e_pcie": e2e,
+            "two_engines": two,
             "spilled_packets": int(st["spilled_packets"]),
             "complex_flows": int(st["complex_flows"]),
             "gather": {"what": "per-rank IPFIX stream (odid = rank) -> rank 0 over RCCL point to point, exactly "

@@ -319,3 +319,23 @@ def test_fused_finish_closes_export_holes():
         st, tm = e.stats(), e.timing()
     assert st["complex_flows"] > 0
     assert tm["ex_compactions"] >= 3
+
+
+def test_two_engines_in_turn():
+    """bench.py's two_engines: cold steps alternating between two engines on one GPU (each its own
+    stream and table), submitted without waiting -- each engine's polled records are exactly the
+    oracle records of its steps."""
+    from ipfixprobe_amd import Engine
+    steps = _steps()
+    dev = [_dev(a, d) for a, d in steps]
+    wants = [oracle_py.run_capture(a, d, 1, cache_exp=20)[0] for a, d in steps]
+    with Engine() as e0, Engine() as e1:
+        engs = (e0, e1)
+        for k, (da, dd) in enumerate(dev):
+            engs[k % 2].submit(da, dd, device=True, asynchronous=True)
+            engs[k % 2].finish()
+        for r in range(2):
+            got = engs[r].poll()
+            want = np.concatenate([wants[k] for k in range(r, len(steps), 2)])
+            diff = flowcmp.diff(got, want)
+            assert not diff, "engine %d: %s" % (r, diff)
