@@ -553,18 +553,26 @@ void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, i
 // guard != nullptr: a finish enqueued right behind a batch before the host has read the
 // batch's control block (guard_holds); when it holds, the host completes the batch and finishes
 // again.
-__global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, ExportView ex,
+// FIN_SCAN_THREADS slots per workgroup: one reservation of export records per workgroup, a
+// returning atomic on the one counter (~11 ns each when they queue: MI355X_MICROARCH.md "fanin") --
+// at 256 slots per workgroup a 2^21-slot table made 8192 of them.  1024: configs[4]'s finish 140 ->
+// 136 us (the reservations mostly overlap the scan's loads; profiles/r06/finish_ab.txt).
+#ifndef IPXG_FINISH_THREADS
+#define IPXG_FINISH_THREADS 1024
+#endif
+constexpr uint32_t FIN_SCAN_THREADS = IPXG_FINISH_THREADS;
+__global__ __launch_bounds__(FIN_SCAN_THREADS) void k_finish(TableView t, uint32_t cap, ExportView ex,
                                                 unsigned long long* stats, BatchCtl* guard, uint32_t ex_before,
                                                 uint32_t live_before) {
-    __shared__ uint32_t scratch[8];
+    __shared__ uint32_t scratch[FIN_SCAN_THREADS / 64 + 1];
     __shared__ uint32_t bbase;
     __shared__ uint32_t pb[6];  // FlowRecordStats buckets of the block's exports
     if (guard && guard_holds(guard, ex_before, live_before, ex.cap)) return;
-    const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
+    const uint32_t base = blockIdx.x * FIN_SCAN_THREADS * SCAN_PER_THREAD;
     uint32_t mask = 0, c = 0;
 #pragma unroll
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
-        const uint32_t s = base + j * 256 + threadIdx.x;
+        const uint32_t s = base + j * FIN_SCAN_THREADS + threadIdx.x;
         if (s >= cap) continue;
         if (t.hot(s).key == 0) continue;  // an empty slot is all zero already
         if (t.hot(s).state & SLOT_LIVE) {
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         z[0] = z[1] = z[2] = z[3] = make_uint4(0, 0, 0, 0);
     }
     uint32_t total;
-    const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
+    const uint32_t off = block_exclusive_scan<FIN_SCAN_THREADS>(c, scratch, &total);
     if (threadIdx.x == 0) bbase = total ? atomicAdd(ex.count, total) : 0;
     if (threadIdx.x < 6) pb[threadIdx.x] = 0;
     __syncthreads();
@@ -585,7 +593,7 @@ __global__ __launch_bounds__(256) void k_finish(TableView t, uint32_t cap, Expor
         const bool mine = mask >> j & 1;
         RecW rec;
         if (mine) {
-            rec = tbl_load_rec(t, base + j * 256 + threadIdx.x);
+            rec = tbl_load_rec(t, base + j * FIN_SCAN_THREADS + threadIdx.x);
             store_export_w(ex, pos++, rec, IPXG_FLOW_END_FORCED);
         }
         {  // the FlowRecordStats buckets, one LDS atomic per wave and bucket present
@@ -656,8 +664,8 @@ void launch_ex_compact(hipStream_t st, ExportView ex, uint32_t lo, uint32_t hi) 
 
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
                    BatchCtl* guard, uint32_t ex_before, uint32_t live_before) {
-    hipLaunchKernelGGL(k_finish, dim3(scan_grid(cap)), dim3(256), 0, st, t, cap, ex, stats, guard, ex_before,
-                       live_before);
+    hipLaunchKernelGGL(k_finish, dim3((cap + FIN_SCAN_THREADS * SCAN_PER_THREAD - 1) / (FIN_SCAN_THREADS * SCAN_PER_THREAD)),
+                       dim3(FIN_SCAN_THREADS), 0, st, t, cap, ex, stats, guard, ex_before, live_before);
 }
 
 __global__ __launch_bounds__(256) void k_rehash(TableView from, uint32_t from_cap, TableView to,
