@@ -164,6 +164,11 @@ struct ipxg_engine {
     uint32_t stream_grid = 0;  // k_bin's workgroups when streamed: two per CU (<= RS_MAX_COLS)
     uint32_t prog_mode = PROG_SC1 | PROG_TILE;  // IPXG_PROG_MODE (timing experiments)
     uint32_t pub_every = 4, rs_sleep = 4;       // IPXG_PUB_EVERY, IPXG_RS_SLEEP (tuning knobs)
+    // every live record's time_last_sec is at least this (k_expire's last scan; packets since then kept
+    // the order, so none is older), or IDLE_FLOOR_NONE: ipxg_expire at a time when none can be idle
+    // scans nothing (the streaming step's expire every batch)
+    int64_t idle_floor = IDLE_FLOOR_NONE;
+    bool no_idle_floor = false;                 // IPXG_NO_IDLE_FLOOR=1: every ipxg_expire scans (A/B)
     bool fin_lorder = true;                     // IPXG_FIN_LORDER=0: a fused finish reserves its exports per pass (A/B)
     uint32_t rec_sc1 = 1;                       // IPXG_REC_SC1: 0 plain record stores, 1 write-through in line mode, 2 always
     // A batch (or finish) whose last kernels and control-block publish are enqueued but whose block
@@ -802,6 +807,7 @@ int ipxg_create(const ipxg_config* cfg, ipxg_engine** out) {
     e->no_stream = !(std::getenv("IPXG_STREAM") != nullptr && std::atoi(std::getenv("IPXG_STREAM")) != 0);
     if (const char* pm = std::getenv("IPXG_PROG_MODE")) e->prog_mode = (uint32_t)std::atoi(pm) & 3u;
     if (const char* fl = std::getenv("IPXG_FIN_LORDER")) e->fin_lorder = std::atoi(fl) != 0;
+    e->no_idle_floor = std::getenv("IPXG_NO_IDLE_FLOOR") != nullptr && std::atoi(std::getenv("IPXG_NO_IDLE_FLOOR")) != 0;
     if (const char* rs = std::getenv("IPXG_REC_SC1")) e->rec_sc1 = (uint32_t)std::max(0, std::atoi(rs));
     if (const char* pe = std::getenv("IPXG_PUB_EVERY")) e->pub_every = std::max(1, std::atoi(pe));
     if (const char* rsl = std::getenv("IPXG_RS_SLEEP")) e->rs_sleep = (uint32_t)std::max(0, std::atoi(rsl));
@@ -2300,9 +2306,18 @@ static void take_batch_knobs(ipxg_engine* e, const BatchCtl& c2, const Params& p
         // loads.  walk=wide|narrow pins it.
         e->wide = (uint64_t)(c2.slow_count + (p.wide ? c2.walked : 0)) * 32 >= n;
     }
+    // a batch not checked against the one before (the first after a finish or reset), or one whose
+    // timestamps went backwards, may have left records older than the idle floor
+    if (c2.nonmono || !(p.prev_valid || p.prev_dev)) e->idle_floor = IDLE_FLOOR_NONE;
     e->prev_valid = true;
     e->prev_sec = c2.last_sec;
     e->prev_usec = c2.last_usec;
+}
+
+// k_expire's scan result (BatchCtl::tls_inv) as the idle floor; 0: it did not scan (the floor stands)
+static void take_idle_floor(ipxg_engine* e, uint32_t tls_inv) {
+    if (tls_inv == 1) e->idle_floor = INT64_MAX;  // (no record left live)
+    else if (tls_inv) e->idle_floor = (int64_t)(uint32_t)~tls_inv;
 }
 
 
@@ -2580,8 +2595,11 @@ static int expire_impl(ipxg_engine* e, int64_t now_sec) {
         if ((rc = ensure_export(e, (size_t)e->live + 2ull * e->inflight.n))) return rc;
         if ((rc = launch_tail(e, false))) return rc;
         e->inflight.on = false;
+        const Params& ip = e->inflight.p;  // (the floor holds behind the batch if its order was checked)
         launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d, e->ctl_d,
-                      &e->ctl_d->expired, e->ex_count, e->live);
+                      &e->ctl_d->expired, e->ex_count, e->live,
+                      (ip.prev_valid || ip.prev_dev) && !e->no_idle_floor ? e->idle_floor : IDLE_FLOOR_NONE,
+                      &e->ctl_d->tls_inv);
         HIPCHK(e, hipGetLastError());
         set_pend(e, GATE_EXPIRE, e->inflight.bv, e->inflight.p, e->inflight.n);
         e->pend.now = now_sec;
@@ -2611,14 +2629,18 @@ static int expire_impl(ipxg_engine* e, int64_t now_sec) {
 // k_expire exported (BatchCtl::expired of the current block).
 static int expire_table(ipxg_engine* e, int64_t now_sec) {
     int rc;
+    if (e->idle_floor != IDLE_FLOOR_NONE && now_sec - (int64_t)e->cfg.inactive_s < e->idle_floor && !e->no_idle_floor)
+        return IPXG_OK;  // no live record can be idle yet: nothing to scan
     if ((rc = ensure_export(e, std::max(e->live, e->keys)))) return rc;
     HIPCHK(e, hipMemsetAsync(&e->ctl_d->expired, 0, sizeof(uint32_t), e->st));
+    HIPCHK(e, hipMemsetAsync(&e->ctl_d->tls_inv, 0, sizeof(uint32_t), e->st));
     launch_expire(e->st, params(e), table_view(e), e->cap, now_sec, export_view(e), e->stats_d, nullptr,
-                  &e->ctl_d->expired);
+                  &e->ctl_d->expired, 0, 0, IDLE_FLOOR_NONE, &e->ctl_d->tls_inv);
     HIPCHK(e, hipGetLastError());
     if ((rc = sync_ctl(e))) return rc;
     const uint32_t x = e->ctl_h->expired;
     e->live = x > e->live ? 0u : e->live - x;
+    take_idle_floor(e, e->ctl_h->tls_inv);
     return IPXG_OK;
 }
 
@@ -2638,6 +2660,7 @@ static int finish_table(ipxg_engine* e) {
     }
     e->keys = e->live = 0;
     e->prev_valid = false;
+    e->idle_floor = IDLE_FLOOR_NONE;
     return IPXG_OK;
 }
 
@@ -2682,9 +2705,14 @@ static int consume_pend(ipxg_engine* e, bool spec) {
         } else if (q.mode == GATE_EXPIRE) {  // k_expire right behind the batch, unless its guard held it
             const bool held = e->ctl_h->hold != 0;
             const uint32_t x = held ? 0u : e->ctl_h->expired;
+            const uint32_t ti = held ? 0u : e->ctl_h->tls_inv;
             rc = post_batch(e, q.bv, q.p, q.n, true, false);
-            if (!rc && !held) e->live = x > e->live ? 0u : e->live - x;
-            else if (!rc) rc = expire_table(e, q.now);  // the batch is complete now: expire normally
+            if (!rc && !held) {
+                e->live = x > e->live ? 0u : e->live - x;
+                take_idle_floor(e, ti);  // (it ran with no host work left by the batch: the scan is exact)
+            } else if (!rc) {
+                rc = expire_table(e, q.now);  // the batch is complete now: expire normally
+            }
         } else if (q.mode == GATE_FIN_FUSED) {
             // k_fin_list exported what it finalised: complete unless it could not fuse (host work)
             // or left complex flows
@@ -2693,6 +2721,7 @@ static int consume_pend(ipxg_engine* e, bool spec) {
             if (!rc && done) {
                 e->keys = e->live = 0;
                 e->prev_valid = false;
+                e->idle_floor = IDLE_FLOOR_NONE;
             } else if (!rc) {
                 rc = finish_table(e);  // the remaining flows
             }
@@ -2708,6 +2737,7 @@ static int consume_pend(ipxg_engine* e, bool spec) {
                 }
                 e->keys = e->live = 0;
                 e->prev_valid = false;
+                e->idle_floor = IDLE_FLOOR_NONE;
             } else if (!rc) {
                 rc = finish_table(e);  // the batch is complete now: finish normally
             }
@@ -2810,6 +2840,7 @@ int ipxg_reset(ipxg_engine* e) {
     e->keys = e->live = 0;
     e->last_touched = 0;
     e->prev_valid = false;
+    e->idle_floor = IDLE_FLOOR_NONE;
     return IPXG_OK;
 }
 

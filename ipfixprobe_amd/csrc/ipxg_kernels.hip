@@ -495,32 +495,51 @@ __device__ __forceinline__ bool guard_holds(BatchCtl* guard, uint32_t ex_before,
 
 __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t cap, int64_t now,
                                                 ExportView ex, unsigned long long* stats, BatchCtl* guard,
-                                                uint32_t* expired, uint32_t ex_before, uint32_t live_before) {
+                                                uint32_t* expired, uint32_t ex_before, uint32_t live_before,
+                                                int64_t floor, uint32_t* tls_inv) {
     __shared__ uint32_t scratch[8];
     __shared__ uint32_t sc[ST_COUNT];
     __shared__ uint32_t bbase;
+    __shared__ uint32_t tmin;
     if (guard && guard_holds(guard, ex_before, live_before, ex.cap)) return;
+    // no live record can be idle: each one's time_last_sec is at least the floor, later than
+    // now - inactive (the batch in front of a guarded expire kept the order: no older packet)
+    if (floor != IDLE_FLOOR_NONE && now - (int64_t)p.inactive_s < floor && !(guard && guard->nonmono)) return;
     if (threadIdx.x < ST_COUNT) sc[threadIdx.x] = 0;
+    if (threadIdx.x == 0) tmin = 0xFFFFFFFFu;
     const uint32_t base = blockIdx.x * 256 * SCAN_PER_THREAD;
-    uint32_t mask = 0, c = 0;
+    uint32_t mask = 0, c = 0, my_min = 0xFFFFFFFFu;
 #pragma unroll
     for (uint32_t j = 0; j < SCAN_PER_THREAD; ++j) {
         const uint32_t s = base + j * 256 + threadIdx.x;
         if (s >= cap) continue;
         const uint64_t key = t.hot(s).key;
         const uint32_t state = t.hot(s).state;
-        if (key != 0 && (state & SLOT_LIVE) &&
-            now - (int64_t)t.line[s].head[RW_TLS] >= (int64_t)p.inactive_s) {
+        if (key == 0 || !(state & SLOT_LIVE)) continue;
+        const uint32_t tls = t.line[s].head[RW_TLS];
+        if (now - (int64_t)tls >= (int64_t)p.inactive_s) {
             // the record leaves with its plugin extensions: nothing is followed any more (a
             // FOLLOW bit left behind kept the dead slot through every rehash and sent the key's
             // next packets to the host walk)
             t.hot(s).state = state & ~(SLOT_LIVE | SLOT_FOLLOW);
             mask |= 1u << j;
             c++;
+        } else {
+            my_min = min(my_min, tls);
         }
     }
+    if (tls_inv) {  // the least time_last_sec left live: wave minimum, one LDS atomic per wave
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) my_min = min(my_min, (uint32_t)__shfl_xor((int)my_min, o));
+        if ((threadIdx.x & 63) == 0 && my_min != 0xFFFFFFFFu) atomicMin(&tmin, my_min);
+    }
     uint32_t total;
-    const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);
+    const uint32_t off = block_exclusive_scan<256>(c, scratch, &total);  // (its barriers: tmin complete)
+    if (tls_inv && threadIdx.x == 0) {  // ~min as a maximum (1: scanned, none left); most blocks find
+                                        // a larger value already there and add no atomic
+        const uint32_t v = tmin == 0xFFFFFFFFu ? 1u : max(~tmin, 2u);
+        if (v > __hip_atomic_load(tls_inv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(tls_inv, v);
+    }
     if (threadIdx.x == 0) bbase = total ? atomicAdd(ex.count, total) : 0;
     if (threadIdx.x == 0 && total && expired) atomicAdd(expired, total);
     __syncthreads();
@@ -543,9 +562,9 @@ __global__ __launch_bounds__(256) void k_expire(Params p, TableView t, uint32_t 
 
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
                    ExportView ex, unsigned long long* stats, BatchCtl* guard, uint32_t* expired,
-                   uint32_t ex_before, uint32_t live_before) {
+                   uint32_t ex_before, uint32_t live_before, int64_t floor, uint32_t* tls_inv) {
     hipLaunchKernelGGL(k_expire, dim3(scan_grid(cap)), dim3(256), 0, st, p, t, cap, now, ex, stats, guard, expired,
-                       ex_before, live_before);
+                       ex_before, live_before, floor, tls_inv);
 }
 
 // Export every live record as FLOW_END_FORCED (finish, cache.cpp:276-288) and empty the

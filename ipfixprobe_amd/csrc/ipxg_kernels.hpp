@@ -77,6 +77,8 @@ struct BatchCtl {
     uint32_t expired;        // records k_expire exported (the host's live count follows it, no table recount)
     uint32_t slow_redo;      // k_bin listed slow packets in a batch launched without k_bin_slow (Params::slow_skip):
                              // k_reduce and k_fin_list returned at once, the host runs all three again
+    uint32_t tls_inv;        // k_expire's scan: ~(the least time_last_sec of the records it left live), 1 with
+                             // none left, 0 when it did not scan (the engine's idle floor, ipxg_engine.cpp)
     uint32_t ex_holes;       // export records a fused k_fin_list reserved but did not fill (end reason 0:
                              // flows that turned complex or found no slot); the host closes them (k_ex_compact)
     uint64_t probe[16];       // IPXG_PROBE builds: per-phase shader clocks (ipxg_probe_counters)
@@ -544,9 +546,14 @@ void launch_complex_walk(hipStream_t st, const BatchView& b, const Params& p, Ta
                          unsigned long long* stats);
 // guard != nullptr: an expire enqueued right behind a batch (ipxg_expire with an asynchronous batch
 // in flight), held back exactly as k_finish's guard; expired: += the records it exports.
+// floor: every live record's time_last_sec is at least this (IDLE_FLOOR_NONE: not known); when no
+// record can be idle at `now` the kernel returns without scanning (a guarded one only behind a
+// batch whose order check held); tls_inv: BatchCtl::tls_inv of the scan.
+constexpr int64_t IDLE_FLOOR_NONE = INT64_MIN;
 void launch_expire(hipStream_t st, const Params& p, TableView t, uint32_t cap, int64_t now,
                    ExportView ex, unsigned long long* stats, BatchCtl* guard, uint32_t* expired,
-                   uint32_t ex_before = 0, uint32_t live_before = 0);
+                   uint32_t ex_before = 0, uint32_t live_before = 0, int64_t floor = IDLE_FLOOR_NONE,
+                   uint32_t* tls_inv = nullptr);
 void launch_finish(hipStream_t st, TableView t, uint32_t cap, ExportView ex, unsigned long long* stats,
                    BatchCtl* guard = nullptr, uint32_t ex_before = 0, uint32_t live_before = 0);
 void launch_publish(hipStream_t st, const uint32_t* ctl, const uint32_t* ex, uint32_t* dst, uint32_t ctl_words,

@@ -480,3 +480,50 @@ def test_wide_walk_ext_and_gre_edges(walk, frag, agg, monkeypatch):
     for k in ("seen_packets", "parsed_packets", "unknown_packets", "ipv4_packets", "ipv6_packets",
               "tcp_packets", "udp_packets", "vlan_packets", "keyless_packets"):
         assert gst[k] == wst[k], k
+
+
+@pytest.mark.parametrize("asynchronous", [False, True])
+def test_expire_idle_floor(asynchronous, monkeypatch):
+    """ipxg_expire after every batch of a stream whose flows go idle at different times: the engine
+    keeps a floor under every live record's last-seen time (k_expire's last scan), and an expire at a
+    time when no record can be idle yet scans nothing.  Each poll equals the same engine's without
+    the floor (IPXG_NO_IDLE_FLOOR: every expire scans) -- with synchronous host batches and with
+    asynchronous device batches (the expire then runs guarded behind the batch in flight).  A batch
+    whose timestamps go backwards drops the floor.  (The expire times run ahead of the packets, so
+    the records are not the no-expire oracle's; the expire semantics themselves are pinned by the
+    stream parity tests.)"""
+    import torch
+    from ipfixprobe_amd import Engine
+    arena, desc = synth.flow_stream(seed=101, n_flows=500, n_pkts=12000, frag=False).batch()
+    desc = desc.copy()
+    i = np.arange(len(desc))
+    desc["ts_sec"] = 1_700_000_000 + i // 100  # 120 s: flows go idle one after another
+    desc["ts_usec"] = (i % 100) * 1000
+    desc["ts_sec"][7000:7100] -= 5  # one batch steps back in time
+    da = torch.from_numpy(np.ascontiguousarray(arena)).cuda() if asynchronous else None
+
+    def run(no_floor):
+        monkeypatch.setenv("IPXG_NO_IDLE_FLOOR", "1" if no_floor else "0")
+        polls, keep = [], []
+        with Engine() as e:
+            for s in range(0, len(desc), 1000):
+                part = desc[s:s + 1000]
+                now = int(part["ts_sec"].max())
+                if asynchronous:
+                    dd = torch.from_numpy(np.ascontiguousarray(part).view(np.uint8).reshape(-1)).cuda()
+                    keep.append(dd)
+                    e.submit(da, dd, device=True, asynchronous=True)
+                else:
+                    e.submit(arena, part)
+                for t in (now - 1, now, now + 3):  # (repeated: the later ones often find nothing idle)
+                    e.expire(t)
+                polls.append(e.poll())
+            e.finish()
+            polls.append(e.poll())
+        return polls
+
+    with_floor, without = run(False), run(True)
+    for k, (a, b) in enumerate(zip(with_floor, without)):
+        d = flowcmp.diff(a, b)
+        assert not d, "poll %d: %s" % (k, d)
+    assert sum(len(g) for g in with_floor[:-1]) > 100  # flows did go idle along the way
