@@ -2314,9 +2314,12 @@ static void take_batch_knobs(ipxg_engine* e, const BatchCtl& c2, const Params& p
     e->prev_usec = c2.last_usec;
 }
 
-// k_expire's scan result (BatchCtl::tls_inv) as the idle floor; 0: it did not scan (the floor stands)
+// k_expire's scan result (BatchCtl::tls_inv) as the idle floor; 0: it did not scan (the floor stands).
+// With no record left live the floor is the last packet's second: every later record is at least
+// that recent (the order held), not "never idle" -- a floor above it skipped the expiry of flows
+// created after the scan (tests/test_stdplugins.py test_expired_followed_flow_leaves_the_host_walk).
 static void take_idle_floor(ipxg_engine* e, uint32_t tls_inv) {
-    if (tls_inv == 1) e->idle_floor = INT64_MAX;  // (no record left live)
+    if (tls_inv == 1) e->idle_floor = e->prev_valid ? (int64_t)e->prev_sec : IDLE_FLOOR_NONE;
     else if (tls_inv) e->idle_floor = (int64_t)(uint32_t)~tls_inv;
 }
 
