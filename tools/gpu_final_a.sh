@@ -28,7 +28,7 @@ for W in ${WORKLOADS:-udp64 imix quic imix10m}; do
     N=$(echo $C | cut -d' ' -f1)
     echo "== pmc $W $N"; date
     timeout -k 10 -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$W/$N -o run -- \
-        python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/pmc_${W}_$N.json 2> $OUT/pmc_${W}_$N.err
+        python3 bench.py $ARGS --no-cpu-baseline --no-e2e --no-two-engines > $OUT/pmc_${W}_$N.json 2> $OUT/pmc_${W}_$N.err
     rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_${W}_$N.err; stop $rc "pmc $W $N"; }
   done
   S=pmc_summary_$W.json; [ $W = udp64 ] && S=pmc_summary.json

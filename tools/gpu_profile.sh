@@ -22,7 +22,7 @@ for W in ${WORKLOADS:-udp64 imix quic}; do
   esac
   echo "== kernel trace $W"; date
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$W -o run -- \
-      python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/kt_$W.json 2> $OUT/kt_$W.err
+      python3 bench.py $ARGS --no-cpu-baseline --no-e2e --no-two-engines > $OUT/kt_$W.json 2> $OUT/kt_$W.err
   rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/kt_$W.err; stop "kernel trace $W" $rc; }
   if [ "${PMC:-1}" = "1" ]; then
     # (each pass its own run: FETCH_SIZE takes 3 of the 4 TCC slots, WRITE_SIZE 2; the fabric
@@ -31,7 +31,7 @@ for W in ${WORKLOADS:-udp64 imix quic}; do
       N=$(echo $C | tr ' ' '_')
       echo "== pmc $W $N"; date
       timeout -k 10 -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$W/$N -o run -- \
-          python3 bench.py $ARGS --no-cpu-baseline --no-e2e > $OUT/pmc_${W}_$N.json 2> $OUT/pmc_${W}_$N.err
+          python3 bench.py $ARGS --no-cpu-baseline --no-e2e --no-two-engines > $OUT/pmc_${W}_$N.json 2> $OUT/pmc_${W}_$N.err
       rc=$?; [ $rc -ne 0 ] && { tail -3 $OUT/pmc_${W}_$N.err; stop "pmc $W $N" $rc; }
     done
   fi
